@@ -1,0 +1,163 @@
+/*
+ * mhmkc.h — C ABI of the MI355X-native k-mer counting stage (libmhmkc.so).
+ *
+ * This is the drop-in boundary for the MetaHipMer2 kcount hot path of ajpowelsnl/mhm2_proxy
+ * (reference: src/kcount/). The reference has no C ABI; its backend seam is two pimpl classes,
+ * SeqBlockInserter<MAX_K> (src/kcount/kcount.hpp:57-69) and HashTableInserter<MAX_K>
+ * (src/kcount/kmer_dht.hpp:95-116), linked either from kcount_cpu.cpp or kcount_gpu.cpp
+ * (src/kcount/CMakeLists.txt:23-43). Every entry point below names the reference interface it
+ * replaces. include/mhmkc_kcount.hpp rebuilds those C++ shapes (Kmer<MAX_K>, KmerCounts, KmerMap,
+ * analyze_kmers) on top of this ABI; INTEGRATION.md shows the binding.
+ *
+ * Semantics are bit-exact with the reference CPU kcount (kcount_cpu.cpp), not with its CUDA
+ * backend (which drops N-k-mers, caps extension counts at 10000 and uses an approximate filter).
+ *
+ * Conventions (mirroring the reference's error behaviour, which DIEs on bad input):
+ *   - every function returns MHMKC_OK (0) or a negative MHMKC_E* code; mhmkc_last_error() holds the
+ *     message; the C++ adapter turns a failure into a fatal error like the reference's DIE;
+ *   - host input buffers are borrowed only for the duration of the call;
+ *   - device input buffers passed to *_device functions must stay valid until mhmkc_finish returns;
+ *   - a handle drives exactly one GPU and is not thread-safe. Multi-GPU = one process (rank) per
+ *     GPU, all ranks calling the same sequence; the k-mer exchange is an RCCL all-to-all inside
+ *     mhmkc_finish (replacing the UPC++ supermer store, src/kcount/kmer_dht.cpp:133-149,222-224).
+ */
+#ifndef MHMKC_H
+#define MHMKC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MHMKC_ABI_VERSION 1
+#define MHMKC_COMM_ID_BYTES 128
+
+enum {
+  MHMKC_OK = 0,
+  MHMKC_EINVAL = -1,      /* bad argument or configuration */
+  MHMKC_ENOMEM = -2,      /* device or host allocation failed */
+  MHMKC_EHIP = -3,        /* HIP runtime error */
+  MHMKC_ERCCL = -4,       /* RCCL error */
+  MHMKC_ESTATE = -5,      /* call out of order (e.g. fetch before finish) */
+  MHMKC_EBADCHAR = -6,    /* input byte outside the PackedRead code range (reference DIE, kcount_cpu.cpp:453-458) */
+  MHMKC_EUNSUPPORTED = -7 /* valid for the reference but not supported here */
+};
+
+typedef struct mhmkc *mhmkc_t;
+
+/* Configuration of one counting round (one k). Replaces the KmerDHT constructor arguments
+ * (src/kcount/kmer_dht.cpp:106-154) and the analyze_kmers parameters (src/kcount/kcount.hpp:71-73). */
+typedef struct {
+  int32_t k;              /* k-mer length; 1 <= k <= 127, k % 32 != 0 */
+  int32_t n_longs;        /* output words per key; 0 = k/32+1 (= MAX_K/32, src/main.cpp:170) */
+  int32_t qual_offset;    /* 33 or 64 (only used by mhmkc_add_seqs' PackedRead-free path) */
+  int32_t qual_cutoff;    /* KCOUNT_QUAL_CUTOFF (CMakeDefinitions.txt:46), default 20 */
+  int32_t dmin_thres;     /* --min-depth-thres (src/options.cpp:289-290), default 2; <= 32768 */
+  double dyn_min_depth;   /* DYN_MIN_DEPTH (CMakeDefinitions.txt:60), default 0.9 */
+  int32_t device;         /* HIP device ordinal; -1 = current device */
+  int32_t rank;           /* this rank, 0 <= rank < n_ranks */
+  int32_t n_ranks;        /* number of GPUs (ranks) sharing the k-mer space */
+  const uint8_t *comm_id; /* MHMKC_COMM_ID_BYTES from mhmkc_comm_id() on rank 0; NULL if n_ranks==1 */
+  void *stream;           /* hipStream_t to run on; NULL = the library creates its own */
+} mhmkc_config;
+
+/* Statistics; replaces the SLOG lines of flush_inserts / insert_into_local_hashtable
+ * (src/kcount/kcount_cpu.cpp:465-488,525-527). Counters are for this rank. */
+typedef struct {
+  uint64_t reads;          /* reads submitted */
+  uint64_t bases;          /* bases submitted */
+  uint64_t occurrences;    /* counted windows i in [1, L-k-1] (records produced by this rank) */
+  uint64_t owned_records;  /* records counted on this rank after the exchange */
+  uint64_t distinct;       /* distinct canonical k-mers owned by this rank */
+  uint64_t purged;         /* dropped at finish: count < 2 or both extensions 'X' */
+  uint64_t n_out;          /* k-mers in the output table (== distinct - purged) */
+  uint64_t dropped;        /* always 0: the table never drops (reference num_dropped) */
+  uint64_t count_sum;      /* sum over distinct k-mers of the unsaturated count (== owned_records) */
+  uint64_t overflow_sweeps;/* extra LDS sweeps needed by over-full fine buckets */
+  uint64_t max_bucket;     /* largest fine bucket, records */
+  uint64_t fine_buckets;   /* number of fine buckets on this rank */
+  uint64_t bytes_sent;     /* bytes sent to other ranks in the exchange */
+  double ms_total;         /* wall time of the last add_reads..finish sequence (device events) */
+  double ms_kernel[8];     /* per-stage device time when profiling is on: see MHMKC_STAGE_* */
+  uint64_t launches[8];    /* per-stage launch count when profiling is on */
+} mhmkc_stats;
+
+enum {
+  MHMKC_STAGE_TILEIDX = 0, /* per-tile first-read index */
+  MHMKC_STAGE_EHIST = 1,   /* extract + coarse histogram */
+  MHMKC_STAGE_ESCAT = 2,   /* extract + coarse scatter */
+  MHMKC_STAGE_XCHG = 3,    /* RCCL all-to-all exchange */
+  MHMKC_STAGE_SHIST = 4,   /* fine histogram */
+  MHMKC_STAGE_SSCAT = 5,   /* fine scatter */
+  MHMKC_STAGE_COUNT = 6,   /* LDS hash-table count + finalize + compaction */
+  MHMKC_STAGE_OTHER = 7    /* scans, memsets */
+};
+
+/* Fill *cfg with the reference defaults (k=21, qual 33/20, dmin 2, dyn 0.9, one rank). */
+int mhmkc_config_init(mhmkc_config *cfg);
+
+/* Create a counter. Replaces KmerDHT<MAX_K>::KmerDHT + HashTableInserter::init
+ * (src/kcount/kmer_dht.cpp:106-154, src/kcount/kcount_cpu.cpp:425-443). With n_ranks > 1 every rank
+ * must call this collectively with the same comm_id. */
+int mhmkc_create(mhmkc_t *h, const mhmkc_config *cfg);
+
+/* Release all device memory and the communicator (HashTableInserter::~HashTableInserter,
+ * src/kcount/kcount_cpu.cpp:420-423). NULL is allowed. */
+void mhmkc_destroy(mhmkc_t h);
+
+/* RCCL unique id for mhmkc_config.comm_id (rank 0 calls it and broadcasts the bytes). */
+int mhmkc_comm_id(uint8_t out[MHMKC_COMM_ID_BYTES]);
+
+/* Add reads in the PackedRead byte layout (src/packed_reads.cpp:73-109): one byte per base,
+ * bits 0-2 = A,C,G,T,N -> 0..4, bits 3-7 = min(q - qual_offset, 31). read_offsets has n_reads+1
+ * entries, read_offsets[0] == 0, read i = bytes[read_offsets[i], read_offsets[i+1]).
+ * Replaces the count_kmers read loop + SeqBlockInserter::process_seq
+ * (src/kcount/kcount.cpp:54-98, src/kcount/kcount_cpu.cpp:73-103). Host buffers. */
+int mhmkc_add_reads(mhmkc_t h, const uint8_t *packed_bytes, const uint64_t *read_offsets, uint64_t n_reads);
+
+/* Same, with device-resident buffers (no copy; must stay valid until mhmkc_finish returns). */
+int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_packed_bytes, const uint64_t *d_read_offsets,
+                           uint64_t n_reads, uint64_t n_bases);
+
+/* Add sequences given as characters, lowercase = quality below the cutoff — the string that
+ * SeqBlockInserter::process_seq receives (src/kcount/kcount.cpp:80-86). Host buffers. depth is the
+ * per-sequence count (reads: 1). Only depth == 1 (the read pass) is supported in this version. */
+int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *seq_offsets, uint64_t n_seqs, uint16_t depth);
+
+/* Exchange (multi-GPU), count and finalize: purge count < 2 and X/X, choose extensions.
+ * Replaces KmerDHT::flush_updates + finish_updates -> HashTableInserter::insert_into_local_hashtable
+ * (src/kcount/kmer_dht.cpp:227-236, src/kcount/kcount_cpu.cpp:490-528). *n_out may be NULL. */
+int mhmkc_finish(mhmkc_t h, uint64_t *n_out);
+
+/* Copy the finished table to host arrays (any may be NULL): keys[n_out*n_longs] in Kmer::longs layout,
+ * counts[n_out], left[n_out], right[n_out] ('A','C','G','T','F' or 'X'). Order is unspecified, as the
+ * reference's KmerMap iteration order is. Replaces the KmerMap fill (kcount_cpu.cpp:503-522). */
+int mhmkc_fetch(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right);
+
+/* Device pointers of the finished table (valid until the next reset/destroy). */
+int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,
+                        const char **d_right, uint64_t *n_out);
+
+/* Statistics of the last round. */
+int mhmkc_get_stats(mhmkc_t h, mhmkc_stats *s);
+
+/* Forget all k-mers (keep allocations) so the handle can count the next batch/round
+ * (KmerDHT::clear_stores + a fresh HashTableInserter, src/kcount/kcount.cpp:156). */
+int mhmkc_reset(mhmkc_t h);
+
+/* Per-stage HIP-event timing (mhmkc_stats.ms_kernel). Off by default. */
+int mhmkc_set_profiling(mhmkc_t h, int on);
+
+/* Last error message of the handle (or of the last failed mhmkc_create when h is NULL). */
+const char *mhmkc_last_error(mhmkc_t h);
+
+/* Library ABI version (MHMKC_ABI_VERSION). */
+int mhmkc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MHMKC_H */

@@ -1,0 +1,172 @@
+"""ctypes bindings of libmhmkc.so (include/mhmkc.h) and libmhmkc_synth.so (include/mhmkc_synth.h).
+
+There is no fallback: if the HIP library is missing, loading raises. The product path never touches
+oracle/ (the CPU checker lives there and is loaded only by tests and the bench's cpu_baseline leg).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libmhmkc.so"
+SYNTH_PATH = PKG / "libmhmkc_synth.so"
+
+MHMKC_COMM_ID_BYTES = 128
+
+ERRORS = {
+    0: "MHMKC_OK",
+    -1: "MHMKC_EINVAL",
+    -2: "MHMKC_ENOMEM",
+    -3: "MHMKC_EHIP",
+    -4: "MHMKC_ERCCL",
+    -5: "MHMKC_ESTATE",
+    -6: "MHMKC_EBADCHAR",
+    -7: "MHMKC_EUNSUPPORTED",
+}
+
+STAGES = ["tileidx", "extract_hist", "extract_scatter", "exchange", "part_hist", "part_scatter", "count", "other"]
+
+# every symbol include/mhmkc.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = [
+    "mhmkc_config_init", "mhmkc_create", "mhmkc_destroy", "mhmkc_comm_id", "mhmkc_add_reads",
+    "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_device_output",
+    "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
+]
+SYNTH_SYMBOLS = ["mhmkc_synth_config_init", "mhmkc_synth_genome", "mhmkc_synth_reads"]
+
+
+class MhmkcConfig(C.Structure):
+    _fields_ = [
+        ("k", C.c_int32),
+        ("n_longs", C.c_int32),
+        ("qual_offset", C.c_int32),
+        ("qual_cutoff", C.c_int32),
+        ("dmin_thres", C.c_int32),
+        ("dyn_min_depth", C.c_double),
+        ("device", C.c_int32),
+        ("rank", C.c_int32),
+        ("n_ranks", C.c_int32),
+        ("comm_id", C.c_void_p),
+        ("stream", C.c_void_p),
+    ]
+
+
+class MhmkcStats(C.Structure):
+    _fields_ = [
+        ("reads", C.c_uint64),
+        ("bases", C.c_uint64),
+        ("occurrences", C.c_uint64),
+        ("owned_records", C.c_uint64),
+        ("distinct", C.c_uint64),
+        ("purged", C.c_uint64),
+        ("n_out", C.c_uint64),
+        ("dropped", C.c_uint64),
+        ("count_sum", C.c_uint64),
+        ("overflow_sweeps", C.c_uint64),
+        ("max_bucket", C.c_uint64),
+        ("fine_buckets", C.c_uint64),
+        ("bytes_sent", C.c_uint64),
+        ("ms_total", C.c_double),
+        ("ms_kernel", C.c_double * 8),
+        ("launches", C.c_uint64 * 8),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("ms_kernel", "launches")}
+        d["ms_kernel"] = {STAGES[i]: self.ms_kernel[i] for i in range(8)}
+        d["launches"] = {STAGES[i]: int(self.launches[i]) for i in range(8)}
+        return d
+
+
+class SynthConfig(C.Structure):
+    _fields_ = [
+        ("genome_len", C.c_uint64),
+        ("read_len", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("sub_rate", C.c_double),
+        ("n_rate", C.c_double),
+        ("lowq_rate", C.c_double),
+        ("subq_prob", C.c_double),
+    ]
+
+
+_lib = None
+_synth = None
+
+
+def _bind_torch_runtime() -> None:
+    """Load torch's HIP runtime before libmhmkc.so when torch is importable.
+
+    torch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1 / librccl.so.1 with the same SONAMEs as
+    /opt/rocm; whichever copy is loaded first serves the whole process. libmhmkc.so works on either,
+    torch only on its own, so torch goes first (measured: tools/probe_runtime.py). MHMKC_NO_TORCH=1
+    skips this (pure C/C++ hosts never load torch).
+    """
+    import os
+
+    if os.environ.get("MHMKC_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401  (loads libtorch_hip -> torch/lib/libamdhip64.so.7)
+    except Exception:
+        pass
+
+
+def lib() -> C.CDLL:
+    """Load libmhmkc.so (raises if it has not been built: no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} is missing: run `python -m mhm2_proxy_amd.build` "
+                          "(the HIP extension is required; there is no CPU fallback)")
+    _bind_torch_runtime()
+    L = C.CDLL(str(LIB_PATH))
+    P, U64, I32, VP = C.POINTER, C.c_uint64, C.c_int, C.c_void_p
+    L.mhmkc_config_init.argtypes = [P(MhmkcConfig)]
+    L.mhmkc_create.argtypes = [P(VP), P(MhmkcConfig)]
+    L.mhmkc_destroy.argtypes = [VP]
+    L.mhmkc_destroy.restype = None
+    L.mhmkc_comm_id.argtypes = [VP]
+    L.mhmkc_add_reads.argtypes = [VP, VP, VP, U64]
+    L.mhmkc_add_reads_device.argtypes = [VP, VP, VP, U64, U64]
+    L.mhmkc_add_seqs.argtypes = [VP, C.c_char_p, VP, U64, C.c_uint16]
+    L.mhmkc_finish.argtypes = [VP, P(U64)]
+    L.mhmkc_fetch.argtypes = [VP, VP, VP, VP, VP]
+    L.mhmkc_device_output.argtypes = [VP, P(VP), P(VP), P(VP), P(VP), P(U64)]
+    L.mhmkc_get_stats.argtypes = [VP, P(MhmkcStats)]
+    L.mhmkc_reset.argtypes = [VP]
+    L.mhmkc_set_profiling.argtypes = [VP, I32]
+    L.mhmkc_last_error.argtypes = [VP]
+    L.mhmkc_last_error.restype = C.c_char_p
+    L.mhmkc_abi_version.argtypes = []
+    _lib = L
+    return L
+
+
+def synth() -> C.CDLL:
+    global _synth
+    if _synth is not None:
+        return _synth
+    if not SYNTH_PATH.exists():
+        raise ImportError(f"{SYNTH_PATH} is missing: run `python -m mhm2_proxy_amd.build`")
+    S = C.CDLL(str(SYNTH_PATH))
+    S.mhmkc_synth_config_init.argtypes = [C.POINTER(SynthConfig), C.c_uint64, C.c_uint32, C.c_uint64]
+    S.mhmkc_synth_genome.argtypes = [C.POINTER(SynthConfig), C.c_void_p]
+    S.mhmkc_synth_reads.argtypes = [C.POINTER(SynthConfig), C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                    C.c_void_p, C.c_int]
+    _synth = S
+    return S
+
+
+class MhmkcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def check(code: int, handle=None) -> None:
+    if code != 0:
+        msg = lib().mhmkc_last_error(handle)
+        raise MhmkcError(code, msg.decode() if msg else "")

@@ -1,0 +1,82 @@
+"""Build the native libraries in-tree (they travel to the GPU box with the repo snapshot).
+
+  mhm2_proxy_amd/libmhmkc.so        hipcc --offload-arch=gfx950: HIP kernels + C ABI (include/mhmkc.h)
+  mhm2_proxy_amd/libmhmkc_synth.so  gcc: deterministic synthetic read generator (include/mhmkc_synth.h)
+  oracle/liboracle.so (+ _ref/)     make -C oracle: the CPU checker (test infrastructure only)
+
+Incremental: a target is rebuilt only when one of its sources is newer.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+ARCH = os.environ.get("MHMKC_OFFLOAD_ARCH", "gfx950")
+
+LIB = PKG / "libmhmkc.so"
+SYNTH = PKG / "libmhmkc_synth.so"
+ORACLE = ROOT / "oracle" / "liboracle.so"
+
+LIB_SOURCES = [CSRC / "kcount_kernels.hip", CSRC / "mhmkc_host.cpp"]
+LIB_DEPS = LIB_SOURCES + [CSRC / "kcount_launch.hpp", CSRC / "kmer_ops.hpp", ROOT / "include" / "mhmkc.h"]
+SYNTH_DEPS = [CSRC / "synth.c", ROOT / "include" / "mhmkc_synth.h"]
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def _run(cmd, cwd=None):
+    print("+", " ".join(str(c) for c in cmd), flush=True)
+    subprocess.run([str(c) for c in cmd], cwd=cwd, check=True)
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return c
+    raise RuntimeError("hipcc not found: libmhmkc.so cannot be built")
+
+
+def build_lib(force: bool = False) -> Path:
+    if force or _stale(LIB, LIB_DEPS):
+        tmp = LIB.with_suffix(".so.tmp")
+        _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+              *LIB_SOURCES, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp])
+        tmp.replace(LIB)
+    return LIB
+
+
+def build_synth(force: bool = False) -> Path:
+    if force or _stale(SYNTH, SYNTH_DEPS):
+        tmp = SYNTH.with_suffix(".so.tmp")
+        _run(["gcc", "-O3", "-fPIC", "-shared", "-Wall", CSRC / "synth.c", "-lpthread", "-o", tmp])
+        tmp.replace(SYNTH)
+    return SYNTH
+
+
+def build_oracle(force: bool = False) -> Path:
+    odir = ROOT / "oracle"
+    if force:
+        _run(["make", "-C", odir, "clean"])
+    _run(["make", "-s", "-C", odir])
+    return ORACLE
+
+
+def build_all(force: bool = False) -> None:
+    build_lib(force)
+    build_synth(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,105 @@
+// Launch interface between the host orchestration (mhmkc_host.cpp) and the gfx950 kernels
+// (kcount_kernels.hip). Plain structs of device pointers; no torch types anywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mhm {
+
+// Read stream in the PackedRead byte layout (src/packed_reads.cpp:73-109) + CSR offsets.
+struct ReadsView {
+  const uint8_t *bytes;   // n_bases bytes: code (bits 0-2) | min(q-off,31) << 3
+  const uint64_t *offs;   // n_reads+1 offsets, offs[0]=0, offs[n_reads]=n_bases
+  uint64_t n_reads;
+  uint64_t n_bases;
+};
+
+// Record planes of one slab: word planes (SoA) + optional ext byte plane.
+struct PlaneSet {
+  uint64_t *w[4];
+  uint8_t *ext;  // nullptr when the ext code is packed into the last key word
+};
+
+struct ExtractParams {
+  ReadsView reads;
+  const uint32_t *tile_first_read;  // per tile: first read r with offs[r] >= tile_lo
+  uint32_t n_tiles;
+  int k;
+  int qual_cutoff;
+  int coarse_bits;                  // coarse digit = h1 >> (64 - coarse_bits)
+  uint32_t n_bins;                  // 1 << coarse_bits
+  unsigned long long *hist;         // [n_bins] (E-hist)
+  unsigned long long *cursor;       // [n_bins] (E-scatter), starts at the bin bases of the slab
+  PlaneSet out;                     // (E-scatter)
+  unsigned int *err;                // bit 0: input byte with code > 4
+};
+
+// One chunk of S work: <= tile records of one (source, coarse bucket) segment.
+struct SChunk {
+  uint64_t start;        // first record index in the source planes
+  uint32_t count;        // records in the chunk
+  uint32_t src;          // index into the source plane-set table
+  uint32_t coarse_local; // coarse bucket index relative to this rank's first owned bucket
+  uint32_t pad;
+};
+
+struct PartitionParams {
+  const SChunk *chunks;
+  uint32_t n_chunks;
+  const PlaneSet *srcs;           // device table of source plane sets
+  int k;
+  int coarse_bits;
+  int fine_bits;
+  unsigned long long *fine_hist;    // [n_coarse_local << fine_bits]
+  unsigned long long *fine_cursor;  // [n_coarse_local << fine_bits]
+  PlaneSet out;
+};
+
+struct CountParams {
+  PlaneSet recs;                      // fine-bucketed records (overwritten in place by overflow)
+  const unsigned long long *bucket_base;
+  const unsigned long long *bucket_n;
+  uint32_t n_buckets;
+  int k;
+  int cap;                            // LDS table slots
+  int limit;                          // max occupied slots before the table closes
+  int dmin_thres;
+  double dyn_mult;                    // 1.0 - DYN_MIN_DEPTH, computed in double on the host
+  int nlo;                            // output words per key
+  uint64_t *out_keys;                 // [out_cap * nlo]
+  uint16_t *out_counts;
+  char *out_left;
+  char *out_right;
+  unsigned long long *out_cursor;
+  unsigned long long *stats;          // [STAT_*]
+};
+
+enum {
+  STAT_DISTINCT = 0,
+  STAT_NOUT = 1,
+  STAT_PURGED = 2,
+  STAT_COUNTSUM = 3,
+  STAT_SWEEPS = 4,
+  STAT_MAXBUCKET = 5,
+  STAT_N = 8
+};
+
+constexpr int E_THREADS = 256;
+constexpr int C_THREADS = 1024;
+
+// Bases per extract tile (== records per S chunk) for NL words per key.
+inline int tile_bases(int nl) { return nl <= 2 ? 4096 : 2048; }
+// LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS).
+inline int count_cap(int nl) { return nl == 1 ? 5120 : nl == 2 ? 4000 : nl == 3 ? 3264 : 2752; }
+inline size_t count_lds_bytes(int nl) { return (size_t)count_cap(nl) * (8 * nl + 4 + 16) + 64; }
+
+hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);
+hipError_t launch_extract_hist(const ExtractParams &p, int nl, bool packed, hipStream_t s);
+hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, hipStream_t s);
+hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s);
+hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s);
+hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor,
+                       uint32_t n, hipStream_t s);
+hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s);
+
+}  // namespace mhm

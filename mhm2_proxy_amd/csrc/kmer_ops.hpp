@@ -1,0 +1,150 @@
+// k-mer bit operations shared by the HIP kernels and the host code of libmhmkc.
+//
+// Layout (identical to the reference Kmer<MAX_K>::longs, src/kmer.cpp:178-188,224-232):
+//   * 2 bits per base, A=0 C=1 G=2 T=3, MSB-first: base j of word l sits at bits 2*(31-j) of w[l];
+//   * NL = k/32 + 1 words (the reference's MAX_K/32 with MAX_K = (k/32+1)*32, src/main.cpp:170);
+//   * the unused low bits of the last word are zero.
+// k % 32 == 0 is rejected by mhmkc_create: only then can a canonical last word be all ones, which
+// the table uses as its EMPTY marker (the reference has the same aliasing, kcount_cpu.cpp:217,236).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define MHM_HD __host__ __device__ __forceinline__
+#else
+#define MHM_HD static inline
+#endif
+
+namespace mhm {
+
+constexpr uint64_t KEY_EMPTY = ~0ull;          // last word of a free table slot
+constexpr uint64_t KEY_BUSY = ~0ull - 1ull;    // last word of a slot whose key is being written
+constexpr int MAX_NL = 4;                      // k <= 127 (MAX_BUILD_KMER 128)
+constexpr int EXT_NONE = 4;                    // no countable extension
+constexpr int EXT_BITS = 6;                    // record ext code = (left << 3) | right
+
+MHM_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+// fmix64 of MurmurHash3 (reference src/hash_funcs.c:65-73).
+MHM_HD uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// h1 of MurmurHash3_x64_128(longs, 8*NL, seed 313): Kmer<MAX_K>::hash() (src/kmer.cpp:465-468 ->
+// src/hash_funcs.c:77-170,185-190). The key bytes are the little-endian words themselves, so a
+// 16-byte block is (w[2b], w[2b+1]) and an odd trailing word is the 8-byte tail k1.
+template <int NL>
+MHM_HD uint64_t murmur3_h1(const uint64_t *w) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = 313, h2 = 313;
+#pragma unroll
+  for (int b = 0; b < NL / 2; b++) {
+    uint64_t k1 = w[2 * b], k2 = w[2 * b + 1];
+    k1 *= c1;
+    k1 = rotl64(k1, 31);
+    k1 *= c2;
+    h1 ^= k1;
+    h1 = rotl64(h1, 27);
+    h1 += h2;
+    h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2;
+    k2 = rotl64(k2, 33);
+    k2 *= c1;
+    h2 ^= k2;
+    h2 = rotl64(h2, 31);
+    h2 += h1;
+    h2 = h2 * 5 + 0x38495ab5;
+  }
+  if (NL & 1) {
+    uint64_t k1 = w[NL - 1];
+    k1 *= c1;
+    k1 = rotl64(k1, 31);
+    k1 *= c2;
+    h1 ^= k1;
+  }
+  h1 ^= (uint64_t)(8 * NL);
+  h2 ^= (uint64_t)(8 * NL);
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+// Reverse the order of the 32 two-bit groups of x.
+MHM_HD uint64_t rev2(uint64_t x) {
+  x = __builtin_bswap64(x);
+  x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+  x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+  return x;
+}
+
+// Top 2*n bits set (the reference's ZERO_MASK[n], src/kmer.cpp:81-87), n in [1, 32].
+MHM_HD uint64_t top_mask(int n) { return n >= 32 ? ~0ull : ~(~0ull >> (2 * n)); }
+
+// Reverse complement of a k-mer held in NL words (same result as Kmer::revcomp, src/kmer.cpp:485-505):
+// complement and reverse every word, reverse the word order, then shift the concatenation left by
+// 2*(32*NL - k) bits so the junk from the zero padding falls off the end.
+template <int NL>
+MHM_HD void revcomp(const uint64_t *w, uint64_t *rc, int k) {
+  uint64_t t[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) t[NL - 1 - i] = rev2(~w[i]);
+  const int sh = 2 * (32 * NL - k);  // in [2, 62] for k % 32 != 0
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    uint64_t v = t[i] << sh;
+    if (i + 1 < NL) v |= t[i + 1] >> (64 - sh);
+    rc[i] = v;
+  }
+  rc[NL - 1] &= top_mask(k - 32 * (NL - 1));
+}
+
+// Word-wise unsigned lexicographic compare == Kmer::operator< (src/kmer.cpp:265-272).
+template <int NL>
+MHM_HD bool kmer_less(const uint64_t *a, const uint64_t *b) {
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    if (a[i] != b[i]) return a[i] < b[i];
+  }
+  return false;
+}
+
+// Packed-record mode: the 6-bit ext code fits into the zero low bits of the last key word.
+MHM_HD bool ext_packs(int k, int nl) { return 2 * (k - 32 * (nl - 1)) + EXT_BITS <= 64; }
+
+// get_ext of the reference (src/kcount/kcount_cpu.cpp:173-182): 'X' when the top count is below the
+// dynamic threshold, 'F' when the runner-up reaches it, otherwise the (then unique) top base.
+// thr = max((int)((1.0 - DYN_MIN_DEPTH) * count), dmin_thres).
+MHM_HD char ext_choice(uint32_t a, uint32_t c, uint32_t g, uint32_t t, int thr) {
+  uint32_t v[4] = {a, c, g, t};
+  uint32_t top = 0, second = 0;
+  int arg = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (v[i] > top) {
+      second = top;
+      top = v[i];
+      arg = i;
+    } else if (v[i] > second) {
+      second = v[i];
+    }
+  }
+  if ((int)top < thr) return 'X';
+  if ((int)second >= thr) return 'F';
+  const char bases[4] = {'A', 'C', 'G', 'T'};
+  return bases[arg];
+}
+
+MHM_HD int dyn_threshold(uint32_t count16, double dyn_mult, int dmin_thres) {
+  int t = (int)(dyn_mult * (double)count16);
+  return t > dmin_thres ? t : dmin_thres;
+}
+
+}  // namespace mhm

@@ -1,0 +1,809 @@
+// Host side of libmhmkc: handle lifetime, device memory arena, stage orchestration, the RCCL
+// exchange and the C ABI declared in include/mhmkc.h.
+//
+// One handle = one GPU = one rank. The reference's per-rank state (KmerDHT + HashTableInserter,
+// src/kcount/kmer_dht.hpp:95-172) maps onto this struct; its UPC++ supermer store
+// (src/kcount/kmer_dht.cpp:133-149,222-224) maps onto the hash-range exchange in exchange().
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mhmkc.h"
+#include "kcount_launch.hpp"
+#include "kmer_ops.hpp"
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    release();
+    size_t want = bytes + bytes / 16 + 4096;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T *as() const {
+    return (T *)p;
+  }
+};
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Records of one add_reads batch, partitioned by coarse bucket (hash range).
+struct Slab {
+  DevBuf buf;
+  mhm::PlaneSet planes{};
+  uint64_t n = 0;
+  std::vector<uint64_t> counts;  // [nb]
+  std::vector<uint64_t> bases;   // [nb] exclusive prefix
+};
+
+// A source of owned records for the fine partition: per owned coarse bucket (local index) a range.
+struct Source {
+  mhm::PlaneSet planes{};
+  std::vector<uint64_t> start;  // [n_owned]
+  std::vector<uint64_t> count;  // [n_owned]
+};
+
+struct Prof {
+  int stage;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct mhmkc {
+  mhmkc_config cfg{};
+  int k = 0, nl = 1, nlo = 1;
+  bool packed = true;
+  int cb = 8, fb = 8;
+  uint32_t nb = 256, nf = 256;
+  uint32_t own_lo = 0, own_hi = 256;  // owned coarse range [own_lo, own_hi)
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  ncclComm_t comm = nullptr;
+
+  std::vector<Slab *> slabs;  // pool; first n_slabs are in use
+  size_t n_slabs = 0;
+  DevBuf d_hist, d_cursor, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
+  DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xcounts;
+  DevBuf d_in_bytes, d_in_offs;
+
+  std::string err;
+  bool finished = false;
+  bool began = false;
+  uint64_t n_out = 0;
+  mhmkc_stats st{};
+  bool profiling = false;
+  std::vector<Prof> prof;
+  std::vector<hipEvent_t> ev_pool;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+
+  int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char *what) {
+    return fail(MHMKC_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+  }
+
+  hipEvent_t take_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void prof_begin(int stage) {
+    if (!profiling) return;
+    Prof p{stage, take_event(), take_event()};
+    (void)hipEventRecord(p.a, stream);
+    prof.push_back(p);
+  }
+  void prof_end() {
+    if (!profiling || prof.empty()) return;
+    (void)hipEventRecord(prof.back().b, stream);
+  }
+  void prof_collect() {
+    for (auto &p : prof) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+        st.ms_kernel[p.stage] += ms;
+        st.launches[p.stage] += 1;
+      }
+      ev_pool.push_back(p.a);
+      ev_pool.push_back(p.b);
+    }
+    prof.clear();
+  }
+
+  uint32_t owner_lo(int r) const { return (uint32_t)(((uint64_t)r * nb + cfg.n_ranks - 1) / cfg.n_ranks); }
+  uint32_t n_owned() const { return own_hi - own_lo; }
+  size_t rec_bytes() const { return 8 * (size_t)nl + (packed ? 0 : 1); }
+
+  int begin_round() {
+    if (finished) return fail(MHMKC_ESTATE, "handle already finished; call mhmkc_reset first");
+    if (!began) {
+      began = true;
+      (void)hipEventRecord(ev_begin, stream);
+    }
+    return MHMKC_OK;
+  }
+
+  Slab *new_slab() {
+    if (n_slabs == slabs.size()) slabs.push_back(new Slab());
+    return slabs[n_slabs++];
+  }
+
+  int set_planes(DevBuf &buf, uint64_t n, mhm::PlaneSet &ps) {
+    const size_t plane = align_up(std::max<uint64_t>(n, 1) * 8, 256);
+    const size_t extb = packed ? 0 : align_up(std::max<uint64_t>(n, 1), 256);
+    hipError_t e = buf.ensure(plane * nl + extb);
+    if (e != hipSuccess) return hip_fail(e, "allocating record planes");
+    char *b = buf.as<char>();
+    for (int w = 0; w < 4; w++) ps.w[w] = w < nl ? (uint64_t *)(b + plane * w) : nullptr;
+    ps.ext = packed ? nullptr : (uint8_t *)(b + plane * nl);
+    return MHMKC_OK;
+  }
+
+  int add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, uint64_t n_bases, int qcut);
+  int exchange(std::vector<Source> &srcs);
+  int finish(uint64_t *n_out_ret);
+};
+
+// ------------------------------------------------------------------------------------------------
+// extract one batch of reads into a coarse-bucketed slab
+
+int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, uint64_t n_bases, int qcut) {
+  int rc = begin_round();
+  if (rc) return rc;
+  st.reads += n_reads;
+  st.bases += n_bases;
+  if (n_reads == 0 || n_bases == 0) return MHMKC_OK;
+  if (n_reads >= 0xffffffffull) return fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
+  const int T = mhm::tile_bases(nl);
+  const uint64_t tiles64 = (n_bases + T - 1) / T;
+  if (tiles64 >= 0x7fffffffull) return fail(MHMKC_EINVAL, "batch too large");
+  const uint32_t tiles = (uint32_t)tiles64;
+  hipError_t e;
+  if ((e = d_tiles.ensure((size_t)tiles * 4)) != hipSuccess) return hip_fail(e, "tile index");
+  if ((e = d_hist.ensure((size_t)nb * 8)) != hipSuccess) return hip_fail(e, "histogram");
+  if ((e = d_cursor.ensure((size_t)nb * 8)) != hipSuccess) return hip_fail(e, "cursor");
+
+  mhm::ExtractParams p{};
+  p.reads = {bytes, offs, n_reads, n_bases};
+  p.tile_first_read = d_tiles.as<uint32_t>();
+  p.n_tiles = tiles;
+  p.k = k;
+  p.qual_cutoff = qcut;
+  p.coarse_bits = cb;
+  p.n_bins = nb;
+  p.hist = d_hist.as<unsigned long long>();
+  p.cursor = d_cursor.as<unsigned long long>();
+  p.err = d_err.as<unsigned int>();
+
+  prof_begin(MHMKC_STAGE_TILEIDX);
+  e = mhm::launch_tile_first_read(p.reads, d_tiles.as<uint32_t>(), tiles, T, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "tile_first_read");
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = hipMemsetAsync(d_hist.p, 0, (size_t)nb * 8, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "memset");
+  prof_begin(MHMKC_STAGE_EHIST);
+  e = mhm::launch_extract_hist(p, nl, packed, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "extract_hist");
+
+  Slab *s = new_slab();
+  s->counts.assign(nb, 0);
+  s->bases.assign(nb, 0);
+  if ((e = hipMemcpyAsync(s->counts.data(), d_hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(e, "histogram D2H");
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_hist");
+  uint64_t tot = 0;
+  for (uint32_t b = 0; b < nb; b++) {
+    s->bases[b] = tot;
+    tot += s->counts[b];
+  }
+  s->n = tot;
+  st.occurrences += tot;
+  if ((rc = set_planes(s->buf, tot, s->planes))) return rc;
+  if ((e = hipMemcpyAsync(d_cursor.p, s->bases.data(), (size_t)nb * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "cursor H2D");
+  p.out = s->planes;
+  prof_begin(MHMKC_STAGE_ESCAT);
+  e = mhm::launch_extract_scatter(p, nl, packed, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "extract_scatter");
+  // the cursor H2D source is a host vector: make sure it has been consumed before it can change
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_scatter");
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// hash-range exchange between ranks (replaces the UPC++ ThreeTierAggrStore<Supermer> traffic,
+// src/kcount/kmer_dht.cpp:133-149,222-224, and its flush/barrier, kmer_dht.cpp:227-231)
+
+int mhmkc::exchange(std::vector<Source> &srcs) {
+  const int G = cfg.n_ranks, me = cfg.rank;
+  const uint32_t no = n_owned();
+  hipError_t e;
+  ncclResult_t nr;
+  // 1. slab counts of every rank
+  uint64_t my_slabs = n_slabs;
+  if ((e = d_xcounts.ensure(8 * (size_t)G * 2)) != hipSuccess) return hip_fail(e, "exchange counts");
+  if ((e = hipMemcpyAsync(d_xcounts.p, &my_slabs, 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "exchange H2D");
+  uint64_t *dx = d_xcounts.as<uint64_t>();
+  if ((nr = ncclAllGather(dx, dx + G, 1, ncclUint64, comm, stream)) != ncclSuccess)
+    return fail(MHMKC_ERCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
+  std::vector<uint64_t> slabs_of(G);
+  if ((e = hipMemcpyAsync(slabs_of.data(), dx + G, 8 * (size_t)G, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(e, "exchange D2H");
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange sync");
+  const uint64_t ms = std::max<uint64_t>(1, *std::max_element(slabs_of.begin(), slabs_of.end()));
+  // 2. all coarse counts [G][ms][nb]
+  std::vector<uint64_t> mine(ms * nb, 0), all((size_t)G * ms * nb, 0);
+  for (size_t s = 0; s < n_slabs; s++) std::copy(slabs[s]->counts.begin(), slabs[s]->counts.end(), mine.begin() + s * nb);
+  if ((e = d_xcounts.ensure(8 * (size_t)(G + 1) * ms * nb)) != hipSuccess) return hip_fail(e, "exchange counts");
+  dx = d_xcounts.as<uint64_t>();
+  if ((e = hipMemcpyAsync(dx, mine.data(), 8 * ms * nb, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "exchange H2D");
+  if ((nr = ncclAllGather(dx, dx + ms * nb, ms * nb, ncclUint64, comm, stream)) != ncclSuccess)
+    return fail(MHMKC_ERCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
+  if ((e = hipMemcpyAsync(all.data(), dx + ms * nb, 8 * (size_t)G * ms * nb, hipMemcpyDeviceToHost, stream)) !=
+      hipSuccess)
+    return hip_fail(e, "exchange D2H");
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange sync");
+  auto cnt = [&](int r, uint64_t s, uint32_t c) { return all[((size_t)r * ms + s) * nb + c]; };
+  // 3. receive layout: for each peer p != me, for each of its slabs s: my owned coarse range
+  uint64_t recv_total = 0;
+  struct Seg {
+    int peer;
+    uint64_t slab, off, n;
+  };
+  std::vector<Seg> rsegs;
+  for (int p = 0; p < G; p++) {
+    if (p == me) continue;
+    for (uint64_t s = 0; s < slabs_of[p]; s++) {
+      uint64_t n = 0;
+      for (uint32_t c = own_lo; c < own_hi; c++) n += cnt(p, s, c);
+      rsegs.push_back({p, s, recv_total, n});
+      recv_total += n;
+    }
+  }
+  mhm::PlaneSet rps{};
+  int rc;
+  if ((rc = set_planes(d_recv, recv_total, rps))) return rc;
+  // 4. grouped send/recv (per pair the calls are issued in the same slab/plane order on both sides)
+  prof_begin(MHMKC_STAGE_XCHG);
+  if ((nr = ncclGroupStart()) != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupStart: %s", ncclGetErrorString(nr));
+  uint64_t sent = 0;
+  for (int p = 0; p < G; p++) {
+    if (p == me) continue;
+    const uint32_t lo = owner_lo(p), hi = owner_lo(p + 1);
+    for (size_t s = 0; s < n_slabs; s++) {
+      const Slab *sl = slabs[s];
+      const uint64_t a = lo < nb ? sl->bases[lo] : sl->n;
+      const uint64_t b = hi < nb ? sl->bases[hi] : sl->n;
+      if (b == a) continue;
+      for (int w = 0; w < nl; w++) ncclSend(sl->planes.w[w] + a, b - a, ncclUint64, p, comm, stream);
+      if (!packed) ncclSend(sl->planes.ext + a, b - a, ncclUint8, p, comm, stream);
+      sent += (b - a) * rec_bytes();
+    }
+  }
+  for (const Seg &g : rsegs) {
+    if (!g.n) continue;
+    for (int w = 0; w < nl; w++) ncclRecv(rps.w[w] + g.off, g.n, ncclUint64, g.peer, comm, stream);
+    if (!packed) ncclRecv(rps.ext + g.off, g.n, ncclUint8, g.peer, comm, stream);
+  }
+  if ((nr = ncclGroupEnd()) != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupEnd: %s", ncclGetErrorString(nr));
+  prof_end();
+  st.bytes_sent += sent;
+  // 5. sources: local slabs (owned range in place) + received segments
+  for (size_t s = 0; s < n_slabs; s++) {
+    Source src;
+    src.planes = slabs[s]->planes;
+    src.start.resize(no);
+    src.count.resize(no);
+    for (uint32_t c = 0; c < no; c++) {
+      src.start[c] = slabs[s]->bases[own_lo + c];
+      src.count[c] = slabs[s]->counts[own_lo + c];
+    }
+    srcs.push_back(std::move(src));
+  }
+  for (const Seg &g : rsegs) {
+    Source src;
+    src.planes = rps;
+    src.start.resize(no);
+    src.count.resize(no);
+    uint64_t o = g.off;
+    for (uint32_t c = 0; c < no; c++) {
+      src.start[c] = o;
+      src.count[c] = cnt(g.peer, g.slab, own_lo + c);
+      o += src.count[c];
+    }
+    srcs.push_back(std::move(src));
+  }
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// fine partition + LDS count + finalize
+
+int mhmkc::finish(uint64_t *n_out_ret) {
+  int rc = begin_round();
+  if (rc) return rc;
+  hipError_t e;
+  const uint32_t no = n_owned();
+  std::vector<Source> srcs;
+  if (cfg.n_ranks > 1) {
+    if ((rc = exchange(srcs))) return rc;
+  } else {
+    for (size_t s = 0; s < n_slabs; s++) {
+      Source src;
+      src.planes = slabs[s]->planes;
+      src.start = slabs[s]->bases;
+      src.count = slabs[s]->counts;
+      srcs.push_back(std::move(src));
+    }
+  }
+  uint64_t owned = 0;
+  for (auto &s : srcs)
+    for (uint32_t c = 0; c < no; c++) owned += s.count[c];
+  st.owned_records = owned;
+
+  // fine bits: aim at ~4 records per LDS table slot per fine bucket
+  const uint64_t per_coarse = owned / std::max<uint32_t>(no, 1);
+  const uint64_t target = (uint64_t)mhm::count_cap(nl) * 4;
+  fb = 4;
+  while (fb < 11 && (per_coarse >> fb) > target) fb++;
+  if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
+  nf = 1u << fb;
+  const uint32_t n_fine = no * nf;
+  st.fine_buckets = n_fine;
+
+  // chunk table
+  const int T = mhm::tile_bases(nl);
+  std::vector<mhm::SChunk> chunks;
+  std::vector<mhm::PlaneSet> ps;
+  for (size_t s = 0; s < srcs.size(); s++) {
+    ps.push_back(srcs[s].planes);
+    for (uint32_t c = 0; c < no; c++) {
+      for (uint64_t o = 0; o < srcs[s].count[c]; o += T) {
+        mhm::SChunk ch{};
+        ch.start = srcs[s].start[c] + o;
+        ch.count = (uint32_t)std::min<uint64_t>(T, srcs[s].count[c] - o);
+        ch.src = (uint32_t)s;
+        ch.coarse_local = c;
+        chunks.push_back(ch);
+      }
+    }
+  }
+  if (chunks.size() >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
+  if ((e = d_chunks.ensure(std::max<size_t>(1, chunks.size()) * sizeof(mhm::SChunk))) != hipSuccess)
+    return hip_fail(e, "chunk table");
+  if ((e = d_srcs.ensure(std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet))) != hipSuccess)
+    return hip_fail(e, "source table");
+  if (!chunks.empty() &&
+      (e = hipMemcpyAsync(d_chunks.p, chunks.data(), chunks.size() * sizeof(mhm::SChunk), hipMemcpyHostToDevice,
+                          stream)) != hipSuccess)
+    return hip_fail(e, "chunk H2D");
+  if (!ps.empty() && (e = hipMemcpyAsync(d_srcs.p, ps.data(), ps.size() * sizeof(mhm::PlaneSet),
+                                         hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "source H2D");
+  if ((e = d_fine_hist.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
+  if ((e = d_fine_base.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
+  if ((e = d_fine_cursor.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine cursor");
+  mhm::PlaneSet r2{};
+  if ((rc = set_planes(d_r2, owned, r2))) return rc;
+  const uint64_t out_cap = owned / 2 + 1;
+  if ((e = d_out_keys.ensure(out_cap * 8 * nlo)) != hipSuccess) return hip_fail(e, "output keys");
+  if ((e = d_out_counts.ensure(out_cap * 2)) != hipSuccess) return hip_fail(e, "output counts");
+  if ((e = d_out_left.ensure(out_cap)) != hipSuccess) return hip_fail(e, "output left");
+  if ((e = d_out_right.ensure(out_cap)) != hipSuccess) return hip_fail(e, "output right");
+  if ((e = d_out_cursor.ensure(8)) != hipSuccess) return hip_fail(e, "output cursor");
+
+  mhm::PartitionParams pp{};
+  pp.chunks = d_chunks.as<mhm::SChunk>();
+  pp.n_chunks = (uint32_t)chunks.size();
+  pp.srcs = d_srcs.as<mhm::PlaneSet>();
+  pp.k = k;
+  pp.coarse_bits = cb;
+  pp.fine_bits = fb;
+  pp.fine_hist = d_fine_hist.as<unsigned long long>();
+  pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
+  pp.out = r2;
+
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d_out_cursor.p, 0, 8, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_N, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "memset");
+  prof_begin(MHMKC_STAGE_SHIST);
+  e = mhm::launch_part_hist(pp, nl, packed, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "part_hist");
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = mhm::launch_scan(d_fine_hist.as<unsigned long long>(), d_fine_base.as<unsigned long long>(),
+                       d_fine_cursor.as<unsigned long long>(), n_fine, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "scan");
+  prof_begin(MHMKC_STAGE_SSCAT);
+  e = mhm::launch_part_scatter(pp, nl, packed, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "part_scatter");
+
+  mhm::CountParams cp{};
+  cp.recs = r2;
+  cp.bucket_base = d_fine_base.as<unsigned long long>();
+  cp.bucket_n = d_fine_hist.as<unsigned long long>();
+  cp.n_buckets = n_fine;
+  cp.k = k;
+  cp.cap = mhm::count_cap(nl);
+  if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)));  // tests only
+  cp.limit = cp.cap * 9 / 10;
+  cp.dmin_thres = cfg.dmin_thres;
+  cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
+  cp.nlo = nlo;
+  cp.out_keys = d_out_keys.as<uint64_t>();
+  cp.out_counts = d_out_counts.as<uint16_t>();
+  cp.out_left = d_out_left.as<char>();
+  cp.out_right = d_out_right.as<char>();
+  cp.out_cursor = d_out_cursor.as<unsigned long long>();
+  cp.stats = d_stats.as<unsigned long long>();
+  prof_begin(MHMKC_STAGE_COUNT);
+  e = mhm::launch_count(cp, nl, packed, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "count");
+  (void)hipEventRecord(ev_end, stream);
+
+  unsigned long long stats[mhm::STAT_N];
+  unsigned int errf = 0;
+  if ((e = hipMemcpyAsync(stats, d_stats.p, sizeof stats, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(e, "stats D2H");
+  if ((e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(e, "error flag D2H");
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "finish");
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, ev_begin, ev_end) == hipSuccess) st.ms_total = ms;
+  prof_collect();
+  finished = true;
+  if (errf & 1u) return fail(MHMKC_EBADCHAR, "input byte with a base code > 4 (not A,C,G,T,N)");
+  if (stats[mhm::STAT_N - 1]) return fail(MHMKC_EHIP, "internal: LDS probe bound exceeded");
+  st.distinct = stats[mhm::STAT_DISTINCT];
+  st.n_out = stats[mhm::STAT_NOUT];
+  st.purged = stats[mhm::STAT_PURGED];
+  st.count_sum = stats[mhm::STAT_COUNTSUM];
+  st.overflow_sweeps = stats[mhm::STAT_SWEEPS];
+  st.max_bucket = stats[mhm::STAT_MAXBUCKET];
+  st.dropped = 0;
+  n_out = st.n_out;
+  if (n_out > out_cap) return fail(MHMKC_EHIP, "internal: output overflow");
+  if (n_out_ret) *n_out_ret = n_out;
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+
+extern "C" {
+
+int mhmkc_abi_version(void) { return MHMKC_ABI_VERSION; }
+
+int mhmkc_config_init(mhmkc_config *cfg) {
+  if (!cfg) return MHMKC_EINVAL;
+  memset(cfg, 0, sizeof *cfg);
+  cfg->k = 21;
+  cfg->n_longs = 0;
+  cfg->qual_offset = 33;
+  cfg->qual_cutoff = 20;
+  cfg->dmin_thres = 2;
+  cfg->dyn_min_depth = 0.9;
+  cfg->device = -1;
+  cfg->rank = 0;
+  cfg->n_ranks = 1;
+  cfg->comm_id = nullptr;
+  cfg->stream = nullptr;
+  return MHMKC_OK;
+}
+
+int mhmkc_comm_id(uint8_t out[MHMKC_COMM_ID_BYTES]) {
+  if (!out) return MHMKC_EINVAL;
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    g_create_error = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+    return MHMKC_ERCCL;
+  }
+  static_assert(sizeof(ncclUniqueId) == MHMKC_COMM_ID_BYTES, "unique id size");
+  memcpy(out, &id, MHMKC_COMM_ID_BYTES);
+  return MHMKC_OK;
+}
+
+int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
+  if (!out || !cfg) {
+    g_create_error = "null argument";
+    return MHMKC_EINVAL;
+  }
+  *out = nullptr;
+  const int k = cfg->k;
+  if (k < 1 || k > 127) {
+    g_create_error = "k must be in [1, 127]";
+    return MHMKC_EINVAL;
+  }
+  if (k % 32 == 0) {
+    g_create_error = "k % 32 == 0 is not supported (EMPTY-slot aliasing, see DESIGN.md)";
+    return MHMKC_EUNSUPPORTED;
+  }
+  const int nl = k / 32 + 1;
+  const int nlo = cfg->n_longs ? cfg->n_longs : nl;
+  if (nlo < nl || nlo > 8) {
+    g_create_error = "n_longs must be 0 or in [k/32+1, 8]";
+    return MHMKC_EINVAL;
+  }
+  if (cfg->qual_cutoff < 0 || cfg->qual_cutoff > 32 || (cfg->qual_offset != 33 && cfg->qual_offset != 64)) {
+    g_create_error = "qual_offset must be 33 or 64 and qual_cutoff in [0, 32]";
+    return MHMKC_EINVAL;
+  }
+  if (cfg->dmin_thres < 0 || cfg->dmin_thres > 32768) {
+    g_create_error = "dmin_thres must be in [0, 32768] (DESIGN.md §3.4)";
+    return MHMKC_EUNSUPPORTED;
+  }
+  if (!(cfg->dyn_min_depth >= 0.0 && cfg->dyn_min_depth <= 1.0)) {
+    g_create_error = "dyn_min_depth must be in [0, 1]";
+    return MHMKC_EINVAL;
+  }
+  if (cfg->n_ranks < 1 || cfg->n_ranks > 64 || cfg->rank < 0 || cfg->rank >= cfg->n_ranks) {
+    g_create_error = "bad rank / n_ranks";
+    return MHMKC_EINVAL;
+  }
+  if (cfg->n_ranks > 1 && !cfg->comm_id) {
+    g_create_error = "comm_id required when n_ranks > 1";
+    return MHMKC_EINVAL;
+  }
+  mhmkc *h = new mhmkc();
+  h->cfg = *cfg;
+  h->k = k;
+  h->nl = nl;
+  h->nlo = nlo;
+  h->packed = mhm::ext_packs(k, nl);
+  int extra = 0;
+  while ((1 << extra) < cfg->n_ranks) extra++;
+  h->cb = 8 + extra;
+  h->nb = 1u << h->cb;
+  h->own_lo = h->owner_lo(cfg->rank);
+  h->own_hi = h->owner_lo(cfg->rank + 1);
+  hipError_t e;
+  if (cfg->device >= 0) {
+    if ((e = hipSetDevice(cfg->device)) != hipSuccess) {
+      g_create_error = std::string("hipSetDevice: ") + hipGetErrorString(e);
+      delete h;
+      return MHMKC_EHIP;
+    }
+  }
+  (void)hipGetDevice(&h->dev);
+  if (cfg->stream) {
+    h->stream = (hipStream_t)cfg->stream;
+  } else {
+    if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) {
+      g_create_error = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+      delete h;
+      return MHMKC_EHIP;
+    }
+    h->own_stream = true;
+  }
+  if ((e = hipEventCreate(&h->ev_begin)) != hipSuccess || (e = hipEventCreate(&h->ev_end)) != hipSuccess ||
+      (e = h->d_err.ensure(16)) != hipSuccess || (e = h->d_stats.ensure(8 * mhm::STAT_N)) != hipSuccess ||
+      (e = hipMemset(h->d_err.p, 0, 16)) != hipSuccess) {
+    g_create_error = std::string("init: ") + hipGetErrorString(e);
+    mhmkc_destroy(h);
+    return MHMKC_EHIP;
+  }
+  if (cfg->n_ranks > 1) {
+    ncclUniqueId id;
+    memcpy(&id, cfg->comm_id, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&h->comm, cfg->n_ranks, id, cfg->rank);
+    if (r != ncclSuccess) {
+      g_create_error = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+      h->comm = nullptr;
+      mhmkc_destroy(h);
+      return MHMKC_ERCCL;
+    }
+  }
+  *out = h;
+  return MHMKC_OK;
+}
+
+void mhmkc_destroy(mhmkc_t h) {
+  if (!h) return;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->comm) ncclCommDestroy(h->comm);
+  for (Slab *s : h->slabs) {
+    s->buf.release();
+    delete s;
+  }
+  DevBuf *bufs[] = {&h->d_hist,     &h->d_cursor,    &h->d_tiles,     &h->d_err,       &h->d_stats,
+                    &h->d_fine_hist, &h->d_fine_base, &h->d_fine_cursor, &h->d_chunks,  &h->d_srcs,
+                    &h->d_r2,       &h->d_out_keys,  &h->d_out_counts, &h->d_out_left, &h->d_out_right,
+                    &h->d_out_cursor, &h->d_recv,    &h->d_xcounts,   &h->d_in_bytes,  &h->d_in_offs};
+  for (DevBuf *b : bufs) b->release();
+  for (auto &p : h->prof) {
+    h->ev_pool.push_back(p.a);
+    h->ev_pool.push_back(p.b);
+  }
+  for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
+  if (h->ev_begin) (void)hipEventDestroy(h->ev_begin);
+  if (h->ev_end) (void)hipEventDestroy(h->ev_end);
+  if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_offs, uint64_t n_reads,
+                           uint64_t n_bases) {
+  if (!h) return MHMKC_EINVAL;
+  if (n_reads && (!d_bytes || !d_offs)) return h->fail(MHMKC_EINVAL, "null device buffer");
+  return h->add_device(d_bytes, d_offs, n_reads, n_bases, h->cfg.qual_cutoff);
+}
+
+static int add_host(mhmkc_t h, const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut) {
+  const uint64_t n_bases = offs[n_reads];
+  hipError_t e;
+  if ((e = h->d_in_bytes.ensure(std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess)
+    return h->hip_fail(e, "input staging");
+  if ((e = h->d_in_offs.ensure((n_reads + 1) * 8)) != hipSuccess) return h->hip_fail(e, "input staging");
+  if (n_bases && (e = hipMemcpyAsync(h->d_in_bytes.p, bytes, n_bases, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+    return h->hip_fail(e, "input H2D");
+  if ((e = hipMemcpyAsync(h->d_in_offs.p, offs, (n_reads + 1) * 8, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+    return h->hip_fail(e, "input H2D");
+  int rc = h->add_device(h->d_in_bytes.as<uint8_t>(), h->d_in_offs.as<uint64_t>(), n_reads, n_bases, qcut);
+  if (rc == MHMKC_OK) {
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return h->hip_fail(e, "add_reads");
+  }
+  return rc;
+}
+
+static int check_offsets(mhmkc_t h, const uint64_t *offs, uint64_t n_reads) {
+  if (offs[0] != 0) return h->fail(MHMKC_EINVAL, "read_offsets[0] must be 0");
+  for (uint64_t i = 0; i < n_reads; i++) {
+    if (offs[i + 1] < offs[i]) return h->fail(MHMKC_EINVAL, "read_offsets must be non-decreasing (read %llu)",
+                                              (unsigned long long)i);
+    if (offs[i + 1] - offs[i] > 65535)
+      return h->fail(MHMKC_EINVAL, "read %llu longer than 65535 (PackedRead read_len is uint16)",
+                     (unsigned long long)i);
+  }
+  return MHMKC_OK;
+}
+
+int mhmkc_add_reads(mhmkc_t h, const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads) {
+  if (!h) return MHMKC_EINVAL;
+  if (!offs || (n_reads && !bytes)) return h->fail(MHMKC_EINVAL, "null host buffer");
+  int rc = check_offsets(h, offs, n_reads);
+  if (rc) return rc;
+  return add_host(h, bytes, offs, n_reads, h->cfg.qual_cutoff);
+}
+
+int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *offs, uint64_t n_seqs, uint16_t depth) {
+  if (!h) return MHMKC_EINVAL;
+  if (!offs || (n_seqs && !seqs)) return h->fail(MHMKC_EINVAL, "null host buffer");
+  if (depth > 1) return h->fail(MHMKC_EUNSUPPORTED, "contig pass (depth > 1) is not supported in this version");
+  if (offs[0] != 0) return h->fail(MHMKC_EINVAL, "seq_offsets[0] must be 0");
+  for (uint64_t i = 0; i < n_seqs; i++)
+    if (offs[i + 1] < offs[i]) return h->fail(MHMKC_EINVAL, "seq_offsets must be non-decreasing");
+  const uint64_t n = offs[n_seqs];
+  // Case carries the quality (SeqBlockInserter::process_seq input, src/kcount/kcount.cpp:80-86;
+  // quals[i] = isupper, src/kcount/kcount_cpu.cpp:309-312): uppercase -> q 31, lowercase -> q 0, and the
+  // batch runs with cutoff 1. Characters other than ACGTN are fatal in the reference
+  // (HashTableInserter::insert_supermer DIE, src/kcount/kcount_cpu.cpp:452-458).
+  std::vector<uint8_t> bytes(n);
+  for (uint64_t i = 0; i < n; i++) {
+    const char c = seqs[i];
+    uint8_t code;
+    switch (c) {
+      case 'A': case 'a': code = 0; break;
+      case 'C': case 'c': code = 1; break;
+      case 'G': case 'g': code = 2; break;
+      case 'T': case 't': code = 3; break;
+      case 'N': case 'n': code = 4; break;
+      default:
+        return h->fail(MHMKC_EBADCHAR, "bad char '%c' (%d) at position %llu", c, (int)c, (unsigned long long)i);
+    }
+    const bool upper = (c >= 'A' && c <= 'Z');
+    bytes[i] = (uint8_t)(code | (upper ? (31u << 3) : 0u));
+  }
+  return add_host(h, bytes.data(), offs, n_seqs, 1);
+}
+
+int mhmkc_finish(mhmkc_t h, uint64_t *n_out) {
+  if (!h) return MHMKC_EINVAL;
+  return h->finish(n_out);
+}
+
+int mhmkc_fetch(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right) {
+  if (!h) return MHMKC_EINVAL;
+  if (!h->finished) return h->fail(MHMKC_ESTATE, "fetch before finish");
+  const uint64_t n = h->n_out;
+  hipError_t e = hipSuccess;
+  if (n && keys) e = hipMemcpyAsync(keys, h->d_out_keys.p, n * 8 * h->nlo, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && n && counts) e = hipMemcpyAsync(counts, h->d_out_counts.p, n * 2, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && n && left) e = hipMemcpyAsync(left, h->d_out_left.p, n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && n && right) e = hipMemcpyAsync(right, h->d_out_right.p, n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return h->hip_fail(e, "fetch");
+  return MHMKC_OK;
+}
+
+int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,
+                        const char **d_right, uint64_t *n_out) {
+  if (!h) return MHMKC_EINVAL;
+  if (!h->finished) return h->fail(MHMKC_ESTATE, "device_output before finish");
+  if (d_keys) *d_keys = h->d_out_keys.as<uint64_t>();
+  if (d_counts) *d_counts = h->d_out_counts.as<uint16_t>();
+  if (d_left) *d_left = h->d_out_left.as<char>();
+  if (d_right) *d_right = h->d_out_right.as<char>();
+  if (n_out) *n_out = h->n_out;
+  return MHMKC_OK;
+}
+
+int mhmkc_get_stats(mhmkc_t h, mhmkc_stats *s) {
+  if (!h || !s) return MHMKC_EINVAL;
+  *s = h->st;
+  return MHMKC_OK;
+}
+
+int mhmkc_reset(mhmkc_t h) {
+  if (!h) return MHMKC_EINVAL;
+  hipError_t e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return h->hip_fail(e, "reset");
+  h->prof_collect();
+  h->n_slabs = 0;
+  h->finished = false;
+  h->began = false;
+  h->n_out = 0;
+  memset(&h->st, 0, sizeof h->st);
+  if ((e = hipMemsetAsync(h->d_err.p, 0, 16, h->stream)) != hipSuccess) return h->hip_fail(e, "reset");
+  return MHMKC_OK;
+}
+
+int mhmkc_set_profiling(mhmkc_t h, int on) {
+  if (!h) return MHMKC_EINVAL;
+  h->profiling = on != 0;
+  return MHMKC_OK;
+}
+
+const char *mhmkc_last_error(mhmkc_t h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+}  // extern "C"

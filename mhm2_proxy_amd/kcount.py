@@ -1,0 +1,503 @@
+"""Host-side mirror of the reference kcount interface over the C ABI of libmhmkc.so.
+
+Reference shapes kept (ajpowelsnl/mhm2_proxy):
+  * PackedRead / PackedReads        src/packed_reads.hpp:60-167, src/packed_reads.cpp:73-159
+  * Kmer<MAX_K> longs layout        src/kmer.hpp:61-160 (here: a tuple/array of n_longs uint64)
+  * KmerCounts{count, left, right}  src/kcount/kmer_dht.hpp:62-68
+  * KmerDHT (local_kmers, get_local_kmer_counts, get_kmer_target_rank, dump_kmers)
+                                    src/kcount/kmer_dht.hpp:118-172, src/kcount/kmer_dht.cpp
+  * analyze_kmers(...)              src/kcount/kcount.hpp:71-73, src/kcount/kcount.cpp:140-157
+
+The counting itself always runs on the GPU through libmhmkc.so; nothing here falls back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import gzip
+import os
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Iterable, NamedTuple, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+NUCLEOTIDE_MAP = "ACGTN"
+_BASE_CODE = {"A": 0, "C": 1, "G": 2, "T": 3, "N": 4}
+_IUPAC = set("URYKMSWBDHV")  # mapped to N by the PackedRead constructor (packed_reads.cpp:90-101)
+
+
+def n_longs_for(k: int) -> int:
+    """N_LONGS of Kmer<MAX_K> with MAX_K = (k/32+1)*32 (src/main.cpp:170, src/kmer.hpp:64)."""
+    return k // 32 + 1
+
+
+# ------------------------------------------------------------------------------------------------
+# Kmer helpers (2-bit MSB-first longs, src/kmer.cpp:178-188)
+
+
+def kmer_from_string(s: str, n_longs: int | None = None) -> tuple:
+    """set_kmer (src/kmer.cpp:274-296): A0 C1 G2 T3, the bit trick maps N to G."""
+    k = len(s)
+    nl = n_longs or n_longs_for(k)
+    longs = [0] * nl
+    for i, ch in enumerate(s):
+        c = ord(ch)
+        x = (c & 4) >> 1
+        code = x + ((x ^ (c & 2)) >> 1)
+        longs[i // 32] |= code << (2 * (31 - i % 32))
+    return tuple(longs)
+
+
+def kmer_to_string(longs: Sequence[int], k: int) -> str:
+    """to_string (src/kmer.cpp:595-634)."""
+    return "".join("ACGT"[(int(longs[i // 32]) >> (2 * (31 - i % 32))) & 3] for i in range(k))
+
+
+def keys_to_strings(keys: np.ndarray, k: int) -> list:
+    """Vectorised to_string for an (n, n_longs) uint64 key array."""
+    keys = np.asarray(keys, dtype=np.uint64)
+    n = keys.shape[0]
+    out = np.empty((n, k), dtype=np.uint8)
+    lut = np.frombuffer(b"ACGT", dtype=np.uint8)
+    for i in range(k):
+        w = keys[:, i // 32]
+        out[:, i] = lut[((w >> np.uint64(2 * (31 - i % 32))) & np.uint64(3)).astype(np.intp)]
+    return [bytes(r).decode() for r in out]
+
+
+# ------------------------------------------------------------------------------------------------
+# PackedReads
+
+
+class PackedReads:
+    """Reads in the PackedRead byte layout: one byte per base, code (A0 C1 G2 T3 N4) | min(q-off,31) << 3.
+
+    Mirrors src/packed_reads.hpp:120-167. Reads are stored contiguously (bytes + CSR offsets) so the
+    whole set can be handed to the device in one copy.
+    """
+
+    def __init__(self, qual_offset: int = 33, fname: str = ""):
+        if qual_offset not in (33, 64):
+            raise ValueError("qual_offset must be 33 or 64")
+        self.qual_offset = qual_offset
+        self.fname = fname
+        self._chunks: list[np.ndarray] = []
+        self._lens: list[int] = []
+        self._ids: list[int] = []
+        self._bytes: np.ndarray | None = None
+        self._offsets: np.ndarray | None = None
+        self.index = 0
+        self.max_read_len = 0
+
+    @classmethod
+    def from_arrays(cls, packed_bytes: np.ndarray, offsets: np.ndarray, qual_offset: int = 33) -> "PackedReads":
+        pr = cls(qual_offset)
+        pr._bytes = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+        pr._offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if pr._offsets.size == 0 or pr._offsets[0] != 0 or int(pr._offsets[-1]) != pr._bytes.size:
+            raise ValueError("offsets must start at 0 and end at len(bytes)")
+        lens = np.diff(pr._offsets)
+        pr.max_read_len = int(lens.max()) if lens.size else 0
+        return pr
+
+    @staticmethod
+    def pack(seq: str, quals: str, qual_offset: int = 33) -> np.ndarray:
+        """PackedRead constructor encoding (src/packed_reads.cpp:73-109); raises on illegal characters
+        (the reference DIEs)."""
+        if len(seq) != len(quals):
+            raise ValueError("seq and quals differ in length")
+        if len(seq) > 65535:
+            raise ValueError("read longer than 65535 (read_len is uint16)")
+        out = np.empty(len(seq), dtype=np.uint8)
+        for i, (ch, q) in enumerate(zip(seq, quals)):
+            if ch in _BASE_CODE:
+                code = _BASE_CODE[ch]
+            elif ch in _IUPAC:
+                code = 4
+            else:
+                raise ValueError(f"Illegal char in comp nucleotide of '{ch}'")
+            qq = min(ord(q) - qual_offset, 31)
+            out[i] = (code | ((qq & 0xFF) << 3)) & 0xFF
+        return out
+
+    def add_read(self, read_id: str, seq: str, quals: str) -> None:
+        """PackedReads::add_read (src/packed_reads.cpp:236-244)."""
+        if self._bytes is not None:
+            self._materialized_to_chunks()
+        self._chunks.append(self.pack(seq, quals, self.qual_offset))
+        self._lens.append(len(seq))
+        self.max_read_len = max(self.max_read_len, len(seq))
+
+    def _materialized_to_chunks(self):
+        b, o = self._bytes, self._offsets
+        self._chunks = [b[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+        self._lens = [int(o[i + 1] - o[i]) for i in range(len(o) - 1)]
+        self._bytes = self._offsets = None
+
+    def _materialize(self):
+        if self._bytes is None:
+            lens = np.asarray(self._lens, dtype=np.uint64)
+            self._offsets = np.zeros(len(lens) + 1, dtype=np.uint64)
+            np.cumsum(lens, out=self._offsets[1:])
+            self._bytes = (np.concatenate(self._chunks) if self._chunks else np.zeros(0, np.uint8)).astype(np.uint8)
+            self._chunks, self._lens = [], []
+
+    @property
+    def packed_bytes(self) -> np.ndarray:
+        self._materialize()
+        return self._bytes
+
+    @property
+    def offsets(self) -> np.ndarray:
+        self._materialize()
+        return self._offsets
+
+    def get_local_num_reads(self) -> int:
+        return len(self.offsets) - 1
+
+    def get_bases(self) -> int:
+        return int(self.offsets[-1])
+
+    def get_max_read_len(self) -> int:
+        return self.max_read_len
+
+    def reset(self) -> None:
+        self.index = 0
+
+    def get_read(self, i: int) -> tuple[str, str, str]:
+        """PackedRead::unpack (src/packed_reads.cpp:147-159); ids are synthetic '@r<i>/1'."""
+        b = self.packed_bytes[int(self.offsets[i]):int(self.offsets[i + 1])]
+        seq = "".join(NUCLEOTIDE_MAP[int(x) & 7] for x in b)
+        quals = "".join(chr(self.qual_offset + (int(x) >> 3)) for x in b)
+        return f"@r{i}/1", seq, quals
+
+    def get_next_read(self):
+        if self.index >= self.get_local_num_reads():
+            return None
+        r = self.get_read(self.index)
+        self.index += 1
+        return r
+
+
+# ------------------------------------------------------------------------------------------------
+# The counter (C ABI wrapper)
+
+
+class KmerCounts(NamedTuple):
+    """KmerCounts (src/kcount/kmer_dht.hpp:62-68) without the dbjg-only uutig_frag pointer."""
+    count: int
+    left: str
+    right: str
+
+
+@dataclass
+class KmerTable:
+    """Finished count table on the host: keys (n, n_longs) uint64, counts uint16, left/right bytes."""
+    k: int
+    keys: np.ndarray
+    counts: np.ndarray
+    left: np.ndarray
+    right: np.ndarray
+
+    def __len__(self) -> int:
+        return int(self.counts.shape[0])
+
+    def sorted(self) -> "KmerTable":
+        """Rows in Kmer::operator< order (word-wise unsigned, src/kmer.cpp:265-272)."""
+        if len(self) == 0:
+            return self
+        order = np.lexsort(tuple(self.keys[:, w] for w in range(self.keys.shape[1] - 1, -1, -1)))
+        return KmerTable(self.k, self.keys[order], self.counts[order], self.left[order], self.right[order])
+
+    def lines(self) -> Iterable[str]:
+        """dump_kmers line format "KMER count L R" (src/kcount/kmer_dht.cpp:243-266)."""
+        strs = keys_to_strings(self.keys, self.k)
+        for s, c, l, r in zip(strs, self.counts, self.left, self.right):
+            yield f"{s} {int(c)} {chr(int(l))} {chr(int(r))}"
+
+
+class KmerCounter:
+    """One GPU's k-mer counter; wraps mhmkc_* (include/mhmkc.h).
+
+    The lifecycle mirrors HashTableInserter (src/kcount/kmer_dht.hpp:95-116): construct (init), add reads
+    (insert_supermer via process_seq), finish (flush_inserts + insert_into_local_hashtable), fetch.
+    """
+
+    def __init__(self, k: int, *, n_longs: int = 0, qual_offset: int = 33, qual_cutoff: int = 20,
+                 dmin_thres: int = 2, dyn_min_depth: float = 0.9, device: int = -1, rank: int = 0,
+                 n_ranks: int = 1, comm_id: bytes | None = None, stream: int | None = None):
+        L = N.lib()
+        cfg = N.MhmkcConfig()
+        N.check(L.mhmkc_config_init(C.byref(cfg)))
+        cfg.k, cfg.n_longs, cfg.qual_offset, cfg.qual_cutoff = k, n_longs, qual_offset, qual_cutoff
+        cfg.dmin_thres, cfg.dyn_min_depth, cfg.device = dmin_thres, dyn_min_depth, device
+        cfg.rank, cfg.n_ranks = rank, n_ranks
+        self._comm_buf = None
+        if comm_id is not None:
+            if len(comm_id) != N.MHMKC_COMM_ID_BYTES:
+                raise ValueError("comm_id must be 128 bytes")
+            self._comm_buf = C.create_string_buffer(bytes(comm_id), N.MHMKC_COMM_ID_BYTES)
+            cfg.comm_id = C.cast(self._comm_buf, C.c_void_p)
+        cfg.stream = stream
+        h = C.c_void_p()
+        N.check(L.mhmkc_create(C.byref(h), C.byref(cfg)))
+        self._h = h
+        self.k = k
+        self.n_longs = n_longs or n_longs_for(k)
+        self.n_out = None
+
+    # -- lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            N.lib().mhmkc_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int) -> None:
+        N.check(rc, self._h)
+
+    # -- input
+    def add_packed_reads(self, packed_bytes: np.ndarray, offsets: np.ndarray) -> None:
+        b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        if o.size < 1:
+            raise ValueError("offsets needs n_reads + 1 entries")
+        self._check(N.lib().mhmkc_add_reads(self._h, b.ctypes.data, o.ctypes.data, o.size - 1))
+
+    def add_packed_reads_device(self, bytes_ptr: int, offsets_ptr: int, n_reads: int, n_bases: int) -> None:
+        self._check(N.lib().mhmkc_add_reads_device(self._h, bytes_ptr, offsets_ptr, n_reads, n_bases))
+
+    def add_tensors(self, bytes_t, offsets_t) -> None:
+        """Device-resident torch tensors (uint8 bytes, int64/uint64 offsets with n_reads+1 entries)."""
+        n_reads = int(offsets_t.numel()) - 1
+        self.add_packed_reads_device(bytes_t.data_ptr(), offsets_t.data_ptr(), n_reads, int(bytes_t.numel()))
+
+    def add_reads(self, reads: PackedReads) -> None:
+        self.add_packed_reads(reads.packed_bytes, reads.offsets)
+
+    def add_seqs(self, seqs: Sequence[str], depth: int = 1) -> None:
+        """Sequences whose lowercase letters mark bases below the quality cutoff (the string given to
+        SeqBlockInserter::process_seq, src/kcount/kcount.cpp:80-86)."""
+        lens = np.fromiter((len(s) for s in seqs), dtype=np.uint64, count=len(seqs))
+        offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        blob = "".join(seqs).encode("ascii")
+        self._check(N.lib().mhmkc_add_seqs(self._h, blob, offs.ctypes.data, len(seqs), depth))
+
+    # -- finish / output
+    def finish(self) -> int:
+        n = C.c_uint64()
+        self._check(N.lib().mhmkc_finish(self._h, C.byref(n)))
+        self.n_out = int(n.value)
+        return self.n_out
+
+    def fetch(self) -> KmerTable:
+        if self.n_out is None:
+            raise RuntimeError("fetch before finish")
+        n = self.n_out
+        keys = np.empty((n, self.n_longs), dtype=np.uint64)
+        counts = np.empty(n, dtype=np.uint16)
+        left = np.empty(n, dtype=np.uint8)
+        right = np.empty(n, dtype=np.uint8)
+        self._check(N.lib().mhmkc_fetch(self._h, keys.ctypes.data, counts.ctypes.data, left.ctypes.data,
+                                        right.ctypes.data))
+        return KmerTable(self.k, keys, counts, left, right)
+
+    def device_output(self) -> dict:
+        ptrs = [C.c_void_p() for _ in range(4)]
+        n = C.c_uint64()
+        self._check(N.lib().mhmkc_device_output(self._h, *(C.byref(p) for p in ptrs), C.byref(n)))
+        return {"keys": ptrs[0].value, "counts": ptrs[1].value, "left": ptrs[2].value, "right": ptrs[3].value,
+                "n_out": int(n.value), "n_longs": self.n_longs}
+
+    def stats(self) -> dict:
+        s = N.MhmkcStats()
+        self._check(N.lib().mhmkc_get_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def reset(self) -> None:
+        self._check(N.lib().mhmkc_reset(self._h))
+        self.n_out = None
+
+    def set_profiling(self, on: bool = True) -> None:
+        self._check(N.lib().mhmkc_set_profiling(self._h, 1 if on else 0))
+
+
+def comm_id() -> bytes:
+    """RCCL unique id for multi-rank counters (rank 0 creates it and broadcasts it)."""
+    buf = C.create_string_buffer(N.MHMKC_COMM_ID_BYTES)
+    N.check(N.lib().mhmkc_comm_id(buf))
+    return buf.raw
+
+
+# ------------------------------------------------------------------------------------------------
+# KmerDHT / analyze_kmers mirror
+
+
+def _quick_hash(v: int) -> int:
+    """quick_hash (src/hash_funcs.c:332-342)."""
+    M = (1 << 64) - 1
+    v = (v * 3935559000370003845 + 2691343689449507681) & M
+    v ^= v >> 21
+    v = (v ^ (v << 37)) & M
+    v ^= v >> 4
+    v = (v * 4768777513237032717) & M
+    v = (v ^ (v << 20)) & M
+    v ^= v >> 41
+    v = (v ^ (v << 5)) & M
+    return v
+
+
+def _revcomp_longs(longs: Sequence[int], k: int) -> tuple:
+    s = kmer_to_string(longs, k)
+    comp = {"A": "T", "C": "G", "G": "C", "T": "A"}
+    return kmer_from_string("".join(comp[c] for c in reversed(s)), len(longs))
+
+
+def minimizer_len(k: int) -> int:
+    """KmerDHT minimizer length (src/kcount/kmer_dht.cpp:114-116)."""
+    return min(27, max(15, k * 2 // 3 + 1))
+
+
+def get_minimizer_fast(longs: Sequence[int], k: int, m: int) -> int:
+    """Greatest least-complement m-mer (Kmer::get_minimizer_fast, src/kmer.cpp:344-403)."""
+    M = (1 << 64) - 1
+    mask = (M << (64 - 2 * m)) & M
+    s = kmer_to_string(longs, k)
+    rc = kmer_to_string(_revcomp_longs(longs, k), k)
+    best = 0
+    for i in range(k - m + 1):
+        f = kmer_from_string(s[i:i + m], 1)[0] & mask
+        r = kmer_from_string(rc[k - m - i:k - i], 1)[0] & mask
+        best = max(best, min(f, r))
+    return best
+
+
+def get_kmer_target_rank(longs: Sequence[int], k: int, rank_n: int) -> int:
+    """KmerDHT::get_kmer_target_rank (src/kcount/kmer_dht.cpp:193-196): the owner rank dbjg expects."""
+    return _quick_hash(get_minimizer_fast(longs, k, minimizer_len(k))) % rank_n
+
+
+class KmerDHT:
+    """Per-rank result holder shaped like KmerDHT<MAX_K> (src/kcount/kmer_dht.hpp:118-172)."""
+
+    def __init__(self, k: int, my_num_kmers: int = 0, *, counter: KmerCounter | None = None, rank: int = 0,
+                 n_ranks: int = 1, **counter_kwargs):
+        self.k = k
+        self.my_num_kmers = my_num_kmers
+        self.rank, self.n_ranks = rank, n_ranks
+        self.counter = counter or KmerCounter(k, rank=rank, n_ranks=n_ranks, **counter_kwargs)
+        self.minimizer_len = minimizer_len(k)
+        self.table: KmerTable | None = None
+        self._map: dict | None = None
+
+    def get_minimizer_len(self) -> int:
+        return self.minimizer_len
+
+    def finish_updates(self) -> None:
+        """flush_updates + finish_updates (src/kcount/kmer_dht.cpp:227-236)."""
+        self.counter.finish()
+        self.table = self.counter.fetch()
+        self._map = None
+
+    @property
+    def local_kmers(self) -> dict:
+        """KmerMap: {longs tuple: KmerCounts} (materialised lazily; use .table for large sets)."""
+        if self._map is None:
+            t = self.table
+            self._map = {tuple(int(x) for x in t.keys[i]): KmerCounts(int(t.counts[i]), chr(int(t.left[i])),
+                                                                       chr(int(t.right[i])))
+                         for i in range(len(t))}
+        return self._map
+
+    def get_local_num_kmers(self) -> int:
+        return 0 if self.table is None else len(self.table)
+
+    def get_num_kmers(self) -> int:
+        return self.get_local_num_kmers()
+
+    def get_local_kmer_counts(self, kmer) -> KmerCounts | None:
+        key = kmer_from_string(kmer) if isinstance(kmer, str) else tuple(int(x) for x in kmer)
+        return self.local_kmers.get(key)
+
+    def get_kmer_target_rank(self, kmer) -> int:
+        longs = kmer_from_string(kmer) if isinstance(kmer, str) else kmer
+        return get_kmer_target_rank(longs, self.k, self.n_ranks)
+
+    def dump_kmers(self, out_dir: str | os.PathLike = ".") -> Path:
+        """dump_kmers (src/kcount/kmer_dht.cpp:243-266): kmers-<k>.txt.gz, lines "KMER count L R"."""
+        name = f"kmers-{self.k}.txt.gz" if self.n_ranks == 1 else f"kmers-{self.k}-rank{self.rank}.txt.gz"
+        path = Path(out_dir) / name
+        with gzip.open(path, "wt") as f:
+            for line in self.table.lines():
+                f.write(line + "\n")
+        return path
+
+    def clear_stores(self) -> None:
+        self.counter.reset()
+
+
+def analyze_kmers(kmer_len: int, prev_kmer_len: int, qual_offset: int, packed_reads_list: Sequence[PackedReads],
+                  dmin_thres: int, ctgs: Sequence, kmer_dht: KmerDHT, dump_kmers: bool = False,
+                  dump_dir: str | os.PathLike = ".") -> None:
+    """analyze_kmers<MAX_K> (src/kcount/kcount.hpp:71-73, src/kcount/kcount.cpp:140-157).
+
+    Counts every read of every PackedReads on this rank's GPU, exchanges by hash range with the other
+    ranks, purges and chooses extensions; the result is kmer_dht.table / kmer_dht.local_kmers.
+    The contig pass (ctgs non-empty, rounds after the first k) is not in this version.
+    """
+    if kmer_len != kmer_dht.k:
+        raise ValueError("kmer_len differs from the KmerDHT's k")
+    if len(ctgs):
+        raise NotImplementedError("contig k-mer pass (add_ctg_kmers) is not implemented in this version")
+    for pr in packed_reads_list:
+        if pr.qual_offset != qual_offset:
+            raise ValueError("PackedReads qual_offset differs")
+        kmer_dht.counter.add_reads(pr)
+    kmer_dht.finish_updates()
+    if dump_kmers:
+        kmer_dht.dump_kmers(dump_dir)
+
+
+# ------------------------------------------------------------------------------------------------
+# synthetic reads
+
+
+def synth_genome(genome_len: int, seed: int) -> np.ndarray:
+    S = N.synth()
+    cfg = N.SynthConfig()
+    S.mhmkc_synth_config_init(C.byref(cfg), genome_len, 150, seed)
+    g = np.empty(genome_len, dtype=np.uint8)
+    if S.mhmkc_synth_genome(C.byref(cfg), g.ctypes.data) != 0:
+        raise RuntimeError("mhmkc_synth_genome failed")
+    return g
+
+
+def synth_reads(genome: np.ndarray, n_reads: int, read_len: int, seed: int, first_read: int = 0,
+                threads: int = 0, **rates) -> tuple[np.ndarray, np.ndarray]:
+    """(packed_bytes, offsets) of reads first_read .. first_read + n_reads - 1 of the global set."""
+    S = N.synth()
+    cfg = N.SynthConfig()
+    S.mhmkc_synth_config_init(C.byref(cfg), genome.size, read_len, seed)
+    for key, val in rates.items():
+        setattr(cfg, key, val)
+    b = np.empty(n_reads * read_len, dtype=np.uint8)
+    o = np.empty(n_reads + 1, dtype=np.uint64)
+    g = np.ascontiguousarray(genome, dtype=np.uint8)
+    nt = threads or min(16, os.cpu_count() or 1)
+    if S.mhmkc_synth_reads(C.byref(cfg), g.ctypes.data, first_read, n_reads, b.ctypes.data, o.ctypes.data, nt) != 0:
+        raise RuntimeError("mhmkc_synth_reads failed")
+    return b, o

@@ -1,0 +1,108 @@
+"""Shared helpers for the parity tests (inputs, table comparison)."""
+from __future__ import annotations
+
+import gzip
+from pathlib import Path
+
+import numpy as np
+
+import mhm2_proxy_amd as m
+import oracle_lib as O
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def synth_set(n_reads: int, genome_len: int, seed: int, read_len: int = 150, **rates):
+    g = m.synth_genome(genome_len, seed)
+    return m.synth_reads(g, n_reads, read_len, seed, **rates)
+
+
+def edge_case_set(seed: int = 5, n: int = 1500):
+    """Variable-length reads incl. L < k, L = k, k+1, k+2, all-N, poly-A (hot k-mer), low quality and
+    every PackedRead code; built deterministically from synthetic reads."""
+    rng = np.random.default_rng(seed)
+    b, o = synth_set(n, 20000, seed)
+    reads = [b[o[i]:o[i + 1]].copy() for i in range(n)]
+    out = []
+    for i, r in enumerate(reads):
+        mode = i % 10
+        if mode == 0:
+            r = r[: int(rng.integers(0, 150))]
+        elif mode == 1:
+            r = r[: int(rng.integers(18, 26))]
+        elif mode == 2:
+            r = np.full(int(rng.integers(20, 150)), 4 | (31 << 3), dtype=np.uint8)  # all N, good quality
+        elif mode == 3:
+            r = np.full(150, 0 | (31 << 3), dtype=np.uint8)  # poly-A
+        elif mode == 4:
+            r = (r & 7) | (np.uint8(5) << 3)  # all low quality
+        elif mode == 5:
+            q = rng.integers(0, 32, size=r.size).astype(np.uint8)
+            r = (r & 7) | (q << 3)
+        out.append(r.astype(np.uint8))
+    out.append(np.zeros(0, np.uint8))
+    lens = np.array([x.size for x in out], dtype=np.uint64)
+    offs = np.zeros(len(out) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return np.concatenate(out).astype(np.uint8), offs
+
+
+def hot_set(n_poly: int = 800, seed: int = 9):
+    """Enough poly-A reads that one canonical k-mer passes 65535 occurrences (u16 saturation) and its
+    extension counters pass the 0xC000 clamp of the LDS counters."""
+    b, o = synth_set(400, 20000, seed)
+    poly = np.full(150, 0 | (31 << 3), dtype=np.uint8)
+    reads = [b[o[i]:o[i + 1]] for i in range(400)] + [poly] * n_poly
+    lens = np.array([x.size for x in reads], dtype=np.uint64)
+    offs = np.zeros(len(reads) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return np.concatenate(reads).astype(np.uint8), offs
+
+
+def oracle_table(b, o, k, **kw) -> m.KmerTable:
+    t = O.kcount(b, o, k, **kw)
+    keys, c, l, r = t.fetch()
+    return m.KmerTable(k, keys, c, l, r)
+
+
+def assert_tables_equal(a: m.KmerTable, b: m.KmerTable, what: str = ""):
+    a, b = a.sorted(), b.sorted()
+    assert len(a) == len(b), f"{what}: {len(a)} vs {len(b)} k-mers"
+    if len(a) == 0:
+        return
+    bad = np.flatnonzero((a.keys != b.keys).any(axis=1) | (a.counts != b.counts) | (a.left != b.left) |
+                         (a.right != b.right))
+    if bad.size:
+        i = int(bad[0])
+        ka = m.keys_to_strings(a.keys[i:i + 1], a.k)[0]
+        kb = m.keys_to_strings(b.keys[i:i + 1], b.k)[0]
+        raise AssertionError(f"{what}: {bad.size} rows differ; first at {i}: {ka} {a.counts[i]} {chr(a.left[i])} "
+                             f"{chr(a.right[i])} vs {kb} {b.counts[i]} {chr(b.left[i])} {chr(b.right[i])}")
+
+
+def read_reads_file(path: Path):
+    """'seq qual' lines (BASELINE.md input format) -> PackedRead bytes + offsets."""
+    seqs = []
+    with gzip.open(path, "rt") as f:
+        for line in f:
+            parts = line.split()
+            seqs.append(m.PackedReads.pack(parts[0], parts[1]) if parts else np.zeros(0, np.uint8))
+    lens = np.array([s.size for s in seqs], dtype=np.uint64)
+    offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    return (np.concatenate(seqs) if seqs else np.zeros(0, np.uint8)).astype(np.uint8), offs
+
+
+def read_table_file(path: Path, k: int) -> m.KmerTable:
+    """dump_kmers lines 'KMER count L R' -> KmerTable."""
+    nl = m.n_longs_for(k)
+    keys, counts, left, right = [], [], [], []
+    with gzip.open(path, "rt") as f:
+        for line in f:
+            s, c, l, r = line.split()
+            keys.append(m.kmer_from_string(s, nl))
+            counts.append(int(c))
+            left.append(ord(l))
+            right.append(ord(r))
+    return m.KmerTable(k, np.array(keys, dtype=np.uint64).reshape(-1, nl), np.array(counts, dtype=np.uint16),
+                       np.array(left, dtype=np.uint8), np.array(right, dtype=np.uint8))

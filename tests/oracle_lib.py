@@ -1,0 +1,175 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY (the CPU checker).
+
+Also binds oracle/_ref/libhashref.so, the reference's own src/hash_funcs.c compiled unmodified
+(oracle/Makefile), when it has been built.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE = ROOT / "oracle" / "liboracle.so"
+HASHREF = ROOT / "oracle" / "_ref" / "libhashref.so"
+
+_o = None
+
+
+def oracle() -> C.CDLL:
+    global _o
+    if _o is None:
+        if not ORACLE.exists():
+            raise ImportError(f"{ORACLE} missing: run `make -C oracle`")
+        L = C.CDLL(str(ORACLE))
+        U64, VP, I = C.c_uint64, C.c_void_p, C.c_int
+        L.orc_murmur3_x64_64.argtypes = [VP, C.c_uint32]
+        L.orc_murmur3_x64_64.restype = U64
+        L.orc_murmur3_x64_128.argtypes = [VP, C.c_uint32, C.c_uint32, VP]
+        L.orc_murmur3_x64_128.restype = None
+        L.orc_quick_hash.argtypes = [U64]
+        L.orc_quick_hash.restype = U64
+        L.orc_kmer_from_string.argtypes = [C.c_char_p, I, I, VP]
+        L.orc_kmer_from_string.restype = None
+        L.orc_kmer_to_string.argtypes = [VP, I, C.c_char_p]
+        L.orc_kmer_to_string.restype = None
+        L.orc_kmer_revcomp.argtypes = [VP, I, I, VP]
+        L.orc_kmer_revcomp.restype = None
+        L.orc_kmer_hash.argtypes = [VP, I]
+        L.orc_kmer_hash.restype = U64
+        L.orc_get_minimizer_fast.argtypes = [VP, I, I, I, I]
+        L.orc_get_minimizer_fast.restype = U64
+        L.orc_minimizer_hash_fast.argtypes = [VP, I, I, I]
+        L.orc_minimizer_hash_fast.restype = U64
+        L.orc_minimizer_len.argtypes = [I]
+        L.orc_kmer_target_rank.argtypes = [VP, I, I, I]
+        L.orc_kcount.argtypes = [VP, VP, U64, I, I, I, I, C.c_double]
+        L.orc_kcount.restype = VP
+        L.orc_extract.argtypes = [VP, VP, U64, I, I, I, VP, VP, U64]
+        L.orc_extract.restype = C.c_int64
+        L.orc_count_records.argtypes = [VP, VP, U64, I, I, C.c_double]
+        L.orc_count_records.restype = VP
+        L.orc_table_size.argtypes = [VP]
+        L.orc_table_size.restype = U64
+        L.orc_table_fetch.argtypes = [VP, VP, VP, VP, VP]
+        L.orc_table_fetch.restype = None
+        L.orc_table_stats.argtypes = [VP, VP]
+        L.orc_table_stats.restype = None
+        L.orc_table_free.argtypes = [VP]
+        L.orc_table_free.restype = None
+        _o = L
+    return _o
+
+
+def hashref():
+    """The reference's compiled hash_funcs.c, or None when oracle/_ref was not built."""
+    if not HASHREF.exists():
+        return None
+    L = C.CDLL(str(HASHREF))
+    L.MurmurHash3_x64_64.argtypes = [C.c_void_p, C.c_uint32]
+    L.MurmurHash3_x64_64.restype = C.c_uint64
+    L.MurmurHash3_x64_128.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+    L.MurmurHash3_x64_128.restype = None
+    L.quick_hash.argtypes = [C.c_uint64]
+    L.quick_hash.restype = C.c_uint64
+    return L
+
+
+class OracleTable:
+    def __init__(self, ptr, n_longs, k):
+        if not ptr:
+            raise ValueError("oracle rejected the input (the reference would DIE)")
+        self.ptr, self.n_longs, self.k = ptr, n_longs, k
+
+    def fetch(self):
+        L = oracle()
+        n = L.orc_table_size(self.ptr)
+        keys = np.empty((n, self.n_longs), dtype=np.uint64)
+        counts = np.empty(n, dtype=np.uint16)
+        left = np.empty(n, dtype=np.uint8)
+        right = np.empty(n, dtype=np.uint8)
+        L.orc_table_fetch(self.ptr, keys.ctypes.data, counts.ctypes.data, left.ctypes.data, right.ctypes.data)
+        return keys, counts, left, right
+
+    def stats(self) -> dict:
+        s = np.zeros(5, dtype=np.uint64)
+        oracle().orc_table_stats(self.ptr, s.ctypes.data)
+        return dict(occurrences=int(s[0]), distinct=int(s[1]), purged=int(s[2]), n_out=int(s[3]), reads=int(s[4]))
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            oracle().orc_table_free(self.ptr)
+            self.ptr = None
+
+
+def kcount(packed_bytes, offsets, k, n_longs=None, qual_cutoff=20, dmin_thres=2, dyn_min_depth=0.9) -> OracleTable:
+    nl = n_longs or (k // 32 + 1)
+    b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ptr = oracle().orc_kcount(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, dmin_thres,
+                              dyn_min_depth)
+    return OracleTable(ptr, nl, k)
+
+
+def extract(packed_bytes, offsets, k, n_longs=None, qual_cutoff=20):
+    nl = n_longs or (k // 32 + 1)
+    b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.diff(o.astype(np.int64))
+    cap = int(np.clip(lens - k - 1, 0, None).sum()) + 1
+    keys = np.empty((cap, nl), dtype=np.uint64)
+    exts = np.empty(cap, dtype=np.uint8)
+    n = oracle().orc_extract(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, keys.ctypes.data,
+                             exts.ctypes.data, cap)
+    if n < 0:
+        raise ValueError("oracle extract failed")
+    return keys[:n], exts[:n]
+
+
+def count_records(keys, exts, k, n_longs=None, dmin_thres=2, dyn_min_depth=0.9) -> OracleTable:
+    nl = n_longs or (k // 32 + 1)
+    kk = np.ascontiguousarray(keys, dtype=np.uint64)
+    ee = np.ascontiguousarray(exts, dtype=np.uint8)
+    ptr = oracle().orc_count_records(kk.ctypes.data, ee.ctypes.data, ee.size, nl, dmin_thres, dyn_min_depth)
+    return OracleTable(ptr, nl, k)
+
+
+def kmer_hash(longs) -> int:
+    a = np.ascontiguousarray(longs, dtype=np.uint64)
+    return int(oracle().orc_kmer_hash(a.ctypes.data, a.size))
+
+
+def kmer_from_string(s: str, n_longs: int) -> np.ndarray:
+    a = np.zeros(n_longs, dtype=np.uint64)
+    oracle().orc_kmer_from_string(s.encode(), len(s), n_longs, a.ctypes.data)
+    return a
+
+
+def kmer_to_string(longs, k: int) -> str:
+    a = np.ascontiguousarray(longs, dtype=np.uint64)
+    buf = C.create_string_buffer(k + 1)
+    oracle().orc_kmer_to_string(a.ctypes.data, k, buf)
+    return buf.value.decode()
+
+
+def kmer_revcomp(longs, k: int) -> np.ndarray:
+    a = np.ascontiguousarray(longs, dtype=np.uint64)
+    out = np.zeros_like(a)
+    oracle().orc_kmer_revcomp(a.ctypes.data, k, a.size, out.ctypes.data)
+    return out
+
+
+def minimizer_fast(longs, k: int, m: int, least_complement: bool = True) -> int:
+    a = np.ascontiguousarray(longs, dtype=np.uint64)
+    return int(oracle().orc_get_minimizer_fast(a.ctypes.data, k, a.size, m, 1 if least_complement else 0))
+
+
+def minimizer_hash_fast(longs, k: int, m: int) -> int:
+    a = np.ascontiguousarray(longs, dtype=np.uint64)
+    return int(oracle().orc_minimizer_hash_fast(a.ctypes.data, k, a.size, m))
+
+
+def target_rank(longs, k: int, rank_n: int) -> int:
+    a = np.ascontiguousarray(longs, dtype=np.uint64)
+    return int(oracle().orc_kmer_target_rank(a.ctypes.data, k, a.size, rank_n))

@@ -1,0 +1,84 @@
+"""The C-ABI libraries load and export every symbol their headers declare (no GPU needed; no compute)."""
+from __future__ import annotations
+
+import ctypes as C
+import re
+from pathlib import Path
+
+import pytest
+
+from mhm2_proxy_amd import _native as N
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared(header: Path) -> list:
+    text = header.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mhmkc_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_headers_match_binding_lists():
+    assert declared(ROOT / "include" / "mhmkc.h") == sorted(N.ABI_SYMBOLS)
+    assert declared(ROOT / "include" / "mhmkc_synth.h") == sorted(N.SYNTH_SYMBOLS)
+
+
+def test_lib_exports_every_declared_symbol():
+    from mhm2_proxy_amd import build
+
+    build.build_lib()  # hipcc cross-compiles gfx950 here without a GPU
+    lib = N.lib()
+    for name in declared(ROOT / "include" / "mhmkc.h"):
+        assert hasattr(lib, name), name
+    assert lib.mhmkc_abi_version() == 1
+
+
+def test_synth_exports_every_declared_symbol():
+    lib = N.synth()
+    for name in declared(ROOT / "include" / "mhmkc_synth.h"):
+        assert hasattr(lib, name), name
+
+
+def test_config_defaults_are_the_reference_defaults():
+    cfg = N.MhmkcConfig()
+    assert N.lib().mhmkc_config_init(C.byref(cfg)) == 0
+    assert (cfg.k, cfg.qual_offset, cfg.qual_cutoff, cfg.dmin_thres) == (21, 33, 20, 2)
+    assert cfg.dyn_min_depth == 0.9 and cfg.n_ranks == 1 and cfg.rank == 0
+
+
+@pytest.mark.parametrize("field,value,code", [("k", 0, -1), ("k", 128, -1), ("k", 32, -7), ("k", 64, -7),
+                                               ("qual_offset", 40, -1), ("dmin_thres", 40000, -7),
+                                               ("n_ranks", 0, -1), ("rank", 3, -1), ("n_longs", 9, -1),
+                                               ("dyn_min_depth", 1.5, -1)])
+def test_create_rejects_bad_config(field, value, code):
+    cfg = N.MhmkcConfig()
+    N.lib().mhmkc_config_init(C.byref(cfg))
+    setattr(cfg, field, value)
+    h = C.c_void_p()
+    assert N.lib().mhmkc_create(C.byref(h), C.byref(cfg)) == code
+    assert not h.value
+    assert N.lib().mhmkc_last_error(None)
+
+
+def test_null_handle_calls_fail_cleanly():
+    L = N.lib()
+    assert L.mhmkc_finish(None, None) == -1
+    assert L.mhmkc_reset(None) == -1
+    assert L.mhmkc_fetch(None, None, None, None, None) == -1
+    L.mhmkc_destroy(None)
+
+
+def test_header_is_plain_c():
+    """The boundary header compiles as C99 (no C++ or torch types in the signatures)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    if not shutil.which("gcc"):
+        pytest.skip("gcc missing")
+    with tempfile.TemporaryDirectory() as d:
+        src = Path(d) / "t.c"
+        src.write_text('#include "mhmkc.h"\n#include "mhmkc_synth.h"\nint main(void){mhmkc_config c; '
+                       'mhmkc_config_init(&c); return c.k == 21 ? 0 : 1;}\n')
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", f"-I{ROOT / 'include'}", str(src)],
+                       check=True)

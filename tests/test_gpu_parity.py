@@ -1,0 +1,201 @@
+"""Parity of the HIP path (through the C ABI of libmhmkc.so) with the CPU oracle and the golden fixtures.
+
+Bit-exact: every (canonical k-mer, count, left, right) row must be identical; order is free, as the
+reference's KmerMap iteration order is.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import mhm2_proxy_amd as m
+import oracle_lib as O
+from common import (GOLDEN, assert_tables_equal, edge_case_set, hot_set, oracle_table, read_reads_file,
+                    read_table_file, synth_set)
+
+pytestmark = pytest.mark.gpu
+
+
+def hip_table(b, o, k, batches=1, **kw):
+    with m.KmerCounter(k, **kw) as c:
+        n = o.size - 1
+        cuts = [n * i // batches for i in range(batches + 1)]
+        for a, z in zip(cuts[:-1], cuts[1:]):
+            base = int(o[a])
+            c.add_packed_reads(b[base:int(o[z])], (o[a:z + 1] - o[a]).astype(np.uint64))
+        c.finish()
+        return c.fetch(), c.stats()
+
+
+def check_stats(st, oracle_stats=None):
+    assert st["count_sum"] == st["owned_records"] == st["occurrences"]
+    assert st["distinct"] == st["n_out"] + st["purged"]
+    assert st["dropped"] == 0
+    if oracle_stats:
+        assert st["occurrences"] == oracle_stats["occurrences"]
+        assert st["distinct"] == oracle_stats["distinct"]
+        assert st["purged"] == oracle_stats["purged"]
+
+
+@pytest.mark.parametrize("k", [21, 33, 55, 63, 77, 99, 15, 31, 45, 127])
+def test_synthetic_vs_oracle(k):
+    b, o = synth_set(2000, 10000, 100 + k)
+    ref = O.kcount(b, o, k)
+    keys, c, l, r = ref.fetch()
+    got, st = hip_table(b, o, k)
+    assert_tables_equal(got, m.KmerTable(k, keys, c, l, r), f"k={k}")
+    check_stats(st, ref.stats())
+
+
+@pytest.mark.parametrize("k", [21, 33, 63, 99])
+def test_edge_cases_vs_oracle(k):
+    b, o = edge_case_set()
+    got, st = hip_table(b, o, k)
+    assert_tables_equal(got, oracle_table(b, o, k), f"edge k={k}")
+    check_stats(st)
+
+
+@pytest.mark.parametrize("k", [21, 63])
+def test_hot_kmer_saturation(k):
+    b, o = hot_set()
+    got, _ = hip_table(b, o, k)
+    exp = oracle_table(b, o, k)
+    assert (exp.counts == 65535).any(), "fixture must saturate a count"
+    assert_tables_equal(got, exp, f"hot k={k}")
+
+
+@pytest.mark.parametrize("cutoff,dmin,dyn", [(0, 2, 0.9), (32, 2, 0.9), (20, 1, 0.9), (20, 5, 0.9), (20, 2, 0.5),
+                                             (20, 2, 1.0), (20, 0, 0.0), (25, 3, 0.75)])
+def test_parameters_vs_oracle(cutoff, dmin, dyn):
+    b, o = synth_set(1500, 8000, 7)
+    got, _ = hip_table(b, o, 21, qual_cutoff=cutoff, dmin_thres=dmin, dyn_min_depth=dyn)
+    exp = oracle_table(b, o, 21, qual_cutoff=cutoff, dmin_thres=dmin, dyn_min_depth=dyn)
+    assert_tables_equal(got, exp, f"cutoff={cutoff} dmin={dmin} dyn={dyn}")
+
+
+@pytest.mark.parametrize("k", [21, 55])
+def test_batches_equal_single(k):
+    b, o = synth_set(3000, 15000, 11)
+    one, _ = hip_table(b, o, k)
+    many, _ = hip_table(b, o, k, batches=5)
+    assert_tables_equal(many, one, "5 batches vs 1")
+
+
+@pytest.mark.parametrize("k", [21, 63])
+def test_forced_overflow_sweeps(k, monkeypatch):
+    """Tiny LDS tables force the multi-sweep path (a closed table overflows whole keys to the next sweep)."""
+    b, o = synth_set(3000, 50000, 13)
+    exp = oracle_table(b, o, k)
+    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
+    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    got, st = hip_table(b, o, k)
+    assert st["overflow_sweeps"] > 0
+    assert_tables_equal(got, exp, "forced overflow")
+    check_stats(st)
+
+
+def test_add_seqs_matches_packed():
+    b, o = synth_set(500, 5000, 21)
+    pr = m.PackedReads.from_arrays(b, o)
+    seqs = []
+    for i in range(pr.get_local_num_reads()):
+        _, s, q = pr.get_read(i)
+        seqs.append("".join(ch.lower() if ord(qq) < 33 + 20 else ch for ch, qq in zip(s, q)))
+    with m.KmerCounter(21) as c:
+        c.add_seqs(seqs)
+        c.finish()
+        got = c.fetch()
+    assert_tables_equal(got, oracle_table(b, o, 21), "add_seqs")
+
+
+def test_reset_and_reuse():
+    b1, o1 = synth_set(800, 6000, 31)
+    b2, o2 = synth_set(900, 7000, 32)
+    with m.KmerCounter(33) as c:
+        for b, o in ((b1, o1), (b2, o2), (b1, o1)):
+            c.add_packed_reads(b, o)
+            c.finish()
+            assert_tables_equal(c.fetch(), oracle_table(b, o, 33), "reuse")
+            c.reset()
+
+
+def test_n_longs_padding():
+    b, o = synth_set(600, 5000, 41)
+    got, _ = hip_table(b, o, 21, n_longs=2)
+    exp = oracle_table(b, o, 21)
+    assert got.keys.shape[1] == 2 and (got.keys[:, 1] == 0).all()
+    assert_tables_equal(m.KmerTable(21, got.keys[:, :1].copy(), got.counts, got.left, got.right), exp, "n_longs=2")
+
+
+def test_device_tensor_input():
+    torch = pytest.importorskip("torch")
+    b, o = synth_set(1000, 8000, 51)
+    bt = torch.from_numpy(b).cuda()
+    ot = torch.from_numpy(o.astype(np.int64)).cuda()
+    with m.KmerCounter(21) as c:
+        c.add_tensors(bt, ot)
+        c.finish()
+        got = c.fetch()
+    assert_tables_equal(got, oracle_table(b, o, 21), "device tensors")
+
+
+def test_bad_input_rejected():
+    b, o = synth_set(50, 2000, 3)
+    b = b.copy()
+    b[17] = 6  # code 6 is not A,C,G,T,N: the reference DIEs
+    with m.KmerCounter(21) as c:
+        c.add_packed_reads(b, o)
+        with pytest.raises(m.kcount.N.MhmkcError) as e:
+            c.finish()
+        assert e.value.code == -6
+
+
+def test_empty_input():
+    with m.KmerCounter(21) as c:
+        c.add_packed_reads(np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+        assert c.finish() == 0
+
+
+@pytest.mark.parametrize("name", sorted(p.name for p in GOLDEN.glob("table_*.tsv.gz")))
+def test_golden_fixtures(name):
+    _, setname, kk = name[:-len(".tsv.gz")].split("_")
+    k = int(kk[1:])
+    b, o = read_reads_file(GOLDEN / f"reads_{setname}.txt.gz")
+    got, _ = hip_table(b, o, k)
+    assert_tables_equal(got, read_table_file(GOLDEN / name, k), name)
+
+
+@pytest.mark.slow
+def test_medium_vs_oracle():
+    """400k reads x 150 bp (51M windows) against the oracle."""
+    b, o = synth_set(400_000, 2_000_000, 77)
+    ref = O.kcount(b, o, 21)
+    keys, c, l, r = ref.fetch()
+    got, st = hip_table(b, o, 21)
+    assert_tables_equal(got, m.KmerTable(21, keys, c, l, r), "medium")
+    check_stats(st, ref.stats())
+
+
+@pytest.mark.slow
+def test_c2_scale_properties():
+    """Config C2 (10M x 150 bp, G = 50 Mbp, k = 21): size-independent properties at full size —
+    one batch equals four batches (order independence), conservation (count_sum == occurrences ==
+    10M * 128), distinct == n_out + purged, every output key is canonical and unique."""
+    g = m.synth_genome(50_000_000, 2)
+    b, o = m.synth_reads(g, 10_000_000, 150, 2)
+    one, st = hip_table(b, o, 21)
+    assert st["occurrences"] == 10_000_000 * 128
+    check_stats(st)
+    four, st4 = hip_table(b, o, 21, batches=4)
+    assert st4["distinct"] == st["distinct"]
+    assert_tables_equal(four, one, "C2: 4 batches vs 1")
+    keys = one.sorted().keys[:, 0]
+    assert (np.diff(keys.astype(np.uint64)) > 0).all()
+    # canonical: key <= revcomp(key) on a sample
+    idx = np.random.default_rng(0).choice(len(keys), 2000, replace=False)
+    for i in idx:
+        kk = np.array([keys[i]], dtype=np.uint64)
+        rc = O.kmer_revcomp(kk, 21)
+        assert int(kk[0]) <= int(rc[0])

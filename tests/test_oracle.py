@@ -1,0 +1,178 @@
+"""Pinning the CPU oracle (runs without a GPU).
+
+  1. MurmurHash3 / quick_hash == the reference's own src/hash_funcs.c compiled unmodified (oracle/_ref);
+  2. SURVEY.md Appendix A known answers (Kmer layout, hash, minimizer, minimizer hash);
+  3. the invariants of the reference's test/kmer-test.cpp (round trip, revcomp, hash, minimizers);
+  4. the C oracle == a literal string-level restatement of the reference code (tests/ref_literal.py);
+  5. the oracle reproduces every committed golden fixture;
+  6. the record path (extract + count) == the read path (used by the multi-rank protocol tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import mhm2_proxy_amd as m
+import oracle_lib as O
+import ref_literal as R
+from common import GOLDEN, assert_tables_equal, edge_case_set, oracle_table, read_reads_file, read_table_file, synth_set
+
+# test/kmer-test.cpp:11-33 (data vectors of the reference's own unit test)
+RANDOM_READ = ("CGCTGTTCCAGATGACGAACCAGGAATTCCGCCAGGTATTCGACTTTATTCGCGAAGTCAAGAAGTTGAACGTCATCAGTGTGAACTACGGTTGCGAAGG"
+               "CTTCCTCGGCAGCTACGAGAAGGATGCACGCATCTGCCCGTTCTTCTGCCGTGCCGGCGTGAACGTGTCCTCGGTGCTTTGCGATGGCAGCATTTCGGCA"
+               "TGCCCGAGCT")
+REPEATS = ["A" * 166, "C" * 166, "G" * 166, "T" * 166, ("ACGT" * 42)[:166], ("TCGA" * 42)[:166], ("CAGT" * 42)[:166]]
+
+
+# ---- 1. reference hash_funcs.c ------------------------------------------------------------------
+
+def test_murmur_and_quick_hash_vs_reference_source():
+    ref = O.hashref()
+    if ref is None:
+        pytest.skip("oracle/_ref/libhashref.so not built (reference tree absent)")
+    rng = np.random.default_rng(0)
+    L = O.oracle()
+    for length in list(range(0, 65)) + [96, 127, 128, 255]:
+        for _ in range(20):
+            buf = rng.integers(0, 256, size=max(length, 1), dtype=np.uint8)
+            assert L.orc_murmur3_x64_64(buf.ctypes.data, length) == ref.MurmurHash3_x64_64(buf.ctypes.data, length)
+            a = np.zeros(2, np.uint64)
+            b = np.zeros(2, np.uint64)
+            seed = int(rng.integers(0, 2**32))
+            L.orc_murmur3_x64_128(buf.ctypes.data, length, seed, a.ctypes.data)
+            ref.MurmurHash3_x64_128(buf.ctypes.data, length, seed, b.ctypes.data)
+            assert (a == b).all()
+    for v in list(rng.integers(0, 2**63, size=2000, dtype=np.uint64)) + [0, 1, 2**64 - 1]:
+        assert L.orc_quick_hash(int(v)) == ref.quick_hash(int(v))
+
+
+# ---- 2. Appendix A known answers ----------------------------------------------------------------
+
+def test_appendix_a_scalars():
+    z = np.zeros(1, np.uint64)
+    assert O.oracle().orc_murmur3_x64_64(z.ctypes.data, 8) == 0x864BA144DF098483
+    assert O.oracle().orc_quick_hash(0) == 0x7B439D0C1FD00DE3
+    assert O.oracle().orc_quick_hash(1) == 0xBEA952A971BA8E83
+
+
+APPENDIX_A = [
+    # (kmer, n_longs, longs, hash, get_minimizer_fast(m, true), minimizer_hash_fast(m))
+    ("ACGTACGTACGTACGTACGTA", 1, [0x1B1B1B1B1B000000], 0xA47F0F8106BE6783, 0xB1B1B1B000000000, 0x7B9CF376CDBE4A50),
+    ("CGCTGTTCCAGATGACGAACC", 1, [0x67BD48E181400000], 0xD3C6722CA54C5474, 0xDB4DE81000000000, 0xFBEED8639C5AE34F),
+    (RANDOM_READ[:63], 2, [0x67BD48E1814A0F59, 0x4ACF61FCF660B420], 0x470509568A42D5B5, 0xCF61FCF660B42000,
+     0xAA95C0BEB14E494F),
+    (RANDOM_READ[:33], 2, [0x67BD48E1814A0F59, 0x4000000000000000], 0x44C66528D74660B1, 0xEF52386052800000,
+     0x2E3C051BDE79A656),
+    (RANDOM_READ[:99], 4, [0x67BD48E1814A0F59, 0x4ACF61FCF660B420, 0xBE06D34BB81C6BE6, 0x0800000000000000],
+     0xF9FAD81E4B9F8AF0, 0xE1BD07DF87D98000, 0x40E1DEA4B0AA5EFD),
+]
+
+
+@pytest.mark.parametrize("kmer,nl,longs,h,mini,mhash", APPENDIX_A)
+def test_appendix_a_kmers(kmer, nl, longs, h, mini, mhash):
+    k = len(kmer)
+    mlen = O.oracle().orc_minimizer_len(k)
+    la = O.kmer_from_string(kmer, nl)
+    assert [int(x) for x in la] == longs
+    assert O.kmer_hash(la) == h
+    assert O.minimizer_fast(la, k, mlen) == mini
+    assert O.minimizer_hash_fast(la, k, mlen) == mhash
+    # the package's host mirror agrees on layout and minimizer hash
+    assert list(m.kmer_from_string(kmer, nl)) == longs
+    assert m.kcount._quick_hash(m.kcount.get_minimizer_fast(longs, k, mlen)) == mhash
+
+
+# ---- 3. test/kmer-test.cpp invariants ----------------------------------------------------------
+
+def slow_revcomp(s: str) -> str:  # test/kmer-test.cpp:35-49
+    return "".join({"A": "T", "C": "G", "G": "C", "T": "A"}.get(c, "N") for c in reversed(s))
+
+
+@pytest.mark.parametrize("max_k", [32, 64])
+def test_kmer_test_invariants(max_k):
+    nl = max_k // 32
+    for k in range(1, max_k):  # the reference test runs k = 1..MAX_K-1 for MAX_K 32 and 64 (:351-373)
+        for seq in REPEATS + [RANDOM_READ]:
+            seen = {}
+            for i in range(len(seq) - k + 1):
+                sub = seq[i:i + k]
+                la = O.kmer_from_string(sub, nl)
+                assert O.kmer_to_string(la, k) == sub  # :45-68
+                rc = O.kmer_revcomp(la, k)
+                assert O.kmer_to_string(rc, k) == slow_revcomp(sub)  # :70-170
+                assert (O.kmer_revcomp(rc, k) == la).all()
+                h = O.kmer_hash(la)
+                if sub in seen:
+                    assert seen[sub] == h
+                else:
+                    assert h not in seen.values()  # :172-245 (distinct k-mers, distinct hashes here)
+                    seen[sub] = h
+                if k >= 15:  # :247-313 symmetric least-complement minimizer
+                    mm = 15
+                    assert O.minimizer_fast(la, k, mm) == O.minimizer_fast(rc, k, mm)
+
+
+# ---- 4. literal restatement ---------------------------------------------------------------------
+
+@pytest.mark.parametrize("k", [21, 33, 63, 77])
+def test_oracle_matches_literal_restatement(k):
+    b, o = synth_set(250, 4000, 300 + k)
+    lit = R.analyze_kmers([b[int(o[i]):int(o[i + 1])] for i in range(o.size - 1)], k)
+    t = oracle_table(b, o, k)
+    orc = {tuple(int(x) for x in t.keys[i]): (int(t.counts[i]), chr(t.left[i]), chr(t.right[i])) for i in range(len(t))}
+    assert orc == lit
+
+
+def test_oracle_matches_literal_edge_cases():
+    b, o = edge_case_set(seed=8, n=300)
+    for k in (21, 31):
+        lit = R.analyze_kmers([b[int(o[i]):int(o[i + 1])] for i in range(o.size - 1)], k)
+        t = oracle_table(b, o, k)
+        orc = {tuple(int(x) for x in t.keys[i]): (int(t.counts[i]), chr(t.left[i]), chr(t.right[i]))
+               for i in range(len(t))}
+        assert orc == lit
+
+
+@pytest.mark.parametrize("dmin,qcut", [(1, 20), (3, 0), (2, 31)])
+def test_oracle_matches_literal_parameters(dmin, qcut):
+    b, o = synth_set(200, 3000, 17)
+    lit = R.analyze_kmers([b[int(o[i]):int(o[i + 1])] for i in range(o.size - 1)], 21, dmin_thres=dmin,
+                          qual_cutoff=qcut)
+    t = oracle_table(b, o, 21, dmin_thres=dmin, qual_cutoff=qcut)
+    orc = {tuple(int(x) for x in t.keys[i]): (int(t.counts[i]), chr(t.left[i]), chr(t.right[i])) for i in range(len(t))}
+    assert orc == lit
+
+
+def test_dynamic_threshold_quirk():
+    """(int)((1.0 - 0.9) * count) is one less than count/10 for multiples of 10."""
+    assert int((1.0 - 0.9) * 10) == 0
+    assert sum(1 for c in range(1, 65536) if c % 10 == 0 and int((1.0 - 0.9) * c) == c // 10 - 1) == 6553
+
+
+# ---- 5. golden fixtures -------------------------------------------------------------------------
+
+@pytest.mark.parametrize("name", sorted(p.name for p in GOLDEN.glob("table_*.tsv.gz")))
+def test_oracle_reproduces_golden(name):
+    _, setname, kk = name[:-len(".tsv.gz")].split("_")
+    k = int(kk[1:])
+    b, o = read_reads_file(GOLDEN / f"reads_{setname}.txt.gz")
+    assert_tables_equal(oracle_table(b, o, k), read_table_file(GOLDEN / name, k), name)
+
+
+def test_golden_s100_literal_k21():
+    b, o = read_reads_file(GOLDEN / "reads_s100.txt.gz")
+    lit = R.analyze_kmers([b[int(o[i]):int(o[i + 1])] for i in range(o.size - 1)], 21)
+    t = read_table_file(GOLDEN / "table_s100_k21.tsv.gz", 21)
+    got = {tuple(int(x) for x in t.keys[i]): (int(t.counts[i]), chr(t.left[i]), chr(t.right[i])) for i in range(len(t))}
+    assert got == lit
+
+
+# ---- 6. record path -----------------------------------------------------------------------------
+
+@pytest.mark.parametrize("k", [21, 63])
+def test_record_path_equals_read_path(k):
+    b, o = edge_case_set(seed=12, n=600)
+    keys, exts = O.extract(b, o, k)
+    a = O.count_records(keys, exts, k)
+    ka, ca, la, ra = a.fetch()
+    assert_tables_equal(m.KmerTable(k, ka, ca, la, ra), oracle_table(b, o, k), "records vs reads")
