@@ -1,0 +1,323 @@
+// mhmkc_kcount.hpp — the reference's kcount C++ interface rebuilt over the C ABI of libmhmkc.so.
+//
+// Shapes kept from ajpowelsnl/mhm2_proxy so contigging.cpp / dbjg_traversal.cpp style callers compile
+// against the same names:
+//   Kmer<MAX_K>                      src/kmer.hpp:61-160   (longs layout, set_k/get_k, hash, revcomp, ...)
+//   KmerCounts                       src/kcount/kmer_dht.hpp:62-68
+//   KmerMap<MAX_K>                   src/kcount/kmer_dht.hpp:92-93 (std::unordered_map here; bytell is vendored
+//                                    in the reference, the container type does not affect the contents)
+//   PackedReads                      src/packed_reads.hpp:120-167 (contiguous bytes + offsets)
+//   HashTableInserter<MAX_K>         src/kcount/kmer_dht.hpp:95-116
+//   SeqBlockInserter<MAX_K>          src/kcount/kcount.hpp:57-69
+//   KmerDHT<MAX_K>                   src/kcount/kmer_dht.hpp:118-172 (one rank; UPC++ dist_object dropped)
+//   analyze_kmers<MAX_K>(...)        src/kcount/kcount.hpp:71-73
+// Errors abort with a message, as the reference's DIE does (upcxx-utils log.hpp:251).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "mhmkc.h"
+
+namespace mhm2 {
+
+using kmer_count_t = uint16_t;
+
+[[noreturn]] inline void die(const std::string &msg) {
+  std::fprintf(stderr, "mhmkc: %s\n", msg.c_str());
+  std::fflush(stderr);
+  std::abort();
+}
+
+inline void check(int rc, mhmkc_t h, const char *what) {
+  if (rc != MHMKC_OK) die(std::string(what) + ": " + mhmkc_last_error(h));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kmer<MAX_K>
+
+template <int MAX_K>
+class Kmer {
+ public:
+  static constexpr int N_LONGS = (MAX_K + 31) / 32;
+
+ private:
+  inline static unsigned k = 0;
+  std::array<uint64_t, N_LONGS> longs{};
+
+  static uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+  static uint64_t fmix(uint64_t v) {
+    v ^= v >> 33;
+    v *= 0xff51afd7ed558ccdull;
+    v ^= v >> 33;
+    v *= 0xc4ceb9fe1a85ec53ull;
+    v ^= v >> 33;
+    return v;
+  }
+
+ public:
+  Kmer() = default;
+  explicit Kmer(const uint64_t *other) { std::memcpy(longs.data(), other, sizeof longs); }
+  explicit Kmer(const char *s) { set_kmer(s); }
+
+  static void set_k(unsigned kk) { k = kk; }
+  static unsigned get_k() { return k; }
+  static unsigned get_N_LONGS() { return N_LONGS; }
+  static unsigned get_MAX_K() { return MAX_K; }
+
+  void set_kmer(const char *s) {  // src/kmer.cpp:274-296
+    longs.fill(0);
+    for (unsigned i = 0; i < k; i++) {
+      uint64_t x = ((uint64_t)s[i] & 4) >> 1;
+      longs[i / 32] |= (x + ((x ^ ((uint64_t)s[i] & 2)) >> 1)) << (2 * (31 - i % 32));
+    }
+  }
+  const uint64_t *get_longs() const { return longs.data(); }
+  bool operator<(const Kmer &o) const { return longs < o.longs; }  // word-wise unsigned (src/kmer.cpp:265-272)
+  bool operator==(const Kmer &o) const { return longs == o.longs; }
+  bool operator!=(const Kmer &o) const { return !(*this == o); }
+
+  // MurmurHash3_x64_64(longs, 8*N_LONGS) with seed 313 (src/kmer.cpp:465-468, src/hash_funcs.c:77-190)
+  uint64_t hash() const {
+    const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+    uint64_t h1 = 313, h2 = 313;
+    for (int b = 0; b < N_LONGS / 2; b++) {
+      uint64_t k1 = longs[2 * b] * c1, k2 = longs[2 * b + 1] * c2;
+      h1 ^= rotl(k1, 31) * c2;
+      h1 = rotl(h1, 27) + h2;
+      h1 = h1 * 5 + 0x52dce729;
+      h2 ^= rotl(k2, 33) * c1;
+      h2 = rotl(h2, 31) + h1;
+      h2 = h2 * 5 + 0x38495ab5;
+    }
+    if (N_LONGS & 1) h1 ^= rotl(longs[N_LONGS - 1] * c1, 31) * c2;
+    h1 ^= 8 * N_LONGS;
+    h2 ^= 8 * N_LONGS;
+    h1 += h2;
+    h2 += h1;
+    h1 = fmix(h1);
+    h2 = fmix(h2);
+    return h1 + h2;
+  }
+
+  Kmer revcomp() const {  // same result as src/kmer.cpp:485-505
+    std::string s = to_string(), r(s.rbegin(), s.rend());
+    for (char &c : r) c = c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : 'A';
+    return Kmer(r.c_str());
+  }
+
+  std::string to_string() const {  // src/kmer.cpp:595-634
+    std::string s(k, 'N');
+    for (unsigned i = 0; i < k; i++) s[i] = "ACGT"[(longs[i / 32] >> (2 * (31 - i % 32))) & 3];
+    return s;
+  }
+};
+
+template <int MAX_K>
+struct KmerHash {
+  size_t operator()(const Kmer<MAX_K> &km) const { return km.hash(); }
+};
+
+// ---------------------------------------------------------------------------------------------
+// KmerCounts / KmerMap
+
+struct KmerCounts {
+  void *uutig_frag = nullptr;  // global_ptr<FragElem> in the reference; dbjg's visited mark
+  kmer_count_t count = 0;
+  char left = 0, right = 0;
+};
+
+template <int MAX_K>
+using KmerMap = std::unordered_map<Kmer<MAX_K>, KmerCounts, KmerHash<MAX_K>>;
+
+// ---------------------------------------------------------------------------------------------
+// PackedReads (byte layout of src/packed_reads.cpp:73-109)
+
+class PackedReads {
+  std::vector<uint8_t> bytes_;
+  std::vector<uint64_t> offsets_{0};
+  int qual_offset_;
+
+ public:
+  explicit PackedReads(int qual_offset) : qual_offset_(qual_offset) {}
+  void add_read(const std::string & /*read_id*/, const std::string &seq, const std::string &quals) {
+    if (seq.size() > 65535) die("read longer than 65535");
+    for (size_t i = 0; i < seq.size(); i++) {
+      uint8_t code;
+      switch (seq[i]) {
+        case 'A': code = 0; break;
+        case 'C': code = 1; break;
+        case 'G': code = 2; break;
+        case 'T': code = 3; break;
+        case 'N': case 'U': case 'R': case 'Y': case 'K': case 'M': case 'S':
+        case 'W': case 'B': case 'D': case 'H': case 'V': code = 4; break;
+        default: die(std::string("Illegal char in comp nucleotide of '") + seq[i] + "'");
+      }
+      int q = quals[i] - qual_offset_;
+      bytes_.push_back((uint8_t)(code | ((unsigned char)(q < 31 ? q : 31) << 3)));
+    }
+    offsets_.push_back(bytes_.size());
+  }
+  int get_qual_offset() const { return qual_offset_; }
+  int64_t get_local_num_reads() const { return (int64_t)offsets_.size() - 1; }
+  const uint8_t *bytes() const { return bytes_.data(); }
+  const uint64_t *offsets() const { return offsets_.data(); }
+};
+
+struct Contig {
+  int64_t id;
+  std::string seq;
+  double depth;
+};
+using Contigs = std::vector<Contig>;
+
+// ---------------------------------------------------------------------------------------------
+// HashTableInserter / KmerDHT / SeqBlockInserter
+
+struct RankInfo {
+  int rank = 0, n_ranks = 1;
+  const uint8_t *comm_id = nullptr;
+  int device = -1;
+};
+
+template <int MAX_K>
+class HashTableInserter {
+  mhmkc_t h_ = nullptr;
+  std::string seq_buf_;
+  std::vector<uint64_t> seq_offs_{0};
+  int dmin_thres_ = 2;
+
+ public:
+  HashTableInserter() = default;
+  ~HashTableInserter() { mhmkc_destroy(h_); }
+  HashTableInserter(const HashTableInserter &) = delete;
+  HashTableInserter &operator=(const HashTableInserter &) = delete;
+
+  void set_dmin_thres(int d) { dmin_thres_ = d; }
+
+  // kcount_cpu.cpp:425-443; the estimate only sized the CPU table, the GPU path sizes itself exactly
+  void init(int /*num_elems*/, bool /*use_qf*/, const RankInfo &ri = RankInfo()) {
+    mhmkc_config cfg;
+    mhmkc_config_init(&cfg);
+    cfg.k = (int)Kmer<MAX_K>::get_k();
+    cfg.n_longs = Kmer<MAX_K>::N_LONGS;
+    cfg.dmin_thres = dmin_thres_;
+    cfg.rank = ri.rank;
+    cfg.n_ranks = ri.n_ranks;
+    cfg.comm_id = ri.comm_id;
+    cfg.device = ri.device;
+    check(mhmkc_create(&h_, &cfg), nullptr, "mhmkc_create");
+  }
+  void init_ctg_kmers(int /*max_elems*/) { die("contig k-mer pass is not supported in this version"); }
+
+  // kcount_cpu.cpp:450-463 (buffered; flushed in flush_inserts)
+  void insert_supermer(const std::string &supermer_seq, kmer_count_t count) {
+    if (count > 1) die("supermer count > 1 (contig pass) is not supported in this version");
+    seq_buf_ += supermer_seq;
+    seq_offs_.push_back(seq_buf_.size());
+  }
+  void add_packed_reads(const PackedReads &pr) {
+    check(mhmkc_add_reads(h_, pr.bytes(), pr.offsets(), (uint64_t)pr.get_local_num_reads()), h_, "mhmkc_add_reads");
+  }
+  void flush_inserts() {
+    if (seq_offs_.size() > 1) {
+      check(mhmkc_add_seqs(h_, seq_buf_.data(), seq_offs_.data(), seq_offs_.size() - 1, 1), h_, "mhmkc_add_seqs");
+      seq_buf_.clear();
+      seq_offs_.assign(1, 0);
+    }
+  }
+  // kcount_cpu.cpp:490-528
+  void insert_into_local_hashtable(KmerMap<MAX_K> &local_kmers) {
+    flush_inserts();
+    uint64_t n = 0;
+    check(mhmkc_finish(h_, &n), h_, "mhmkc_finish");
+    std::vector<uint64_t> keys(n * Kmer<MAX_K>::N_LONGS);
+    std::vector<uint16_t> counts(n);
+    std::vector<char> left(n), right(n);
+    check(mhmkc_fetch(h_, keys.data(), counts.data(), left.data(), right.data()), h_, "mhmkc_fetch");
+    local_kmers.reserve(local_kmers.size() + n);
+    for (uint64_t i = 0; i < n; i++) {
+      KmerCounts kc;
+      kc.count = counts[i];
+      kc.left = left[i];
+      kc.right = right[i];
+      local_kmers.emplace(Kmer<MAX_K>(&keys[i * Kmer<MAX_K>::N_LONGS]), kc);
+    }
+  }
+  mhmkc_stats stats() const {
+    mhmkc_stats s;
+    check(mhmkc_get_stats(h_, &s), h_, "mhmkc_get_stats");
+    return s;
+  }
+};
+
+template <int MAX_K>
+class KmerDHT {
+  KmerMap<MAX_K> local_kmers;
+  HashTableInserter<MAX_K> ht_inserter;
+  RankInfo ri;
+  int minimizer_len;
+
+ public:
+  // src/kcount/kmer_dht.cpp:106-154 (store sizes and RPC limits have no meaning without UPC++)
+  KmerDHT(uint64_t my_num_kmers, int dmin_thres = 2, const RankInfo &rank_info = RankInfo()) : ri(rank_info) {
+    minimizer_len = std::min(27, std::max(15, (int)Kmer<MAX_K>::get_k() * 2 / 3 + 1));
+    ht_inserter.set_dmin_thres(dmin_thres);
+    ht_inserter.init((int)my_num_kmers, false, ri);
+  }
+  int get_minimizer_len() const { return minimizer_len; }
+  void add_supermer(const std::string &seq, kmer_count_t count) { ht_inserter.insert_supermer(seq, count); }
+  void add_packed_reads(const PackedReads &pr) { ht_inserter.add_packed_reads(pr); }
+  void flush_updates() { ht_inserter.flush_inserts(); }
+  void finish_updates() { ht_inserter.insert_into_local_hashtable(local_kmers); }
+  KmerCounts *get_local_kmer_counts(const Kmer<MAX_K> &kmer) {
+    auto it = local_kmers.find(kmer);
+    return it == local_kmers.end() ? nullptr : &it->second;
+  }
+  int64_t get_local_num_kmers() const { return (int64_t)local_kmers.size(); }
+  typename KmerMap<MAX_K>::iterator local_kmers_begin() { return local_kmers.begin(); }
+  typename KmerMap<MAX_K>::iterator local_kmers_end() { return local_kmers.end(); }
+  HashTableInserter<MAX_K> &inserter() { return ht_inserter; }
+  // src/kcount/kmer_dht.cpp:243-266 (plain text; the reference gzips through zstr)
+  void dump_kmers(const std::string &fname) {
+    std::ofstream f(fname);
+    for (auto &e : local_kmers) f << e.first.to_string() << " " << e.second.count << " " << e.second.left << " "
+                                  << e.second.right << "\n";
+  }
+};
+
+template <int MAX_K>
+struct SeqBlockInserter {
+  SeqBlockInserter(int /*qual_offset*/, int /*minimizer_len*/) {}
+  // kcount_cpu.cpp:73-103 at one rank: the whole sequence is one supermer when it has >= k+2 bases
+  void process_seq(std::string &seq, kmer_count_t depth, KmerDHT<MAX_K> &dht) {
+    if (!depth) depth = 1;
+    if (seq.length() >= Kmer<MAX_K>::get_k() + 2) dht.add_supermer(seq, depth);
+  }
+  void done_processing(KmerDHT<MAX_K> &) {}
+};
+
+// src/kcount/kcount.hpp:71-73 / kcount.cpp:140-157
+template <int MAX_K>
+void analyze_kmers(unsigned kmer_len, unsigned /*prev_kmer_len*/, int qual_offset,
+                   std::vector<PackedReads *> &packed_reads_list, int /*dmin_thres: set on KmerDHT*/, Contigs &ctgs,
+                   KmerDHT<MAX_K> &kmer_dht, bool dump_kmers) {
+  if (kmer_len != Kmer<MAX_K>::get_k()) die("kmer_len differs from Kmer<MAX_K>::get_k()");
+  if (!ctgs.empty()) die("contig k-mer pass (add_ctg_kmers) is not supported in this version");
+  for (auto *pr : packed_reads_list) {
+    if (pr->get_qual_offset() != qual_offset) die("qual_offset mismatch");
+    kmer_dht.add_packed_reads(*pr);
+  }
+  kmer_dht.flush_updates();
+  kmer_dht.finish_updates();
+  if (dump_kmers) kmer_dht.dump_kmers("kmers-" + std::to_string(kmer_len) + ".txt");
+}
+
+}  // namespace mhm2

@@ -1,0 +1,80 @@
+// Drives the reference-shaped C++ adapter (include/mhmkc_kcount.hpp) the way contigging.cpp drives
+// analyze_kmers (src/contigging.cpp:109-119), then prints the table sorted by k-mer in dump_kmers
+// format. Modes:
+//   adapter_test kat                      Kmer<MAX_K> known answers only (no GPU)
+//   adapter_test reads <k> <seqqual.txt>  analyze_kmers over PackedReads
+//   adapter_test seqs  <k> <seqqual.txt>  SeqBlockInserter::process_seq over lowercase-masked strings
+#include <algorithm>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+
+#include "mhmkc_kcount.hpp"
+
+using namespace mhm2;
+
+template <int MAX_K>
+int run(const std::string &mode, int k, const std::string &path) {
+  Kmer<MAX_K>::set_k(k);
+  std::ifstream in(path);
+  std::string line;
+  PackedReads pr(33);
+  std::vector<std::pair<std::string, std::string>> reads;
+  while (std::getline(in, line)) {
+    std::istringstream ss(line);
+    std::string s, q;
+    ss >> s >> q;
+    pr.add_read("@r/1", s, q);
+    reads.emplace_back(s, q);
+  }
+  KmerDHT<MAX_K> dht(1000, 2);
+  Contigs ctgs;
+  if (mode == "reads") {
+    std::vector<PackedReads *> list{&pr};
+    analyze_kmers<MAX_K>(k, 0, 33, list, 2, ctgs, dht, false);
+  } else {
+    SeqBlockInserter<MAX_K> sbi(33, dht.get_minimizer_len());
+    for (auto &r : reads) {  // count_kmers: lowercase bases below the quality cutoff (kcount.cpp:80-85)
+      std::string s = r.first;
+      if (s.size() < (size_t)k) continue;
+      for (size_t i = 0; i < s.size(); i++) {
+        int q = std::min(r.second[i] - 33, 31);
+        if (q < 20) s[i] = (char)std::tolower(s[i]);
+      }
+      sbi.process_seq(s, 0, dht);
+    }
+    sbi.done_processing(dht);
+    dht.flush_updates();
+    dht.finish_updates();
+  }
+  std::vector<std::string> lines;
+  for (auto it = dht.local_kmers_begin(); it != dht.local_kmers_end(); ++it) {
+    std::ostringstream os;
+    os << it->first.to_string() << " " << it->second.count << " " << it->second.left << " " << it->second.right;
+    lines.push_back(os.str());
+  }
+  std::sort(lines.begin(), lines.end());
+  for (auto &l : lines) std::cout << l << "\n";
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  std::string mode = argc > 1 ? argv[1] : "kat";
+  if (mode == "kat") {
+    Kmer<32>::set_k(21);
+    Kmer<32> a("ACGTACGTACGTACGTACGTA");
+    Kmer<64>::set_k(63);
+    Kmer<64> b("CGCTGTTCCAGATGACGAACCAGGAATTCCGCCAGGTATTCGACTTTATTCGCGAAGTCAAGA");
+    bool ok = a.get_longs()[0] == 0x1b1b1b1b1b000000ull && a.hash() == 0xa47f0f8106be6783ull &&
+              b.get_longs()[0] == 0x67bd48e1814a0f59ull && b.get_longs()[1] == 0x4acf61fcf660b420ull &&
+              b.hash() == 0x470509568a42d5b5ull && a.revcomp().revcomp() == a &&
+              a.revcomp().to_string() == "TACGTACGTACGTACGTACGT";
+    std::cout << (ok ? "KAT OK" : "KAT FAIL") << "\n";
+    return ok ? 0 : 1;
+  }
+  int k = std::atoi(argv[2]);
+  if (k < 32) return run<32>(mode, k, argv[3]);
+  if (k < 64) return run<64>(mode, k, argv[3]);
+  if (k < 96) return run<96>(mode, k, argv[3]);
+  return run<128>(mode, k, argv[3]);
+}

@@ -1,0 +1,43 @@
+"""The reference-shaped C++ adapter (include/mhmkc_kcount.hpp) over the C ABI."""
+import gzip
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+SRC = ROOT / "tests" / "cpp" / "adapter_test.cpp"
+GOLDEN = ROOT / "tests" / "golden"
+
+
+def build(tmp: Path) -> Path:
+    if not shutil.which("g++"):
+        pytest.skip("g++ missing")
+    exe = tmp / "adapter_test"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", f"-I{ROOT / 'include'}", str(SRC),
+                    f"-L{ROOT / 'mhm2_proxy_amd'}", "-lmhmkc", f"-Wl,-rpath,{ROOT / 'mhm2_proxy_amd'}",
+                    "-o", str(exe)], check=True)
+    return exe
+
+
+def test_adapter_compiles_and_kmer_kats(tmp_path):
+    from mhm2_proxy_amd import build as b
+
+    b.build_lib()
+    exe = build(tmp_path)
+    out = subprocess.run([str(exe), "kat"], capture_output=True, text=True, env={"MHMKC_NO_TORCH": "1"})
+    assert out.stdout.strip() == "KAT OK", out.stdout + out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,k,setname", [("reads", 21, "s100"), ("reads", 63, "s100"), ("seqs", 33, "s100"),
+                                            ("reads", 21, "edge"), ("seqs", 21, "edge")])
+def test_adapter_matches_golden(mode, k, setname, tmp_path):
+    exe = build(tmp_path)
+    reads = tmp_path / "reads.txt"
+    reads.write_text(gzip.open(GOLDEN / f"reads_{setname}.txt.gz", "rt").read())
+    out = subprocess.run([str(exe), mode, str(k), str(reads)], capture_output=True, text=True, check=True)
+    got = out.stdout.splitlines()
+    exp = sorted(gzip.open(GOLDEN / f"table_{setname}_k{k}.tsv.gz", "rt").read().splitlines())
+    assert got == exp
