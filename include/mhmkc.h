@@ -79,6 +79,7 @@ typedef struct {
   uint64_t max_bucket;     /* largest fine bucket, records */
   uint64_t fine_buckets;   /* number of fine buckets on this rank */
   uint64_t bytes_sent;     /* bytes sent to other ranks in the exchange */
+  uint64_t exact_reruns;   /* capped partition passes redone with exact bucket sizes (skewed input) */
   double ms_total;         /* wall time of the last add_reads..finish sequence (device events) */
   double ms_kernel[8];     /* per-stage device time when profiling is on: see MHMKC_STAGE_* */
   uint64_t launches[8];    /* per-stage launch count when profiling is on */

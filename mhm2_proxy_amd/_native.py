@@ -8,8 +8,11 @@ from __future__ import annotations
 import ctypes as C
 from pathlib import Path
 
+import os
+
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libmhmkc.so"
+# MHMKC_LIB selects another build of the same library (performance experiments, tools/ab.sh)
+LIB_PATH = Path(os.environ["MHMKC_LIB"]) if os.environ.get("MHMKC_LIB") else PKG / "libmhmkc.so"
 SYNTH_PATH = PKG / "libmhmkc_synth.so"
 
 MHMKC_COMM_ID_BYTES = 128
@@ -67,6 +70,7 @@ class MhmkcStats(C.Structure):
         ("max_bucket", C.c_uint64),
         ("fine_buckets", C.c_uint64),
         ("bytes_sent", C.c_uint64),
+        ("exact_reruns", C.c_uint64),
         ("ms_total", C.c_double),
         ("ms_kernel", C.c_double * 8),
         ("launches", C.c_uint64 * 8),

@@ -14,21 +14,24 @@
 // Semantics follow the reference CPU kcount at one rank, cited per function.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kcount_launch.hpp"
 #include "kmer_ops.hpp"
 
 namespace mhm {
 
+#ifndef MHMKC_TILE1
+#define MHMKC_TILE1 4096
+#endif
 template <int NL>
 constexpr int kTile() {
-  return NL <= 2 ? 4096 : 2048;
+  return NL == 1 ? MHMKC_TILE1 : 2048;
 }
 template <int NL>
 constexpr int kGroups() {
   return kTile<NL>() / 32 + NL + 2;
 }
-
-constexpr size_t WSUM_BYTES = 64;  // block-scan scratch at the start of the scatter region
 
 constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -139,19 +142,21 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
           wv[i] = x;
         }
       }
+      // SWAR over 4 bytes: c = base code (A,C,G,T,N = 0..4; 5..7 bad), q = min(quality, 31).
+      // Bytes past the data are zero (code A, quality 0) and are never inside a counted window.
+      // bit 7 of each byte of q + qbias is q >= qcut (qcut clamped to [0, 32]: q <= 31)
+      const uint32_t qbias = 0x80808080u - 0x01010101u * (uint32_t)min(max(qcut, 0), 32);
       uint32_t bad = 0;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-#pragma unroll
-        for (int bj = 0; bj < 4; bj++) {
-          const int j = 4 * i + bj;
-          const uint32_t byte = (wv[i] >> (8 * bj)) & 0xffu;
-          const uint32_t c = byte & 7u, q = byte >> 3;
-          const uint32_t code = (c == 4u) ? 2u : (c & 3u);
-          bad |= (c > 4u) & ((uint64_t)j < rem);
-          f |= (uint64_t)code << (62 - 2 * j);
-          gd |= (uint32_t)((q >= (uint32_t)qcut) & (c < 4u)) << (31 - j);
-        }
+        const uint32_t c = wv[i] & 0x07070707u, q = (wv[i] >> 3) & 0x1f1f1f1fu;
+        const uint32_t t = (c & 0x03030303u) | ((c >> 1) & 0x02020202u);  // N (4) -> G (2)
+        const uint32_t ok = (~c >> 2) & ((q + qbias) >> 7) & 0x01010101u;  // code < 4 && q >= qcut
+        bad |= (c + 0x03030303u) & 0x08080808u;                            // code > 4
+        const uint32_t t8 = ((t & 3u) << 6) | ((t >> 4) & 0x30u) | ((t >> 14) & 0x0cu) | ((t >> 24) & 3u);
+        const uint32_t g4 = ((ok & 1u) << 3) | ((ok >> 6) & 4u) | ((ok >> 15) & 2u) | ((ok >> 24) & 1u);
+        f |= (uint64_t)t8 << (56 - 8 * i);
+        gd |= g4 << (28 - 4 * i);
       }
       if (bad) atomicOr(err, 1u);
     }
@@ -172,63 +177,107 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
   __syncthreads();
 }
 
-// Build the record of the window starting at global base p (tile-local position lp).
-// Valid iff the window and both neighbours lie in one read: the interior windows i in [1, L-k-1]
+// First read start at or after tile-local position q (LARGE when none in the staged groups).
+template <int NL>
+__device__ __forceinline__ int next_start(const uint32_t *start, int q) {
+  constexpr int NG = kGroups<NL>();
+  int g = q >> 5;
+  uint32_t m = start[g] & (~0u >> (q & 31));
+  while (m == 0) {
+    if (++g >= NG) return 1 << 30;
+    m = start[g];
+  }
+  return g * 32 + __clz(m);
+}
+
+// Walk the W consecutive windows of this thread (tile positions W*tid .. W*tid + W-1), rolling the
+// forward and reverse-complement words by one base per window instead of re-extracting them.
+// A window is counted iff it and both neighbours lie in one read: the interior windows i in [1, L-k-1]
 // of get_kmers_and_exts (src/kcount/kcount_cpu.cpp:316-334); at one rank the supermer is the read
 // (kcount_cpu.cpp:84-101). Canonical = min(fwd, revcomp) (kcount_cpu.cpp:326-332);
 // extensions are the neighbour bases, '0' (none) when low quality, complemented and swapped when the
 // reverse complement is used (comp_nucleotide, src/utils.cpp:121-143).
-template <int NL>
-__device__ __forceinline__ bool make_record(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
-                                            int lp, uint64_t p, uint64_t n_bases, int k, uint64_t *key,
-                                            uint32_t &e) {
-  if (p + (uint64_t)k >= n_bases) return false;
+//
+// Branch-free: the incoming bases, their quality bits and the read starts of the thread's span are
+// funnel-loaded into registers once, so the fully unrolled loop is straight-line ALU work with
+// constant shifts. Window p (tile position) is valid iff the last read start at or before p + k
+// (tracked in `last`) is before p, and p + k is inside the data. emit(i, key, ext, valid) is called for
+// every window; key/ext are meaningless when !valid.
+template <int NL, typename Emit>
+__device__ __forceinline__ void walk_windows(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
+                                             uint32_t tile, uint64_t n_bases, int k, Emit &&emit) {
+  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+  static_assert(W <= 32, "one 32-bit mask per thread span");
+  const int klast = k - 32 * (NL - 1);
+  const uint64_t tmask = top_mask(klast);
+  const int lp0 = 32 + W * (int)threadIdx.x;
+  auto codes64 = [&](int q) {  // the 32 codes from tile position q, first in the top bits
+    const int g = q >> 5, sh = (q & 31) * 2;
+    uint64_t v = fwd[g];
+    if (sh) v = (v << sh) | (fwd[g + 1] >> (64 - sh));
+    return v;
+  };
+  auto bits32 = [&](const uint32_t *a, int q) {  // the 32 bits from tile position q, first in bit 31
+    const int g = q >> 5, sh = q & 31;
+    uint32_t v = a[g];
+    if (sh) v = (v << sh) | (a[g + 1] >> (32 - sh));
+    return v;
+  };
+  uint64_t fw[NL], rc[NL];
+#pragma unroll
+  for (int m = 0; m < NL; m++) fw[m] = codes64(lp0 + 32 * m);
+  fw[NL - 1] &= tmask;
+  revcomp<NL>(fw, rc, k);
+  const uint64_t incoming = codes64(lp0 + k);         // base entering at window i: lp0 + k + i
+  const uint32_t gl_bits = bits32(good, lp0 - 1);      // left neighbour of window i: lp0 - 1 + i
+  const uint32_t gr_bits = bits32(good, lp0 + k);      // right neighbour: lp0 + k + i
+  const uint32_t st_bits = bits32(start, lp0 + k);     // read starts at lp0 + k + i
+  // last read start in [lp0, lp0 + k - 1] (at most 5 groups), else lp0 - 1
+  int last = lp0 - 1;
   {
-    const int a = lp, b = lp + k;
-    const int ga = a >> 5, gb = b >> 5;
-    for (int g = ga; g <= gb; g++) {
-      uint32_t m = ~0u;
-      if (g == ga) m &= ~0u >> (a & 31);
-      if (g == gb) m &= ~0u << (31 - (b & 31));
-      if (start[g] & m) return false;
+    const int q0 = lp0, q1 = lp0 + k - 1;
+    for (int g = q1 >> 5; g >= (q0 >> 5); g--) {
+      uint32_t m = start[g];
+      const int lo = max(q0, g * 32), hi = min(q1, g * 32 + 31);
+      m &= (~0u >> (lo - g * 32)) & (~0u << (31 - (hi - g * 32)));
+      if (m) {
+        last = g * 32 + 31 - (__ffs(m) - 1);
+        break;
+      }
     }
   }
-  uint64_t fw[NL];
+  // data end in tile positions: window p needs p + k < end (p + k is the right neighbour)
+  const int64_t end64 = (int64_t)n_bases - ((int64_t)tile * T - 32);
+  const int end = end64 > (int64_t)(1 << 30) ? (1 << 30) : (int)end64;
+  uint32_t cl = (uint32_t)(codes64(lp0 - 1) >> 62);
 #pragma unroll
-  for (int m = 0; m < NL; m++) {
-    const int pos = lp + 32 * m;
-    const int g = pos >> 5, s = (pos & 31) * 2;
-    uint64_t v = fwd[g];
-    if (s) v = (v << s) | (fwd[g + 1] >> (64 - s));
-    fw[m] = v;
-  }
-  fw[NL - 1] &= top_mask(k - 32 * (NL - 1));
-  uint64_t rc[NL];
-  revcomp<NL>(fw, rc, k);
-  int l, r;
-  {
-    const int q = lp - 1, g = q >> 5, j = q & 31;
-    const int code = (int)((fwd[g] >> (62 - 2 * j)) & 3u);
-    l = ((good[g] >> (31 - j)) & 1u) ? code : EXT_NONE;
-  }
-  {
-    const int q = lp + k, g = q >> 5, j = q & 31;
-    const int code = (int)((fwd[g] >> (62 - 2 * j)) & 3u);
-    r = ((good[g] >> (31 - j)) & 1u) ? code : EXT_NONE;
-  }
-  if (kmer_less<NL>(rc, fw)) {
+  for (int i = 0; i < W; i++) {
+    const int lp = lp0 + i;
+    const uint32_t cr = (uint32_t)(incoming >> (62 - 2 * i)) & 3u;
+    const uint32_t gl = (gl_bits >> (31 - i)) & 1u, gr = (gr_bits >> (31 - i)) & 1u;
+    if ((st_bits >> (31 - i)) & 1u) last = lp + k;
+    const bool valid = (last < lp) && (lp + k < end);
+    int l = gl ? (int)cl : EXT_NONE, r = gr ? (int)cr : EXT_NONE;
+    const bool use_rc = kmer_less<NL>(rc, fw);
+    uint64_t key[NL];
 #pragma unroll
-    for (int m = 0; m < NL; m++) key[m] = rc[m];
-    const int nl_ = (r == EXT_NONE) ? EXT_NONE : 3 - r;
-    const int nr_ = (l == EXT_NONE) ? EXT_NONE : 3 - l;
-    l = nl_;
-    r = nr_;
-  } else {
+    for (int m = 0; m < NL; m++) key[m] = use_rc ? rc[m] : fw[m];
+    const int lr = (r == EXT_NONE) ? EXT_NONE : 3 - r, rr = (l == EXT_NONE) ? EXT_NONE : 3 - l;
+    if (use_rc) {
+      l = lr;
+      r = rr;
+    }
+    emit(i, key, (uint32_t)((l << 3) | r), valid);
+    // roll to the next window: base lp leaves, base lp + k (cr) enters
+    cl = (uint32_t)(fw[0] >> 62);
 #pragma unroll
-    for (int m = 0; m < NL; m++) key[m] = fw[m];
+    for (int m = 0; m < NL - 1; m++) fw[m] = (fw[m] << 2) | (fw[m + 1] >> 62);
+    fw[NL - 1] = (fw[NL - 1] << 2) | ((uint64_t)cr << (64 - 2 * klast));
+#pragma unroll
+    for (int m = NL - 1; m > 0; m--) rc[m] = (rc[m] >> 2) | (rc[m - 1] << 62);
+    rc[0] = (rc[0] >> 2) | ((uint64_t)(3u - cr) << 62);
+    rc[NL - 1] &= tmask;
   }
-  e = (uint32_t)((l << 3) | r);
-  return true;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -264,18 +313,10 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
   for (uint32_t b = threadIdx.x; b < p.n_bins; b += E_THREADS) hist[b] = 0;
   const uint32_t tile = blockIdx.x;
   load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
-  const uint64_t p0 = (uint64_t)tile * T;
   const int sh = 64 - p.coarse_bits;
-#pragma unroll 2
-  for (int j = 0; j < W; j++) {
-    const int lt = threadIdx.x + j * E_THREADS;
-    uint64_t key[NL];
-    uint32_t e;
-    if (make_record<NL>(fwd, good, start, lt + 32, p0 + lt, p.reads.n_bases, p.k, key, e)) {
-      const uint64_t h = murmur3_h1<NL>(key);
-      atomicAdd(&hist[(uint32_t)(h >> sh)], 1u);
-    }
-  }
+  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.k, [&](int, const uint64_t *key, uint32_t, bool valid) {
+    if (valid) atomicAdd(&hist[(uint32_t)(part_hash<NL>(key) >> sh)], 1u);
+  });
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < p.n_bins; b += E_THREADS) {
     const uint32_t c = hist[b];
@@ -284,80 +325,132 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// LDS-staged scatter shared by extract_scatter and part_scatter.
-// Records are first staged in arrival order (raw[w][i], inf[i] = valid<<31 | e<<16 | digit), then
-// ranked per bin through a permutation so that each bin's run is written with consecutive lanes.
-// Dynamic LDS layout of the scatter region (all offsets multiples of 16):
-//   wsum[16] u32 | lcnt[nb] u32 | lpre[nb] u32 | goff[nb] u64 | raw[NL][T] u64 | inf[T] u32 | perm[T] u16
-template <int NL>
-struct ScatterLds {
-  uint32_t *wsum, *lcnt, *lpre;
-  unsigned long long *goff;
-  uint64_t *raw;
-  uint32_t *inf;
-  uint16_t *perm;
+// Register-resident scatter shared by extract_scatter and part_scatter.
+// Each thread holds its W records (rk, inf = valid<<31 | e<<16 | bin). LDS only holds per-bin counters:
+// a returning LDS atomic ranks every record inside its bin, one global atomic per non-empty bin reserves
+// the workgroup's run, and every lane stores its own records. The stores of one bin land in the same
+// segment, which is written by blocks of one XCD only (E_NSUB segments per coarse bucket, fine buckets
+// per coarse bucket), so partial lines merge in that XCD's L2 before they reach HBM.
+// LDS: lcnt[nb] u32 | pad to 16 B | goff[nb] u64.
+
+// Bin limits of capped layouts: bin b may use [.., lim.base + b * lim.stride + lim.cap); lim.cap == 0: none.
+struct BinLimit {
+  uint64_t base, stride, cap;
+  __device__ __forceinline__ uint64_t end(uint32_t b) const { return base + (uint64_t)b * stride + cap; }
 };
 
-template <int NL>
-__device__ __forceinline__ ScatterLds<NL> carve_scatter(unsigned char *smem, uint32_t nb) {
-  constexpr int T = kTile<NL>();
-  ScatterLds<NL> s;
-  s.wsum = (uint32_t *)smem;
-  s.lcnt = (uint32_t *)(smem + WSUM_BYTES);
-  s.lpre = s.lcnt + nb;
-  s.goff = (unsigned long long *)(s.lpre + nb);
-  s.raw = (uint64_t *)(s.goff + nb);
-  s.inf = (uint32_t *)(s.raw + NL * T);
-  s.perm = (uint16_t *)(s.inf + T);
-  return s;
+__host__ __device__ constexpr size_t scatter_cnt_bytes(uint32_t nb) { return ((size_t)nb * 4 + 15) & ~(size_t)15; }
+__host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t nb) { return scatter_cnt_bytes(nb) + (size_t)nb * 8; }
+
+__device__ __forceinline__ void scatter_clear(uint32_t *lcnt, uint32_t nb) {
+  for (uint32_t b = threadIdx.x; b < nb; b += E_THREADS) lcnt[b] = 0;
 }
 
-// bins are powers of two >= 256, so every carve offset stays a multiple of 16
-template <int NL>
-__host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t nb) {
-  return WSUM_BYTES + (size_t)nb * 4 * 2 + (size_t)nb * 8 + (size_t)NL * kTile<NL>() * 8 + (size_t)kTile<NL>() * 4 +
-         (size_t)kTile<NL>() * 2;
-}
-
-template <int NL>
-__device__ __forceinline__ void scatter_clear(const ScatterLds<NL> &s, uint32_t nb) {
-  for (uint32_t b = threadIdx.x; b < nb; b += E_THREADS) s.lcnt[b] = 0;
-}
-
-// Called after every thread has written its raw/inf entries and counted them into lcnt.
-template <int NL, bool PACKED>
-__device__ void scatter_from_raw(const ScatterLds<NL> &s, uint32_t nb, unsigned long long *cursor, const PlaneSet &out) {
-  constexpr int T = kTile<NL>(), W = T / E_THREADS;
-  const int tid = threadIdx.x;
+// Bin b's cursor is cursor[b * cstride]. In a capped layout a bin that would overflow sets err bit 1
+// and its excess records are not written (the host then redoes the pass with exact bin sizes).
+// Called after lcnt has been cleared and a barrier.
+template <int NL, bool PACKED, int W>
+__device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
+                                             unsigned char *smem, unsigned long long *cursor, uint32_t cstride,
+                                             const PlaneSet &out, const BinLimit lim, unsigned int *err) {
+  uint32_t *lcnt = (uint32_t *)smem;
+  unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
+  uint32_t rank[W];
+#pragma unroll
+  for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
   __syncthreads();
-  for (uint32_t b = tid; b < nb; b += E_THREADS) {
-    const uint32_t c = s.lcnt[b];
-    s.goff[b] = c ? atomicAdd(&cursor[b], (unsigned long long)c) : 0ull;
-    s.lpre[b] = c;
+  for (uint32_t b = threadIdx.x; b < nb; b += E_THREADS) {
+    const uint32_t c = lcnt[b];
+    const unsigned long long off = c ? atomicAdd(&cursor[(uint64_t)b * cstride], (unsigned long long)c) : 0ull;
+    if (lim.cap && c && off + c > lim.end(b)) atomicOr(err, 2u);
+    goff[b] = off;
   }
   __syncthreads();
-  const uint32_t total = block_excl_scan<E_THREADS>(s.lpre, (int)nb, s.wsum);
-  for (uint32_t b = tid; b < nb; b += E_THREADS) s.lcnt[b] = 0;
-  __syncthreads();
+#pragma unroll
   for (int j = 0; j < W; j++) {
-    const int i = tid + j * E_THREADS;
-    const uint32_t inf = s.inf[i];
-    if (inf >> 31) {
-      const uint32_t d = inf & 0xffffu;
-      s.perm[s.lpre[d] + atomicAdd(&s.lcnt[d], 1u)] = (uint16_t)i;
+    if (inf[j] >> 31) {
+      const uint32_t d = inf[j] & 0xffffu;
+      const unsigned long long dst = goff[d] + rank[j];
+      if (lim.cap && dst >= lim.end(d)) continue;
+#pragma unroll
+      for (int w = 0; w < NL; w++) out.w[w][dst] = rk[j][w];
+      if (!PACKED) out.ext[dst] = (uint8_t)((inf[j] >> 16) & 63u);
+    }
+  }
+}
+
+// Staged variant: the records are first written to LDS in bin order, then copied out so that consecutive
+// lanes store consecutive addresses of one bin (runs of ~T/nb records instead of one line per lane).
+// LDS: counters [lcnt | goff | lstart | wsum] then the stage area [NL][T] u64 | sbin[T] u16 | sext[T] u8,
+// which may alias the tile (the first barrier below is after every thread's walk).
+__host__ __device__ constexpr size_t staged_cnt_bytes(uint32_t nb) {
+  return scatter_lds_bytes(nb) + (((size_t)nb * 4 + 15) & ~(size_t)15) + 32;
+}
+__host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packed) {
+  return (size_t)nl * T * 8 + (size_t)T * 2 + (packed ? 0 : (size_t)T);
+}
+
+template <int NL, bool PACKED, int W>
+__device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
+                                               unsigned char *smem, unsigned char *area,
+                                               unsigned long long *cursor, uint32_t cstride, const PlaneSet &out,
+                                               const BinLimit lim, unsigned int *err) {
+  constexpr int T = W * E_THREADS;
+  uint32_t *lcnt = (uint32_t *)smem;
+  unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
+  uint32_t *lstart = (uint32_t *)(smem + scatter_lds_bytes(nb));
+  uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - 32);
+  uint64_t *stage = (uint64_t *)area;
+  uint16_t *sbin = (uint16_t *)(stage + NL * T);
+  uint8_t *sext = (uint8_t *)(sbin + T);
+  uint32_t rank[W];
+#pragma unroll
+  for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += E_THREADS) {
+    const uint32_t c = lcnt[b];
+    const unsigned long long off = c ? atomicAdd(&cursor[(uint64_t)b * cstride], (unsigned long long)c) : 0ull;
+    if (lim.cap && c && off + c > lim.end(b)) atomicOr(err, 2u);
+    goff[b] = off;
+    lstart[b] = c;
+  }
+  __syncthreads();
+  const uint32_t total = block_excl_scan<E_THREADS>(lstart, (int)nb, wsum);
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    if (inf[j] >> 31) {
+      const uint32_t d = inf[j] & 0xffffu;
+      const uint32_t pos = lstart[d] + rank[j];
+#pragma unroll
+      for (int w = 0; w < NL; w++) stage[w * T + pos] = rk[j][w];
+      sbin[pos] = (uint16_t)d;
+      if (!PACKED) sext[pos] = (uint8_t)((inf[j] >> 16) & 63u);
     }
   }
   __syncthreads();
-  for (uint32_t i = tid; i < total; i += E_THREADS) {
-    const uint32_t src = s.perm[i];
-    const uint32_t inf = s.inf[src];
-    const uint32_t d = inf & 0xffffu;
-    const unsigned long long dst = s.goff[d] + (i - s.lpre[d]);
 #pragma unroll
-    for (int w = 0; w < NL; w++) out.w[w][dst] = s.raw[w * T + src];
-    if (!PACKED) out.ext[dst] = (uint8_t)((inf >> 16) & 63u);
+  for (int j = 0; j < W; j++) {
+    const uint32_t pos = threadIdx.x + j * E_THREADS;
+    if (pos < total) {
+      const uint32_t d = sbin[pos];
+      const unsigned long long dst = goff[d] + (pos - lstart[d]);
+      if (lim.cap && dst >= lim.end(d)) continue;
+#pragma unroll
+      for (int w = 0; w < NL; w++) out.w[w][dst] = stage[w * T + pos];
+      if (!PACKED) out.ext[dst] = sext[pos];
+    }
   }
 }
+
+#ifndef MHMKC_ESTAGE
+#define MHMKC_ESTAGE 1
+#endif
+constexpr bool kEStaged = MHMKC_ESTAGE != 0;
+
+#ifndef MHMKC_PSTAGE
+#define MHMKC_PSTAGE 1
+#endif
+constexpr bool kPStaged = MHMKC_PSTAGE != 0;
 
 // ------------------------------------------------------------------------------------------------
 // extract: scatter into coarse buckets
@@ -368,48 +461,82 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   extern __shared__ __align__(16) unsigned char smem0[];
   uint64_t *fwd;
   uint32_t *good, *start;
-  const ScatterLds<NL> s = carve_scatter<NL>(carve_tile<NL>(smem0, fwd, good, start), p.n_bins);
-  scatter_clear<NL>(s, p.n_bins);
+  unsigned char *smem, *area;
+  if (kEStaged) {  // counters first, then the tile aliased by the stage area
+    smem = smem0;
+    area = smem0 + staged_cnt_bytes(p.n_bins);
+    carve_tile<NL>(area, fwd, good, start);
+  } else {
+    smem = carve_tile<NL>(smem0, fwd, good, start);
+    area = nullptr;
+  }
+  scatter_clear((uint32_t *)smem, p.n_bins);
   const uint32_t tile = blockIdx.x;
   load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
-  const uint64_t p0 = (uint64_t)tile * T;
   const int sh = 64 - p.coarse_bits;
-  for (int j = 0; j < W; j++) {
-    const int lt = threadIdx.x + j * E_THREADS;
-    uint64_t key[NL];
-    uint32_t e = 0, inf = 0;
-    if (make_record<NL>(fwd, good, start, lt + 32, p0 + lt, p.reads.n_bases, p.k, key, e)) {
-      const uint32_t d = (uint32_t)(murmur3_h1<NL>(key) >> sh);
-      if (PACKED) key[NL - 1] |= e;
+  // stored hash bits, branch-free (hbits == 0: none)
+  const int hsh = p.hbits ? 64 - p.hbits : 0;
+  const uint64_t hmask = p.hbits ? ~0ull : 0ull;
+  uint64_t rk[W][NL];
+  uint32_t inf[W];
+  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.k,
+                   [&](int i, const uint64_t *key, uint32_t e, bool valid) {
+                     const uint64_t h = part_hash<NL>(key);
 #pragma unroll
-      for (int w = 0; w < NL; w++) s.raw[w * T + lt] = key[w];
-      inf = (1u << 31) | (e << 16) | d;
-      atomicAdd(&s.lcnt[d], 1u);
-    }
-    s.inf[lt] = inf;
-  }
-  scatter_from_raw<NL, PACKED>(s, p.n_bins, p.cursor, p.out);
+                     for (int w = 0; w < NL; w++) rk[i][w] = key[w];
+                     if (PACKED) {
+                       rk[i][NL - 1] |= e;
+                       rk[i][NL - 1] |= (((h << p.coarse_bits) >> hsh) & hmask) << EXT_BITS;
+                     }
+                     inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(h >> sh) : 0u;
+                     // materialise the record now: otherwise its inputs (key, e, h) are sunk into the
+                     // scatter's conditional store and stay live across its barriers (~7 VGPRs/window)
+#pragma unroll
+                     for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[i][w]));
+                     asm volatile("" : "+v"(inf[i]));
+                   });
+  const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
+  const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
+  if (kEStaged)
+    scatter_staged<NL, PACKED, W>(rk, inf, p.n_bins, smem, area, p.cursor + sub * CPAD, E_NSUB * CPAD, p.out, lim,
+                                  p.err);
+  else
+    scatter_regs<NL, PACKED, W>(rk, inf, p.n_bins, smem, p.cursor + sub * CPAD, E_NSUB * CPAD, p.out, lim, p.err);
 }
 
 // ------------------------------------------------------------------------------------------------
 // partition coarse -> fine
 
-// Load one record of a chunk and compute its fine digit (hash recomputed from the key).
+// Fine digit of a record: from the hash bits stored next to the ext code when there are enough of them,
+// otherwise by recomputing MurmurHash3 of the key. rk holds the raw record words.
 template <int NL, bool PACKED>
-__device__ __forceinline__ uint32_t chunk_record(const PlaneSet &src, uint64_t idx, int shf, uint64_t fmask,
-                                                 uint64_t *rk, uint32_t &e) {
-#pragma unroll
-  for (int w = 0; w < NL; w++) rk[w] = src.w[w][idx];
+__device__ __forceinline__ uint32_t fine_digit(const uint64_t *rk, const PartitionParams &p) {
+  const uint64_t fmask = (1ull << p.fine_bits) - 1;
+  if (PACKED && p.hbits >= p.fine_bits) {
+    const uint64_t stored = (rk[NL - 1] >> EXT_BITS) & ((1ull << p.hbits) - 1);
+    return (uint32_t)((stored >> (p.hbits - p.fine_bits)) & fmask);
+  }
   uint64_t key[NL];
 #pragma unroll
   for (int w = 0; w < NL; w++) key[w] = rk[w];
-  if (PACKED) {
-    e = (uint32_t)(key[NL - 1] & 63u);
-    key[NL - 1] &= ~63ull;
-  } else {
-    e = src.ext[idx];
+  if (PACKED) key[NL - 1] &= ~((1ull << (EXT_BITS + p.hbits)) - 1);
+  return (uint32_t)((part_hash<NL>(key) >> (64 - p.coarse_bits - p.fine_bits)) & fmask);
+}
+
+// All W records of a thread are loaded before any is processed (W * 8 B * NL in flight per lane).
+template <int NL, bool PACKED, int W>
+__device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch, uint64_t (&rk)[W][NL],
+                                           uint32_t (&re)[W]) {
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const uint32_t i = threadIdx.x + j * E_THREADS;
+    re[j] = 0;
+    if (i < ch.count) {
+#pragma unroll
+      for (int w = 0; w < NL; w++) rk[j][w] = src.w[w][ch.start + i];
+      re[j] = PACKED ? (uint32_t)(rk[j][NL - 1] & 63u) : src.ext[ch.start + i];
+    }
   }
-  return (uint32_t)((murmur3_h1<NL>(key) >> shf) & fmask);
 }
 
 template <int NL, bool PACKED>
@@ -420,17 +547,13 @@ __global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
   for (uint32_t b = threadIdx.x; b < nf; b += E_THREADS) hist[b] = 0;
   const SChunk ch = p.chunks[blockIdx.x];
   const PlaneSet src = p.srcs[ch.src];
-  const int shf = 64 - p.coarse_bits - p.fine_bits;
-  const uint64_t fmask = nf - 1;
+  uint64_t rk[W][NL];
+  uint32_t re[W];
+  load_chunk<NL, PACKED, W>(src, ch, rk, re);
   __syncthreads();
-#pragma unroll 4
+#pragma unroll
   for (int j = 0; j < W; j++) {
-    const uint32_t i = threadIdx.x + j * E_THREADS;
-    if (i < ch.count) {
-      uint64_t rk[NL];
-      uint32_t e;
-      atomicAdd(&hist[chunk_record<NL, PACKED>(src, ch.start + i, shf, fmask, rk, e)], 1u);
-    }
+    if (threadIdx.x + j * E_THREADS < ch.count) atomicAdd(&hist[fine_digit<NL, PACKED>(rk[j], p)], 1u);
   }
   __syncthreads();
   unsigned long long *g = p.fine_hist + (uint64_t)ch.coarse_local * nf;
@@ -445,29 +568,50 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t nf = 1u << p.fine_bits;
-  const ScatterLds<NL> s = carve_scatter<NL>(smem, nf);
-  scatter_clear<NL>(s, nf);
+  scatter_clear((uint32_t *)smem, nf);
   const SChunk ch = p.chunks[blockIdx.x];
   const PlaneSet src = p.srcs[ch.src];
-  const int shf = 64 - p.coarse_bits - p.fine_bits;
-  const uint64_t fmask = nf - 1;
-  __syncthreads();
-#pragma unroll 4
-  for (int j = 0; j < W; j++) {
-    const uint32_t i = threadIdx.x + j * E_THREADS;
-    uint32_t inf = 0;
-    if (i < ch.count) {
-      uint64_t rk[NL];
-      uint32_t e;
-      const uint32_t d = chunk_record<NL, PACKED>(src, ch.start + i, shf, fmask, rk, e);
+  uint64_t rk[W][NL];
+  uint32_t re[W], inf[W];
+  load_chunk<NL, PACKED, W>(src, ch, rk, re);
 #pragma unroll
-      for (int w = 0; w < NL; w++) s.raw[w * T + i] = rk[w];
-      inf = (1u << 31) | (e << 16) | d;
-      atomicAdd(&s.lcnt[d], 1u);
-    }
-    s.inf[i] = inf;
+  for (int j = 0; j < W; j++) {
+    inf[j] = (threadIdx.x + j * E_THREADS < ch.count) ? ((1u << 31) | (re[j] << 16) | fine_digit<NL, PACKED>(rk[j], p))
+                                                       : 0u;
   }
-  scatter_from_raw<NL, PACKED>(s, nf, p.fine_cursor + (uint64_t)ch.coarse_local * nf, p.out);
+  __syncthreads();
+  BinLimit lim{0, 0, 0};
+  if (p.coarse_fcap) {
+    const uint64_t fc = p.coarse_fcap[ch.coarse_local];
+    lim = BinLimit{p.coarse_base[ch.coarse_local], fc, fc};
+  }
+  unsigned long long *cur = p.fine_cursor + (uint64_t)ch.coarse_local * nf;
+  if (kPStaged)
+    scatter_staged<NL, PACKED, W>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
+  else
+    scatter_regs<NL, PACKED, W>(rk, inf, nf, smem, cur, 1, p.out, lim, p.err);
+}
+
+// capped fine layout
+__global__ void k_init_fine(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap, uint32_t n_coarse,
+                            int fine_bits, unsigned long long *base, unsigned long long *cursor) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ((uint64_t)n_coarse << fine_bits)) return;
+  const uint64_t c = i >> fine_bits, d = i & ((1ull << fine_bits) - 1);
+  const unsigned long long b = coarse_base[c] + d * coarse_fcap[c];
+  base[i] = b;
+  cursor[i] = b;
+}
+
+// sum over reads of max(0, L - k - 1): the counted windows of a batch
+__global__ __launch_bounds__(256) void k_count_windows(ReadsView rv, int k, unsigned long long *out) {
+  unsigned long long acc = 0;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads; r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t L = rv.offs[r + 1] - rv.offs[r];
+    if (L > (uint64_t)k + 1) acc += L - k - 1;
+  }
+  acc = wave_sum_u64(acc);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -509,11 +653,28 @@ __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, uns
 // ------------------------------------------------------------------------------------------------
 // count: LDS open-addressing hash table per fine bucket
 
+// Records per thread per round of k_count (register budget: 1024 threads -> <= 128 VGPRs).
+template <int NL>
+constexpr int count_rpt() {
+  return NL == 1 ? 4 : 2;
+}
+
+// LDS slot hash of k_count. All keys of a fine bucket share their top MurmurHash3 bits, so the slot
+// uses an independent multiplicative mix of the key words (performance only; any function is correct).
+template <int NL>
+__device__ __forceinline__ uint32_t slot_hash(const uint64_t *key) {
+  uint64_t h = key[0] * 0x9E3779B97F4A7C15ull;
+#pragma unroll
+  for (int w = 1; w < NL; w++) h = (h ^ (h >> 31) ^ key[w]) * 0xC2B2AE3D27D4EB4Full;
+  h ^= h >> 29;
+  return (uint32_t)(h >> 32);
+}
+
 struct CountLds {
   uint64_t *keys;  // [NL][cap]
   uint32_t *cnt;   // [cap]
   uint32_t *ext;   // [4][cap]: (A|C<<16, G|T<<16) left, then right
-  int cap;
+  int cap;         // multiple of 4: slots are probed in groups of 4
 };
 
 __device__ __forceinline__ bool reserve_slot(int *s_res, int *s_closed, int limit) {
@@ -526,55 +687,88 @@ __device__ __forceinline__ bool reserve_slot(int *s_res, int *s_closed, int limi
   return true;
 }
 
-// Returns the slot holding key (inserting it if allowed), -1 when the table is closed and the key
-// is absent, -2 on an internal bound violation.
+// The last key words of one 4-slot group (two ds_read_b128; the group is 32-byte aligned).
+__device__ __forceinline__ void read_group(const uint64_t *last, int g, uint64_t (&v)[4]) {
+  const ulonglong2 *q = (const ulonglong2 *)(last + 4 * g);
+  const ulonglong2 a = q[0], b = q[1];
+  v[0] = a.x, v[1] = a.y, v[2] = b.x, v[3] = b.y;
+}
+
 template <int NL>
-__device__ int lds_insert_or_find(const CountLds &t, const uint64_t *key, int slot, int *s_res, int *s_closed,
+__device__ __forceinline__ bool rest_equal(const CountLds &t, int slot, const uint64_t *key) {
+  bool eq = true;
+#pragma unroll
+  for (int w = 0; w < NL - 1; w++) eq &= (t.keys[w * t.cap + slot] == key[w]);
+  return eq;
+}
+
+// Grouped linear probing: a lane reads 4 slots at a time, so the loop a wave runs is bounded by the
+// longest probe of its 64 lanes counted in groups (one group nearly always), not in single slots.
+// Invariant: a key lies in group g' > g only if g had no empty slot when it was inserted; slots never
+// empty again, so an empty slot in g proves the key is absent from later groups.
+// Returns the slot holding key (inserting it if allowed), -1 when the table is closed and the key is
+// absent, -2 on an internal bound violation.
+template <int NL>
+__device__ int lds_insert_or_find(const CountLds &t, const uint64_t *key, int g, int *s_res, int *s_closed,
                                   int limit) {
   uint64_t *last = t.keys + (NL - 1) * t.cap;
+  const int ng = t.cap >> 2;
+  const uint64_t kl = key[NL - 1];
   for (int iter = 0; iter < (1 << 22); iter++) {
-    const uint64_t cur = __hip_atomic_load(&last[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (cur == KEY_EMPTY) {
+    uint64_t v[4];
+    read_group(last, g, v);
+    int empty = -1;
+    bool busy = false, found = false;
+    int slot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (!found && v[i] == kl && (NL == 1 || rest_equal<NL>(t, 4 * g + i, key))) {
+        found = true;
+        slot = 4 * g + i;
+      }
+      if (v[i] == KEY_EMPTY && empty < 0) empty = i;
+      if (NL > 1 && v[i] == KEY_BUSY) busy = true;
+    }
+    if (found) return slot;
+    if (busy) continue;  // a writer publishes within its own iteration
+    if (empty >= 0) {
       if (!reserve_slot(s_res, s_closed, limit)) return -1;
-      const uint64_t want = (NL == 1) ? key[0] : KEY_BUSY;
-      const uint64_t old = atomicCAS((unsigned long long *)&last[slot], (unsigned long long)KEY_EMPTY,
+      const int sl = 4 * g + empty;
+      const uint64_t want = (NL == 1) ? kl : KEY_BUSY;
+      const uint64_t old = atomicCAS((unsigned long long *)&last[sl], (unsigned long long)KEY_EMPTY,
                                      (unsigned long long)want);
       if (old == KEY_EMPTY) {
         if (NL > 1) {
 #pragma unroll
-          for (int w = 0; w < NL - 1; w++) t.keys[w * t.cap + slot] = key[w];
-          __hip_atomic_store(&last[slot], key[NL - 1], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          for (int w = 0; w < NL - 1; w++) t.keys[w * t.cap + sl] = key[w];
+          __hip_atomic_store(&last[sl], kl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        return slot;
+        return sl;
       }
       atomicSub(s_res, 1);
-      continue;  // re-examine the slot that was just taken
+      continue;  // the slot was just taken: re-read the group
     }
-    if (NL > 1 && cur == KEY_BUSY) continue;  // writer publishes within its own iteration
-    if (cur == key[NL - 1]) {
-      bool eq = true;
-#pragma unroll
-      for (int w = 0; w < NL - 1; w++) eq &= (t.keys[w * t.cap + slot] == key[w]);
-      if (eq) return slot;
-    }
-    slot = (slot + 1 == t.cap) ? 0 : slot + 1;
+    g = (g + 1 == ng) ? 0 : g + 1;
   }
   return -2;
 }
 
 template <int NL>
-__device__ int lds_find(const CountLds &t, const uint64_t *key, int slot) {
+__device__ int lds_find(const CountLds &t, const uint64_t *key, int g) {
   const uint64_t *last = t.keys + (NL - 1) * t.cap;
-  for (int iter = 0; iter < t.cap + 1; iter++) {
-    const uint64_t cur = __hip_atomic_load(&last[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (cur == KEY_EMPTY) return -1;
-    if (cur == key[NL - 1]) {
-      bool eq = true;
+  const int ng = t.cap >> 2;
+  const uint64_t kl = key[NL - 1];
+  for (int iter = 0; iter < ng + 1; iter++) {
+    uint64_t v[4];
+    read_group(last, g, v);
+    bool empty = false;
 #pragma unroll
-      for (int w = 0; w < NL - 1; w++) eq &= (t.keys[w * t.cap + slot] == key[w]);
-      if (eq) return slot;
+    for (int i = 0; i < 4; i++) {
+      if (v[i] == kl && (NL == 1 || rest_equal<NL>(t, 4 * g + i, key))) return 4 * g + i;
+      empty |= (v[i] == KEY_EMPTY);
     }
-    slot = (slot + 1 == t.cap) ? 0 : slot + 1;
+    if (empty) return -1;
+    g = (g + 1 == ng) ? 0 : g + 1;
   }
   return -1;
 }
@@ -583,7 +777,7 @@ __device__ int lds_find(const CountLds &t, const uint64_t *key, int slot) {
 // LDS atomic. A half that reaches 0xC000 is clamped back to 0x8000 by CAS. Exact for the reference's
 // get_ext, which only compares counters against thresholds <= max(6553, dmin_thres) <= 32768
 // (DESIGN.md §3.4); the reference saturates the same counters at 65535 (kcount_cpu.cpp:148-164).
-__device__ __forceinline__ void ext_inc(uint32_t *p, int half) {
+__device__ __forceinline__ void ext_inc_checked(uint32_t *p, int half) {
   const uint32_t inc = half ? 0x10000u : 1u;
   const uint32_t old = atomicAdd(p, inc);
   const uint32_t v = half ? (old >> 16) : (old & 0xffffu);
@@ -601,12 +795,19 @@ __device__ __forceinline__ void ext_inc(uint32_t *p, int half) {
 }
 
 // insert_supermer_from_read's per-k-mer update (src/kcount/kcount_cpu.cpp:343-352): count + 1,
-// left/right extension + 1 when they are A/C/G/T.
+// left/right extension + 1 when they are A/C/G/T. An extension counter never exceeds its k-mer's count,
+// so while the count is below 0xBFFF the extension adds need no return value (no clamp possible; lanes
+// racing past the boundary overshoot 0xC000 by at most the workgroup size before a checked add clamps).
 __device__ __forceinline__ void lds_update(const CountLds &t, int slot, uint32_t e) {
-  atomicAdd(&t.cnt[slot], 1u);
-  const int l = (int)(e >> 3), r = (int)(e & 7u);
-  if (l < 4) ext_inc(&t.ext[(l >> 1) * t.cap + slot], l & 1);
-  if (r < 4) ext_inc(&t.ext[(2 + (r >> 1)) * t.cap + slot], r & 1);
+  const uint32_t old = atomicAdd(&t.cnt[slot], 1u);
+  const int l = (int)((e >> 3) & 7u), r = (int)(e & 7u);
+  if (old < 0xBFFFu) {
+    if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
+    if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
+  } else {
+    if (l < 4) ext_inc_checked(&t.ext[(l >> 1) * t.cap + slot], l & 1);
+    if (r < 4) ext_inc_checked(&t.ext[(2 + (r >> 1)) * t.cap + slot], r & 1);
+  }
 }
 
 // Final decision for one table slot: insert_into_local_hashtable (src/kcount/kcount_cpu.cpp:503-517):
@@ -626,13 +827,16 @@ __device__ __forceinline__ bool slot_survives(const CountLds &t, int slot, const
   return !(L == 'X' && R == 'X');
 }
 
+// e receives the raw low bits of the record (ext code in bits 0-5, stored hash bits above) so that an
+// overflowing record is written back unchanged; the key has them cleared.
 template <int NL, bool PACKED>
-__device__ __forceinline__ void load_record(const PlaneSet &ps, uint64_t idx, uint64_t *key, uint32_t &e) {
+__device__ __forceinline__ void load_record(const PlaneSet &ps, uint64_t idx, uint64_t low_mask, uint64_t *key,
+                                            uint32_t &e) {
 #pragma unroll
   for (int w = 0; w < NL; w++) key[w] = ps.w[w][idx];
   if (PACKED) {
-    e = (uint32_t)(key[NL - 1] & 63u);
-    key[NL - 1] &= ~63ull;
+    e = (uint32_t)(key[NL - 1] & low_mask);
+    key[NL - 1] &= ~low_mask;
   } else {
     e = ps.ext[idx];
   }
@@ -645,6 +849,9 @@ __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, c
   if (!PACKED) ps.ext[idx] = (uint8_t)e;
 }
 
+// Table slots per thread in the finalize pass.
+constexpr int C_SPT = 5;
+
 template <int NL, bool PACKED>
 __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -653,22 +860,23 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   t.keys = (uint64_t *)smem;
   t.cnt = (uint32_t *)(t.keys + NL * t.cap);
   t.ext = t.cnt + t.cap;
-  // scalars live after the table in the same dynamic region (count_lds_bytes adds 64 bytes)
+  // scalars live after the table in the same dynamic region (count_lds_bytes adds 128 bytes)
   unsigned long long *s_u64 = (unsigned long long *)(t.ext + 4 * t.cap);
   unsigned long long &s_gbase = s_u64[0];
   unsigned long long *s_red = s_u64 + 1;  // [3]
   int &s_res = *(int *)(s_u64 + 4);
   int &s_closed = *((int *)(s_u64 + 4) + 1);
   unsigned int &s_ovf = *(unsigned int *)(s_u64 + 5);
-  unsigned int &s_nsurv = *((unsigned int *)(s_u64 + 5) + 1);
-  unsigned int &s_wr = *(unsigned int *)(s_u64 + 6);
-  unsigned int &s_err = *((unsigned int *)(s_u64 + 6) + 1);
+  unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
+  unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
 
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
   const uint32_t b = blockIdx.x;
-  uint64_t n = p.bucket_n[b];
-  const uint64_t n0 = n;
   const uint64_t base = p.bucket_base[b];
+  uint64_t n = p.bucket_end[b] - base;
+  const uint64_t n0 = n;
+  const uint64_t low_mask = (1ull << (EXT_BITS + p.hbits)) - 1;
   PlaneSet ps = p.recs;
 #pragma unroll
   for (int w = 0; w < NL; w++) ps.w[w] += base;
@@ -677,105 +885,141 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   uint32_t sweeps = 0;
   unsigned long long my_occ = 0, my_purged = 0, my_sum = 0, my_out = 0;
   while (true) {
-    for (int i = tid; i < t.cap; i += C_THREADS) {
-      t.keys[(NL - 1) * t.cap + i] = KEY_EMPTY;
-      t.cnt[i] = 0;
-      t.ext[i] = 0;
-      t.ext[t.cap + i] = 0;
-      t.ext[2 * t.cap + i] = 0;
-      t.ext[3 * t.cap + i] = 0;
+    {  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
+      uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
+      const int n_ones = t.cap * 8 / 16;
+      for (int i = tid; i < n_ones; i += C_THREADS) ones[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+      uint4 *zeros = (uint4 *)t.cnt;
+      const int n_zeros = t.cap * 20 / 16;
+      for (int i = tid; i < n_zeros; i += C_THREADS) zeros[i] = make_uint4(0, 0, 0, 0);
     }
     if (tid == 0) {
       s_res = 0;
       s_closed = 0;
       s_ovf = 0;
-      s_nsurv = 0;
-      s_wr = 0;
       s_err = 0;
     }
     __syncthreads();
 
-    uint64_t nk[NL];
-    uint32_t ne = 0;
-    bool nh = (uint64_t)tid < n;
-    if (nh) load_record<NL, PACKED>(ps, tid, nk, ne);
-    for (uint64_t r0 = 0; r0 < n; r0 += C_THREADS) {
-      uint64_t key[NL];
+    // R records per thread per round, the next round prefetched into registers, so that every CU keeps
+    // R * 8 KB of record loads in flight.
+    constexpr int R = count_rpt<NL>();
+    constexpr uint32_t NONE = 0xffffffffu;
+    const uint64_t RND = (uint64_t)R * C_THREADS;
+    const int ng = t.cap >> 2;
+    uint64_t nk[R][NL];
+    uint32_t ne[R];
 #pragma unroll
-      for (int w = 0; w < NL; w++) key[w] = nk[w];
-      const uint32_t e = ne;
-      const bool have = nh;
-      const uint64_t nxt = r0 + C_THREADS + tid;
-      nh = nxt < n;
-      if (nh) load_record<NL, PACKED>(ps, nxt, nk, ne);
-      int s0 = 0;
-      bool tent = false;
-      if (have) {
-        const uint64_t h = murmur3_h1<NL>(key);
-        s0 = (int)(((uint64_t)(uint32_t)h * (uint64_t)t.cap) >> 32);
-        const int slot = lds_insert_or_find<NL>(t, key, s0, &s_res, &s_closed, p.limit);
-        if (slot >= 0)
-          lds_update(t, slot, e);
-        else if (slot == -1)
-          tent = true;
-        else
-          s_err = 1;
+    for (int j = 0; j < R; j++) {
+      const uint64_t i = (uint64_t)tid + (uint64_t)j * C_THREADS;
+      ne[j] = NONE;
+      if (i < n) load_record<NL, PACKED>(ps, i, low_mask, nk[j], ne[j]);
+    }
+    for (uint64_t r0 = 0; r0 < n; r0 += RND) {
+      uint64_t ck[R][NL];
+      uint32_t ce[R];
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        ce[j] = ne[j];
+#pragma unroll
+        for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
+      }
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        const uint64_t i = r0 + RND + (uint64_t)tid + (uint64_t)j * C_THREADS;
+        ne[j] = NONE;
+        if (i < n) load_record<NL, PACKED>(ps, i, low_mask, nk[j], ne[j]);
+      }
+      uint32_t tent = 0;
+      int g0[R];
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        g0[j] = 0;
+        if (ce[j] != NONE) {
+          g0[j] = (int)(((uint64_t)slot_hash<NL>(ck[j]) * (uint64_t)ng) >> 32);
+          const int slot = lds_insert_or_find<NL>(t, ck[j], g0[j], &s_res, &s_closed, p.limit);
+          if (slot >= 0)
+            lds_update(t, slot, ce[j]);
+          else if (slot == -1)
+            tent |= 1u << j;
+          else
+            s_err = 1;
+        }
       }
       __syncthreads();
       if (tent) {
         // The table closed this round: keys inserted concurrently are visible now; a key still absent
         // is never inserted in this sweep, so all its occurrences go to the next sweep together.
-        const int slot = lds_find<NL>(t, key, s0);
-        if (slot >= 0) {
-          lds_update(t, slot, e);
-        } else {
-          const unsigned int pos = atomicAdd(&s_ovf, 1u);
-          store_record<NL, PACKED>(ps, pos, key, e);  // pos < r0 + C_THREADS: already consumed
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+          if ((tent >> j) & 1u) {
+            const int slot = lds_find<NL>(t, ck[j], g0[j]);
+            if (slot >= 0) {
+              lds_update(t, slot, ce[j]);
+            } else {
+              const unsigned int pos = atomicAdd(&s_ovf, 1u);
+              store_record<NL, PACKED>(ps, pos, ck[j], ce[j]);  // pos < r0 + RND: already consumed
+            }
+          }
         }
       }
     }
     __syncthreads();
 
-    // finalize: survivors of this sweep -> output table
-    uint32_t occ = 0, purged = 0, surv = 0;
+    // finalize in one pass: decisions in registers, wave-prefix offsets, one global reservation
+    uint32_t occ = 0, surv_mask = 0;
     unsigned long long sum = 0;
-    for (int slot = tid; slot < t.cap; slot += C_THREADS) {
-      if (t.keys[(NL - 1) * t.cap + slot] != KEY_EMPTY) {
+    uint16_t c16[C_SPT];
+    char L[C_SPT], R_[C_SPT];
+#pragma unroll
+    for (int j = 0; j < C_SPT; j++) {
+      const int slot = tid + j * C_THREADS;
+      c16[j] = 0;
+      L[j] = R_[j] = 0;
+      if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != KEY_EMPTY) {
         occ++;
         sum += t.cnt[slot];
-        uint16_t c16;
-        char L, R;
-        if (slot_survives(t, slot, p, c16, L, R))
-          surv++;
-        else
-          purged++;
+        if (slot_survives(t, slot, p, c16[j], L[j], R_[j])) surv_mask |= 1u << j;
       }
     }
-    surv = wave_sum_u32(surv);
-    if ((tid & 63) == 0 && surv) atomicAdd(&s_nsurv, surv);
-    __syncthreads();
-    if (tid == 0) s_gbase = s_nsurv ? atomicAdd(p.out_cursor, (unsigned long long)s_nsurv) : 0ull;
-    __syncthreads();
-    for (int slot = tid; slot < t.cap; slot += C_THREADS) {
-      if (t.keys[(NL - 1) * t.cap + slot] != KEY_EMPTY) {
-        uint16_t c16;
-        char L, R;
-        if (slot_survives(t, slot, p, c16, L, R)) {
-          const unsigned long long g = s_gbase + atomicAdd(&s_wr, 1u);
-          uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
+    const uint32_t mine = __popc(surv_mask);
+    uint32_t incl = mine;
 #pragma unroll
-          for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
-          for (int w = NL; w < p.nlo; w++) ok[w] = 0;
-          p.out_counts[g] = c16;
-          p.out_left[g] = L;
-          p.out_right[g] = R;
-        }
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_wave[wid] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      for (int w = 0; w < C_THREADS / 64; w++) {
+        const uint32_t c = s_wave[w];
+        s_wave[w] = acc;
+        acc += c;
+      }
+      s_gbase = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      my_out += acc;
+    }
+    __syncthreads();
+    unsigned long long g = s_gbase + s_wave[wid] + (incl - mine);
+#pragma unroll
+    for (int j = 0; j < C_SPT; j++) {
+      if ((surv_mask >> j) & 1u) {
+        const int slot = tid + j * C_THREADS;
+        uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
+#pragma unroll
+        for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
+        for (int w = NL; w < p.nlo; w++) ok[w] = 0;
+        p.out_counts[g] = c16[j];
+        p.out_left[g] = L[j];
+        p.out_right[g] = R_[j];
+        g++;
       }
     }
     my_occ += occ;
-    my_purged += purged;
+    my_purged += occ - mine;
     my_sum += sum;
-    if (tid == 0) my_out += s_nsurv;
     __syncthreads();
     if (s_err && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
     if (s_ovf == 0) break;
@@ -796,7 +1040,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     s_red[2] = 0;
   }
   __syncthreads();
-  if ((tid & 63) == 0) {
+  if (lane == 0) {
     atomicAdd(&s_red[0], my_occ);
     atomicAdd(&s_red[1], my_purged);
     atomicAdd(&s_red[2], my_sum);
@@ -845,7 +1089,9 @@ static hipError_t do_extract_hist(const ExtractParams &p, hipStream_t s) {
 
 template <int NL, bool PK>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
-  const size_t lds = tile_lds_bytes<NL>() + scatter_lds_bytes<NL>(p.n_bins);
+  constexpr int T = kTile<NL>();
+  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_lds_bytes<NL>(), staged_area_bytes(NL, T, PK))
+                              : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
   hipError_t e = allow_lds(k_extract_scatter<NL, PK>, lds);
   if (e != hipSuccess) return e;
   k_extract_scatter<NL, PK><<<dim3(p.n_tiles), dim3(E_THREADS), lds, s>>>(p);
@@ -863,7 +1109,8 @@ static hipError_t do_part_hist(const PartitionParams &p, hipStream_t s) {
 
 template <int NL, bool PK>
 static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
-  const size_t lds = scatter_lds_bytes<NL>(1u << p.fine_bits);
+  const uint32_t nf = 1u << p.fine_bits;
+  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kTile<NL>(), PK) : scatter_lds_bytes(nf);
   hipError_t e = allow_lds(k_part_scatter<NL, PK>, lds);
   if (e != hipSuccess) return e;
   k_part_scatter<NL, PK><<<dim3(p.n_chunks), dim3(E_THREADS), lds, s>>>(p);
@@ -882,6 +1129,23 @@ static hipError_t do_count(const CountParams &p, hipStream_t s) {
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s) {
   if (!n_tiles) return hipSuccess;
   k_tile_first_read<<<dim3((n_tiles + 255) / 256), dim3(256), 0, s>>>(r, out, n_tiles, tile);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, hipStream_t s) {
+  if (!r.n_reads) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>(2048, (r.n_reads + 255) / 256);
+  k_count_windows<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap,
+                            uint32_t n_coarse, int fine_bits, unsigned long long *base, unsigned long long *cursor,
+                            hipStream_t s) {
+  const uint64_t n = (uint64_t)n_coarse << fine_bits;
+  if (!n) return hipSuccess;
+  k_init_fine<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(coarse_base, coarse_fcap, n_coarse, fine_bits,
+                                                                      base, cursor);
   return hipGetLastError();
 }
 

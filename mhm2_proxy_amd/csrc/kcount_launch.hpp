@@ -28,10 +28,13 @@ struct ExtractParams {
   int qual_cutoff;
   int coarse_bits;                  // coarse digit = h1 >> (64 - coarse_bits)
   uint32_t n_bins;                  // 1 << coarse_bits
+  int hbits;                        // hash bits stored in the record after the ext code (0: none)
   unsigned long long *hist;         // [n_bins] (E-hist)
-  unsigned long long *cursor;       // [n_bins] (E-scatter), starts at the bin bases of the slab
+  unsigned long long *cursor;       // [n_bins * E_NSUB] (E-scatter): segment (b, s) at index b * E_NSUB + s
+  uint64_t bin_cap;                 // capped mode: segment (b, s) owns [i*bin_cap, (i+1)*bin_cap), i = b*E_NSUB+s,
+                                    // s = blockIdx % E_NSUB; 0 = exact bases, everything in segment (b, 0)
   PlaneSet out;                     // (E-scatter)
-  unsigned int *err;                // bit 0: input byte with code > 4
+  unsigned int *err;                // bit 0: input byte with code > 4; bit 1: a capped bin overflowed
 };
 
 // One chunk of S work: <= tile records of one (source, coarse bucket) segment.
@@ -50,15 +53,20 @@ struct PartitionParams {
   int k;
   int coarse_bits;
   int fine_bits;
+  int hbits;                        // hash bits stored in the records (fine digit read from them if >= fine_bits)
   unsigned long long *fine_hist;    // [n_coarse_local << fine_bits]
   unsigned long long *fine_cursor;  // [n_coarse_local << fine_bits]
+  const unsigned long long *coarse_base;  // capped mode: first fine bucket of coarse bucket c starts here
+  const unsigned long long *coarse_fcap;  // capped mode: capacity of every fine bucket of c; nullptr = exact
+  unsigned int *err;                      // bit 1: a capped fine bucket overflowed
   PlaneSet out;
 };
 
 struct CountParams {
   PlaneSet recs;                      // fine-bucketed records (overwritten in place by overflow)
   const unsigned long long *bucket_base;
-  const unsigned long long *bucket_n;
+  const unsigned long long *bucket_end;  // == the fine cursors after the scatter
+  int hbits;                           // stored hash bits to strip from the last key word
   uint32_t n_buckets;
   int k;
   int cap;                            // LDS table slots
@@ -85,15 +93,36 @@ enum {
 };
 
 constexpr int E_THREADS = 256;
+constexpr int E_NSUB = 8;
+#ifndef MHMKC_CPAD
+#define MHMKC_CPAD 1
+#endif
+constexpr uint32_t CPAD = MHMKC_CPAD;  // cursor spacing in u64 words (segment i's cursor at i * CPAD)  // segments per coarse bucket: one per group of blocks sharing an XCD
 constexpr int C_THREADS = 1024;
 
+// Hash bits stored in a packed record next to the ext code (bits [6, 6 + hbits) of the last word).
+inline int stored_hash_bits(int k, int nl, bool packed) {
+  if (!packed) return 0;
+  const int room = 64 - 2 * (k - 32 * (nl - 1)) - 6;
+  return room >= 16 ? 16 : (room >= 8 ? room : 0);
+}
+
 // Bases per extract tile (== records per S chunk) for NL words per key.
-inline int tile_bases(int nl) { return nl <= 2 ? 4096 : 2048; }
+#ifndef MHMKC_TILE1
+#define MHMKC_TILE1 4096
+#endif
+inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : 2048; }
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS).
 inline int count_cap(int nl) { return nl == 1 ? 5120 : nl == 2 ? 4000 : nl == 3 ? 3264 : 2752; }
-inline size_t count_lds_bytes(int nl) { return (size_t)count_cap(nl) * (8 * nl + 4 + 16) + 64; }
+inline size_t count_lds_bytes(int nl) { return (size_t)count_cap(nl) * (8 * nl + 4 + 16) + 128; }
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);
+// total counted windows sum(max(0, L - k - 1)) of a batch, added to *out
+hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, hipStream_t s);
+// capped fine layout: base/cursor of bucket (c, d) = coarse_base[c] + d * coarse_fcap[c]
+hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap,
+                            uint32_t n_coarse, int fine_bits, unsigned long long *base, unsigned long long *cursor,
+                            hipStream_t s);
 hipError_t launch_extract_hist(const ExtractParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s);

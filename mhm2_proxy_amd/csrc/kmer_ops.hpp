@@ -77,6 +77,28 @@ MHM_HD uint64_t murmur3_h1(const uint64_t *w) {
   return h1;
 }
 
+#ifndef MHMKC_PART_HASH
+#define MHMKC_PART_HASH 0
+#endif
+// Hash that assigns a k-mer to its rank / coarse bucket / fine bucket. 0: Kmer::hash (MurmurHash3 h1);
+// 1: a two-multiply mixer (the partition is internal: any function gives the same table).
+template <int NL>
+MHM_HD uint64_t part_hash(const uint64_t *w) {
+#if MHMKC_PART_HASH == 0
+  return murmur3_h1<NL>(w);
+#else
+  uint64_t h = w[0];
+#pragma unroll
+  for (int i = 1; i < NL; i++) h = (h ^ (h >> 31)) * 0x9E3779B97F4A7C15ull + w[i];
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  h *= 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  return h;
+#endif
+}
+
 // Reverse the order of the 32 two-bit groups of x.
 MHM_HD uint64_t rev2(uint64_t x) {
   x = __builtin_bswap64(x);

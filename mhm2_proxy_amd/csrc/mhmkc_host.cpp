@@ -51,20 +51,24 @@ struct DevBuf {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Records of one add_reads batch, partitioned by coarse bucket (hash range).
+// Records of one add_reads batch, partitioned by coarse bucket (hash range). Every coarse bucket b is
+// E_NSUB segments i = b * E_NSUB + s (one per group of blocks sharing an XCD in the capped layout; in
+// the exact layout segment s = 0 holds the whole bucket and the others are empty). Segments are in
+// bucket order, so a range of buckets is one contiguous span (with gaps in the capped layout).
+constexpr uint32_t NSUB = mhm::E_NSUB;
 struct Slab {
   DevBuf buf;
   mhm::PlaneSet planes{};
   uint64_t n = 0;
-  std::vector<uint64_t> counts;  // [nb]
-  std::vector<uint64_t> bases;   // [nb] exclusive prefix
+  std::vector<uint64_t> counts;  // [nb * NSUB]
+  std::vector<uint64_t> bases;   // [nb * NSUB + 1] segment starts, bases[nb * NSUB] = end of the slab
 };
 
-// A source of owned records for the fine partition: per owned coarse bucket (local index) a range.
+// A source of owned records for the fine partition: per owned coarse bucket (local index) and segment.
 struct Source {
   mhm::PlaneSet planes{};
-  std::vector<uint64_t> start;  // [n_owned]
-  std::vector<uint64_t> count;  // [n_owned]
+  std::vector<uint64_t> start;  // [n_owned * NSUB]
+  std::vector<uint64_t> count;  // [n_owned * NSUB]
 };
 
 struct Prof {
@@ -78,7 +82,7 @@ struct mhmkc {
   mhmkc_config cfg{};
   int k = 0, nl = 1, nlo = 1;
   bool packed = true;
-  int cb = 8, fb = 8;
+  int cb = 8, fb = 8, hbits = 0;
   uint32_t nb = 256, nf = 256;
   uint32_t own_lo = 0, own_hi = 256;  // owned coarse range [own_lo, own_hi)
   int dev = 0;
@@ -185,6 +189,9 @@ struct mhmkc {
 // ------------------------------------------------------------------------------------------------
 // extract one batch of reads into a coarse-bucketed slab
 
+// Coarse buckets are sized from the exact window count (+4 % and 4096 records of slack each), which lets
+// one extract pass write the records. A bucket that would overflow (only skewed inputs: very repetitive
+// reads) makes the pass redo itself with an exact histogram first (extract_hist).
 int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, uint64_t n_bases, int qcut) {
   int rc = begin_round();
   if (rc) return rc;
@@ -198,8 +205,9 @@ int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
   const uint32_t tiles = (uint32_t)tiles64;
   hipError_t e;
   if ((e = d_tiles.ensure((size_t)tiles * 4)) != hipSuccess) return hip_fail(e, "tile index");
-  if ((e = d_hist.ensure((size_t)nb * 8)) != hipSuccess) return hip_fail(e, "histogram");
-  if ((e = d_cursor.ensure((size_t)nb * 8)) != hipSuccess) return hip_fail(e, "cursor");
+  if ((e = d_hist.ensure((size_t)nb * 8 + 8)) != hipSuccess) return hip_fail(e, "histogram");
+  if ((e = d_cursor.ensure((size_t)nb * NSUB * mhm::CPAD * 8)) != hipSuccess) return hip_fail(e, "cursor");
+  unsigned long long *d_wins = d_hist.as<unsigned long long>() + nb;
 
   mhm::ExtractParams p{};
   p.reads = {bytes, offs, n_reads, n_bases};
@@ -209,46 +217,84 @@ int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
   p.qual_cutoff = qcut;
   p.coarse_bits = cb;
   p.n_bins = nb;
+  p.hbits = hbits;
   p.hist = d_hist.as<unsigned long long>();
   p.cursor = d_cursor.as<unsigned long long>();
   p.err = d_err.as<unsigned int>();
 
   prof_begin(MHMKC_STAGE_TILEIDX);
   e = mhm::launch_tile_first_read(p.reads, d_tiles.as<uint32_t>(), tiles, T, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(d_wins, 0, 8, stream);
+  if (e == hipSuccess) e = mhm::launch_count_windows(p.reads, k, d_wins, stream);
   prof_end();
-  if (e != hipSuccess) return hip_fail(e, "tile_first_read");
-  prof_begin(MHMKC_STAGE_OTHER);
-  e = hipMemsetAsync(d_hist.p, 0, (size_t)nb * 8, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "memset");
-  prof_begin(MHMKC_STAGE_EHIST);
-  e = mhm::launch_extract_hist(p, nl, packed, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "extract_hist");
+  if (e != hipSuccess) return hip_fail(e, "tile index / window count");
+  uint64_t wins = 0;
+  if ((e = hipMemcpyAsync(&wins, d_wins, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(e, "window count D2H");
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "window count");
+  if (wins == 0) return MHMKC_OK;
 
-  Slab *s = new_slab();
-  s->counts.assign(nb, 0);
-  s->bases.assign(nb, 0);
-  if ((e = hipMemcpyAsync(s->counts.data(), d_hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-    return hip_fail(e, "histogram D2H");
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_hist");
-  uint64_t tot = 0;
-  for (uint32_t b = 0; b < nb; b++) {
-    s->bases[b] = tot;
-    tot += s->counts[b];
+  Slab *sl = new_slab();
+  const uint32_t nseg = nb * NSUB;
+  sl->counts.assign(nseg, 0);
+  sl->bases.assign(nseg + 1, 0);
+  std::vector<uint64_t> cur((size_t)nseg * mhm::CPAD), hist(nb);
+  const uint64_t expect = wins / nseg;
+  const uint64_t cap = align_up(expect + expect / 25 + 1024, 64);
+  bool exact = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
+  for (int attempt = 0; attempt < 2; attempt++) {
+    if (exact) {
+      prof_begin(MHMKC_STAGE_OTHER);
+      e = hipMemsetAsync(d_hist.p, 0, (size_t)nb * 8, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "memset");
+      prof_begin(MHMKC_STAGE_EHIST);
+      e = mhm::launch_extract_hist(p, nl, packed, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "extract_hist");
+      if ((e = hipMemcpyAsync(hist.data(), d_hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return hip_fail(e, "histogram D2H");
+      if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_hist");
+      uint64_t tot = 0;
+      for (uint32_t b = 0; b < nb; b++) {
+        sl->bases[b * NSUB] = tot;
+        tot += hist[b];
+        for (uint32_t q = 1; q < NSUB; q++) sl->bases[b * NSUB + q] = tot;  // empty segments
+      }
+      sl->bases[nseg] = tot;
+      p.bin_cap = 0;
+    } else {
+      for (uint32_t i = 0; i <= nseg; i++) sl->bases[i] = (uint64_t)i * cap;
+      p.bin_cap = cap;
+    }
+    if ((rc = set_planes(sl->buf, sl->bases[nseg], sl->planes))) return rc;
+    for (uint32_t i = 0; i < nseg; i++) cur[(size_t)i * mhm::CPAD] = sl->bases[i];
+    if ((e = hipMemcpyAsync(d_cursor.p, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
+      return hip_fail(e, "cursor H2D");
+    p.out = sl->planes;
+    prof_begin(MHMKC_STAGE_ESCAT);
+    e = mhm::launch_extract_scatter(p, nl, packed, stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "extract_scatter");
+    unsigned int errf = 0;
+    if ((e = hipMemcpyAsync(cur.data(), d_cursor.p, cur.size() * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+      return hip_fail(e, "cursor D2H");
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_scatter");
+    if (!(errf & 2u)) break;
+    // a capped bucket overflowed: clear the flag (keep the bad-input bit) and redo with exact sizes
+    errf &= ~2u;
+    if ((e = hipMemcpy(d_err.p, &errf, 4, hipMemcpyHostToDevice)) != hipSuccess) return hip_fail(e, "flag reset");
+    exact = true;
+    st.exact_reruns++;
   }
-  s->n = tot;
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < nseg; i++) {
+    sl->counts[i] = cur[(size_t)i * mhm::CPAD] - sl->bases[i];
+    tot += sl->counts[i];
+  }
+  sl->n = tot;
   st.occurrences += tot;
-  if ((rc = set_planes(s->buf, tot, s->planes))) return rc;
-  if ((e = hipMemcpyAsync(d_cursor.p, s->bases.data(), (size_t)nb * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
-    return hip_fail(e, "cursor H2D");
-  p.out = s->planes;
-  prof_begin(MHMKC_STAGE_ESCAT);
-  e = mhm::launch_extract_scatter(p, nl, packed, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "extract_scatter");
-  // the cursor H2D source is a host vector: make sure it has been consumed before it can change
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_scatter");
   return MHMKC_OK;
 }
 
@@ -261,7 +307,7 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
   const uint32_t no = n_owned();
   hipError_t e;
   ncclResult_t nr;
-  // 1. slab counts of every rank
+  // 1. number of slabs of every rank
   uint64_t my_slabs = n_slabs;
   if ((e = d_xcounts.ensure(8 * (size_t)G * 2)) != hipSuccess) return hip_fail(e, "exchange counts");
   if ((e = hipMemcpyAsync(d_xcounts.p, &my_slabs, 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
@@ -274,21 +320,27 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
     return hip_fail(e, "exchange D2H");
   if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange sync");
   const uint64_t ms = std::max<uint64_t>(1, *std::max_element(slabs_of.begin(), slabs_of.end()));
-  // 2. all coarse counts [G][ms][nb]
-  std::vector<uint64_t> mine(ms * nb, 0), all((size_t)G * ms * nb, 0);
-  for (size_t s = 0; s < n_slabs; s++) std::copy(slabs[s]->counts.begin(), slabs[s]->counts.end(), mine.begin() + s * nb);
-  if ((e = d_xcounts.ensure(8 * (size_t)(G + 1) * ms * nb)) != hipSuccess) return hip_fail(e, "exchange counts");
+  // 2. per slab: segment counts [nseg] and segment starts [nseg + 1] (capped slabs have gaps), of every rank
+  const uint32_t nseg = nb * NSUB;
+  const size_t per = 2 * (size_t)nseg + 1;
+  std::vector<uint64_t> mine(ms * per, 0), all((size_t)G * ms * per, 0);
+  for (size_t s = 0; s < n_slabs; s++) {
+    std::copy(slabs[s]->counts.begin(), slabs[s]->counts.end(), mine.begin() + s * per);
+    std::copy(slabs[s]->bases.begin(), slabs[s]->bases.end(), mine.begin() + s * per + nseg);
+  }
+  if ((e = d_xcounts.ensure(8 * (size_t)(G + 1) * ms * per)) != hipSuccess) return hip_fail(e, "exchange counts");
   dx = d_xcounts.as<uint64_t>();
-  if ((e = hipMemcpyAsync(dx, mine.data(), 8 * ms * nb, hipMemcpyHostToDevice, stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(dx, mine.data(), 8 * ms * per, hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "exchange H2D");
-  if ((nr = ncclAllGather(dx, dx + ms * nb, ms * nb, ncclUint64, comm, stream)) != ncclSuccess)
+  if ((nr = ncclAllGather(dx, dx + ms * per, ms * per, ncclUint64, comm, stream)) != ncclSuccess)
     return fail(MHMKC_ERCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
-  if ((e = hipMemcpyAsync(all.data(), dx + ms * nb, 8 * (size_t)G * ms * nb, hipMemcpyDeviceToHost, stream)) !=
+  if ((e = hipMemcpyAsync(all.data(), dx + ms * per, 8 * (size_t)G * ms * per, hipMemcpyDeviceToHost, stream)) !=
       hipSuccess)
     return hip_fail(e, "exchange D2H");
   if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange sync");
-  auto cnt = [&](int r, uint64_t s, uint32_t c) { return all[((size_t)r * ms + s) * nb + c]; };
-  // 3. receive layout: for each peer p != me, for each of its slabs s: my owned coarse range
+  auto cnt = [&](int r, uint64_t s, uint32_t i) { return all[((size_t)r * ms + s) * per + i]; };
+  auto bas = [&](int r, uint64_t s, uint32_t i) { return all[((size_t)r * ms + s) * per + nseg + i]; };
+  // 3. receive layout: for each peer p != me, for each of its slabs s, the span of my owned range
   uint64_t recv_total = 0;
   struct Seg {
     int peer;
@@ -298,8 +350,7 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
   for (int p = 0; p < G; p++) {
     if (p == me) continue;
     for (uint64_t s = 0; s < slabs_of[p]; s++) {
-      uint64_t n = 0;
-      for (uint32_t c = own_lo; c < own_hi; c++) n += cnt(p, s, c);
+      const uint64_t n = bas(p, s, own_hi * NSUB) - bas(p, s, own_lo * NSUB);
       rsegs.push_back({p, s, recv_total, n});
       recv_total += n;
     }
@@ -316,8 +367,7 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
     const uint32_t lo = owner_lo(p), hi = owner_lo(p + 1);
     for (size_t s = 0; s < n_slabs; s++) {
       const Slab *sl = slabs[s];
-      const uint64_t a = lo < nb ? sl->bases[lo] : sl->n;
-      const uint64_t b = hi < nb ? sl->bases[hi] : sl->n;
+      const uint64_t a = sl->bases[lo * NSUB], b = sl->bases[hi * NSUB];
       if (b == a) continue;
       for (int w = 0; w < nl; w++) ncclSend(sl->planes.w[w] + a, b - a, ncclUint64, p, comm, stream);
       if (!packed) ncclSend(sl->planes.ext + a, b - a, ncclUint8, p, comm, stream);
@@ -336,24 +386,18 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
   for (size_t s = 0; s < n_slabs; s++) {
     Source src;
     src.planes = slabs[s]->planes;
-    src.start.resize(no);
-    src.count.resize(no);
-    for (uint32_t c = 0; c < no; c++) {
-      src.start[c] = slabs[s]->bases[own_lo + c];
-      src.count[c] = slabs[s]->counts[own_lo + c];
-    }
+    src.start.assign(slabs[s]->bases.begin() + own_lo * NSUB, slabs[s]->bases.begin() + own_hi * NSUB);
+    src.count.assign(slabs[s]->counts.begin() + own_lo * NSUB, slabs[s]->counts.begin() + own_hi * NSUB);
     srcs.push_back(std::move(src));
   }
   for (const Seg &g : rsegs) {
     Source src;
     src.planes = rps;
-    src.start.resize(no);
-    src.count.resize(no);
-    uint64_t o = g.off;
-    for (uint32_t c = 0; c < no; c++) {
-      src.start[c] = o;
-      src.count[c] = cnt(g.peer, g.slab, own_lo + c);
-      o += src.count[c];
+    src.start.resize((size_t)no * NSUB);
+    src.count.resize((size_t)no * NSUB);
+    for (uint32_t i = 0; i < no * NSUB; i++) {
+      src.start[i] = g.off + (bas(g.peer, g.slab, own_lo * NSUB + i) - bas(g.peer, g.slab, own_lo * NSUB));
+      src.count[i] = cnt(g.peer, g.slab, own_lo * NSUB + i);
     }
     srcs.push_back(std::move(src));
   }
@@ -363,6 +407,8 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
 // ------------------------------------------------------------------------------------------------
 // fine partition + LDS count + finalize
 
+// Fine buckets are capped at 1.25x their expected size (+256): a single scatter pass, no histogram. If a
+// bucket overflows, the count kernel's results are discarded and the pass is redone with part_hist + scan.
 int mhmkc::finish(uint64_t *n_out_ret) {
   int rc = begin_round();
   if (rc) return rc;
@@ -375,21 +421,25 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     for (size_t s = 0; s < n_slabs; s++) {
       Source src;
       src.planes = slabs[s]->planes;
-      src.start = slabs[s]->bases;
+      src.start.assign(slabs[s]->bases.begin(), slabs[s]->bases.begin() + (size_t)nb * NSUB);
       src.count = slabs[s]->counts;
       srcs.push_back(std::move(src));
     }
   }
+  std::vector<uint64_t> per_coarse(no, 0);
   uint64_t owned = 0;
   for (auto &s : srcs)
-    for (uint32_t c = 0; c < no; c++) owned += s.count[c];
+    for (uint32_t i = 0; i < no * NSUB; i++) {
+      per_coarse[i / NSUB] += s.count[i];
+      owned += s.count[i];
+    }
   st.owned_records = owned;
 
   // fine bits: aim at ~4 records per LDS table slot per fine bucket
-  const uint64_t per_coarse = owned / std::max<uint32_t>(no, 1);
+  const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
   const uint64_t target = (uint64_t)mhm::count_cap(nl) * 4;
   fb = 4;
-  while (fb < 11 && (per_coarse >> fb) > target) fb++;
+  while (fb < 11 && (avg_coarse >> fb) > target) fb++;
   if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
   nf = 1u << fb;
   const uint32_t n_fine = no * nf;
@@ -401,22 +451,33 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   std::vector<mhm::PlaneSet> ps;
   for (size_t s = 0; s < srcs.size(); s++) {
     ps.push_back(srcs[s].planes);
-    for (uint32_t c = 0; c < no; c++) {
-      for (uint64_t o = 0; o < srcs[s].count[c]; o += T) {
+    for (uint32_t i = 0; i < no * NSUB; i++) {
+      for (uint64_t o = 0; o < srcs[s].count[i]; o += T) {
         mhm::SChunk ch{};
-        ch.start = srcs[s].start[c] + o;
-        ch.count = (uint32_t)std::min<uint64_t>(T, srcs[s].count[c] - o);
+        ch.start = srcs[s].start[i] + o;
+        ch.count = (uint32_t)std::min<uint64_t>(T, srcs[s].count[i] - o);
         ch.src = (uint32_t)s;
-        ch.coarse_local = c;
+        ch.coarse_local = i / NSUB;
         chunks.push_back(ch);
       }
     }
   }
   if (chunks.size() >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
+  // capped fine layout
+  std::vector<uint64_t> cfit(2 * (size_t)no);  // [coarse_base | coarse_fcap]
+  uint64_t r2_size = 0;
+  for (uint32_t c = 0; c < no; c++) {
+    const uint64_t ex = per_coarse[c] >> fb;
+    const uint64_t fcap = align_up(ex + ex / 4 + 256, 16);
+    cfit[c] = r2_size;
+    cfit[no + c] = fcap;
+    r2_size += fcap << fb;
+  }
   if ((e = d_chunks.ensure(std::max<size_t>(1, chunks.size()) * sizeof(mhm::SChunk))) != hipSuccess)
     return hip_fail(e, "chunk table");
-  if ((e = d_srcs.ensure(std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet))) != hipSuccess)
+  if ((e = d_srcs.ensure(std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 16 * (size_t)no)) != hipSuccess)
     return hip_fail(e, "source table");
+  unsigned long long *d_cfit = (unsigned long long *)(d_srcs.as<char>() + align_up(ps.size() * sizeof(mhm::PlaneSet), 16));
   if (!chunks.empty() &&
       (e = hipMemcpyAsync(d_chunks.p, chunks.data(), chunks.size() * sizeof(mhm::SChunk), hipMemcpyHostToDevice,
                           stream)) != hipSuccess)
@@ -424,11 +485,11 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if (!ps.empty() && (e = hipMemcpyAsync(d_srcs.p, ps.data(), ps.size() * sizeof(mhm::PlaneSet),
                                          hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "source H2D");
+  if (no && (e = hipMemcpyAsync(d_cfit, cfit.data(), 16 * (size_t)no, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "layout H2D");
   if ((e = d_fine_hist.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
   if ((e = d_fine_base.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
   if ((e = d_fine_cursor.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine cursor");
-  mhm::PlaneSet r2{};
-  if ((rc = set_planes(d_r2, owned, r2))) return rc;
   const uint64_t out_cap = owned / 2 + 1;
   if ((e = d_out_keys.ensure(out_cap * 8 * nlo)) != hipSuccess) return hip_fail(e, "output keys");
   if ((e = d_out_counts.ensure(out_cap * 2)) != hipSuccess) return hip_fail(e, "output counts");
@@ -443,38 +504,19 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   pp.k = k;
   pp.coarse_bits = cb;
   pp.fine_bits = fb;
+  pp.hbits = hbits;
   pp.fine_hist = d_fine_hist.as<unsigned long long>();
   pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
-  pp.out = r2;
-
-  prof_begin(MHMKC_STAGE_OTHER);
-  e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
-  if (e == hipSuccess) e = hipMemsetAsync(d_out_cursor.p, 0, 8, stream);
-  if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_N, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "memset");
-  prof_begin(MHMKC_STAGE_SHIST);
-  e = mhm::launch_part_hist(pp, nl, packed, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "part_hist");
-  prof_begin(MHMKC_STAGE_OTHER);
-  e = mhm::launch_scan(d_fine_hist.as<unsigned long long>(), d_fine_base.as<unsigned long long>(),
-                       d_fine_cursor.as<unsigned long long>(), n_fine, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "scan");
-  prof_begin(MHMKC_STAGE_SSCAT);
-  e = mhm::launch_part_scatter(pp, nl, packed, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "part_scatter");
+  pp.err = d_err.as<unsigned int>();
 
   mhm::CountParams cp{};
-  cp.recs = r2;
   cp.bucket_base = d_fine_base.as<unsigned long long>();
-  cp.bucket_n = d_fine_hist.as<unsigned long long>();
+  cp.bucket_end = d_fine_cursor.as<unsigned long long>();
+  cp.hbits = hbits;
   cp.n_buckets = n_fine;
   cp.k = k;
   cp.cap = mhm::count_cap(nl);
-  if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)));  // tests only
+  if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
   cp.limit = cp.cap * 9 / 10;
   cp.dmin_thres = cfg.dmin_thres;
   cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
@@ -485,19 +527,61 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.out_right = d_out_right.as<char>();
   cp.out_cursor = d_out_cursor.as<unsigned long long>();
   cp.stats = d_stats.as<unsigned long long>();
-  prof_begin(MHMKC_STAGE_COUNT);
-  e = mhm::launch_count(cp, nl, packed, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "count");
-  (void)hipEventRecord(ev_end, stream);
 
+  bool exact = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
   unsigned long long stats[mhm::STAT_N];
   unsigned int errf = 0;
-  if ((e = hipMemcpyAsync(stats, d_stats.p, sizeof stats, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-    return hip_fail(e, "stats D2H");
-  if ((e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-    return hip_fail(e, "error flag D2H");
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "finish");
+  for (int attempt = 0; attempt < 2; attempt++) {
+    mhm::PlaneSet r2{};
+    prof_begin(MHMKC_STAGE_OTHER);
+    e = hipMemsetAsync(d_out_cursor.p, 0, 8, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_N, stream);
+    if (e == hipSuccess && exact) e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
+    if (e == hipSuccess && !exact)
+      e = mhm::launch_init_fine(d_cfit, d_cfit + no, no, fb, d_fine_base.as<unsigned long long>(),
+                                d_fine_cursor.as<unsigned long long>(), stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "fine layout");
+    if (exact) {
+      pp.coarse_base = nullptr;
+      pp.coarse_fcap = nullptr;
+      prof_begin(MHMKC_STAGE_SHIST);
+      e = mhm::launch_part_hist(pp, nl, packed, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "part_hist");
+      prof_begin(MHMKC_STAGE_OTHER);
+      e = mhm::launch_scan(d_fine_hist.as<unsigned long long>(), d_fine_base.as<unsigned long long>(),
+                           d_fine_cursor.as<unsigned long long>(), n_fine, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "scan");
+      if ((rc = set_planes(d_r2, owned, r2))) return rc;
+    } else {
+      pp.coarse_base = d_cfit;
+      pp.coarse_fcap = d_cfit + no;
+      if ((rc = set_planes(d_r2, r2_size, r2))) return rc;
+    }
+    pp.out = r2;
+    prof_begin(MHMKC_STAGE_SSCAT);
+    e = mhm::launch_part_scatter(pp, nl, packed, stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "part_scatter");
+    cp.recs = r2;
+    prof_begin(MHMKC_STAGE_COUNT);
+    e = mhm::launch_count(cp, nl, packed, stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "count");
+    (void)hipEventRecord(ev_end, stream);
+    if ((e = hipMemcpyAsync(stats, d_stats.p, sizeof stats, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+      return hip_fail(e, "stats D2H");
+    if ((e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+      return hip_fail(e, "error flag D2H");
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "finish");
+    if (!(errf & 2u)) break;
+    errf &= ~2u;
+    if ((e = hipMemcpy(d_err.p, &errf, 4, hipMemcpyHostToDevice)) != hipSuccess) return hip_fail(e, "flag reset");
+    exact = true;
+    st.exact_reruns++;
+  }
   float ms = 0;
   if (hipEventElapsedTime(&ms, ev_begin, ev_end) == hipSuccess) st.ms_total = ms;
   prof_collect();
@@ -601,9 +685,13 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   h->nl = nl;
   h->nlo = nlo;
   h->packed = mhm::ext_packs(k, nl);
+  h->hbits = mhm::stored_hash_bits(k, nl, h->packed);
   int extra = 0;
   while ((1 << extra) < cfg->n_ranks) extra++;
-  h->cb = 8 + extra;
+#ifndef MHMKC_CB0
+#define MHMKC_CB0 8
+#endif
+  h->cb = MHMKC_CB0 + extra;
   h->nb = 1u << h->cb;
   h->own_lo = h->owner_lo(cfg->rank);
   h->own_hi = h->owner_lo(cfg->rank + 1);

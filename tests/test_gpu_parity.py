@@ -59,11 +59,25 @@ def test_edge_cases_vs_oracle(k):
 
 @pytest.mark.parametrize("k", [21, 63])
 def test_hot_kmer_saturation(k):
+    """One k-mer with > 65535 occurrences: u16 saturation, the LDS extension-counter clamp, and the
+    capped coarse/fine buckets overflowing into the exact (histogram) fallback."""
     b, o = hot_set()
-    got, _ = hip_table(b, o, k)
+    got, st = hip_table(b, o, k)
     exp = oracle_table(b, o, k)
     assert (exp.counts == 65535).any(), "fixture must saturate a count"
+    assert st["exact_reruns"] >= 1
     assert_tables_equal(got, exp, f"hot k={k}")
+
+
+@pytest.mark.parametrize("k", [21, 63, 99])
+def test_exact_partition_path(k, monkeypatch):
+    """The histogram-sized (exact) partition path, forced for ordinary input."""
+    b, o = synth_set(2500, 12000, 17 + k)
+    exp = oracle_table(b, o, k)
+    monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+    got, st = hip_table(b, o, k)
+    assert_tables_equal(got, exp, "exact path")
+    check_stats(st)
 
 
 @pytest.mark.parametrize("cutoff,dmin,dyn", [(0, 2, 0.9), (32, 2, 0.9), (20, 1, 0.9), (20, 5, 0.9), (20, 2, 0.5),

@@ -5,8 +5,11 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-timeout -k 10 900 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "pytest exit $?" >> gpurun_out/pytest_gpu.log
+timeout -k 10 900 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest exit $rc" >> gpurun_out/pytest_gpu.log
 tail -5 gpurun_out/pytest_gpu.log
+# test failures (1) still allow the measurements; a crash, abort or time limit ends the call
+if [ $rc -gt 1 ]; then echo "pytest ended abnormally ($rc)"; exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail gpurun_out/smoke.log; exit 1; }
 cat gpurun_out/smoke.log
 timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; tail -20 gpurun_out/bench.log; exit 1; }
