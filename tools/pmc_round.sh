@@ -18,6 +18,6 @@ GROUPS_DEFAULT=(
 )
 for grp in "${GROUPS_DEFAULT[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d $OUT/p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT.p$i.log 2>&1 || { echo "pass $i failed: $grp"; tail -5 $OUT.p$i.log; }
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d $OUT/p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py $ARGS > $OUT.p$i.log 2>&1 || { echo "pass $i failed: $grp"; tail -5 $OUT.p$i.log; exit 1; }
 done
 echo done
