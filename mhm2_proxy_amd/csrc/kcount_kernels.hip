@@ -35,6 +35,14 @@ constexpr int kGroups() {
 
 constexpr size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// Load through a pointer known to be global memory. Pointers read from device tables (PlaneSet of a
+// partition source) lose their address space and would otherwise become flat loads, which also count
+// against lgkmcnt and are waited for together with LDS operations.
+template <typename T>
+__device__ __forceinline__ T gload(const T *p) {
+  return *(const __attribute__((address_space(1))) T *)p;
+}
+
 // All LDS is carved from the one dynamic region at 16-byte aligned offsets (cdna_hip_programming.md
 // Guideline 17): fwd[NG] u64 | good[NG] u32 | start[NG] u32 | rest.
 template <int NL>
@@ -523,20 +531,24 @@ __device__ __forceinline__ uint32_t fine_digit(const uint64_t *rk, const Partiti
   return (uint32_t)((part_hash<NL>(key) >> (64 - p.coarse_bits - p.fine_bits)) & fmask);
 }
 
-// All W records of a thread are loaded before any is processed (W * 8 B * NL in flight per lane).
+// All W records of a thread are loaded before any is processed (W * 8 B * NL in flight per lane). The
+// loads are unconditional (lanes past the chunk end re-read its last record) so that no use of a loaded
+// value sits inside a branch: a conditional load whose value is consumed in its own branch makes the
+// compiler wait for it there, one load after the other. Callers check i < ch.count themselves.
 template <int NL, bool PACKED, int W>
 __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch, uint64_t (&rk)[W][NL],
                                            uint32_t (&re)[W]) {
+  uint32_t rx[W];
 #pragma unroll
   for (int j = 0; j < W; j++) {
     const uint32_t i = threadIdx.x + j * E_THREADS;
-    re[j] = 0;
-    if (i < ch.count) {
+    const uint64_t idx = ch.start + (i < ch.count ? i : ch.count - 1);
 #pragma unroll
-      for (int w = 0; w < NL; w++) rk[j][w] = src.w[w][ch.start + i];
-      re[j] = PACKED ? (uint32_t)(rk[j][NL - 1] & 63u) : src.ext[ch.start + i];
-    }
+    for (int w = 0; w < NL; w++) rk[j][w] = gload(src.w[w] + idx);
+    rx[j] = PACKED ? 0u : (uint32_t)gload(src.ext + idx);
   }
+#pragma unroll
+  for (int j = 0; j < W; j++) re[j] = PACKED ? (uint32_t)(rk[j][NL - 1] & 63u) : rx[j];
 }
 
 template <int NL, bool PACKED>
@@ -677,15 +689,15 @@ struct CountLds {
   int cap;         // multiple of 4: slots are probed in groups of 4
 };
 
-__device__ __forceinline__ bool reserve_slot(int *s_res, int *s_closed, int limit) {
-  if (__hip_atomic_load(s_closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-  const int old = atomicAdd(s_res, 1);
-  if (old >= limit) {
-    __hip_atomic_store(s_closed, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return false;
-  }
-  return true;
-}
+// Groups a key may probe before its record is deferred to the next sweep of its bucket.
+#ifndef MHMKC_CPROBE
+#define MHMKC_CPROBE 64
+#endif
+constexpr int C_PROBE = MHMKC_CPROBE;
+// First-group reads a lane keeps in flight in k_count.
+#ifndef MHMKC_CBATCH
+#define MHMKC_CBATCH 2
+#endif
 
 // The last key words of one 4-slot group (two ds_read_b128; the group is 32-byte aligned).
 __device__ __forceinline__ void read_group(const uint64_t *last, int g, uint64_t (&v)[4]) {
@@ -702,38 +714,49 @@ __device__ __forceinline__ bool rest_equal(const CountLds &t, int slot, const ui
   return eq;
 }
 
-// Grouped linear probing: a lane reads 4 slots at a time, so the loop a wave runs is bounded by the
-// longest probe of its 64 lanes counted in groups (one group nearly always), not in single slots.
-// Invariant: a key lies in group g' > g only if g had no empty slot when it was inserted; slots never
-// empty again, so an empty slot in g proves the key is absent from later groups.
-// Returns the slot holding key (inserting it if allowed), -1 when the table is closed and the key is
-// absent, -2 on an internal bound violation.
+// Result of looking at one group for key: >= 0 the slot holding it, -1 - i an empty slot i (and the key is
+// not in the group), G_FULL no empty slot and no key, G_BUSY a multi-word key is being written.
+constexpr int G_FULL = -8, G_BUSY = -9;
 template <int NL>
-__device__ int lds_insert_or_find(const CountLds &t, const uint64_t *key, int g, int *s_res, int *s_closed,
-                                  int limit) {
+__device__ __forceinline__ int examine_group(const CountLds &t, const uint64_t *key, int g, const uint64_t (&v)[4]) {
+  const uint64_t kl = key[NL - 1];
+  int found = -1, empty = -1;
+  bool busy = false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (found < 0 && v[i] == kl && (NL == 1 || rest_equal<NL>(t, 4 * g + i, key))) found = i;
+    if (v[i] == KEY_EMPTY && empty < 0) empty = i;
+    if (NL > 1 && v[i] == KEY_BUSY) busy = true;
+  }
+  if (found >= 0) return 4 * g + found;
+  if (busy) return G_BUSY;
+  return empty >= 0 ? -1 - empty : G_FULL;
+}
+
+// Find-or-insert of key, starting at group g whose examination (examine_group) gave r: the caller reads
+// the first group of all its records back to back and keeps only that verdict. Grouped linear probing
+// over at most C_PROBE groups; slots are claimed by a CAS on the last key word (multi-word keys: CAS to
+// BUSY, write the other words, publish the last word with a release store; readers re-read a BUSY group)
+// and are never freed within a sweep.
+// Returns the slot, -1 when the key is absent and all its C_PROBE groups are full (the record is deferred
+// to the next sweep), -2 on an internal bound violation.
+// Deferral is per key, never per occurrence: a key is deferred only when its C_PROBE groups held neither
+// the key nor an empty slot; slots only fill, so the key can never be inserted later in the sweep, and had
+// it been inserted earlier this lookup would have found it. Every occurrence of a key is therefore counted
+// in the same sweep; no occupancy counter is needed.
+template <int NL>
+__device__ int lds_insert(const CountLds &t, const uint64_t *key, int g, int r) {
   uint64_t *last = t.keys + (NL - 1) * t.cap;
   const int ng = t.cap >> 2;
   const uint64_t kl = key[NL - 1];
-  for (int iter = 0; iter < (1 << 22); iter++) {
-    uint64_t v[4];
-    read_group(last, g, v);
-    int empty = -1;
-    bool busy = false, found = false;
-    int slot = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if (!found && v[i] == kl && (NL == 1 || rest_equal<NL>(t, 4 * g + i, key))) {
-        found = true;
-        slot = 4 * g + i;
-      }
-      if (v[i] == KEY_EMPTY && empty < 0) empty = i;
-      if (NL > 1 && v[i] == KEY_BUSY) busy = true;
-    }
-    if (found) return slot;
-    if (busy) continue;  // a writer publishes within its own iteration
-    if (empty >= 0) {
-      if (!reserve_slot(s_res, s_closed, limit)) return -1;
-      const int sl = 4 * g + empty;
+  int probed = 0;
+  for (int iter = 0; iter < (1 << 20); iter++) {
+    if (r >= 0) return r;
+    if (r == G_FULL) {
+      if (++probed == C_PROBE) return -1;
+      g = (g + 1 == ng) ? 0 : g + 1;
+    } else if (r != G_BUSY) {
+      const int sl = 4 * g + (-1 - r);
       const uint64_t want = (NL == 1) ? kl : KEY_BUSY;
       const uint64_t old = atomicCAS((unsigned long long *)&last[sl], (unsigned long long)KEY_EMPTY,
                                      (unsigned long long)want);
@@ -745,70 +768,75 @@ __device__ int lds_insert_or_find(const CountLds &t, const uint64_t *key, int g,
         }
         return sl;
       }
-      atomicSub(s_res, 1);
-      continue;  // the slot was just taken: re-read the group
+      if (NL == 1 && old == kl) return sl;  // the winner inserted this very key
+      // otherwise the slot was just taken: look at the group again
     }
-    g = (g + 1 == ng) ? 0 : g + 1;
+    uint64_t v[4];
+    read_group(last, g, v);
+    r = examine_group<NL>(t, key, g, v);
   }
   return -2;
 }
 
-template <int NL>
-__device__ int lds_find(const CountLds &t, const uint64_t *key, int g) {
-  const uint64_t *last = t.keys + (NL - 1) * t.cap;
-  const int ng = t.cap >> 2;
-  const uint64_t kl = key[NL - 1];
-  for (int iter = 0; iter < ng + 1; iter++) {
-    uint64_t v[4];
-    read_group(last, g, v);
-    bool empty = false;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if (v[i] == kl && (NL == 1 || rest_equal<NL>(t, 4 * g + i, key))) return 4 * g + i;
-      empty |= (v[i] == KEY_EMPTY);
-    }
-    if (empty) return -1;
-    g = (g + 1 == ng) ? 0 : g + 1;
-  }
-  return -1;
-}
-
-// Saturating-at-the-decision-level extension counter: 16-bit halves of a u32, incremented with one
-// LDS atomic. A half that reaches 0xC000 is clamped back to 0x8000 by CAS. Exact for the reference's
-// get_ext, which only compares counters against thresholds <= max(6553, dmin_thres) <= 32768
-// (DESIGN.md §3.4); the reference saturates the same counters at 65535 (kcount_cpu.cpp:148-164).
-__device__ __forceinline__ void ext_inc_checked(uint32_t *p, int half) {
-  const uint32_t inc = half ? 0x10000u : 1u;
-  const uint32_t old = atomicAdd(p, inc);
-  const uint32_t v = half ? (old >> 16) : (old & 0xffffu);
-  if (v >= 0xC000u) {
-    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (int iter = 0; iter < 4096; iter++) {
-      const uint32_t f = half ? (cur >> 16) : (cur & 0xffffu);
-      if (f < 0xC000u) break;
-      const uint32_t nw = half ? ((cur & 0xffffu) | 0x80000000u) : ((cur & 0xffff0000u) | 0x8000u);
-      const uint32_t prev = atomicCAS(p, cur, nw);
-      if (prev == cur) break;
-      cur = prev;
-    }
-  }
-}
-
 // insert_supermer_from_read's per-k-mer update (src/kcount/kcount_cpu.cpp:343-352): count + 1,
-// left/right extension + 1 when they are A/C/G/T. An extension counter never exceeds its k-mer's count,
-// so while the count is below 0xBFFF the extension adds need no return value (no clamp possible; lanes
-// racing past the boundary overshoot 0xC000 by at most the workgroup size before a checked add clamps).
-__device__ __forceinline__ void lds_update(const CountLds &t, int slot, uint32_t e) {
+// left/right extension + 1 when they are A/C/G/T (ExtCounts::inc ignores the rest, :152-164).
+// Extension counters are 16-bit halves of u32 LDS words, added without a return value; the old count
+// is returned for the saturation check (lds_clamp).
+__device__ __forceinline__ uint32_t lds_add(const CountLds &t, int slot, uint32_t e) {
+#if MHMKC_EXP_NORTN
+  atomicAdd(&t.cnt[slot], 1u);
+  const uint32_t old = 0;
+#else
   const uint32_t old = atomicAdd(&t.cnt[slot], 1u);
+#endif
+#if MHMKC_EXP_NOEXT
+  return old;
+#endif
   const int l = (int)((e >> 3) & 7u), r = (int)(e & 7u);
-  if (old < 0xBFFFu) {
-    if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
-    if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
-  } else {
-    if (l < 4) ext_inc_checked(&t.ext[(l >> 1) * t.cap + slot], l & 1);
-    if (r < 4) ext_inc_checked(&t.ext[(2 + (r >> 1)) * t.cap + slot], r & 1);
+  if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
+  if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
+  return old;
+}
+
+// Saturation at the decision level: a 16-bit half that reached 0xC000 is CAS-clamped back to 0x8000.
+// Exact for the reference's get_ext, which only compares counters against thresholds
+// <= max((int)(0.1 * 65535), dmin_thres) <= 32768, and whose top base is unique whenever it is chosen
+// (DESIGN.md §3.4); the reference saturates the same counters at 65535 (kcount_cpu.cpp:148-164).
+// When to check: a half never exceeds its k-mer's count, and between a lane's count add and its own
+// extension add fewer than S = records per round other adds happen (the round barrier closes the
+// round). So a lane whose count add returned old < 0xC000 - 2S cannot push a half to 0xC000, and every
+// add that does is followed by its own lane's clamp before another S adds: a half stays below
+// 0xC000 + S < 0x10000 and never carries into its neighbour.
+__device__ __forceinline__ void ext_clamp(uint32_t *p, int half) {
+  uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int iter = 0; iter < 4096; iter++) {
+    const uint32_t f = half ? (cur >> 16) : (cur & 0xffffu);
+    if (f < 0xC000u) break;
+    const uint32_t nw = half ? ((cur & 0xffffu) | 0x80000000u) : ((cur & 0xffff0000u) | 0x8000u);
+    const uint32_t prev = atomicCAS(p, cur, nw);
+    if (prev == cur) break;
+    cur = prev;
   }
 }
+
+__device__ __forceinline__ void lds_clamp(const CountLds &t, int slot, uint32_t e) {
+  const int l = (int)((e >> 3) & 7u), r = (int)(e & 7u);
+  if (l < 4) ext_clamp(&t.ext[(l >> 1) * t.cap + slot], l & 1);
+  if (r < 4) ext_clamp(&t.ext[(2 + (r >> 1)) * t.cap + slot], r & 1);
+}
+
+// Diagnostic phase stamps of k_count (MHMKC_STAMP builds only): wave cycles per phase, summed into
+// stats[8..15]: clear, load wait, insert/update, round barrier, overflow handling, finalize.
+#ifndef MHMKC_STAMP
+#define MHMKC_STAMP 0
+#endif
+#if MHMKC_STAMP
+#define STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define STAMP_ADD(i, v) st_acc[i] += (v)
+#else
+#define STAMP(var)
+#define STAMP_ADD(i, v)
+#endif
 
 // Final decision for one table slot: insert_into_local_hashtable (src/kcount/kcount_cpu.cpp:503-517):
 // count < 2 -> purged; left/right = get_ext(count) (kcount_cpu.cpp:173-182, with the exact double
@@ -864,11 +892,13 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned long long *s_u64 = (unsigned long long *)(t.ext + 4 * t.cap);
   unsigned long long &s_gbase = s_u64[0];
   unsigned long long *s_red = s_u64 + 1;  // [3]
-  int &s_res = *(int *)(s_u64 + 4);
-  int &s_closed = *((int *)(s_u64 + 4) + 1);
+  unsigned int *s_nmiss = (unsigned int *)(s_u64 + 4);  // [2] miss-list lengths, alternating rounds
   unsigned int &s_ovf = *(unsigned int *)(s_u64 + 5);
   unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
   unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
+  // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
+  uint64_t *s_mkey = (uint64_t *)(smem + count_table_bytes(NL));
+  uint32_t *s_me = (uint32_t *)(s_mkey + NL * miss_cap(NL));
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -884,7 +914,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 
   uint32_t sweeps = 0;
   unsigned long long my_occ = 0, my_purged = 0, my_sum = 0, my_out = 0;
+#if MHMKC_STAMP
+  uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
   while (true) {
+    STAMP(t_sw0);
     {  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
       uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
       const int n_ones = t.cap * 8 / 16;
@@ -894,77 +928,152 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       for (int i = tid; i < n_zeros; i += C_THREADS) zeros[i] = make_uint4(0, 0, 0, 0);
     }
     if (tid == 0) {
-      s_res = 0;
-      s_closed = 0;
+      s_nmiss[0] = 0;
+      s_nmiss[1] = 0;
       s_ovf = 0;
       s_err = 0;
     }
     __syncthreads();
+    STAMP(t_sw1);
+    STAMP_ADD(0, t_sw1 - t_sw0);
 
     // R records per thread per round, the next round prefetched into registers, so that every CU keeps
-    // R * 8 KB of record loads in flight.
+    // R * 8 KB of record loads in flight. A round has two phases:
+    //   A. every lane looks its records up in their home group; found keys are counted at once, the
+    //      others (new keys, keys displaced by a full group) are appended to a miss list in LDS;
+    //   B. after a barrier the miss list is worked off densely, one record per lane (probing, CAS insert,
+    //      counting), so the ~20 % of records that need the slow path no longer hold every wave of the
+    //      workgroup in a divergent loop.
     constexpr int R = count_rpt<NL>();
     constexpr uint32_t NONE = 0xffffffffu;
-    const uint64_t RND = (uint64_t)R * C_THREADS;
+    constexpr uint32_t RND = (uint32_t)R * C_THREADS;
+    constexpr uint32_t HOT = 0xC000u - 2u * RND;  // see ext_clamp
+    static_assert(HOT > 0x8000u, "round too large for the extension-counter clamp");
+    constexpr int MC = miss_cap(NL);
     const int ng = t.cap >> 2;
+    const uint64_t *last = t.keys + (NL - 1) * t.cap;
+    // Raw records of the next round, loaded unconditionally (lanes past the end re-read the last record)
+    // and split into key / ext only when the round starts, so the loads stay in flight (see load_chunk).
     uint64_t nk[R][NL];
-    uint32_t ne[R];
+    uint32_t nx[R];
+    auto prefetch = [&](uint64_t first) {
 #pragma unroll
-    for (int j = 0; j < R; j++) {
-      const uint64_t i = (uint64_t)tid + (uint64_t)j * C_THREADS;
-      ne[j] = NONE;
-      if (i < n) load_record<NL, PACKED>(ps, i, low_mask, nk[j], ne[j]);
-    }
-    for (uint64_t r0 = 0; r0 < n; r0 += RND) {
+      for (int j = 0; j < R; j++) {
+        const uint64_t i = first + (uint64_t)tid + (uint64_t)j * C_THREADS;
+        const uint64_t idx = i < n ? i : n - 1;
+#pragma unroll
+        for (int w = 0; w < NL; w++) nk[j][w] = ps.w[w][idx];
+        nx[j] = PACKED ? 0u : (uint32_t)ps.ext[idx];
+      }
+    };
+    if (n) prefetch(0);
+    int rnd = 0;
+    for (uint64_t r0 = 0; r0 < n; r0 += RND, rnd++) {
+      STAMP(t_r0);
       uint64_t ck[R][NL];
       uint32_t ce[R];
 #pragma unroll
       for (int j = 0; j < R; j++) {
-        ce[j] = ne[j];
+        const bool valid = r0 + tid + (uint64_t)j * C_THREADS < n;
 #pragma unroll
         for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
-      }
-#pragma unroll
-      for (int j = 0; j < R; j++) {
-        const uint64_t i = r0 + RND + (uint64_t)tid + (uint64_t)j * C_THREADS;
-        ne[j] = NONE;
-        if (i < n) load_record<NL, PACKED>(ps, i, low_mask, nk[j], ne[j]);
-      }
-      uint32_t tent = 0;
-      int g0[R];
-#pragma unroll
-      for (int j = 0; j < R; j++) {
-        g0[j] = 0;
-        if (ce[j] != NONE) {
-          g0[j] = (int)(((uint64_t)slot_hash<NL>(ck[j]) * (uint64_t)ng) >> 32);
-          const int slot = lds_insert_or_find<NL>(t, ck[j], g0[j], &s_res, &s_closed, p.limit);
-          if (slot >= 0)
-            lds_update(t, slot, ce[j]);
-          else if (slot == -1)
-            tent |= 1u << j;
-          else
-            s_err = 1;
+        if (PACKED) {
+          ce[j] = valid ? (uint32_t)(ck[j][NL - 1] & low_mask) : NONE;
+          ck[j][NL - 1] &= ~low_mask;
+        } else {
+          ce[j] = valid ? nx[j] : NONE;
         }
       }
+#if MHMKC_STAMP
+#pragma unroll
+      for (int j = 0; j < R; j++) asm volatile("" ::"v"(ck[j][0]), "v"(ce[j]));
+#endif
+      STAMP(t_r1);
+      STAMP_ADD(1, t_r1 - t_r0);
+      if (r0 + RND < n) prefetch(r0 + RND);
+      unsigned int *nmiss = &s_nmiss[rnd & 1];
+      // A. home-group lookups
+      uint32_t old[R], defer = 0, okm = 0;
+      int slot[R];
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        old[j] = 0;
+        slot[j] = -3;
+        if (ce[j] == NONE) continue;
+        const int g = (int)(((uint64_t)slot_hash<NL>(ck[j]) * (uint64_t)ng) >> 32);
+        uint64_t v[4];
+        read_group(last, g, v);
+        int r = examine_group<NL>(t, ck[j], g, v);
+        if (r < 0) {
+          const unsigned int q = atomicAdd(nmiss, 1u);
+          if (q < (unsigned int)MC) {  // handed to phase B
+#pragma unroll
+            for (int w = 0; w < NL; w++) s_mkey[w * MC + q] = ck[j][w];
+            s_me[q] = ce[j];
+            continue;
+          }
+          r = lds_insert<NL>(t, ck[j], g, r);  // list full (first rounds of a bucket): in place
+          if (r == -1) {
+            defer |= 1u << j;
+            continue;
+          }
+          if (r < 0) {
+            s_err = 1;
+            continue;
+          }
+        }
+        slot[j] = r;
+        old[j] = lds_add(t, r, ce[j]);
+        okm |= 1u << j;
+      }
+#pragma unroll
+      for (int j = 0; j < R; j++)
+        if (((okm >> j) & 1u) && old[j] >= HOT) lds_clamp(t, slot[j], ce[j]);
+      STAMP(t_r2);
+      STAMP_ADD(2, t_r2 - t_r1);
       __syncthreads();
-      if (tent) {
-        // The table closed this round: keys inserted concurrently are visible now; a key still absent
-        // is never inserted in this sweep, so all its occurrences go to the next sweep together.
+      STAMP(t_r3);
+      STAMP_ADD(3, t_r3 - t_r2);
+      // deferred records go back to the front of the bucket, to positions every lane has consumed
+      // (< r0 + RND), for the next sweep
+      if (defer) {
 #pragma unroll
         for (int j = 0; j < R; j++) {
-          if ((tent >> j) & 1u) {
-            const int slot = lds_find<NL>(t, ck[j], g0[j]);
-            if (slot >= 0) {
-              lds_update(t, slot, ce[j]);
-            } else {
-              const unsigned int pos = atomicAdd(&s_ovf, 1u);
-              store_record<NL, PACKED>(ps, pos, ck[j], ce[j]);  // pos < r0 + RND: already consumed
-            }
+          if ((defer >> j) & 1u) {
+            const unsigned int pos = atomicAdd(&s_ovf, 1u);
+            store_record<NL, PACKED>(ps, pos, ck[j], ce[j]);
           }
         }
       }
+      // B. the miss list, densely
+      const unsigned int M = min(*nmiss, (unsigned int)MC);
+      if (tid == 0) s_nmiss[(rnd + 1) & 1] = 0;  // the next round's list (the previous one's is done)
+      for (unsigned int q = tid; q < M; q += C_THREADS) {
+        uint64_t key[NL];
+#pragma unroll
+        for (int w = 0; w < NL; w++) key[w] = s_mkey[w * MC + q];
+        const uint32_t e = s_me[q];
+        const int g = (int)(((uint64_t)slot_hash<NL>(key) * (uint64_t)ng) >> 32);
+        uint64_t v[4];
+        read_group(last, g, v);
+        const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
+        if (r >= 0) {
+          if (lds_add(t, r, e) >= HOT) lds_clamp(t, r, e);
+        } else if (r == -1) {
+          const unsigned int pos = atomicAdd(&s_ovf, 1u);
+          store_record<NL, PACKED>(ps, pos, key, e);
+        } else {
+          s_err = 1;
+        }
+      }
+      __syncthreads();
+#if MHMKC_STAMP
+      const uint64_t t_r4 = __builtin_amdgcn_s_memtime();
+      STAMP_ADD(4, t_r4 - t_r3);
+#endif
     }
     __syncthreads();
+    STAMP(t_f0);
 
     // finalize in one pass: decisions in registers, wave-prefix offsets, one global reservation
     uint32_t occ = 0, surv_mask = 0;
@@ -1021,6 +1130,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     my_purged += occ - mine;
     my_sum += sum;
     __syncthreads();
+    STAMP(t_f1);
+    STAMP_ADD(5, t_f1 - t_f0);
     if (s_err && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
     if (s_ovf == 0) break;
     n = s_ovf;
@@ -1030,6 +1141,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     __syncthreads();
   }
 
+#if MHMKC_STAMP
+  if (lane == 0)
+    for (int i = 0; i < 6; i++) atomicAdd(&p.stats[8 + i], (unsigned long long)st_acc[i]);
+#endif
   // block reduction of the statistics
   my_occ = wave_sum_u64(my_occ);
   my_purged = wave_sum_u64(my_purged);

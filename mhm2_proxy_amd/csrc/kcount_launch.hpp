@@ -70,7 +70,6 @@ struct CountParams {
   uint32_t n_buckets;
   int k;
   int cap;                            // LDS table slots
-  int limit;                          // max occupied slots before the table closes
   int dmin_thres;
   double dyn_mult;                    // 1.0 - DYN_MIN_DEPTH, computed in double on the host
   int nlo;                            // output words per key
@@ -91,6 +90,7 @@ enum {
   STAT_MAXBUCKET = 5,
   STAT_N = 8
 };
+constexpr int STAT_ALLOC = 16;  // stats[8..13]: k_count phase stamps in MHMKC_STAMP builds
 
 constexpr int E_THREADS = 256;
 constexpr int E_NSUB = 8;
@@ -113,8 +113,19 @@ inline int stored_hash_bits(int k, int nl, bool packed) {
 #endif
 inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : 2048; }
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS).
-inline int count_cap(int nl) { return nl == 1 ? 5120 : nl == 2 ? 4000 : nl == 3 ? 3264 : 2752; }
-inline size_t count_lds_bytes(int nl) { return (size_t)count_cap(nl) * (8 * nl + 4 + 16) + 128; }
+// k_count LDS: table (keys, count, 4 extension words per slot) + 128 B of scalars + the miss list of a
+// round's phase B (key words + ext code per entry); together <= 160 KiB.
+__host__ __device__ constexpr int count_cap(int nl) { return nl == 1 ? 5120 : nl == 2 ? 4000 : nl == 3 ? 3264 : 2752; }
+__host__ __device__ constexpr size_t count_table_bytes(int nl) { return (size_t)count_cap(nl) * (8 * nl + 4 + 16) + 128; }
+__host__ __device__ constexpr int miss_cap(int nl) {
+  return (int)(((163840 - count_table_bytes(nl)) / (8 * nl + 4)) & ~(size_t)63);
+}
+__host__ __device__ constexpr size_t count_lds_bytes(int nl) {
+  return count_table_bytes(nl) + (size_t)miss_cap(nl) * (8 * nl + 4);
+}
+static_assert(count_lds_bytes(1) <= 163840 && count_lds_bytes(2) <= 163840 && count_lds_bytes(3) <= 163840 &&
+                  count_lds_bytes(4) <= 163840,
+              "k_count LDS budget");
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);
 // total counted windows sum(max(0, L - k - 1)) of a batch, added to *out

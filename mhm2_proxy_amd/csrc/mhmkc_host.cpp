@@ -517,7 +517,6 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.k = k;
   cp.cap = mhm::count_cap(nl);
   if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
-  cp.limit = cp.cap * 9 / 10;
   cp.dmin_thres = cfg.dmin_thres;
   cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
   cp.nlo = nlo;
@@ -529,13 +528,13 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.stats = d_stats.as<unsigned long long>();
 
   bool exact = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
-  unsigned long long stats[mhm::STAT_N];
+  unsigned long long stats[mhm::STAT_ALLOC];
   unsigned int errf = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     mhm::PlaneSet r2{};
     prof_begin(MHMKC_STAGE_OTHER);
     e = hipMemsetAsync(d_out_cursor.p, 0, 8, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_N, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_ALLOC, stream);
     if (e == hipSuccess && exact) e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
     if (e == hipSuccess && !exact)
       e = mhm::launch_init_fine(d_cfit, d_cfit + no, no, fb, d_fine_base.as<unsigned long long>(),
@@ -588,6 +587,14 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   finished = true;
   if (errf & 1u) return fail(MHMKC_EBADCHAR, "input byte with a base code > 4 (not A,C,G,T,N)");
   if (stats[mhm::STAT_N - 1]) return fail(MHMKC_EHIP, "internal: LDS probe bound exceeded");
+  if (getenv("MHMKC_PRINT_STAMPS")) {  // k_count phase cycles of an MHMKC_STAMP build (diagnostics)
+    const char *names[6] = {"clear", "loadwait", "insert", "barrier", "overflow", "finalize"};
+    double tot = 0;
+    for (int i = 0; i < 6; i++) tot += (double)stats[8 + i];
+    fprintf(stderr, "k_count stamps:");
+    for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f%%", names[i], tot > 0 ? 100.0 * stats[8 + i] / tot : 0.0);
+    fprintf(stderr, " (total %.3g wave-cycles)\n", tot);
+  }
   st.distinct = stats[mhm::STAT_DISTINCT];
   st.n_out = stats[mhm::STAT_NOUT];
   st.purged = stats[mhm::STAT_PURGED];
@@ -715,7 +722,7 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     h->own_stream = true;
   }
   if ((e = hipEventCreate(&h->ev_begin)) != hipSuccess || (e = hipEventCreate(&h->ev_end)) != hipSuccess ||
-      (e = h->d_err.ensure(16)) != hipSuccess || (e = h->d_stats.ensure(8 * mhm::STAT_N)) != hipSuccess ||
+      (e = h->d_err.ensure(16)) != hipSuccess || (e = h->d_stats.ensure(8 * mhm::STAT_ALLOC)) != hipSuccess ||
       (e = hipMemset(h->d_err.p, 0, 16)) != hipSuccess) {
     g_create_error = std::string("init: ") + hipGetErrorString(e);
     mhmkc_destroy(h);
