@@ -666,15 +666,22 @@ __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, uns
 // count: LDS open-addressing hash table per fine bucket
 
 // Records per thread per round of k_count (register budget: 1024 threads -> <= 128 VGPRs).
+#ifndef MHMKC_CRPT
+#define MHMKC_CRPT 4
+#endif
 template <int NL>
 constexpr int count_rpt() {
-  return NL == 1 ? 4 : 2;
+  return NL == 1 ? MHMKC_CRPT : 2;
 }
 
 // LDS slot hash of k_count. All keys of a fine bucket share their top MurmurHash3 bits, so the slot
 // uses an independent multiplicative mix of the key words (performance only; any function is correct).
 template <int NL>
 __device__ __forceinline__ uint32_t slot_hash(const uint64_t *key) {
+  if (NL == 1) {  // 32-bit mix of the two halves (two quarter-rate multiplies instead of a 64-bit product)
+    const uint32_t x = (uint32_t)(key[0] >> 32) * 0x9E3779B1u + (uint32_t)key[0] * 0x85EBCA77u;
+    return x ^ (x >> 15);
+  }
   uint64_t h = key[0] * 0x9E3779B97F4A7C15ull;
 #pragma unroll
   for (int w = 1; w < NL; w++) h = (h ^ (h >> 31) ^ key[w]) * 0xC2B2AE3D27D4EB4Full;
@@ -902,22 +909,61 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const uint32_t b = blockIdx.x;
-  const uint64_t base = p.bucket_base[b];
-  uint64_t n = p.bucket_end[b] - base;
-  const uint64_t n0 = n;
   const uint64_t low_mask = (1ull << (EXT_BITS + p.hbits)) - 1;
-  PlaneSet ps = p.recs;
-#pragma unroll
-  for (int w = 0; w < NL; w++) ps.w[w] += base;
-  if (!PACKED) ps.ext += base;
 
-  uint32_t sweeps = 0;
-  unsigned long long my_occ = 0, my_purged = 0, my_sum = 0, my_out = 0;
+  constexpr int R = count_rpt<NL>();
+  constexpr uint32_t NONE = 0xffffffffu;
+  constexpr uint32_t RND = (uint32_t)R * C_THREADS;
+  constexpr uint32_t HOT = 0xC000u - 2u * RND;  // see ext_clamp
+  static_assert(HOT > 0x8000u, "round too large for the extension-counter clamp");
+  constexpr int MC = miss_cap(NL);
+  constexpr int C_BATCH = MHMKC_CBATCH < R ? MHMKC_CBATCH : R;
+  static_assert(R % C_BATCH == 0, "batch must divide the records per round");
+  const int ng = t.cap >> 2;
+  const uint64_t *last = t.keys + (NL - 1) * t.cap;
+
+  // Persistent workgroups: workgroup w counts buckets w, w + G, w + 2G, ... (G = grid size). The first
+  // round of the next bucket is loaded while the current one is finalized, so no bucket starts with an
+  // exposed HBM round trip.
+  // Raw records of the next round, loaded unconditionally (lanes past the end re-read the last record)
+  // and split into key / ext only when the round starts, so the loads stay in flight (see load_chunk).
+  uint64_t nk[R][NL];
+  uint32_t nx[R];
+  auto prefetch = [&](const PlaneSet &src, uint32_t cnt, uint32_t first) {
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      const uint32_t i = first + (uint32_t)tid + (uint32_t)j * C_THREADS;
+      const uint32_t idx = i < cnt ? i : cnt - 1;
+#pragma unroll
+      for (int w = 0; w < NL; w++) nk[j][w] = src.w[w][idx];
+      nx[j] = PACKED ? 0u : (uint32_t)src.ext[idx];
+    }
+  };
+  auto bucket = [&](uint32_t bb, PlaneSet &src, uint32_t &cnt) {
+    const uint64_t base = p.bucket_base[bb];
+    cnt = (uint32_t)(p.bucket_end[bb] - base);  // < 2^32 records per bucket (host check)
+    src = p.recs;
+#pragma unroll
+    for (int w = 0; w < NL; w++) src.w[w] += base;
+    if (!PACKED) src.ext += base;
+  };
+
+  unsigned long long my_occ = 0, my_purged = 0, my_sum = 0, my_out = 0, my_sweeps = 0, my_maxb = 0;
 #if MHMKC_STAMP
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
 #endif
-  while (true) {
+  uint32_t b = blockIdx.x;
+  PlaneSet ps;
+  uint32_t n;
+  bucket(b, ps, n);
+  if (n) prefetch(ps, n, 0);
+  while (true) {  // buckets
+  my_maxb = my_maxb > n ? my_maxb : n;
+  bool first_sweep = true;
+  uint32_t nb_next = 0;
+  PlaneSet ps_next;
+  const uint32_t b_next = b + gridDim.x;
+  while (true) {  // sweeps of bucket b
     STAMP(t_sw0);
     {  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
       uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
@@ -944,37 +990,16 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     //   B. after a barrier the miss list is worked off densely, one record per lane (probing, CAS insert,
     //      counting), so the ~20 % of records that need the slow path no longer hold every wave of the
     //      workgroup in a divergent loop.
-    constexpr int R = count_rpt<NL>();
-    constexpr uint32_t NONE = 0xffffffffu;
-    constexpr uint32_t RND = (uint32_t)R * C_THREADS;
-    constexpr uint32_t HOT = 0xC000u - 2u * RND;  // see ext_clamp
-    static_assert(HOT > 0x8000u, "round too large for the extension-counter clamp");
-    constexpr int MC = miss_cap(NL);
-    const int ng = t.cap >> 2;
-    const uint64_t *last = t.keys + (NL - 1) * t.cap;
-    // Raw records of the next round, loaded unconditionally (lanes past the end re-read the last record)
-    // and split into key / ext only when the round starts, so the loads stay in flight (see load_chunk).
-    uint64_t nk[R][NL];
-    uint32_t nx[R];
-    auto prefetch = [&](uint64_t first) {
-#pragma unroll
-      for (int j = 0; j < R; j++) {
-        const uint64_t i = first + (uint64_t)tid + (uint64_t)j * C_THREADS;
-        const uint64_t idx = i < n ? i : n - 1;
-#pragma unroll
-        for (int w = 0; w < NL; w++) nk[j][w] = ps.w[w][idx];
-        nx[j] = PACKED ? 0u : (uint32_t)ps.ext[idx];
-      }
-    };
-    if (n) prefetch(0);
+    if (!first_sweep && n) prefetch(ps, n, 0);  // a re-sweep reads the deferred records
+    first_sweep = false;
     int rnd = 0;
-    for (uint64_t r0 = 0; r0 < n; r0 += RND, rnd++) {
+    for (uint32_t r0 = 0; r0 < n; r0 += RND, rnd++) {
       STAMP(t_r0);
       uint64_t ck[R][NL];
       uint32_t ce[R];
 #pragma unroll
       for (int j = 0; j < R; j++) {
-        const bool valid = r0 + tid + (uint64_t)j * C_THREADS < n;
+        const bool valid = r0 + (uint32_t)tid + (uint32_t)j * C_THREADS < n;
 #pragma unroll
         for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
         if (PACKED) {
@@ -990,40 +1015,59 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #endif
       STAMP(t_r1);
       STAMP_ADD(1, t_r1 - t_r0);
-      if (r0 + RND < n) prefetch(r0 + RND);
+      if (r0 + RND < n) prefetch(ps, n, r0 + RND);
+#if MHMKC_EXP_LOADONLY
+      {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < R; j++) acc ^= ce[j] ^ (uint32_t)ck[j][0];
+        if (acc == 0x12345u) s_err = 1;
+        __syncthreads();
+        continue;
+      }
+#endif
       unsigned int *nmiss = &s_nmiss[rnd & 1];
-      // A. home-group lookups
+      // A. home-group lookups: the first groups of all R records are read in batches of C_BATCH (the
+      //    reads of a batch in flight together), then found records are counted, missed ones listed.
       uint32_t old[R], defer = 0, okm = 0;
-      int slot[R];
+      int slot[R], g[R];
+#pragma unroll
+      for (int j0 = 0; j0 < R; j0 += C_BATCH) {
+        uint64_t v[C_BATCH][4];
+#pragma unroll
+        for (int j = j0; j < j0 + C_BATCH; j++) {
+          g[j] = (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
+          read_group(last, g[j], v[j - j0]);  // also for an invalid lane: harmless, keeps the batch uniform
+        }
+#pragma unroll
+        for (int j = j0; j < j0 + C_BATCH; j++) slot[j] = examine_group<NL>(t, ck[j], g[j], v[j - j0]);
+      }
 #pragma unroll
       for (int j = 0; j < R; j++) {
         old[j] = 0;
-        slot[j] = -3;
-        if (ce[j] == NONE) continue;
-        const int g = (int)(((uint64_t)slot_hash<NL>(ck[j]) * (uint64_t)ng) >> 32);
-        uint64_t v[4];
-        read_group(last, g, v);
-        int r = examine_group<NL>(t, ck[j], g, v);
+        if (ce[j] == NONE) {
+          slot[j] = -3;
+          continue;
+        }
+        int r = slot[j];
         if (r < 0) {
           const unsigned int q = atomicAdd(nmiss, 1u);
           if (q < (unsigned int)MC) {  // handed to phase B
 #pragma unroll
             for (int w = 0; w < NL; w++) s_mkey[w * MC + q] = ck[j][w];
             s_me[q] = ce[j];
+            slot[j] = -3;
             continue;
           }
-          r = lds_insert<NL>(t, ck[j], g, r);  // list full (first rounds of a bucket): in place
-          if (r == -1) {
-            defer |= 1u << j;
-            continue;
-          }
-          if (r < 0) {
-            s_err = 1;
-            continue;
-          }
+          r = lds_insert<NL>(t, ck[j], g[j], r);  // list full (first rounds of a bucket): in place
+          if (r == -1) defer |= 1u << j;
+          if (r == -2) s_err = 1;
+          slot[j] = r;
+          if (r < 0) continue;
         }
-        slot[j] = r;
+#if !MHMKC_EXP_NOATOM
         old[j] = lds_add(t, r, ce[j]);
+#endif
         okm |= 1u << j;
       }
 #pragma unroll
@@ -1046,14 +1090,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         }
       }
       // B. the miss list, densely
+#if MHMKC_EXP_NOB
+      const unsigned int M = 0;
+#else
       const unsigned int M = min(*nmiss, (unsigned int)MC);
+#endif
       if (tid == 0) s_nmiss[(rnd + 1) & 1] = 0;  // the next round's list (the previous one's is done)
       for (unsigned int q = tid; q < M; q += C_THREADS) {
         uint64_t key[NL];
 #pragma unroll
         for (int w = 0; w < NL; w++) key[w] = s_mkey[w * MC + q];
         const uint32_t e = s_me[q];
-        const int g = (int)(((uint64_t)slot_hash<NL>(key) * (uint64_t)ng) >> 32);
+        const int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
         uint64_t v[4];
         read_group(last, g, v);
         const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
@@ -1074,6 +1122,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     }
     __syncthreads();
     STAMP(t_f0);
+    // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
+    const bool last_sweep = s_ovf == 0;
+    if (last_sweep && b_next < p.n_buckets) {
+      bucket(b_next, ps_next, nb_next);
+      if (nb_next) prefetch(ps_next, nb_next, 0);
+    }
 
     // finalize in one pass: decisions in registers, wave-prefix offsets, one global reservation
     uint32_t occ = 0, surv_mask = 0;
@@ -1088,7 +1142,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != KEY_EMPTY) {
         occ++;
         sum += t.cnt[slot];
+#if !MHMKC_EXP_NOFIN
         if (slot_survives(t, slot, p, c16[j], L[j], R_[j])) surv_mask |= 1u << j;
+#endif
       }
     }
     const uint32_t mine = __popc(surv_mask);
@@ -1133,13 +1189,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP(t_f1);
     STAMP_ADD(5, t_f1 - t_f0);
     if (s_err && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
-    if (s_ovf == 0) break;
+    if (last_sweep) break;
     n = s_ovf;
-    sweeps++;
+    my_sweeps++;
     // overflow records were written by this workgroup: make them visible to its own loads
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
     __syncthreads();
-  }
+  }  // sweeps
+  if (b_next >= p.n_buckets) break;
+  b = b_next;  // the finalize above ended with a barrier: the table may be cleared for the next bucket
+  ps = ps_next;
+  n = nb_next;
+  }  // buckets
 
 #if MHMKC_STAMP
   if (lane == 0)
@@ -1166,8 +1227,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     atomicAdd(&p.stats[STAT_PURGED], s_red[1]);
     atomicAdd(&p.stats[STAT_COUNTSUM], s_red[2]);
     atomicAdd(&p.stats[STAT_NOUT], my_out);
-    if (sweeps) atomicAdd(&p.stats[STAT_SWEEPS], (unsigned long long)sweeps);
-    atomicMax(&p.stats[STAT_MAXBUCKET], (unsigned long long)n0);
+    // sweep count and largest bucket are the same in every wave of the workgroup
+    if (my_sweeps) atomicAdd(&p.stats[STAT_SWEEPS], my_sweeps);
+    atomicMax(&p.stats[STAT_MAXBUCKET], my_maxb);
   }
 }
 
@@ -1237,7 +1299,8 @@ static hipError_t do_count(const CountParams &p, hipStream_t s) {
   const size_t lds = count_lds_bytes(NL);
   hipError_t e = allow_lds(k_count<NL, PK>, lds);
   if (e != hipSuccess) return e;
-  k_count<NL, PK><<<dim3(p.n_buckets), dim3(C_THREADS), lds, s>>>(p);
+  const uint32_t grid = p.grid && p.grid < p.n_buckets ? p.grid : p.n_buckets;
+  k_count<NL, PK><<<dim3(grid), dim3(C_THREADS), lds, s>>>(p);
   return hipGetLastError();
 }
 

@@ -68,6 +68,7 @@ struct CountParams {
   const unsigned long long *bucket_end;  // == the fine cursors after the scatter
   int hbits;                           // stored hash bits to strip from the last key word
   uint32_t n_buckets;
+  uint32_t grid;                      // persistent workgroups (one per CU); 0 = one per bucket
   int k;
   int cap;                            // LDS table slots
   int dmin_thres;

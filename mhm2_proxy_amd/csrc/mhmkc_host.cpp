@@ -86,6 +86,7 @@ struct mhmkc {
   uint32_t nb = 256, nf = 256;
   uint32_t own_lo = 0, own_hi = 256;  // owned coarse range [own_lo, own_hi)
   int dev = 0;
+  int n_cu = 0;  // compute units: persistent k_count workgroups
   hipStream_t stream = nullptr;
   bool own_stream = false;
   ncclComm_t comm = nullptr;
@@ -434,6 +435,9 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       owned += s.count[i];
     }
   st.owned_records = owned;
+  for (uint32_t c = 0; c < no; c++)  // k_count indexes a bucket with 32 bits
+    if (per_coarse[c] >= 0xffffffffull)
+      return fail(MHMKC_EUNSUPPORTED, "more than 2^32 records in one hash bucket (split the input into batches of ranks)");
 
   // fine bits: aim at ~4 records per LDS table slot per fine bucket
   const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
@@ -514,6 +518,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.bucket_end = d_fine_cursor.as<unsigned long long>();
   cp.hbits = hbits;
   cp.n_buckets = n_fine;
+  cp.grid = (uint32_t)std::max(0, n_cu);  // one persistent workgroup per CU (k_count needs ~160 KB of LDS)
   cp.k = k;
   cp.cap = mhm::count_cap(nl);
   if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
@@ -711,6 +716,7 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     }
   }
   (void)hipGetDevice(&h->dev);
+  if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, h->dev) != hipSuccess) h->n_cu = 0;
   if (cfg->stream) {
     h->stream = (hipStream_t)cfg->stream;
   } else {
