@@ -259,6 +259,7 @@ typedef struct {
   uint16_t count;
   uint16_t left[4];  /* A C G T */
   uint16_t right[4];
+  uint8_t from_ctg; /* KmerExtsCounts::from_ctg (kcount_cpu.cpp:191-196) */
 } ext_counts;
 
 static uint16_t inc_with_limit(int c1, int c2) { /* :148-151 */
@@ -339,7 +340,8 @@ static int tbl_init(orc_table *t, int n_longs, uint64_t cap) {
   return t->keys && t->vals && t->used;
 }
 
-static ext_counts *tbl_get(orc_table *t, const uint64_t *key);
+static ext_counts *tbl_get2(orc_table *t, const uint64_t *key, int *is_new);
+static ext_counts *tbl_get(orc_table *t, const uint64_t *key) { return tbl_get2(t, key, NULL); }
 
 static int tbl_grow(orc_table *t) {
   orc_table nt;
@@ -359,7 +361,8 @@ static int tbl_grow(orc_table *t) {
   return 1;
 }
 
-static ext_counts *tbl_get(orc_table *t, const uint64_t *key) {
+static ext_counts *tbl_get2(orc_table *t, const uint64_t *key, int *is_new) {
+  if (is_new) *is_new = 0;
   if ((t->n + 1) * 10 > t->cap * 7) {
     if (!tbl_grow(t)) return NULL;
   }
@@ -372,6 +375,7 @@ static ext_counts *tbl_get(orc_table *t, const uint64_t *key) {
   t->used[s] = 1;
   memcpy(t->keys + s * nl, key, 8 * (size_t)nl);
   t->n++;
+  if (is_new) *is_new = 1;
   return &t->vals[s];
 }
 
@@ -497,6 +501,108 @@ orc_table *orc_kcount(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
     if (L < k) continue;         /* kcount.cpp:78 */
     if (L < k + 2) continue;     /* process_seq emits the supermer only when length >= k+2 */
     if (!insert_supermer(t, seq, L, k, 1)) return NULL;
+  }
+  if (!tbl_finalize(t, dmin_thres, dyn_min_depth)) return NULL;
+  return t;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * The contig pass: add_ctg_kmers (src/kcount/kcount.cpp:100-138) -> SeqBlockInserter::process_seq with
+ * count = depth (kcount_cpu.cpp:73-103: depth 0 -> 1; one supermer per contig at one rank) ->
+ * insert_supermer_from_ctg (kcount_cpu.cpp:356-406), applied in contig order after the read pass.
+ * Literal restatement, order-dependent exactly as the reference is. */
+static int insert_ctg_supermer(orc_table *t, char *sm, int len, int k, int count, int dmin_thres,
+                               double dyn_min_depth) {
+  const int nl = t->n_longs;
+  char quals[65536];
+  for (int i = 0; i < len; i++) { /* get_kmers_and_exts, kcount_cpu.cpp:307-335 */
+    char b = sm[i];
+    char u = (b >= 'a' && b <= 'z') ? (char)(b - 32) : b;
+    if (u != 'A' && u != 'C' && u != 'G' && u != 'T' && u != 'N') return 0; /* DIE, :453-458 */
+    quals[i] = (b >= 'A' && b <= 'Z');
+    sm[i] = u;
+  }
+  uint64_t kmer[8], rc[8];
+  for (int i = 1; i < len - k; i++) {
+    window_kmer(sm, i, k, nl, kmer);
+    char left = quals[i - 1] ? sm[i - 1] : '0';
+    char right = quals[i + k] ? sm[i + k] : '0';
+    orc_kmer_revcomp(kmer, k, nl, rc);
+    if (kmer_less(rc, kmer, nl)) {
+      memcpy(kmer, rc, 8 * (size_t)nl);
+      char tmp = left;
+      left = comp_nucleotide(right);
+      right = comp_nucleotide(tmp);
+    }
+    int is_new = 0;
+    ext_counts *v = tbl_get2(t, kmer, &is_new); /* KmerMapExts::insert(kmer, true): never full here */
+    if (!v) return 0;
+    int insert_it = 0;
+    int c = count;
+    if (is_new) {
+      insert_it = 1;
+    } else if (!v->from_ctg) { /* existing entry is from a read */
+      if (v->count == 1) {
+        insert_it = 1;
+      } else {
+        const char l = get_ext(v->left, v->count, dmin_thres, dyn_min_depth);
+        const char r = get_ext(v->right, v->count, dmin_thres, dyn_min_depth);
+        if (l == 'X' || l == 'F' || r == 'X' || r == 'F') insert_it = 1; /* non-UU */
+      }
+    } else if (v->count) { /* existing entry from a contig */
+      insert_it = 1;
+      const char l = get_ext(v->left, v->count, dmin_thres, dyn_min_depth);
+      const char r = get_ext(v->right, v->count, dmin_thres, dyn_min_depth);
+      if (l != left || r != right)
+        c = 0; /* the two contig k-mers disagree: purge later */
+      else
+        c = c < v->count ? c : v->count;
+    }
+    if (insert_it) {
+      memset(v, 0, sizeof *v);
+      v->count = (uint16_t)c;
+      v->from_ctg = 1;
+      ext_inc(v->left, left, c);
+      ext_inc(v->right, right, c);
+    }
+  }
+  return 1;
+}
+
+/* Read pass + contig pass + finalize. ctg_chars: contigs back to back (case = quality, as for reads),
+ * ctg_offs: n_ctgs + 1 offsets, ctg_depths: Contig::get_uint16_t_depth() values (contigs.hpp:65). */
+orc_table *orc_kcount_ctgs(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, const char *ctg_chars,
+                           const uint64_t *ctg_offs, const uint16_t *ctg_depths, uint64_t n_ctgs, int k, int n_longs,
+                           int qual_cutoff, int dmin_thres, double dyn_min_depth) {
+  static const char nucleotide_map[5] = {'A', 'C', 'G', 'T', 'N'};
+  init_tables();
+  if (k < 1 || n_longs < (k + 31) / 32 || n_longs > 8) return NULL;
+  orc_table *t = (orc_table *)malloc(sizeof(orc_table));
+  if (!t || !tbl_init(t, n_longs, 1 << 16)) return NULL;
+  char seq[65536];
+  for (uint64_t r = 0; r < n_reads; r++) { /* the read pass, as orc_kcount */
+    const uint64_t L64 = offs[r + 1] - offs[r];
+    if (L64 > 65535) return NULL;
+    const int L = (int)L64;
+    t->reads++;
+    for (int i = 0; i < L; i++) {
+      const uint8_t b = bytes[offs[r] + i];
+      if ((b & 7) > 4) return NULL;
+      seq[i] = nucleotide_map[b & 7];
+      if ((b >> 3) < qual_cutoff) seq[i] += 32;
+    }
+    if (L < k + 2) continue;
+    if (!insert_supermer(t, seq, L, k, 1)) return NULL;
+  }
+  static char cseq[1 << 20];
+  for (uint64_t c = 0; c < n_ctgs; c++) { /* add_ctg_kmers, contig order */
+    const uint64_t L64 = ctg_offs[c + 1] - ctg_offs[c];
+    if (L64 >= sizeof cseq) return NULL;
+    const int L = (int)L64;
+    if (L < k + 2) continue; /* kcount.cpp:128 */
+    memcpy(cseq, ctg_chars + ctg_offs[c], (size_t)L);
+    const int depth = ctg_depths[c] ? ctg_depths[c] : 1; /* process_seq: if (!depth) depth = 1 */
+    if (!insert_ctg_supermer(t, cseq, L, k, depth, dmin_thres, dyn_min_depth)) return NULL;
   }
   if (!tbl_finalize(t, dmin_thres, dyn_min_depth)) return NULL;
   return t;

@@ -59,6 +59,60 @@ def hot_set(n_poly: int = 800, seed: int = 9):
     return np.concatenate(reads).astype(np.uint8), offs
 
 
+def ctg_set(seed: int = 21, n_reads: int = 300, genome_len: int = 6000, n_ctgs: int = 200):
+    """Reads plus contigs for the contig pass (add_ctg_kmers): genome substrings (both strands), exact
+    duplicates with other depths (min rule), mutated copies (read entries replaced, contig conflicts),
+    overlapping pieces, novel sequence (keys absent from the reads), N bases, lowercase (low quality),
+    contigs shorter than k + 2 (skipped) and depths 0, 1, 2, 3, ..., 65535."""
+    rng = np.random.default_rng(seed)
+    g = m.synth_genome(genome_len, seed)
+    b, o = m.synth_reads(g, n_reads, 150, seed)
+    gs = "".join("ACGT"[int(x)] for x in g)
+    comp = {"A": "T", "C": "G", "G": "C", "T": "A", "N": "N"}
+    seqs, depths = [], []
+    depth_choices = [0, 1, 2, 3, 5, 12, 40, 300, 65535]
+    for i in range(n_ctgs):
+        mode = i % 8
+        L = int(rng.integers(10, 420))
+        st = int(rng.integers(0, genome_len - L))
+        s = gs[st:st + L]
+        if mode in (1, 7) and seqs:  # exact duplicate of an earlier contig, other depth
+            s = seqs[int(rng.integers(0, len(seqs)))].upper()
+        elif mode == 6 and seqs:  # mutated copy of an earlier contig: shared k-mers, other extensions
+            s = list(seqs[int(rng.integers(0, len(seqs)))].upper())
+            for _ in range(max(1, len(s) // 50)):
+                j = int(rng.integers(0, len(s)))
+                s[j] = "ACGT"[(("ACGTN".index(s[j]) + int(rng.integers(1, 4))) % 4)]
+            s = "".join(s)
+        elif mode == 2:  # point mutations
+            s = list(s)
+            for _ in range(max(1, L // 60)):
+                j = int(rng.integers(0, L))
+                s[j] = "ACGT"[(("ACGT".index(s[j]) + int(rng.integers(1, 4))) % 4)]
+            s = "".join(s)
+        elif mode == 3:  # novel sequence
+            s = "".join("ACGT"[int(x)] for x in rng.integers(0, 4, L))
+        elif mode == 4:  # N bases
+            s = list(s)
+            for _ in range(2):
+                s[int(rng.integers(0, L))] = "N"
+            s = "".join(s)
+        elif mode == 5:  # lowercase stretch (bases below the quality cutoff)
+            j = int(rng.integers(0, L))
+            s = s[:j] + s[j:j + 5].lower() + s[j + 5:]
+        if rng.integers(0, 2):
+            s = "".join(comp.get(c.upper(), c.upper()) if c.isupper() else comp[c.upper()].lower() for c in reversed(s))
+        seqs.append(s)
+        depths.append(int(depth_choices[int(rng.integers(0, len(depth_choices)))]))
+    return b, o, seqs, np.array(depths, dtype=np.uint16)
+
+
+def oracle_ctg_table(b, o, seqs, depths, k, **kw) -> m.KmerTable:
+    t = O.kcount_ctgs(b, o, seqs, depths, k, **kw)
+    keys, c, l, r = t.fetch()
+    return m.KmerTable(k, keys, c, l, r)
+
+
 def oracle_table(b, o, k, **kw) -> m.KmerTable:
     t = O.kcount(b, o, k, **kw)
     keys, c, l, r = t.fetch()

@@ -46,6 +46,8 @@ def oracle() -> C.CDLL:
         L.orc_kmer_target_rank.argtypes = [VP, I, I, I]
         L.orc_kcount.argtypes = [VP, VP, U64, I, I, I, I, C.c_double]
         L.orc_kcount.restype = VP
+        L.orc_kcount_ctgs.argtypes = [VP, VP, U64, VP, VP, VP, U64, I, I, I, I, C.c_double]
+        L.orc_kcount_ctgs.restype = VP
         L.orc_extract.argtypes = [VP, VP, U64, I, I, I, VP, VP, U64]
         L.orc_extract.restype = C.c_int64
         L.orc_count_records.argtypes = [VP, VP, U64, I, I, C.c_double]
@@ -109,6 +111,21 @@ def kcount(packed_bytes, offsets, k, n_longs=None, qual_cutoff=20, dmin_thres=2,
     o = np.ascontiguousarray(offsets, dtype=np.uint64)
     ptr = oracle().orc_kcount(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, dmin_thres,
                               dyn_min_depth)
+    return OracleTable(ptr, nl, k)
+
+
+def kcount_ctgs(packed_bytes, offsets, ctg_seqs, ctg_depths, k, n_longs=None, qual_cutoff=20, dmin_thres=2,
+                dyn_min_depth=0.9) -> OracleTable:
+    """Read pass + contig pass (add_ctg_kmers) + finalize. ctg_seqs: list of str; ctg_depths: uint16 values."""
+    nl = n_longs or (k // 32 + 1)
+    b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    blob = "".join(ctg_seqs).encode("ascii")
+    co = np.zeros(len(ctg_seqs) + 1, dtype=np.uint64)
+    np.cumsum([len(x) for x in ctg_seqs], out=co[1:])
+    d = np.ascontiguousarray(ctg_depths, dtype=np.uint16)
+    ptr = oracle().orc_kcount_ctgs(b.ctypes.data, o.ctypes.data, o.size - 1, blob, co.ctypes.data, d.ctypes.data,
+                                   len(ctg_seqs), k, nl, qual_cutoff, dmin_thres, dyn_min_depth)
     return OracleTable(ptr, nl, k)
 
 

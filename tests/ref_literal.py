@@ -120,9 +120,11 @@ def get_kmers_and_exts(supermer_seq: str, k: int, n_longs: int):
     return out
 
 
-def analyze_kmers(reads, k: int, qual_offset: int = 33, dmin_thres: int = 2, qual_cutoff: int = KCOUNT_QUAL_CUTOFF):
-    """count_kmers + finish at rank_n()==1 (src/kcount/kcount.cpp:54-98,140-157; kcount_cpu.cpp:73-103,
-    337-354, 490-528). reads: iterable of PackedRead byte strings. Returns {kmer longs: (count, L, R)}."""
+def analyze_kmers(reads, k: int, qual_offset: int = 33, dmin_thres: int = 2, qual_cutoff: int = KCOUNT_QUAL_CUTOFF,
+                  ctgs=()):
+    """count_kmers + [add_ctg_kmers] + finish at rank_n()==1 (src/kcount/kcount.cpp:54-157;
+    kcount_cpu.cpp:73-103, 337-406, 490-528). reads: iterable of PackedRead byte strings; ctgs: iterable of
+    (contig sequence, uint16 depth) in contig order. Returns {kmer longs: (count, L, R)}."""
     n_longs = k // 32 + 1
     table: dict = {}
     for packed in reads:
@@ -143,6 +145,37 @@ def analyze_kmers(reads, k: int, qual_offset: int = 33, dmin_thres: int = 2, qua
             e.count = min(e.count + 1, U16_MAX)
             e.left_exts.inc(left, 1)
             e.right_exts.inc(right, 1)
+    for seq, depth in ctgs:  # add_ctg_kmers (kcount.cpp:125-130)
+        if len(seq) < k + 2:
+            continue
+        depth = depth or 1  # SeqBlockInserter::process_seq (kcount_cpu.cpp:75)
+        for kmer, left, right in get_kmers_and_exts(seq, k, n_longs):  # insert_supermer_from_ctg (:356-406)
+            count = depth
+            e = table.get(kmer)
+            is_new = e is None
+            if is_new:
+                e = table[kmer] = KmerExtsCounts()
+            insert_it = False
+            if is_new:
+                insert_it = True
+            elif not e.from_ctg:
+                if e.count == 1:
+                    insert_it = True
+                else:
+                    le, re_ = e.left_exts.get_ext(e.count, dmin_thres), e.right_exts.get_ext(e.count, dmin_thres)
+                    if le in "XF" or re_ in "XF":
+                        insert_it = True
+            elif e.count:
+                insert_it = True
+                le, re_ = e.left_exts.get_ext(e.count, dmin_thres), e.right_exts.get_ext(e.count, dmin_thres)
+                if le != left or re_ != right:
+                    count = 0
+                else:
+                    count = min(count, e.count)
+            if insert_it:
+                e.left_exts, e.right_exts, e.count, e.from_ctg = ExtCounts(), ExtCounts(), count, True
+                e.left_exts.inc(left, count)
+                e.right_exts.inc(right, count)
     out = {}
     for kmer, e in table.items():
         if e.count < 2:

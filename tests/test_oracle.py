@@ -15,7 +15,8 @@ import pytest
 import mhm2_proxy_amd as m
 import oracle_lib as O
 import ref_literal as R
-from common import GOLDEN, assert_tables_equal, edge_case_set, oracle_table, read_reads_file, read_table_file, synth_set
+from common import (GOLDEN, assert_tables_equal, ctg_set, edge_case_set, oracle_ctg_table, oracle_table, read_reads_file,
+                    read_table_file, synth_set)
 
 # test/kmer-test.cpp:11-33 (data vectors of the reference's own unit test)
 RANDOM_READ = ("CGCTGTTCCAGATGACGAACCAGGAATTCCGCCAGGTATTCGACTTTATTCGCGAAGTCAAGAAGTTGAACGTCATCAGTGTGAACTACGGTTGCGAAGG"
@@ -141,6 +142,20 @@ def test_oracle_matches_literal_parameters(dmin, qcut):
     t = oracle_table(b, o, 21, dmin_thres=dmin, qual_cutoff=qcut)
     orc = {tuple(int(x) for x in t.keys[i]): (int(t.counts[i]), chr(t.left[i]), chr(t.right[i])) for i in range(len(t))}
     assert orc == lit
+
+
+@pytest.mark.parametrize("k,dmin", [(21, 2), (21, 1), (21, 3), (33, 2), (63, 4)])
+def test_oracle_contig_pass_matches_literal(k, dmin):
+    """The contig pass (add_ctg_kmers -> insert_supermer_from_ctg, order-dependent) in the C oracle equals
+    the literal restatement."""
+    b, o, seqs, depths = ctg_set(seed=40 + k + dmin)
+    lit = R.analyze_kmers([b[int(o[i]):int(o[i + 1])] for i in range(o.size - 1)], k, dmin_thres=dmin,
+                          ctgs=list(zip(seqs, [int(d) for d in depths])))
+    t = oracle_ctg_table(b, o, seqs, depths, k, dmin_thres=dmin)
+    orc = {tuple(int(x) for x in t.keys[i]): (int(t.counts[i]), chr(t.left[i]), chr(t.right[i])) for i in range(len(t))}
+    assert orc == lit
+    plain = oracle_table(b, o, k, dmin_thres=dmin)
+    assert len(t) != len(plain) or (t.sorted().counts != plain.sorted().counts).any(), "contigs changed nothing"
 
 
 def test_dynamic_threshold_quirk():
