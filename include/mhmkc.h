@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 1
+#define MHMKC_ABI_VERSION 2
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -80,6 +80,7 @@ typedef struct {
   uint64_t fine_buckets;   /* number of fine buckets on this rank */
   uint64_t bytes_sent;     /* bytes sent to other ranks in the exchange */
   uint64_t exact_reruns;   /* capped partition passes redone with exact bucket sizes (skewed input) */
+  uint64_t ctg_kmers;      /* distinct contig k-mers of the contig pass (0 without contigs) */
   double ms_total;         /* wall time of the last add_reads..finish sequence (device events) */
   double ms_kernel[8];     /* per-stage device time when profiling is on: see MHMKC_STAGE_* */
   uint64_t launches[8];    /* per-stage launch count when profiling is on */
@@ -126,6 +127,15 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_packed_bytes, const uint6
  * SeqBlockInserter::process_seq receives (src/kcount/kcount.cpp:80-86). Host buffers. depth is the
  * per-sequence count (reads: 1). Only depth == 1 (the read pass) is supported in this version. */
 int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *seq_offsets, uint64_t n_seqs, uint16_t depth);
+
+/* Add contigs for the contig pass of rounds after the first k (add_ctg_kmers, src/kcount/kcount.cpp:100-138;
+ * insert_supermer_from_ctg, src/kcount/kcount_cpu.cpp:356-406). seqs: contig sequences back to back (case
+ * = quality as for reads; contigs are uppercase), seq_offsets: n_ctgs+1 offsets, depths:
+ * Contig::get_uint16_t_depth() (src/contigs.hpp:65), 0 counting as 1. The contig pass runs inside
+ * mhmkc_finish after every read, over the contigs in the order they were added (the reference's order,
+ * which its rules depend on). Contigs shorter than k+2 contribute nothing. Host buffers. Single rank
+ * (n_ranks == 1) in this version. */
+int mhmkc_add_ctgs(mhmkc_t h, const char *seqs, const uint64_t *seq_offsets, const uint16_t *depths, uint64_t n_ctgs);
 
 /* Exchange (multi-GPU), count and finalize: purge count < 2 and X/X, choose extensions.
  * Replaces KmerDHT::flush_updates + finish_updates -> HashTableInserter::insert_into_local_hashtable

@@ -33,7 +33,7 @@ STAGES = ["tileidx", "extract_hist", "extract_scatter", "exchange", "part_hist",
 # every symbol include/mhmkc.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = [
     "mhmkc_config_init", "mhmkc_create", "mhmkc_destroy", "mhmkc_comm_id", "mhmkc_add_reads",
-    "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_device_output",
+    "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_add_ctgs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_device_output",
     "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
 ]
 SYNTH_SYMBOLS = ["mhmkc_synth_config_init", "mhmkc_synth_genome", "mhmkc_synth_reads"]
@@ -71,6 +71,7 @@ class MhmkcStats(C.Structure):
         ("fine_buckets", C.c_uint64),
         ("bytes_sent", C.c_uint64),
         ("exact_reruns", C.c_uint64),
+        ("ctg_kmers", C.c_uint64),
         ("ms_total", C.c_double),
         ("ms_kernel", C.c_double * 8),
         ("launches", C.c_uint64 * 8),
@@ -136,6 +137,7 @@ def lib() -> C.CDLL:
     L.mhmkc_add_reads.argtypes = [VP, VP, VP, U64]
     L.mhmkc_add_reads_device.argtypes = [VP, VP, VP, U64, U64]
     L.mhmkc_add_seqs.argtypes = [VP, C.c_char_p, VP, U64, C.c_uint16]
+    L.mhmkc_add_ctgs.argtypes = [VP, C.c_char_p, VP, VP, U64]
     L.mhmkc_finish.argtypes = [VP, P(U64)]
     L.mhmkc_fetch.argtypes = [VP, VP, VP, VP, VP]
     L.mhmkc_device_output.argtypes = [VP, P(VP), P(VP), P(VP), P(VP), P(U64)]

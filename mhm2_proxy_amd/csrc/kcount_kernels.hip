@@ -862,6 +862,104 @@ __device__ __forceinline__ bool slot_survives(const CountLds &t, int slot, const
   return !(L == 'X' && R == 'X');
 }
 
+// Contig pass, applied in k_count once a sweep has inserted its reads (kcount_ctg.hip folds the contig
+// occurrences of every k-mer; see there). For each folded contig k-mer of bucket b not yet applied: if the
+// key is in this sweep's table its read entry is kept when it has count >= 2 and unique extensions on both
+// sides (UU), otherwise it is replaced by the contig entry (insert_supermer_from_ctg,
+// src/kcount/kcount_cpu.cpp:367-404); a key absent from the table is absent from the reads once the
+// bucket's last sweep has run (deferred keys are counted in a later sweep), and is finalized here
+// directly (insert_into_local_hashtable, kcount_cpu.cpp:503-522).
+template <int NL>
+__device__ void ctg_apply(const CountLds &t, const CountParams &p, uint32_t b, bool last_sweep,
+                          unsigned long long *s_range) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    auto lower = [&](uint32_t v) {
+      uint64_t lo = 0, hi = p.ctg_n;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (p.ctg_bucket[mid] < v)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      return lo;
+    };
+    s_range[0] = lower(b);
+    s_range[1] = lower(b + 1);
+  }
+  __syncthreads();
+  const uint64_t q0 = s_range[0], q1 = s_range[1];
+  const int ng = t.cap >> 2;
+  const uint64_t *last = t.keys + (NL - 1) * t.cap;
+  for (uint64_t q = q0 + tid; q < q1; q += C_THREADS) {
+    if (p.ctg_done[q]) continue;
+    uint64_t key[NL];
+#pragma unroll
+    for (int w = 0; w < NL; w++) key[w] = p.ctg_keys[w][q];
+    const uint32_t st = p.ctg_state[q];
+    const uint32_t c = st & 0xffffu, l = (st >> 16) & 7u, r = (st >> 19) & 7u;
+    int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
+    int slot = -1;
+    for (int pr = 0; pr < C_PROBE; pr++) {  // find only: a key in the table is within its probe window
+      uint64_t v[4];
+      read_group(last, g, v);
+      const int e = examine_group<NL>(t, key, g, v);
+      if (e >= 0) {
+        slot = e;
+        break;
+      }
+      if (e != G_FULL) break;  // an empty slot: absent
+      g = (g + 1 == ng) ? 0 : g + 1;
+    }
+    if (slot >= 0) {
+      const uint32_t rc = t.cnt[slot] > 65535u ? 65535u : t.cnt[slot];
+      bool keep = false;
+      if (rc >= 2) {
+        const int thr = dyn_threshold(rc, p.dyn_mult, p.dmin_thres);
+        const uint32_t e0 = t.ext[slot], e1 = t.ext[t.cap + slot], e2 = t.ext[2 * t.cap + slot],
+                       e3 = t.ext[3 * t.cap + slot];
+        const char L = ext_choice(e0 & 0xffffu, e0 >> 16, e1 & 0xffffu, e1 >> 16, thr);
+        const char R = ext_choice(e2 & 0xffffu, e2 >> 16, e3 & 0xffffu, e3 >> 16, thr);
+        keep = L != 'X' && L != 'F' && R != 'X' && R != 'F';
+      }
+      if (!keep) {  // {count, left[l] = right[r] = count, from_ctg}; halves >= 0xC000 as 0x8000 (§3.4)
+        const uint32_t h = c >= 0xC000u ? 0x8000u : c;
+        uint32_t ew[4] = {0, 0, 0, 0};
+        if (l < 4) ew[l >> 1] |= h << ((l & 1u) * 16);
+        if (r < 4) ew[2 + (r >> 1)] |= h << ((r & 1u) * 16);
+        t.cnt[slot] = c;
+#pragma unroll
+        for (int i = 0; i < 4; i++) t.ext[i * t.cap + slot] = ew[i];
+      }
+      p.ctg_done[q] = 1;
+    } else if (last_sweep) {
+      const int thr = dyn_threshold(c, p.dyn_mult, p.dmin_thres);
+      uint32_t cl[4] = {0, 0, 0, 0}, cr[4] = {0, 0, 0, 0};
+      if (l < 4) cl[l] = c;
+      if (r < 4) cr[r] = c;
+      const char L = ext_choice(cl[0], cl[1], cl[2], cl[3], thr), R = ext_choice(cr[0], cr[1], cr[2], cr[3], thr);
+      atomicAdd(&p.stats[STAT_DISTINCT], 1ull);
+      atomicAdd(&p.stats[STAT_COUNTSUM], (unsigned long long)c);
+      if (c >= 2 && !(L == 'X' && R == 'X')) {
+        const unsigned long long o = atomicAdd(p.out_cursor, 1ull);
+        uint64_t *ok = p.out_keys + o * (uint64_t)p.nlo;
+#pragma unroll
+        for (int w = 0; w < NL; w++) ok[w] = key[w];
+        for (int w = NL; w < p.nlo; w++) ok[w] = 0;
+        p.out_counts[o] = (uint16_t)c;
+        p.out_left[o] = L;
+        p.out_right[o] = R;
+        atomicAdd(&p.stats[STAT_NOUT], 1ull);
+      } else {
+        atomicAdd(&p.stats[STAT_PURGED], 1ull);
+      }
+      p.ctg_done[q] = 1;
+    }
+  }
+  __syncthreads();
+}
+
 // e receives the raw low bits of the record (ext code in bits 0-5, stored hash bits above) so that an
 // overflowing record is written back unchanged; the key has them cleared.
 template <int NL, bool PACKED>
@@ -1124,6 +1222,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP(t_f0);
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
+    if (p.ctg_n) ctg_apply<NL>(t, p, b, last_sweep, s_red);
     if (last_sweep && b_next < p.n_buckets) {
       bucket(b_next, ps_next, nb_next);
       if (nb_next) prefetch(ps_next, nb_next, 0);

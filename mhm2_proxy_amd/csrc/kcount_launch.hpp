@@ -80,7 +80,38 @@ struct CountParams {
   char *out_right;
   unsigned long long *out_cursor;
   unsigned long long *stats;          // [STAT_*]
+  // contig pass (kcount_ctg.hip): folded contig k-mers sorted by bucket; 0 entries = no contig pass
+  uint64_t ctg_n;
+  const uint64_t *ctg_keys[4];        // [NL][ctg_n] canonical key words
+  const uint32_t *ctg_state;          // count (16 bits) | left code << 16 | right code << 19
+  const uint32_t *ctg_bucket;         // local fine bucket of each entry (sorted ascending)
+  uint8_t *ctg_done;                  // [ctg_n] applied (zeroed before the launch)
 };
+
+// Contig pass state word of one folded contig k-mer (kcount_ctg.hip).
+__host__ __device__ inline uint32_t ctg_state_word(uint32_t count, uint32_t l, uint32_t r) {
+  return (count & 0xffffu) | (l << 16) | (r << 19);
+}
+
+// Input of the contig-pass extraction: contigs in the PackedRead byte layout (case -> quality 31 / 0).
+struct CtgView {
+  const uint8_t *bytes;
+  const uint64_t *offs;        // [n_ctgs + 1]
+  const uint16_t *depth;       // [n_ctgs]: Contig::get_uint16_t_depth() (0 counts as 1)
+  const uint64_t *win_prefix;  // [n_ctgs + 1]: counted windows before each contig
+  uint64_t n_ctgs;
+  uint64_t n_windows;
+};
+
+// Contig pass (kcount_ctg.hip). Scratch sizes come from ctg_scratch_bytes.
+size_t ctg_scratch_bytes(uint64_t n_windows, int nl);
+// Extract, sort by key (stable: contig order kept within a key), fold every key's contig occurrences in
+// order (insert_supermer_from_ctg) and sort the folded k-mers by local fine bucket. Outputs (n_out of them)
+// go to out_keys[NL] (SoA, each out_cap long), out_state, out_bucket.
+hipError_t ctg_prepare(const CtgView &cv, int k, int nl, int qual_cutoff, int dmin_thres, double dyn_mult,
+                       int coarse_bits, int fine_bits, uint32_t own_lo, void *scratch, size_t scratch_bytes,
+                       uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,
+                       unsigned int *err, hipStream_t s);
 
 enum {
   STAT_DISTINCT = 0,

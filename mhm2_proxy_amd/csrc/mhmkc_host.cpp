@@ -96,6 +96,14 @@ struct mhmkc {
   DevBuf d_hist, d_cursor, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xcounts;
   DevBuf d_in_bytes, d_in_offs;
+  // contig pass (add_ctg_kmers): contigs in the PackedRead byte layout, kept on the host until finish
+  std::vector<uint8_t> ctg_bytes;
+  std::vector<uint64_t> ctg_offs{0}, ctg_win{0};  // byte offsets, counted-window prefix
+  std::vector<uint16_t> ctg_depth;
+  DevBuf d_ctg_bytes, d_ctg_offs, d_ctg_win, d_ctg_depth, d_ctg_scratch, d_ctg_state, d_ctg_bucket, d_ctg_done;
+  DevBuf d_ctg_keys[4];
+  uint64_t ctg_n = 0;  // folded contig k-mers of the last finish
+  int prepare_ctgs();
 
   std::string err;
   bool finished = false;
@@ -406,6 +414,48 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// contig pass: extract, fold and bucket the contig k-mers (kcount_ctg.hip); k_count applies them
+
+int mhmkc::prepare_ctgs() {
+  ctg_n = 0;
+  const uint64_t W = ctg_win.back();
+  if (!W) return MHMKC_OK;
+  if (cfg.n_ranks > 1) return fail(MHMKC_EUNSUPPORTED, "the contig pass is single-rank in this version");
+  hipError_t e;
+  const uint64_t nc = ctg_depth.size();
+  if ((e = d_ctg_bytes.ensure(ctg_bytes.size() + 64)) != hipSuccess ||
+      (e = d_ctg_offs.ensure((nc + 1) * 8)) != hipSuccess || (e = d_ctg_win.ensure((nc + 1) * 8)) != hipSuccess ||
+      (e = d_ctg_depth.ensure(nc * 2 + 2)) != hipSuccess)
+    return hip_fail(e, "contig staging");
+  if ((e = hipMemcpyAsync(d_ctg_bytes.p, ctg_bytes.data(), ctg_bytes.size(), hipMemcpyHostToDevice, stream)) !=
+          hipSuccess ||
+      (e = hipMemcpyAsync(d_ctg_offs.p, ctg_offs.data(), (nc + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_ctg_win.p, ctg_win.data(), (nc + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_ctg_depth.p, ctg_depth.data(), nc * 2, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "contig H2D");
+  const size_t sb = mhm::ctg_scratch_bytes(W, nl);
+  if ((e = d_ctg_scratch.ensure(sb)) != hipSuccess) return hip_fail(e, "contig scratch");
+  uint64_t *keys[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int w = 0; w < nl; w++) {
+    if ((e = d_ctg_keys[w].ensure(W * 8)) != hipSuccess) return hip_fail(e, "contig keys");
+    keys[w] = d_ctg_keys[w].as<uint64_t>();
+  }
+  if ((e = d_ctg_state.ensure(W * 4)) != hipSuccess || (e = d_ctg_bucket.ensure(W * 4)) != hipSuccess ||
+      (e = d_ctg_done.ensure(W)) != hipSuccess)
+    return hip_fail(e, "contig entries");
+  mhm::CtgView cv{d_ctg_bytes.as<uint8_t>(), d_ctg_offs.as<uint64_t>(), d_ctg_depth.as<uint16_t>(),
+                  d_ctg_win.as<uint64_t>(), nc, W};
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = mhm::ctg_prepare(cv, k, nl, 1, cfg.dmin_thres, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, d_ctg_scratch.p, sb, keys,
+                       d_ctg_state.as<uint32_t>(), d_ctg_bucket.as<uint32_t>(), &ctg_n, d_err.as<unsigned int>(),
+                       stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "contig pass");
+  st.ctg_kmers = ctg_n;
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 // fine partition + LDS count + finalize
 
 // Fine buckets are capped at 1.25x their expected size (+256): a single scatter pass, no histogram. If a
@@ -448,6 +498,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   nf = 1u << fb;
   const uint32_t n_fine = no * nf;
   st.fine_buckets = n_fine;
+  if ((rc = prepare_ctgs())) return rc;
 
   // chunk table
   const int T = mhm::tile_bases(nl);
@@ -494,7 +545,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if ((e = d_fine_hist.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
   if ((e = d_fine_base.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
   if ((e = d_fine_cursor.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine cursor");
-  const uint64_t out_cap = owned / 2 + 1;
+  const uint64_t out_cap = owned / 2 + ctg_n + 1;
   if ((e = d_out_keys.ensure(out_cap * 8 * nlo)) != hipSuccess) return hip_fail(e, "output keys");
   if ((e = d_out_counts.ensure(out_cap * 2)) != hipSuccess) return hip_fail(e, "output counts");
   if ((e = d_out_left.ensure(out_cap)) != hipSuccess) return hip_fail(e, "output left");
@@ -531,6 +582,11 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.out_right = d_out_right.as<char>();
   cp.out_cursor = d_out_cursor.as<unsigned long long>();
   cp.stats = d_stats.as<unsigned long long>();
+  cp.ctg_n = ctg_n;
+  for (int w = 0; w < 4; w++) cp.ctg_keys[w] = w < nl ? d_ctg_keys[w].as<uint64_t>() : nullptr;
+  cp.ctg_state = d_ctg_state.as<uint32_t>();
+  cp.ctg_bucket = d_ctg_bucket.as<uint32_t>();
+  cp.ctg_done = d_ctg_done.as<uint8_t>();
 
   bool exact = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
   unsigned long long stats[mhm::STAT_ALLOC];
@@ -540,6 +596,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     prof_begin(MHMKC_STAGE_OTHER);
     e = hipMemsetAsync(d_out_cursor.p, 0, 8, stream);
     if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_ALLOC, stream);
+    if (e == hipSuccess && ctg_n) e = hipMemsetAsync(d_ctg_done.p, 0, ctg_n, stream);
     if (e == hipSuccess && exact) e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
     if (e == hipSuccess && !exact)
       e = mhm::launch_init_fine(d_cfit, d_cfit + no, no, fb, d_fine_base.as<unsigned long long>(),
@@ -762,6 +819,10 @@ void mhmkc_destroy(mhmkc_t h) {
                     &h->d_r2,       &h->d_out_keys,  &h->d_out_counts, &h->d_out_left, &h->d_out_right,
                     &h->d_out_cursor, &h->d_recv,    &h->d_xcounts,   &h->d_in_bytes,  &h->d_in_offs};
   for (DevBuf *b : bufs) b->release();
+  DevBuf *cbufs[] = {&h->d_ctg_bytes, &h->d_ctg_offs, &h->d_ctg_win,   &h->d_ctg_depth, &h->d_ctg_scratch,
+                     &h->d_ctg_state, &h->d_ctg_bucket, &h->d_ctg_done, &h->d_ctg_keys[0], &h->d_ctg_keys[1],
+                     &h->d_ctg_keys[2], &h->d_ctg_keys[3]};
+  for (DevBuf *b : cbufs) b->release();
   for (auto &p : h->prof) {
     h->ev_pool.push_back(p.a);
     h->ev_pool.push_back(p.b);
@@ -848,6 +909,45 @@ int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *offs, uint64_t n
   return add_host(h, bytes.data(), offs, n_seqs, 1);
 }
 
+int mhmkc_add_ctgs(mhmkc_t h, const char *seqs, const uint64_t *offs, const uint16_t *depths, uint64_t n_ctgs) {
+  if (!h) return MHMKC_EINVAL;
+  if (!offs || (n_ctgs && (!seqs || !depths))) return h->fail(MHMKC_EINVAL, "null host buffer");
+  if (h->finished) return h->fail(MHMKC_ESTATE, "handle already finished; call mhmkc_reset first");
+  if (offs[0] != 0) return h->fail(MHMKC_EINVAL, "seq_offsets[0] must be 0");
+  for (uint64_t i = 0; i < n_ctgs; i++)
+    if (offs[i + 1] < offs[i]) return h->fail(MHMKC_EINVAL, "seq_offsets must be non-decreasing");
+  const uint64_t n = offs[n_ctgs];
+  const size_t b0 = h->ctg_bytes.size();
+  h->ctg_bytes.resize(b0 + n);
+  // case carries the quality as for reads (get_kmers_and_exts: quals[i] = isupper, kcount_cpu.cpp:309-313);
+  // contigs are uppercase. Characters other than ACGTN are fatal (insert_supermer DIE, :452-458).
+  for (uint64_t i = 0; i < n; i++) {
+    const char c = seqs[i];
+    uint8_t code;
+    switch (c) {
+      case 'A': case 'a': code = 0; break;
+      case 'C': case 'c': code = 1; break;
+      case 'G': case 'g': code = 2; break;
+      case 'T': case 't': code = 3; break;
+      case 'N': case 'n': code = 4; break;
+      default:
+        h->ctg_bytes.resize(b0);
+        return h->fail(MHMKC_EBADCHAR, "bad char '%c' (%d) in contig position %llu", c, (int)c, (unsigned long long)i);
+    }
+    h->ctg_bytes[b0 + i] = (uint8_t)(code | ((c >= 'A' && c <= 'Z') ? (31u << 3) : 0u));
+  }
+  const uint64_t k = (uint64_t)h->k;
+  for (uint64_t i = 0; i < n_ctgs; i++) {
+    const uint64_t L = offs[i + 1] - offs[i];
+    h->ctg_offs.push_back(b0 + offs[i + 1]);
+    // add_ctg_kmers skips contigs shorter than k + 2 (src/kcount/kcount.cpp:128); interior windows only
+    h->ctg_win.push_back(h->ctg_win.back() + (L >= k + 2 ? L - k - 1 : 0));
+    h->ctg_depth.push_back(depths[i]);
+  }
+  if (h->ctg_win.back() >= 0xffffffffull) return h->fail(MHMKC_EINVAL, "at most 2^32-1 contig k-mers per round");
+  return MHMKC_OK;
+}
+
 int mhmkc_finish(mhmkc_t h, uint64_t *n_out) {
   if (!h) return MHMKC_EINVAL;
   return h->finish(n_out);
@@ -891,6 +991,11 @@ int mhmkc_reset(mhmkc_t h) {
   if (e != hipSuccess) return h->hip_fail(e, "reset");
   h->prof_collect();
   h->n_slabs = 0;
+  h->ctg_bytes.clear();
+  h->ctg_offs.assign(1, 0);
+  h->ctg_win.assign(1, 0);
+  h->ctg_depth.clear();
+  h->ctg_n = 0;
   h->finished = false;
   h->began = false;
   h->n_out = 0;

@@ -297,6 +297,19 @@ class KmerCounter:
         blob = "".join(seqs).encode("ascii")
         self._check(N.lib().mhmkc_add_seqs(self._h, blob, offs.ctypes.data, len(seqs), depth))
 
+    def add_ctgs(self, seqs: Sequence[str], depths) -> None:
+        """Contigs for the contig pass (add_ctg_kmers, src/kcount/kcount.cpp:100-138): uint16 depths as
+        Contig::get_uint16_t_depth() gives them (src/contigs.hpp:65). Applied at finish, after the reads,
+        in the order added."""
+        d = np.ascontiguousarray(depths, dtype=np.uint16)
+        if d.size != len(seqs):
+            raise ValueError("one depth per contig")
+        lens = np.fromiter((len(s) for s in seqs), dtype=np.uint64, count=len(seqs))
+        offs = np.zeros(len(seqs) + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        blob = "".join(seqs).encode("ascii")
+        self._check(N.lib().mhmkc_add_ctgs(self._h, blob, offs.ctypes.data, d.ctypes.data, len(seqs)))
+
     # -- finish / output
     def finish(self) -> int:
         n = C.c_uint64()
@@ -456,17 +469,23 @@ def analyze_kmers(kmer_len: int, prev_kmer_len: int, qual_offset: int, packed_re
     """analyze_kmers<MAX_K> (src/kcount/kcount.hpp:71-73, src/kcount/kcount.cpp:140-157).
 
     Counts every read of every PackedReads on this rank's GPU, exchanges by hash range with the other
-    ranks, purges and chooses extensions; the result is kmer_dht.table / kmer_dht.local_kmers.
-    The contig pass (ctgs non-empty, rounds after the first k) is not in this version.
+    ranks, applies the contig pass when ctgs is not empty (add_ctg_kmers, kcount.cpp:100-138; single rank),
+    purges and chooses extensions; the result is kmer_dht.table / kmer_dht.local_kmers. ctgs: objects with
+    .seq and .depth (a float, as Contig), or (seq, depth) pairs.
     """
     if kmer_len != kmer_dht.k:
         raise ValueError("kmer_len differs from the KmerDHT's k")
-    if len(ctgs):
-        raise NotImplementedError("contig k-mer pass (add_ctg_kmers) is not implemented in this version")
     for pr in packed_reads_list:
         if pr.qual_offset != qual_offset:
             raise ValueError("PackedReads qual_offset differs")
         kmer_dht.counter.add_reads(pr)
+    if len(ctgs):
+        seqs, depths = [], []
+        for c in ctgs:
+            seq, depth = (c.seq, c.depth) if hasattr(c, "seq") else (c[0], c[1])
+            seqs.append(seq)
+            depths.append(min(int(depth), 65535))  # Contig::get_uint16_t_depth (src/contigs.hpp:65)
+        kmer_dht.counter.add_ctgs(seqs, depths)
     kmer_dht.finish_updates()
     if dump_kmers:
         kmer_dht.dump_kmers(dump_dir)

@@ -12,8 +12,8 @@ import pytest
 
 import mhm2_proxy_amd as m
 import oracle_lib as O
-from common import (GOLDEN, assert_tables_equal, edge_case_set, hot_set, oracle_table, read_reads_file,
-                    read_table_file, synth_set)
+from common import (GOLDEN, assert_tables_equal, ctg_set, edge_case_set, hot_set, oracle_ctg_table, oracle_table,
+                    read_reads_file, read_table_file, synth_set)
 
 pytestmark = pytest.mark.gpu
 
@@ -213,3 +213,70 @@ def test_c2_scale_properties():
         kk = np.array([keys[i]], dtype=np.uint64)
         rc = O.kmer_revcomp(kk, 21)
         assert int(kk[0]) <= int(rc[0])
+
+
+# ---- contig pass (add_ctg_kmers -> insert_supermer_from_ctg) ----------------------------------------
+
+def ctg_table(b, o, seqs, depths, k, splits=1, **kw):
+    with m.KmerCounter(k, **kw) as c:
+        c.add_packed_reads(b, o)
+        cuts = [len(seqs) * i // splits for i in range(splits + 1)]
+        for a, z in zip(cuts[:-1], cuts[1:]):
+            c.add_ctgs(seqs[a:z], depths[a:z])
+        c.finish()
+        return c.fetch(), c.stats()
+
+
+@pytest.mark.parametrize("k,dmin", [(21, 2), (21, 1), (21, 3), (33, 2), (55, 2), (63, 4), (77, 2), (99, 3), (31, 2)])
+def test_contig_pass_vs_oracle(k, dmin):
+    """Reads, then contigs in order (replacement of non-UU / singleton read entries, min of agreeing contig
+    depths, conflicts purged, contig-only k-mers), bit-exact with the reference's sequential rules."""
+    b, o, seqs, depths = ctg_set(seed=40 + k + dmin)
+    got, st = ctg_table(b, o, seqs, depths, k, dmin_thres=dmin)
+    assert st["ctg_kmers"] > 0
+    assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, k, dmin_thres=dmin), f"contigs k={k} dmin={dmin}")
+    assert st["distinct"] == st["n_out"] + st["purged"]
+
+
+def test_contig_pass_order_kept_across_calls():
+    b, o, seqs, depths = ctg_set(seed=77)
+    got, _ = ctg_table(b, o, seqs, depths, 21, splits=4)
+    assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, 21), "contigs in 4 calls")
+
+
+@pytest.mark.parametrize("k", [21, 63])
+def test_contig_pass_with_overflow_sweeps(k, monkeypatch):
+    """Tiny LDS tables: read entries are spread over several sweeps of a bucket; a contig k-mer must meet
+    its read entry in whichever sweep holds it, and only count as contig-only after the last sweep."""
+    b, o, seqs, depths = ctg_set(seed=91, n_reads=600)
+    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
+    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    got, st = ctg_table(b, o, seqs, depths, k)
+    assert st["overflow_sweeps"] > 0
+    assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, k), "contigs + overflow sweeps")
+
+
+def test_contig_pass_exact_partition(monkeypatch):
+    b, o, seqs, depths = ctg_set(seed=92)
+    monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+    got, _ = ctg_table(b, o, seqs, depths, 33)
+    assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, 33), "contigs, exact partition")
+
+
+def test_contigs_without_reads():
+    _, _, seqs, depths = ctg_set(seed=93)
+    b, o = np.zeros(0, np.uint8), np.zeros(1, np.uint64)
+    got, st = ctg_table(b, o, seqs, depths, 21)
+    assert st["occurrences"] == 0
+    assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, 21), "contigs only")
+
+
+def test_analyze_kmers_with_contigs():
+    """The analyze_kmers mirror (src/kcount/kcount.cpp:140-157) with a Contigs list."""
+    b, o, seqs, depths = ctg_set(seed=94)
+    pr = m.PackedReads.from_arrays(b, o)
+    dht = m.KmerDHT(21)
+    ctgs = [(s_, float(d) + 0.7) for s_, d in zip(seqs, depths)]  # get_uint16_t_depth truncates
+    m.analyze_kmers(21, 0, 33, [pr], 2, ctgs, dht)
+    assert_tables_equal(dht.table, oracle_ctg_table(b, o, seqs, depths, 21), "analyze_kmers + contigs")
+    dht.counter.close()
