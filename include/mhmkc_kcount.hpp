@@ -175,6 +175,7 @@ struct Contig {
   int64_t id;
   std::string seq;
   double depth;
+  uint16_t get_uint16_t_depth() const { return (depth > UINT16_MAX ? UINT16_MAX : depth); }  // contigs.hpp:65
 };
 using Contigs = std::vector<Contig>;
 
@@ -190,8 +191,10 @@ struct RankInfo {
 template <int MAX_K>
 class HashTableInserter {
   mhmkc_t h_ = nullptr;
-  std::string seq_buf_;
-  std::vector<uint64_t> seq_offs_{0};
+  std::string seq_buf_, ctg_buf_;
+  std::vector<uint64_t> seq_offs_{0}, ctg_offs_{0};
+  std::vector<uint16_t> ctg_depths_;
+  bool using_ctg_kmers_ = false;
   int dmin_thres_ = 2;
 
  public:
@@ -215,11 +218,22 @@ class HashTableInserter {
     cfg.device = ri.device;
     check(mhmkc_create(&h_, &cfg), nullptr, "mhmkc_create");
   }
-  void init_ctg_kmers(int /*max_elems*/) { die("contig k-mer pass is not supported in this version"); }
+  // kcount_cpu.cpp:445-448: later supermers are contig supermers (insert_supermer_from_ctg)
+  void init_ctg_kmers(int /*max_elems*/) {
+    flush_inserts();
+    using_ctg_kmers_ = true;
+  }
 
-  // kcount_cpu.cpp:450-463 (buffered; flushed in flush_inserts)
+  // kcount_cpu.cpp:450-463 (buffered; flushed in flush_inserts). Read supermers have count 1; contig
+  // supermers carry the contig depth and are applied after every read, in order (mhmkc_add_ctgs).
   void insert_supermer(const std::string &supermer_seq, kmer_count_t count) {
-    if (count > 1) die("supermer count > 1 (contig pass) is not supported in this version");
+    if (using_ctg_kmers_) {
+      ctg_buf_ += supermer_seq;
+      ctg_offs_.push_back(ctg_buf_.size());
+      ctg_depths_.push_back(count);
+      return;
+    }
+    if (count > 1) die("read supermer with count > 1");
     seq_buf_ += supermer_seq;
     seq_offs_.push_back(seq_buf_.size());
   }
@@ -231,6 +245,13 @@ class HashTableInserter {
       check(mhmkc_add_seqs(h_, seq_buf_.data(), seq_offs_.data(), seq_offs_.size() - 1, 1), h_, "mhmkc_add_seqs");
       seq_buf_.clear();
       seq_offs_.assign(1, 0);
+    }
+    if (ctg_offs_.size() > 1) {
+      check(mhmkc_add_ctgs(h_, ctg_buf_.data(), ctg_offs_.data(), ctg_depths_.data(), ctg_offs_.size() - 1), h_,
+            "mhmkc_add_ctgs");
+      ctg_buf_.clear();
+      ctg_offs_.assign(1, 0);
+      ctg_depths_.clear();
     }
   }
   // kcount_cpu.cpp:490-528
@@ -274,6 +295,7 @@ class KmerDHT {
   }
   int get_minimizer_len() const { return minimizer_len; }
   void add_supermer(const std::string &seq, kmer_count_t count) { ht_inserter.insert_supermer(seq, count); }
+  void init_ctg_kmers(int max_elems) { ht_inserter.init_ctg_kmers(max_elems); }  // kmer_dht.cpp:169-172
   void add_packed_reads(const PackedReads &pr) { ht_inserter.add_packed_reads(pr); }
   void flush_updates() { ht_inserter.flush_inserts(); }
   void finish_updates() { ht_inserter.insert_into_local_hashtable(local_kmers); }
@@ -310,12 +332,22 @@ void analyze_kmers(unsigned kmer_len, unsigned /*prev_kmer_len*/, int qual_offse
                    std::vector<PackedReads *> &packed_reads_list, int /*dmin_thres: set on KmerDHT*/, Contigs &ctgs,
                    KmerDHT<MAX_K> &kmer_dht, bool dump_kmers) {
   if (kmer_len != Kmer<MAX_K>::get_k()) die("kmer_len differs from Kmer<MAX_K>::get_k()");
-  if (!ctgs.empty()) die("contig k-mer pass (add_ctg_kmers) is not supported in this version");
   for (auto *pr : packed_reads_list) {
     if (pr->get_qual_offset() != qual_offset) die("qual_offset mismatch");
     kmer_dht.add_packed_reads(*pr);
   }
   kmer_dht.flush_updates();
+  if (!ctgs.empty()) {  // add_ctg_kmers (kcount.cpp:100-138): one supermer per contig at one rank, in order
+    kmer_dht.init_ctg_kmers(0);
+    SeqBlockInserter<MAX_K> sbi(0, kmer_dht.get_minimizer_len());
+    for (auto &ctg : ctgs) {
+      if (ctg.seq.length() < kmer_len + 2) continue;
+      std::string seq = ctg.seq;
+      sbi.process_seq(seq, ctg.get_uint16_t_depth(), kmer_dht);
+    }
+    sbi.done_processing(kmer_dht);
+    kmer_dht.flush_updates();
+  }
   kmer_dht.finish_updates();
   if (dump_kmers) kmer_dht.dump_kmers("kmers-" + std::to_string(kmer_len) + ".txt");
 }

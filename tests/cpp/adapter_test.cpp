@@ -4,6 +4,7 @@
 //   adapter_test kat                      Kmer<MAX_K> known answers only (no GPU)
 //   adapter_test reads <k> <seqqual.txt>  analyze_kmers over PackedReads
 //   adapter_test seqs  <k> <seqqual.txt>  SeqBlockInserter::process_seq over lowercase-masked strings
+//   adapter_test ctgs  <k> <seqqual.txt> <ctgs.txt>  analyze_kmers with a Contigs list ("SEQ DEPTH" lines)
 #include <algorithm>
 #include <fstream>
 #include <iostream>
@@ -14,7 +15,7 @@
 using namespace mhm2;
 
 template <int MAX_K>
-int run(const std::string &mode, int k, const std::string &path) {
+int run(const std::string &mode, int k, const std::string &path, const std::string &ctg_path) {
   Kmer<MAX_K>::set_k(k);
   std::ifstream in(path);
   std::string line;
@@ -29,7 +30,18 @@ int run(const std::string &mode, int k, const std::string &path) {
   }
   KmerDHT<MAX_K> dht(1000, 2);
   Contigs ctgs;
-  if (mode == "reads") {
+  if (mode == "ctgs") {
+    std::ifstream cin_(ctg_path);
+    int64_t id = 0;
+    while (std::getline(cin_, line)) {
+      std::istringstream ss(line);
+      Contig c;
+      c.id = id++;
+      ss >> c.seq >> c.depth;
+      ctgs.push_back(c);
+    }
+  }
+  if (mode == "reads" || mode == "ctgs") {
     std::vector<PackedReads *> list{&pr};
     analyze_kmers<MAX_K>(k, 0, 33, list, 2, ctgs, dht, false);
   } else {
@@ -73,8 +85,9 @@ int main(int argc, char **argv) {
     return ok ? 0 : 1;
   }
   int k = std::atoi(argv[2]);
-  if (k < 32) return run<32>(mode, k, argv[3]);
-  if (k < 64) return run<64>(mode, k, argv[3]);
-  if (k < 96) return run<96>(mode, k, argv[3]);
-  return run<128>(mode, k, argv[3]);
+  const std::string ctg_path = argc > 4 ? argv[4] : "";
+  if (k < 32) return run<32>(mode, k, argv[3], ctg_path);
+  if (k < 64) return run<64>(mode, k, argv[3], ctg_path);
+  if (k < 96) return run<96>(mode, k, argv[3], ctg_path);
+  return run<128>(mode, k, argv[3], ctg_path);
 }

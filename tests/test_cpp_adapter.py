@@ -41,3 +41,28 @@ def test_adapter_matches_golden(mode, k, setname, tmp_path):
     got = out.stdout.splitlines()
     exp = sorted(gzip.open(GOLDEN / f"table_{setname}_k{k}.tsv.gz", "rt").read().splitlines())
     assert got == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [21, 63])
+def test_adapter_contig_pass(k, tmp_path):
+    """analyze_kmers with a Contigs list through the C++ adapter equals the oracle's contig pass."""
+    import sys
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    import mhm2_proxy_amd as m
+    from common import ctg_set, oracle_ctg_table
+
+    exe = build(tmp_path)
+    b, o, seqs, depths = ctg_set(seed=120 + k)
+    pr = m.PackedReads.from_arrays(b, o)
+    reads = tmp_path / "reads.txt"
+    with open(reads, "w") as f:
+        for i in range(pr.get_local_num_reads()):
+            _, s_, q = pr.get_read(i)
+            f.write(f"{s_} {q}\n")
+    ctgs = tmp_path / "ctgs.txt"
+    ctgs.write_text("".join(f"{s_} {int(d)}.25\n" for s_, d in zip(seqs, depths)))
+    out = subprocess.run([str(exe), "ctgs", str(k), str(reads), str(ctgs)], capture_output=True, text=True, check=True)
+    exp = sorted(oracle_ctg_table(b, o, seqs, depths, k).lines())
+    assert out.stdout.splitlines() == exp
