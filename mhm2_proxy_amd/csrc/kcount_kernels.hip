@@ -531,6 +531,26 @@ __device__ __forceinline__ uint32_t fine_digit(const uint64_t *rk, const Partiti
   return (uint32_t)((part_hash<NL>(key) >> (64 - p.coarse_bits - p.fine_bits)) & fmask);
 }
 
+// The chunk a partition workgroup works on: its run from the per-chunk run index, then its tile of it.
+template <int T>
+__device__ __forceinline__ SChunk chunk_of(const PartitionParams &p, uint32_t c) {
+  const SRun r = p.runs[p.chunk_run[c]];
+  const uint64_t o = (uint64_t)(c - r.chunk0) * T;
+  SChunk ch;
+  ch.start = r.start + o;
+  ch.count = (uint32_t)(r.count - o < (uint64_t)T ? r.count - o : (uint64_t)T);
+  ch.src = r.src;
+  ch.coarse_local = r.coarse_local;
+  ch.pad = 0;
+  return ch;
+}
+
+__global__ __launch_bounds__(256) void k_chunk_runs(const SRun *runs, uint32_t *chunk_run, int tile) {
+  const SRun r = runs[blockIdx.x];
+  const uint32_t n = (uint32_t)((r.count + tile - 1) / tile);
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) chunk_run[r.chunk0 + i] = blockIdx.x;
+}
+
 // All W records of a thread are loaded before any is processed (W * 8 B * NL in flight per lane). The
 // loads are unconditional (lanes past the chunk end re-read its last record) so that no use of a loaded
 // value sits inside a branch: a conditional load whose value is consumed in its own branch makes the
@@ -557,7 +577,7 @@ __global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
   extern __shared__ __align__(16) uint32_t hist[];  // the only LDS object
   const uint32_t nf = 1u << p.fine_bits;
   for (uint32_t b = threadIdx.x; b < nf; b += E_THREADS) hist[b] = 0;
-  const SChunk ch = p.chunks[blockIdx.x];
+  const SChunk ch = chunk_of<T>(p, blockIdx.x);
   const PlaneSet src = p.srcs[ch.src];
   uint64_t rk[W][NL];
   uint32_t re[W];
@@ -581,7 +601,7 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t nf = 1u << p.fine_bits;
   scatter_clear((uint32_t *)smem, nf);
-  const SChunk ch = p.chunks[blockIdx.x];
+  const SChunk ch = chunk_of<T>(p, blockIdx.x);
   const PlaneSet src = p.srcs[ch.src];
   uint64_t rk[W][NL];
   uint32_t re[W], inf[W];
@@ -1444,6 +1464,12 @@ hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipSt
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_chunks) return hipSuccess;
   MHM_DISPATCH(nl, packed, do_part_scatter, (p, s));
+}
+
+hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_run, int tile, hipStream_t s) {
+  if (!n_runs) return hipSuccess;
+  k_chunk_runs<<<dim3(n_runs), dim3(256), 0, s>>>(runs, chunk_run, tile);
+  return hipGetLastError();
 }
 
 hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor, uint32_t n,

@@ -46,8 +46,17 @@ struct SChunk {
   uint32_t pad;
 };
 
+// A run = one non-empty (source, segment) span, cut into tile-sized chunks; chunk0 = its first chunk.
+struct SRun {
+  uint64_t start, count;
+  uint32_t src, coarse_local;
+  uint32_t chunk0, pad;
+};
+
 struct PartitionParams {
-  const SChunk *chunks;
+  const SRun *runs;                 // [n_runs]
+  const uint32_t *chunk_run;        // [n_chunks]: run of each chunk (launch_chunk_runs fills it)
+  uint32_t n_runs;
   uint32_t n_chunks;
   const PlaneSet *srcs;           // device table of source plane sets
   int k;
@@ -168,6 +177,8 @@ hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigne
                             hipStream_t s);
 hipError_t launch_extract_hist(const ExtractParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, hipStream_t s);
+// chunk_run[c] for every chunk of the runs (one workgroup per run)
+hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_run, int tile, hipStream_t s);
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor,

@@ -500,24 +500,21 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   st.fine_buckets = n_fine;
   if ((rc = prepare_ctgs())) return rc;
 
-  // chunk table
+  // run table: one entry per non-empty (source, segment) span; the device expands it into chunks
   const int T = mhm::tile_bases(nl);
-  std::vector<mhm::SChunk> chunks;
+  std::vector<mhm::SRun> runs;
   std::vector<mhm::PlaneSet> ps;
+  uint64_t n_chunks = 0;
   for (size_t s = 0; s < srcs.size(); s++) {
     ps.push_back(srcs[s].planes);
     for (uint32_t i = 0; i < no * NSUB; i++) {
-      for (uint64_t o = 0; o < srcs[s].count[i]; o += T) {
-        mhm::SChunk ch{};
-        ch.start = srcs[s].start[i] + o;
-        ch.count = (uint32_t)std::min<uint64_t>(T, srcs[s].count[i] - o);
-        ch.src = (uint32_t)s;
-        ch.coarse_local = i / NSUB;
-        chunks.push_back(ch);
-      }
+      const uint64_t cnt = srcs[s].count[i];
+      if (!cnt) continue;
+      runs.push_back({srcs[s].start[i], cnt, (uint32_t)s, i / NSUB, (uint32_t)n_chunks, 0});
+      n_chunks += (cnt + T - 1) / T;
     }
   }
-  if (chunks.size() >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
+  if (n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
   // capped fine layout
   std::vector<uint64_t> cfit(2 * (size_t)no);  // [coarse_base | coarse_fcap]
   uint64_t r2_size = 0;
@@ -528,15 +525,21 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     cfit[no + c] = fcap;
     r2_size += fcap << fb;
   }
-  if ((e = d_chunks.ensure(std::max<size_t>(1, chunks.size()) * sizeof(mhm::SChunk))) != hipSuccess)
+  if ((e = d_chunks.ensure(std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun) + 4 * (n_chunks + 1) + 256)) !=
+      hipSuccess)
     return hip_fail(e, "chunk table");
+  mhm::SRun *d_runs = d_chunks.as<mhm::SRun>();
+  uint32_t *d_chunk_run = (uint32_t *)(d_chunks.as<char>() + align_up(runs.size() * sizeof(mhm::SRun), 256));
   if ((e = d_srcs.ensure(std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 16 * (size_t)no)) != hipSuccess)
     return hip_fail(e, "source table");
   unsigned long long *d_cfit = (unsigned long long *)(d_srcs.as<char>() + align_up(ps.size() * sizeof(mhm::PlaneSet), 16));
-  if (!chunks.empty() &&
-      (e = hipMemcpyAsync(d_chunks.p, chunks.data(), chunks.size() * sizeof(mhm::SChunk), hipMemcpyHostToDevice,
-                          stream)) != hipSuccess)
-    return hip_fail(e, "chunk H2D");
+  if (!runs.empty()) {
+    if ((e = hipMemcpyAsync(d_runs, runs.data(), runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, stream)) !=
+        hipSuccess)
+      return hip_fail(e, "run table H2D");
+    if ((e = mhm::launch_chunk_runs(d_runs, (uint32_t)runs.size(), d_chunk_run, T, stream)) != hipSuccess)
+      return hip_fail(e, "chunk index");
+  }
   if (!ps.empty() && (e = hipMemcpyAsync(d_srcs.p, ps.data(), ps.size() * sizeof(mhm::PlaneSet),
                                          hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "source H2D");
@@ -553,8 +556,10 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if ((e = d_out_cursor.ensure(8)) != hipSuccess) return hip_fail(e, "output cursor");
 
   mhm::PartitionParams pp{};
-  pp.chunks = d_chunks.as<mhm::SChunk>();
-  pp.n_chunks = (uint32_t)chunks.size();
+  pp.runs = d_runs;
+  pp.chunk_run = d_chunk_run;
+  pp.n_runs = (uint32_t)runs.size();
+  pp.n_chunks = (uint32_t)n_chunks;
   pp.srcs = d_srcs.as<mhm::PlaneSet>();
   pp.k = k;
   pp.coarse_bits = cb;
