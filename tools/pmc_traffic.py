@@ -1,0 +1,25 @@
+"""Per-launch HBM traffic of each stage from a PMC summary (tools/pmc_summary.py output) ->
+profiles/pmc_traffic.json, which bench.py reports as roofline.traffic.
+
+traffic = (FETCH_SIZE * 2 + WRITE_SIZE) * 1024 bytes per launch: rocprofv3 reports both in KiB, and on
+gfx950 FETCH_SIZE counts half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section); the
+counts kernel's 8-byte loads match its algorithmic read volume under the same correction (within 0.2 %).
+  python tools/pmc_traffic.py <tag>
+"""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+tag = sys.argv[1] if len(sys.argv) > 1 else "pmc"
+summ = json.loads((ROOT / "gpurun_out" / f"{tag}_summary.json").read_text())
+stage_of = {"k_extract_scatter": "extract_scatter", "k_extract_hist": "extract_hist", "k_part_scatter": "part_scatter",
+            "k_part_hist": "part_hist", "k_count": "count"}
+out = {}
+for kern, c in summ.items():
+    base = kern.split("<")[0]
+    if base in stage_of and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out[stage_of[base]] = int((c["FETCH_SIZE"] * 2 + c["WRITE_SIZE"]) * 1024)
+doc = {"per_launch_bytes": out, "source": f"gpurun_out/{tag}", "formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024"}
+(ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(doc, indent=1) + "\n")
+print(json.dumps(doc, indent=1))
