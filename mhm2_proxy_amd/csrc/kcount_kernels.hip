@@ -415,12 +415,22 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
 #pragma unroll
   for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += E_THREADS) {
-    const uint32_t c = lcnt[b];
-    const unsigned long long off = c ? atomicAdd(&cursor[(uint64_t)b * cstride], (unsigned long long)c) : 0ull;
-    if (lim.cap && c && off + c > lim.end(b)) atomicOr(err, 2u);
-    goff[b] = off;
-    lstart[b] = c;
+  // Reserve each bin's run in the global layout. The returned offsets stay in registers while the bins are
+  // scanned and the records staged, so the atomics' round trip overlaps that LDS work (a bin count up to
+  // SCATTER_MAX_BINS = 8 * E_THREADS).
+  unsigned long long off[8];
+  uint32_t cnt[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t b = threadIdx.x + i * E_THREADS;
+    off[i] = 0;
+    cnt[i] = 0;
+    if (b < nb) {
+      const uint32_t c = lcnt[b];
+      cnt[i] = c;
+      if (c) off[i] = atomicAdd(&cursor[(uint64_t)b * cstride], (unsigned long long)c);
+      lstart[b] = c;
+    }
   }
   __syncthreads();
   const uint32_t total = block_excl_scan<E_THREADS>(lstart, (int)nb, wsum);
@@ -433,6 +443,14 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       for (int w = 0; w < NL; w++) stage[w * T + pos] = rk[j][w];
       sbin[pos] = (uint16_t)d;
       if (!PACKED) sext[pos] = (uint8_t)((inf[j] >> 16) & 63u);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t b = threadIdx.x + i * E_THREADS;
+    if (b < nb) {
+      if (lim.cap && cnt[i] && off[i] + cnt[i] > lim.end(b)) atomicOr(err, 2u);
+      goff[b] = off[i];
     }
   }
   __syncthreads();
@@ -506,10 +524,10 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
   if (kEStaged)
-    scatter_staged<NL, PACKED, W>(rk, inf, p.n_bins, smem, area, p.cursor + sub * CPAD, E_NSUB * CPAD, p.out, lim,
+    scatter_staged<NL, PACKED, W>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
                                   p.err);
   else
-    scatter_regs<NL, PACKED, W>(rk, inf, p.n_bins, smem, p.cursor + sub * CPAD, E_NSUB * CPAD, p.out, lim, p.err);
+    scatter_regs<NL, PACKED, W>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.err);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -30,7 +30,7 @@ struct ExtractParams {
   uint32_t n_bins;                  // 1 << coarse_bits
   int hbits;                        // hash bits stored in the record after the ext code (0: none)
   unsigned long long *hist;         // [n_bins] (E-hist)
-  unsigned long long *cursor;       // [n_bins * E_NSUB] (E-scatter): segment (b, s) at index b * E_NSUB + s
+  unsigned long long *cursor;       // [E_NSUB * n_bins] (E-scatter): cursor of segment (b, s) at s * n_bins + b
   uint64_t bin_cap;                 // capped mode: segment (b, s) owns [i*bin_cap, (i+1)*bin_cap), i = b*E_NSUB+s,
                                     // s = blockIdx % E_NSUB; 0 = exact bases, everything in segment (b, 0)
   PlaneSet out;                     // (E-scatter)

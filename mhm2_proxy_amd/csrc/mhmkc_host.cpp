@@ -247,7 +247,10 @@ int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
   const uint32_t nseg = nb * NSUB;
   sl->counts.assign(nseg, 0);
   sl->bases.assign(nseg + 1, 0);
-  std::vector<uint64_t> cur((size_t)nseg * mhm::CPAD), hist(nb);
+  // device cursors are sub-major (cursor[s * nb + b]): the 64 lanes of one atomic instruction then hit 64
+  // consecutive words, which the memory-side atomic unit serves as whole lines
+  std::vector<uint64_t> cur((size_t)nseg), hist(nb);
+  auto cidx = [&](uint32_t i) { return (size_t)(i % NSUB) * nb + i / NSUB; };
   const uint64_t expect = wins / nseg;
   const uint64_t cap = align_up(expect + expect / 25 + 1024, 64);
   bool exact = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
@@ -277,7 +280,7 @@ int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
       p.bin_cap = cap;
     }
     if ((rc = set_planes(sl->buf, sl->bases[nseg], sl->planes))) return rc;
-    for (uint32_t i = 0; i < nseg; i++) cur[(size_t)i * mhm::CPAD] = sl->bases[i];
+    for (uint32_t i = 0; i < nseg; i++) cur[cidx(i)] = sl->bases[i];
     if ((e = hipMemcpyAsync(d_cursor.p, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
       return hip_fail(e, "cursor H2D");
     p.out = sl->planes;
@@ -299,7 +302,7 @@ int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
   }
   uint64_t tot = 0;
   for (uint32_t i = 0; i < nseg; i++) {
-    sl->counts[i] = cur[(size_t)i * mhm::CPAD] - sl->bases[i];
+    sl->counts[i] = cur[cidx(i)] - sl->bases[i];
     tot += sl->counts[i];
   }
   sl->n = tot;
@@ -745,8 +748,10 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     g_create_error = "dyn_min_depth must be in [0, 1]";
     return MHMKC_EINVAL;
   }
-  if (cfg->n_ranks < 1 || cfg->n_ranks > 64 || cfg->rank < 0 || cfg->rank >= cfg->n_ranks) {
-    g_create_error = "bad rank / n_ranks";
+  // up to 8 ranks (one node): the coarse partition then has <= 2^11 bins, what a scatter workgroup keeps
+  // in registers (scatter_staged)
+  if (cfg->n_ranks < 1 || cfg->n_ranks > 8 || cfg->rank < 0 || cfg->rank >= cfg->n_ranks) {
+    g_create_error = "bad rank / n_ranks (1..8 ranks, one per GPU of a node)";
     return MHMKC_EINVAL;
   }
   if (cfg->n_ranks > 1 && !cfg->comm_id) {
