@@ -49,15 +49,15 @@ def parse():
 def algorithmic_bytes(stage: str, st: dict, k: int) -> float:
     """Algorithmic HBM bytes of one launch of a stage."""
     nl = k // 32 + 1
-    rec = 8 * nl + (0 if 2 * (k - 32 * (nl - 1)) + 6 <= 64 else 1)
+    rec, frec = st["coarse_record_bytes"], st["fine_record_bytes"]  # 5 / 4 B compact (k <= 21), else 8 * nl (+1)
     occ, owned, bases = st["occurrences"], st["owned_records"], st["bases"]
     out = st["n_out"] * (8 * nl + 4)
     return {
         "extract_hist": bases,
         "extract_scatter": bases + occ * rec,
         "part_hist": owned * rec,
-        "part_scatter": 2 * owned * rec,
-        "count": owned * rec + out,
+        "part_scatter": owned * (rec + frec),
+        "count": owned * frec + out,
         "exchange": st["bytes_sent"],
     }.get(stage, 0.0)
 

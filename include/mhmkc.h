@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 2
+#define MHMKC_ABI_VERSION 3
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -81,6 +81,8 @@ typedef struct {
   uint64_t bytes_sent;     /* bytes sent to other ranks in the exchange */
   uint64_t exact_reruns;   /* capped partition passes redone with exact bucket sizes (skewed input) */
   uint64_t ctg_kmers;      /* distinct contig k-mers of the contig pass (0 without contigs) */
+  uint64_t coarse_record_bytes; /* HBM bytes per k-mer record after extraction (5 for compact records) */
+  uint64_t fine_record_bytes;   /* HBM bytes per k-mer record after the fine partition (4 when compact) */
   double ms_total;         /* wall time of the last add_reads..finish sequence (device events) */
   double ms_kernel[8];     /* per-stage device time when profiling is on: see MHMKC_STAGE_* */
   uint64_t launches[8];    /* per-stage launch count when profiling is on */

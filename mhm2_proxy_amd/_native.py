@@ -72,6 +72,8 @@ class MhmkcStats(C.Structure):
         ("bytes_sent", C.c_uint64),
         ("exact_reruns", C.c_uint64),
         ("ctg_kmers", C.c_uint64),
+        ("coarse_record_bytes", C.c_uint64),
+        ("fine_record_bytes", C.c_uint64),
         ("ms_total", C.c_double),
         ("ms_kernel", C.c_double * 8),
         ("launches", C.c_uint64 * 8),

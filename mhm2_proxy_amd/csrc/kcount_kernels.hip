@@ -13,6 +13,7 @@
 //                    and compaction into the output table.
 // Semantics follow the reference CPU kcount at one rank, cited per function.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <algorithm>
 
@@ -310,7 +311,14 @@ __global__ void k_tile_first_read(ReadsView rv, uint32_t *out, uint32_t n_tiles,
 // ------------------------------------------------------------------------------------------------
 // extract: histogram
 
-template <int NL, bool PACKED>
+// Partition hash of a window's key: MurmurHash3 h1 (part_hash), or the key bijection of compact records.
+template <int NL, bool CMP>
+__device__ __forceinline__ uint64_t window_hash(const uint64_t *key, int k) {
+  if (CMP) return cpart_hash(key[0], 2 * k);
+  return part_hash<NL>(key);
+}
+
+template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
   load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
   const int sh = 64 - p.coarse_bits;
   walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.k, [&](int, const uint64_t *key, uint32_t, bool valid) {
-    if (valid) atomicAdd(&hist[(uint32_t)(part_hash<NL>(key) >> sh)], 1u);
+    if (valid) atomicAdd(&hist[(uint32_t)(window_hash<NL, CMP>(key, p.k) >> sh)], 1u);
   });
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < p.n_bins; b += E_THREADS) {
@@ -341,6 +349,25 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
 // per coarse bucket), so partial lines merge in that XCD's L2 before they reach HBM.
 // LDS: lcnt[nb] u32 | pad to 16 B | goff[nb] u64.
 
+// Global store formats of a scatter: the record words (+ the ext byte plane when not packed), or a
+// compact record (kmer_ops.hpp cmix) split into a u32 plane w[0] + a byte plane ext (coarse buckets,
+// <= 40 bits) or a u32 plane alone (fine buckets, <= 32 bits).
+enum { SF_WORDS = 0, SF_C40 = 1, SF_C32 = 2 };
+
+template <int NL, bool PACKED, int SF>
+__device__ __forceinline__ void store_out(const PlaneSet &out, uint64_t dst, const uint64_t *v, uint32_t ext) {
+  if (SF == SF_C40) {
+    ((uint32_t *)out.w[0])[dst] = (uint32_t)v[0];
+    out.ext[dst] = (uint8_t)(v[0] >> 32);
+  } else if (SF == SF_C32) {
+    ((uint32_t *)out.w[0])[dst] = (uint32_t)v[0];
+  } else {
+#pragma unroll
+    for (int w = 0; w < NL; w++) out.w[w][dst] = v[w];
+    if (!PACKED) out.ext[dst] = (uint8_t)ext;
+  }
+}
+
 // Bin limits of capped layouts: bin b may use [.., lim.base + b * lim.stride + lim.cap); lim.cap == 0: none.
 struct BinLimit {
   uint64_t base, stride, cap;
@@ -357,7 +384,7 @@ __device__ __forceinline__ void scatter_clear(uint32_t *lcnt, uint32_t nb) {
 // Bin b's cursor is cursor[b * cstride]. In a capped layout a bin that would overflow sets err bit 1
 // and its excess records are not written (the host then redoes the pass with exact bin sizes).
 // Called after lcnt has been cleared and a barrier.
-template <int NL, bool PACKED, int W>
+template <int NL, bool PACKED, int W, int SF>
 __device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
                                              unsigned char *smem, unsigned long long *cursor, uint32_t cstride,
                                              const PlaneSet &out, const BinLimit lim, unsigned int *err) {
@@ -380,9 +407,7 @@ __device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const 
       const uint32_t d = inf[j] & 0xffffu;
       const unsigned long long dst = goff[d] + rank[j];
       if (lim.cap && dst >= lim.end(d)) continue;
-#pragma unroll
-      for (int w = 0; w < NL; w++) out.w[w][dst] = rk[j][w];
-      if (!PACKED) out.ext[dst] = (uint8_t)((inf[j] >> 16) & 63u);
+      store_out<NL, PACKED, SF>(out, dst, rk[j], (inf[j] >> 16) & 63u);
     }
   }
 }
@@ -398,7 +423,7 @@ __host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packe
   return (size_t)nl * T * 8 + (size_t)T * 2 + (packed ? 0 : (size_t)T);
 }
 
-template <int NL, bool PACKED, int W>
+template <int NL, bool PACKED, int W, int SF>
 __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
                                                unsigned char *smem, unsigned char *area,
                                                unsigned long long *cursor, uint32_t cstride, const PlaneSet &out,
@@ -461,9 +486,10 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       const uint32_t d = sbin[pos];
       const unsigned long long dst = goff[d] + (pos - lstart[d]);
       if (lim.cap && dst >= lim.end(d)) continue;
+      uint64_t v[NL];
 #pragma unroll
-      for (int w = 0; w < NL; w++) out.w[w][dst] = stage[w * T + pos];
-      if (!PACKED) out.ext[dst] = sext[pos];
+      for (int w = 0; w < NL; w++) v[w] = stage[w * T + pos];
+      store_out<NL, PACKED, SF>(out, dst, v, PACKED ? 0u : sext[pos]);
     }
   }
 }
@@ -481,7 +507,7 @@ constexpr bool kPStaged = MHMKC_PSTAGE != 0;
 // ------------------------------------------------------------------------------------------------
 // extract: scatter into coarse buckets
 
-template <int NL, bool PACKED>
+template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
   extern __shared__ __align__(16) unsigned char smem0[];
@@ -503,14 +529,17 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   // stored hash bits, branch-free (hbits == 0: none)
   const int hsh = p.hbits ? 64 - p.hbits : 0;
   const uint64_t hmask = p.hbits ? ~0ull : 0ull;
+  const int csh = 64 - (2 * p.k - p.coarse_bits);  // compact: keep the low 2k - cb bits of the mixed key
   uint64_t rk[W][NL];
   uint32_t inf[W];
   walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.k,
                    [&](int i, const uint64_t *key, uint32_t e, bool valid) {
-                     const uint64_t h = part_hash<NL>(key);
+                     const uint64_t h = window_hash<NL, CMP>(key, p.k);
 #pragma unroll
                      for (int w = 0; w < NL; w++) rk[i][w] = key[w];
-                     if (PACKED) {
+                     if (CMP) {
+                       rk[i][0] = (((h << p.coarse_bits) >> csh) << EXT_BITS) | e;
+                     } else if (PACKED) {
                        rk[i][NL - 1] |= e;
                        rk[i][NL - 1] |= (((h << p.coarse_bits) >> hsh) & hmask) << EXT_BITS;
                      }
@@ -523,11 +552,12 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
                    });
   const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
+  constexpr int SF = CMP ? SF_C40 : SF_WORDS;
   if (kEStaged)
-    scatter_staged<NL, PACKED, W>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
-                                  p.err);
+    scatter_staged<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
+                                      p.err);
   else
-    scatter_regs<NL, PACKED, W>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.err);
+    scatter_regs<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.err);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -535,9 +565,10 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
 
 // Fine digit of a record: from the hash bits stored next to the ext code when there are enough of them,
 // otherwise by recomputing MurmurHash3 of the key. rk holds the raw record words.
-template <int NL, bool PACKED>
+template <int NL, bool PACKED, bool CMP>
 __device__ __forceinline__ uint32_t fine_digit(const uint64_t *rk, const PartitionParams &p) {
   const uint64_t fmask = (1ull << p.fine_bits) - 1;
+  if (CMP) return (uint32_t)((rk[0] >> (EXT_BITS + 2 * p.k - p.coarse_bits - p.fine_bits)) & fmask);
   if (PACKED && p.hbits >= p.fine_bits) {
     const uint64_t stored = (rk[NL - 1] >> EXT_BITS) & ((1ull << p.hbits) - 1);
     return (uint32_t)((stored >> (p.hbits - p.fine_bits)) & fmask);
@@ -547,6 +578,15 @@ __device__ __forceinline__ uint32_t fine_digit(const uint64_t *rk, const Partiti
   for (int w = 0; w < NL; w++) key[w] = rk[w];
   if (PACKED) key[NL - 1] &= ~((1ull << (EXT_BITS + p.hbits)) - 1);
   return (uint32_t)((part_hash<NL>(key) >> (64 - p.coarse_bits - p.fine_bits)) & fmask);
+}
+
+// Chunk of this workgroup: workgroups are dealt to the XCDs round-robin, so workgroup b runs on XCD b % 8
+// and takes the (b / 8)-th chunk of XCD class b % 8. All chunks of a coarse bucket then write their fine
+// buckets from one XCD, whose L2 merges the partial lines of consecutive chunks before they reach HBM.
+__device__ __forceinline__ bool xcd_chunk(const PartitionParams &p, uint32_t &c) {
+  const uint32_t x = blockIdx.x & 7u;
+  c = p.xcd_start[x] + (blockIdx.x >> 3);
+  return c < p.xcd_start[x + 1];
 }
 
 // The chunk a partition workgroup works on: its run from the per-chunk run index, then its tile of it.
@@ -573,7 +613,7 @@ __global__ __launch_bounds__(256) void k_chunk_runs(const SRun *runs, uint32_t *
 // loads are unconditional (lanes past the chunk end re-read its last record) so that no use of a loaded
 // value sits inside a branch: a conditional load whose value is consumed in its own branch makes the
 // compiler wait for it there, one load after the other. Callers check i < ch.count themselves.
-template <int NL, bool PACKED, int W>
+template <int NL, bool PACKED, bool CMP, int W>
 __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch, uint64_t (&rk)[W][NL],
                                            uint32_t (&re)[W]) {
   uint32_t rx[W];
@@ -581,29 +621,40 @@ __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch
   for (int j = 0; j < W; j++) {
     const uint32_t i = threadIdx.x + j * E_THREADS;
     const uint64_t idx = ch.start + (i < ch.count ? i : ch.count - 1);
+    if (CMP) {  // coarse compact record: low 32 bits + high byte
+      rk[j][0] = (uint64_t)gload((const uint32_t *)src.w[0] + idx);
+      rx[j] = (uint32_t)gload(src.ext + idx);
+      continue;
+    }
 #pragma unroll
     for (int w = 0; w < NL; w++) rk[j][w] = gload(src.w[w] + idx);
     rx[j] = PACKED ? 0u : (uint32_t)gload(src.ext + idx);
+  }
+  if (CMP) {
+#pragma unroll
+    for (int j = 0; j < W; j++) rk[j][0] |= (uint64_t)rx[j] << 32;
   }
 #pragma unroll
   for (int j = 0; j < W; j++) re[j] = PACKED ? (uint32_t)(rk[j][NL - 1] & 63u) : rx[j];
 }
 
-template <int NL, bool PACKED>
+template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
   extern __shared__ __align__(16) uint32_t hist[];  // the only LDS object
   const uint32_t nf = 1u << p.fine_bits;
   for (uint32_t b = threadIdx.x; b < nf; b += E_THREADS) hist[b] = 0;
-  const SChunk ch = chunk_of<T>(p, blockIdx.x);
+  uint32_t c;
+  if (!xcd_chunk(p, c)) return;  // no chunk left in this workgroup's XCD class (uniform: before any barrier)
+  const SChunk ch = chunk_of<T>(p, c);
   const PlaneSet src = p.srcs[ch.src];
   uint64_t rk[W][NL];
   uint32_t re[W];
-  load_chunk<NL, PACKED, W>(src, ch, rk, re);
+  load_chunk<NL, PACKED, CMP, W>(src, ch, rk, re);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < W; j++) {
-    if (threadIdx.x + j * E_THREADS < ch.count) atomicAdd(&hist[fine_digit<NL, PACKED>(rk[j], p)], 1u);
+    if (threadIdx.x + j * E_THREADS < ch.count) atomicAdd(&hist[fine_digit<NL, PACKED, CMP>(rk[j], p)], 1u);
   }
   __syncthreads();
   unsigned long long *g = p.fine_hist + (uint64_t)ch.coarse_local * nf;
@@ -613,21 +664,27 @@ __global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
   }
 }
 
-template <int NL, bool PACKED>
+template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t nf = 1u << p.fine_bits;
   scatter_clear((uint32_t *)smem, nf);
-  const SChunk ch = chunk_of<T>(p, blockIdx.x);
+  uint32_t c;
+  if (!xcd_chunk(p, c)) return;  // no chunk left in this workgroup's XCD class (uniform: before any barrier)
+  const SChunk ch = chunk_of<T>(p, c);
   const PlaneSet src = p.srcs[ch.src];
   uint64_t rk[W][NL];
   uint32_t re[W], inf[W];
-  load_chunk<NL, PACKED, W>(src, ch, rk, re);
+  load_chunk<NL, PACKED, CMP, W>(src, ch, rk, re);
+  // compact: the fine record keeps the bits below the fine digit (+ the ext code), <= 32 bits
+  const uint64_t cmask = (1ull << (EXT_BITS + 2 * p.k - p.coarse_bits - p.fine_bits)) - 1;
 #pragma unroll
   for (int j = 0; j < W; j++) {
-    inf[j] = (threadIdx.x + j * E_THREADS < ch.count) ? ((1u << 31) | (re[j] << 16) | fine_digit<NL, PACKED>(rk[j], p))
-                                                       : 0u;
+    inf[j] = (threadIdx.x + j * E_THREADS < ch.count)
+                 ? ((1u << 31) | (re[j] << 16) | fine_digit<NL, PACKED, CMP>(rk[j], p))
+                 : 0u;
+    if (CMP) rk[j][0] &= cmask;
   }
   __syncthreads();
   BinLimit lim{0, 0, 0};
@@ -636,10 +693,11 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
     lim = BinLimit{p.coarse_base[ch.coarse_local], fc, fc};
   }
   unsigned long long *cur = p.fine_cursor + (uint64_t)ch.coarse_local * nf;
+  constexpr int SF = CMP ? SF_C32 : SF_WORDS;
   if (kPStaged)
-    scatter_staged<NL, PACKED, W>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
+    scatter_staged<NL, PACKED, W, SF>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
   else
-    scatter_regs<NL, PACKED, W>(rk, inf, nf, smem, cur, 1, p.out, lim, p.err);
+    scatter_regs<NL, PACKED, W, SF>(rk, inf, nf, smem, cur, 1, p.out, lim, p.err);
 }
 
 // capped fine layout
@@ -727,8 +785,9 @@ __device__ __forceinline__ uint32_t slot_hash(const uint64_t *key) {
   return (uint32_t)(h >> 32);
 }
 
+template <typename K>  // key word type: uint64_t, or uint32_t for compact records
 struct CountLds {
-  uint64_t *keys;  // [NL][cap]
+  K *keys;         // [NL][cap]
   uint32_t *cnt;   // [cap]
   uint32_t *ext;   // [4][cap]: (A|C<<16, G|T<<16) left, then right
   int cap;         // multiple of 4: slots are probed in groups of 4
@@ -750,9 +809,14 @@ __device__ __forceinline__ void read_group(const uint64_t *last, int g, uint64_t
   const ulonglong2 a = q[0], b = q[1];
   v[0] = a.x, v[1] = a.y, v[2] = b.x, v[3] = b.y;
 }
+// 32-bit keys: one ds_read_b128 per group
+__device__ __forceinline__ void read_group(const uint32_t *last, int g, uint32_t (&v)[4]) {
+  const uint4 a = *(const uint4 *)(last + 4 * g);
+  v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
+}
 
-template <int NL>
-__device__ __forceinline__ bool rest_equal(const CountLds &t, int slot, const uint64_t *key) {
+template <int NL, typename K>
+__device__ __forceinline__ bool rest_equal(const CountLds<K> &t, int slot, const uint64_t *key) {
   bool eq = true;
 #pragma unroll
   for (int w = 0; w < NL - 1; w++) eq &= (t.keys[w * t.cap + slot] == key[w]);
@@ -762,16 +826,16 @@ __device__ __forceinline__ bool rest_equal(const CountLds &t, int slot, const ui
 // Result of looking at one group for key: >= 0 the slot holding it, -1 - i an empty slot i (and the key is
 // not in the group), G_FULL no empty slot and no key, G_BUSY a multi-word key is being written.
 constexpr int G_FULL = -8, G_BUSY = -9;
-template <int NL>
-__device__ __forceinline__ int examine_group(const CountLds &t, const uint64_t *key, int g, const uint64_t (&v)[4]) {
-  const uint64_t kl = key[NL - 1];
+template <int NL, typename K>
+__device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_t *key, int g, const K (&v)[4]) {
+  const K kl = (K)key[NL - 1];
   int found = -1, empty = -1;
   bool busy = false;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     if (found < 0 && v[i] == kl && (NL == 1 || rest_equal<NL>(t, 4 * g + i, key))) found = i;
-    if (v[i] == KEY_EMPTY && empty < 0) empty = i;
-    if (NL > 1 && v[i] == KEY_BUSY) busy = true;
+    if (v[i] == (K)KEY_EMPTY && empty < 0) empty = i;
+    if (NL > 1 && v[i] == (K)KEY_BUSY) busy = true;
   }
   if (found >= 0) return 4 * g + found;
   if (busy) return G_BUSY;
@@ -789,11 +853,11 @@ __device__ __forceinline__ int examine_group(const CountLds &t, const uint64_t *
 // the key nor an empty slot; slots only fill, so the key can never be inserted later in the sweep, and had
 // it been inserted earlier this lookup would have found it. Every occurrence of a key is therefore counted
 // in the same sweep; no occupancy counter is needed.
-template <int NL>
-__device__ int lds_insert(const CountLds &t, const uint64_t *key, int g, int r) {
-  uint64_t *last = t.keys + (NL - 1) * t.cap;
+template <int NL, typename K>
+__device__ int lds_insert(const CountLds<K> &t, const uint64_t *key, int g, int r) {
+  K *last = t.keys + (NL - 1) * t.cap;
   const int ng = t.cap >> 2;
-  const uint64_t kl = key[NL - 1];
+  const K kl = (K)key[NL - 1];
   int probed = 0;
   for (int iter = 0; iter < (1 << 20); iter++) {
     if (r >= 0) return r;
@@ -802,13 +866,16 @@ __device__ int lds_insert(const CountLds &t, const uint64_t *key, int g, int r) 
       g = (g + 1 == ng) ? 0 : g + 1;
     } else if (r != G_BUSY) {
       const int sl = 4 * g + (-1 - r);
-      const uint64_t want = (NL == 1) ? kl : KEY_BUSY;
-      const uint64_t old = atomicCAS((unsigned long long *)&last[sl], (unsigned long long)KEY_EMPTY,
-                                     (unsigned long long)want);
-      if (old == KEY_EMPTY) {
+      const K want = (NL == 1) ? kl : (K)KEY_BUSY;
+      K old;
+      if constexpr (sizeof(K) == 4)
+        old = atomicCAS((unsigned int *)&last[sl], 0xffffffffu, (unsigned int)want);
+      else
+        old = atomicCAS((unsigned long long *)&last[sl], (unsigned long long)KEY_EMPTY, (unsigned long long)want);
+      if (old == (K)KEY_EMPTY) {
         if (NL > 1) {
 #pragma unroll
-          for (int w = 0; w < NL - 1; w++) t.keys[w * t.cap + sl] = key[w];
+          for (int w = 0; w < NL - 1; w++) t.keys[w * t.cap + sl] = (K)key[w];
           __hip_atomic_store(&last[sl], kl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         return sl;
@@ -816,7 +883,7 @@ __device__ int lds_insert(const CountLds &t, const uint64_t *key, int g, int r) 
       if (NL == 1 && old == kl) return sl;  // the winner inserted this very key
       // otherwise the slot was just taken: look at the group again
     }
-    uint64_t v[4];
+    K v[4];
     read_group(last, g, v);
     r = examine_group<NL>(t, key, g, v);
   }
@@ -827,7 +894,8 @@ __device__ int lds_insert(const CountLds &t, const uint64_t *key, int g, int r) 
 // left/right extension + 1 when they are A/C/G/T (ExtCounts::inc ignores the rest, :152-164).
 // Extension counters are 16-bit halves of u32 LDS words, added without a return value; the old count
 // is returned for the saturation check (lds_clamp).
-__device__ __forceinline__ uint32_t lds_add(const CountLds &t, int slot, uint32_t e) {
+template <typename K>
+__device__ __forceinline__ uint32_t lds_add(const CountLds<K> &t, int slot, uint32_t e) {
 #if MHMKC_EXP_NORTN
   atomicAdd(&t.cnt[slot], 1u);
   const uint32_t old = 0;
@@ -864,7 +932,8 @@ __device__ __forceinline__ void ext_clamp(uint32_t *p, int half) {
   }
 }
 
-__device__ __forceinline__ void lds_clamp(const CountLds &t, int slot, uint32_t e) {
+template <typename K>
+__device__ __forceinline__ void lds_clamp(const CountLds<K> &t, int slot, uint32_t e) {
   const int l = (int)((e >> 3) & 7u), r = (int)(e & 7u);
   if (l < 4) ext_clamp(&t.ext[(l >> 1) * t.cap + slot], l & 1);
   if (r < 4) ext_clamp(&t.ext[(2 + (r >> 1)) * t.cap + slot], r & 1);
@@ -886,7 +955,8 @@ __device__ __forceinline__ void lds_clamp(const CountLds &t, int slot, uint32_t 
 // Final decision for one table slot: insert_into_local_hashtable (src/kcount/kcount_cpu.cpp:503-517):
 // count < 2 -> purged; left/right = get_ext(count) (kcount_cpu.cpp:173-182, with the exact double
 // expression of the dynamic threshold); both 'X' -> purged.
-__device__ __forceinline__ bool slot_survives(const CountLds &t, int slot, const CountParams &p, uint16_t &c16,
+template <typename K>
+__device__ __forceinline__ bool slot_survives(const CountLds<K> &t, int slot, const CountParams &p, uint16_t &c16,
                                               char &L, char &R) {
   const uint32_t c32 = t.cnt[slot];
   const uint32_t c = c32 > 65535u ? 65535u : c32;
@@ -907,8 +977,8 @@ __device__ __forceinline__ bool slot_survives(const CountLds &t, int slot, const
 // src/kcount/kcount_cpu.cpp:367-404); a key absent from the table is absent from the reads once the
 // bucket's last sweep has run (deferred keys are counted in a later sweep), and is finalized here
 // directly (insert_into_local_hashtable, kcount_cpu.cpp:503-522).
-template <int NL>
-__device__ void ctg_apply(const CountLds &t, const CountParams &p, uint32_t b, bool last_sweep,
+template <int NL, bool CMP, typename K>
+__device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b, bool last_sweep,
                           unsigned long long *s_range) {
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -929,7 +999,7 @@ __device__ void ctg_apply(const CountLds &t, const CountParams &p, uint32_t b, b
   __syncthreads();
   const uint64_t q0 = s_range[0], q1 = s_range[1];
   const int ng = t.cap >> 2;
-  const uint64_t *last = t.keys + (NL - 1) * t.cap;
+  const K *last = t.keys + (NL - 1) * t.cap;
   for (uint64_t q = q0 + tid; q < q1; q += C_THREADS) {
     if (p.ctg_done[q]) continue;
     uint64_t key[NL];
@@ -937,12 +1007,19 @@ __device__ void ctg_apply(const CountLds &t, const CountParams &p, uint32_t b, b
     for (int w = 0; w < NL; w++) key[w] = p.ctg_keys[w][q];
     const uint32_t st = p.ctg_state[q];
     const uint32_t c = st & 0xffffu, l = (st >> 16) & 7u, r = (st >> 19) & 7u;
-    int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
+    uint64_t tkey[NL];  // the key as the table holds it
+#pragma unroll
+    for (int w = 0; w < NL; w++) tkey[w] = key[w];
+    if (CMP) {  // compact: the mixed key's bits below the bucket digits, above the ext code
+      const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
+      tkey[0] = (cmix(key[0] >> (64 - B), B) & ((1ull << rb) - 1)) << EXT_BITS;
+    }
+    int g = (int)__umulhi(slot_hash<NL>(tkey), (uint32_t)ng);
     int slot = -1;
     for (int pr = 0; pr < C_PROBE; pr++) {  // find only: a key in the table is within its probe window
-      uint64_t v[4];
+      K v[4];
       read_group(last, g, v);
-      const int e = examine_group<NL>(t, key, g, v);
+      const int e = examine_group<NL>(t, tkey, g, v);
       if (e >= 0) {
         slot = e;
         break;
@@ -998,37 +1075,26 @@ __device__ void ctg_apply(const CountLds &t, const CountParams &p, uint32_t b, b
   __syncthreads();
 }
 
-// e receives the raw low bits of the record (ext code in bits 0-5, stored hash bits above) so that an
-// overflowing record is written back unchanged; the key has them cleared.
-template <int NL, bool PACKED>
-__device__ __forceinline__ void load_record(const PlaneSet &ps, uint64_t idx, uint64_t low_mask, uint64_t *key,
-                                            uint32_t &e) {
-#pragma unroll
-  for (int w = 0; w < NL; w++) key[w] = ps.w[w][idx];
-  if (PACKED) {
-    e = (uint32_t)(key[NL - 1] & low_mask);
-    key[NL - 1] &= ~low_mask;
-  } else {
-    e = ps.ext[idx];
-  }
-}
-
-template <int NL, bool PACKED>
+// A deferred record goes back unchanged: key | raw low bits (ext code, stored hash bits).
+template <int NL, bool PACKED, bool CMP>
 __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, const uint64_t *key, uint32_t e) {
+  if (CMP) {
+    ((uint32_t *)ps.w[0])[idx] = (uint32_t)(key[0] | e);
+    return;
+  }
 #pragma unroll
   for (int w = 0; w < NL; w++) ps.w[w][idx] = (w == NL - 1 && PACKED) ? (key[w] | e) : key[w];
   if (!PACKED) ps.ext[idx] = (uint8_t)e;
 }
 
-// Table slots per thread in the finalize pass.
-constexpr int C_SPT = 5;
 
-template <int NL, bool PACKED>
+template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   extern __shared__ __align__(16) unsigned char smem[];
-  CountLds t;
+  using K = typename std::conditional<CMP, uint32_t, uint64_t>::type;
+  CountLds<K> t;
   t.cap = p.cap;
-  t.keys = (uint64_t *)smem;
+  t.keys = (K *)smem;
   t.cnt = (uint32_t *)(t.keys + NL * t.cap);
   t.ext = t.cnt + t.cap;
   // scalars live after the table in the same dynamic region (count_lds_bytes adds 128 bytes)
@@ -1040,8 +1106,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
   unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
   // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
-  uint64_t *s_mkey = (uint64_t *)(smem + count_table_bytes(NL));
-  uint32_t *s_me = (uint32_t *)(s_mkey + NL * miss_cap(NL));
+  constexpr int MC = miss_cap(NL, CMP);
+  K *s_mkey = (K *)(smem + count_table_bytes(NL, CMP));
+  uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
+  constexpr int SPT = (count_cap(NL, CMP) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -1052,11 +1120,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   constexpr uint32_t RND = (uint32_t)R * C_THREADS;
   constexpr uint32_t HOT = 0xC000u - 2u * RND;  // see ext_clamp
   static_assert(HOT > 0x8000u, "round too large for the extension-counter clamp");
-  constexpr int MC = miss_cap(NL);
   constexpr int C_BATCH = MHMKC_CBATCH < R ? MHMKC_CBATCH : R;
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
   const int ng = t.cap >> 2;
-  const uint64_t *last = t.keys + (NL - 1) * t.cap;
+  const K *last = t.keys + (NL - 1) * t.cap;
 
   // Persistent workgroups: workgroup w counts buckets w, w + G, w + 2G, ... (G = grid size). The first
   // round of the next bucket is loaded while the current one is finalized, so no bucket starts with an
@@ -1070,8 +1137,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     for (int j = 0; j < R; j++) {
       const uint32_t i = first + (uint32_t)tid + (uint32_t)j * C_THREADS;
       const uint32_t idx = i < cnt ? i : cnt - 1;
+      if (CMP) {
+        nk[j][0] = ((const uint32_t *)src.w[0])[idx];
+      } else {
 #pragma unroll
-      for (int w = 0; w < NL; w++) nk[j][w] = src.w[w][idx];
+        for (int w = 0; w < NL; w++) nk[j][w] = src.w[w][idx];
+      }
       nx[j] = PACKED ? 0u : (uint32_t)src.ext[idx];
     }
   };
@@ -1079,8 +1150,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     const uint64_t base = p.bucket_base[bb];
     cnt = (uint32_t)(p.bucket_end[bb] - base);  // < 2^32 records per bucket (host check)
     src = p.recs;
+    if (CMP) {
+      src.w[0] = (uint64_t *)((uint32_t *)src.w[0] + base);
+    } else {
 #pragma unroll
-    for (int w = 0; w < NL; w++) src.w[w] += base;
+      for (int w = 0; w < NL; w++) src.w[w] += base;
+    }
     if (!PACKED) src.ext += base;
   };
 
@@ -1103,7 +1178,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP(t_sw0);
     {  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
       uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
-      const int n_ones = t.cap * 8 / 16;
+      const int n_ones = t.cap * (int)sizeof(K) / 16;
       for (int i = tid; i < n_ones; i += C_THREADS) ones[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
       uint4 *zeros = (uint4 *)t.cnt;
       const int n_zeros = t.cap * 20 / 16;
@@ -1169,7 +1244,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       int slot[R], g[R];
 #pragma unroll
       for (int j0 = 0; j0 < R; j0 += C_BATCH) {
-        uint64_t v[C_BATCH][4];
+        K v[C_BATCH][4];
 #pragma unroll
         for (int j = j0; j < j0 + C_BATCH; j++) {
           g[j] = (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
@@ -1190,7 +1265,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           const unsigned int q = atomicAdd(nmiss, 1u);
           if (q < (unsigned int)MC) {  // handed to phase B
 #pragma unroll
-            for (int w = 0; w < NL; w++) s_mkey[w * MC + q] = ck[j][w];
+            for (int w = 0; w < NL; w++) s_mkey[w * MC + q] = (K)ck[j][w];
             s_me[q] = ce[j];
             slot[j] = -3;
             continue;
@@ -1221,7 +1296,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         for (int j = 0; j < R; j++) {
           if ((defer >> j) & 1u) {
             const unsigned int pos = atomicAdd(&s_ovf, 1u);
-            store_record<NL, PACKED>(ps, pos, ck[j], ce[j]);
+            store_record<NL, PACKED, CMP>(ps, pos, ck[j], ce[j]);
           }
         }
       }
@@ -1238,14 +1313,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         for (int w = 0; w < NL; w++) key[w] = s_mkey[w * MC + q];
         const uint32_t e = s_me[q];
         const int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
-        uint64_t v[4];
+        K v[4];
         read_group(last, g, v);
         const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
         if (r >= 0) {
           if (lds_add(t, r, e) >= HOT) lds_clamp(t, r, e);
         } else if (r == -1) {
           const unsigned int pos = atomicAdd(&s_ovf, 1u);
-          store_record<NL, PACKED>(ps, pos, key, e);
+          store_record<NL, PACKED, CMP>(ps, pos, key, e);
         } else {
           s_err = 1;
         }
@@ -1260,7 +1335,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP(t_f0);
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
-    if (p.ctg_n) ctg_apply<NL>(t, p, b, last_sweep, s_red);
+    if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, s_red);
     if (last_sweep && b_next < p.n_buckets) {
       bucket(b_next, ps_next, nb_next);
       if (nb_next) prefetch(ps_next, nb_next, 0);
@@ -1269,14 +1344,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     // finalize in one pass: decisions in registers, wave-prefix offsets, one global reservation
     uint32_t occ = 0, surv_mask = 0;
     unsigned long long sum = 0;
-    uint16_t c16[C_SPT];
-    char L[C_SPT], R_[C_SPT];
+    uint16_t c16[SPT];
+    char L[SPT], R_[SPT];
 #pragma unroll
-    for (int j = 0; j < C_SPT; j++) {
+    for (int j = 0; j < SPT; j++) {
       const int slot = tid + j * C_THREADS;
       c16[j] = 0;
       L[j] = R_[j] = 0;
-      if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != KEY_EMPTY) {
+      if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != (K)KEY_EMPTY) {
         occ++;
         sum += t.cnt[slot];
 #if !MHMKC_EXP_NOFIN
@@ -1306,12 +1381,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     __syncthreads();
     unsigned long long g = s_gbase + s_wave[wid] + (incl - mine);
 #pragma unroll
-    for (int j = 0; j < C_SPT; j++) {
+    for (int j = 0; j < SPT; j++) {
       if ((surv_mask >> j) & 1u) {
         const int slot = tid + j * C_THREADS;
         uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
+        if (CMP) {  // key = cunmix(global fine bucket digits | stored bits)
+          const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
+          const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          ok[0] = cunmix(y, B) << (64 - B);
+        } else {
 #pragma unroll
-        for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
+          for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
+        }
         for (int w = NL; w < p.nlo; w++) ok[w] = 0;
         p.out_counts[g] = c16[j];
         p.out_left[g] = L[j];
@@ -1392,52 +1473,53 @@ static hipError_t allow_lds(K kernel, size_t lds) {
   return hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
-template <int NL, bool PK>
+// CMP: compact records (NL = 1, packed), selected by the params' compact flag
+template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_hist(const ExtractParams &p, hipStream_t s) {
   const size_t lds = tile_lds_bytes<NL>() + (size_t)p.n_bins * 4;
-  hipError_t e = allow_lds(k_extract_hist<NL, PK>, lds);
+  hipError_t e = allow_lds(k_extract_hist<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_extract_hist<NL, PK><<<dim3(p.n_tiles), dim3(E_THREADS), lds, s>>>(p);
+  k_extract_hist<NL, PK, CMP><<<dim3(p.n_tiles), dim3(E_THREADS), lds, s>>>(p);
   return hipGetLastError();
 }
 
-template <int NL, bool PK>
+template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
   constexpr int T = kTile<NL>();
   const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_lds_bytes<NL>(), staged_area_bytes(NL, T, PK))
                               : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
-  hipError_t e = allow_lds(k_extract_scatter<NL, PK>, lds);
+  hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_extract_scatter<NL, PK><<<dim3(p.n_tiles), dim3(E_THREADS), lds, s>>>(p);
+  k_extract_scatter<NL, PK, CMP><<<dim3(p.n_tiles), dim3(E_THREADS), lds, s>>>(p);
   return hipGetLastError();
 }
 
-template <int NL, bool PK>
+template <int NL, bool PK, bool CMP = false>
 static hipError_t do_part_hist(const PartitionParams &p, hipStream_t s) {
   const size_t lds = ((size_t)1 << p.fine_bits) * 4;
-  hipError_t e = allow_lds(k_part_hist<NL, PK>, lds);
+  hipError_t e = allow_lds(k_part_hist<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_part_hist<NL, PK><<<dim3(p.n_chunks), dim3(E_THREADS), lds, s>>>(p);
+  k_part_hist<NL, PK, CMP><<<dim3(p.grid), dim3(E_THREADS), lds, s>>>(p);
   return hipGetLastError();
 }
 
-template <int NL, bool PK>
+template <int NL, bool PK, bool CMP = false>
 static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
   const uint32_t nf = 1u << p.fine_bits;
   const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kTile<NL>(), PK) : scatter_lds_bytes(nf);
-  hipError_t e = allow_lds(k_part_scatter<NL, PK>, lds);
+  hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_part_scatter<NL, PK><<<dim3(p.n_chunks), dim3(E_THREADS), lds, s>>>(p);
+  k_part_scatter<NL, PK, CMP><<<dim3(p.grid), dim3(E_THREADS), lds, s>>>(p);
   return hipGetLastError();
 }
 
-template <int NL, bool PK>
+template <int NL, bool PK, bool CMP = false>
 static hipError_t do_count(const CountParams &p, hipStream_t s) {
-  const size_t lds = count_lds_bytes(NL);
-  hipError_t e = allow_lds(k_count<NL, PK>, lds);
+  const size_t lds = count_lds_bytes(NL, CMP);
+  hipError_t e = allow_lds(k_count<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
   const uint32_t grid = p.grid && p.grid < p.n_buckets ? p.grid : p.n_buckets;
-  k_count<NL, PK><<<dim3(grid), dim3(C_THREADS), lds, s>>>(p);
+  k_count<NL, PK, CMP><<<dim3(grid), dim3(C_THREADS), lds, s>>>(p);
   return hipGetLastError();
 }
 
@@ -1466,21 +1548,25 @@ hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigne
 
 hipError_t launch_extract_hist(const ExtractParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_tiles) return hipSuccess;
+  if (p.compact) return do_extract_hist<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_extract_hist, (p, s));
 }
 
 hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_tiles) return hipSuccess;
+  if (p.compact) return do_extract_scatter<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_extract_scatter, (p, s));
 }
 
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_chunks) return hipSuccess;
+  if (p.compact) return do_part_hist<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_part_hist, (p, s));
 }
 
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_chunks) return hipSuccess;
+  if (p.compact) return do_part_scatter<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_part_scatter, (p, s));
 }
 
@@ -1498,6 +1584,7 @@ hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, u
 
 hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_buckets) return hipSuccess;
+  if (p.compact) return do_count<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_count, (p, s));
 }
 

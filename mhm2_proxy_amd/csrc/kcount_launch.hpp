@@ -29,6 +29,7 @@ struct ExtractParams {
   int coarse_bits;                  // coarse digit = h1 >> (64 - coarse_bits)
   uint32_t n_bins;                  // 1 << coarse_bits
   int hbits;                        // hash bits stored in the record after the ext code (0: none)
+  int compact;                      // compact records (kmer_ops.hpp cmix): out = u32 plane w[0] + byte plane ext
   unsigned long long *hist;         // [n_bins] (E-hist)
   unsigned long long *cursor;       // [E_NSUB * n_bins] (E-scatter): cursor of segment (b, s) at s * n_bins + b
   uint64_t bin_cap;                 // capped mode: segment (b, s) owns [i*bin_cap, (i+1)*bin_cap), i = b*E_NSUB+s,
@@ -58,11 +59,16 @@ struct PartitionParams {
   const uint32_t *chunk_run;        // [n_chunks]: run of each chunk (launch_chunk_runs fills it)
   uint32_t n_runs;
   uint32_t n_chunks;
+  // XCD-aware launch: the chunks are ordered by XCD class (coarse bucket % 8); class x holds chunks
+  // [xcd_start[x], xcd_start[x + 1]) and is served by the workgroups b with b % 8 == x (grid = 8 * largest)
+  uint32_t xcd_start[9];
+  uint32_t grid;
   const PlaneSet *srcs;           // device table of source plane sets
   int k;
   int coarse_bits;
   int fine_bits;
   int hbits;                        // hash bits stored in the records (fine digit read from them if >= fine_bits)
+  int compact;                      // compact records: sources u32 + byte planes, out one u32 plane
   unsigned long long *fine_hist;    // [n_coarse_local << fine_bits]
   unsigned long long *fine_cursor;  // [n_coarse_local << fine_bits]
   const unsigned long long *coarse_base;  // capped mode: first fine bucket of coarse bucket c starts here
@@ -76,6 +82,9 @@ struct CountParams {
   const unsigned long long *bucket_base;
   const unsigned long long *bucket_end;  // == the fine cursors after the scatter
   int hbits;                           // stored hash bits to strip from the last key word
+  int compact;                         // compact records (u32 plane w[0]); the key is rebuilt from the bucket
+  int coarse_bits, fine_bits;
+  uint32_t bucket0;                    // global index of local fine bucket 0 (own_lo << fine_bits)
   uint32_t n_buckets;
   uint32_t grid;                      // persistent workgroups (one per CU); 0 = one per bucket
   int k;
@@ -117,8 +126,8 @@ size_t ctg_scratch_bytes(uint64_t n_windows, int nl);
 // Extract, sort by key (stable: contig order kept within a key), fold every key's contig occurrences in
 // order (insert_supermer_from_ctg) and sort the folded k-mers by local fine bucket. Outputs (n_out of them)
 // go to out_keys[NL] (SoA, each out_cap long), out_state, out_bucket.
-hipError_t ctg_prepare(const CtgView &cv, int k, int nl, int qual_cutoff, int dmin_thres, double dyn_mult,
-                       int coarse_bits, int fine_bits, uint32_t own_lo, void *scratch, size_t scratch_bytes,
+hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool compact, int qual_cutoff, int dmin_thres,
+                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, void *scratch, size_t scratch_bytes,
                        uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,
                        unsigned int *err, hipStream_t s);
 
@@ -153,19 +162,25 @@ inline int stored_hash_bits(int k, int nl, bool packed) {
 #define MHMKC_TILE1 4096
 #endif
 inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : 2048; }
-// LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS).
+// LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS); compact records keep
+// 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
 // k_count LDS: table (keys, count, 4 extension words per slot) + 128 B of scalars + the miss list of a
 // round's phase B (key words + ext code per entry); together <= 160 KiB.
-__host__ __device__ constexpr int count_cap(int nl) { return nl == 1 ? 5120 : nl == 2 ? 4000 : nl == 3 ? 3264 : 2752; }
-__host__ __device__ constexpr size_t count_table_bytes(int nl) { return (size_t)count_cap(nl) * (8 * nl + 4 + 16) + 128; }
-__host__ __device__ constexpr int miss_cap(int nl) {
-  return (int)(((163840 - count_table_bytes(nl)) / (8 * nl + 4)) & ~(size_t)63);
+__host__ __device__ constexpr int count_key_bytes(bool cmp) { return cmp ? 4 : 8; }
+__host__ __device__ constexpr int count_cap(int nl, bool cmp = false) {
+  return cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? 4000 : nl == 3 ? 3264 : 2752;
 }
-__host__ __device__ constexpr size_t count_lds_bytes(int nl) {
-  return count_table_bytes(nl) + (size_t)miss_cap(nl) * (8 * nl + 4);
+__host__ __device__ constexpr size_t count_table_bytes(int nl, bool cmp = false) {
+  return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 128;
+}
+__host__ __device__ constexpr int miss_cap(int nl, bool cmp = false) {
+  return (int)(((163840 - count_table_bytes(nl, cmp)) / (count_key_bytes(cmp) * nl + 4)) & ~(size_t)63);
+}
+__host__ __device__ constexpr size_t count_lds_bytes(int nl, bool cmp = false) {
+  return count_table_bytes(nl, cmp) + (size_t)miss_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4);
 }
 static_assert(count_lds_bytes(1) <= 163840 && count_lds_bytes(2) <= 163840 && count_lds_bytes(3) <= 163840 &&
-                  count_lds_bytes(4) <= 163840,
+                  count_lds_bytes(4) <= 163840 && count_lds_bytes(1, true) <= 163840,
               "k_count LDS budget");
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);

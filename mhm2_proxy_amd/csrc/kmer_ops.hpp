@@ -99,6 +99,54 @@ MHM_HD uint64_t part_hash(const uint64_t *w) {
 #endif
 }
 
+// ------------------------------------------------------------------------------------------------
+// Compact records (one key word, 10 <= k <= 21). The partition hash of a compact key is
+// a bijection y = cmix(x) of its B = 2k key bits x, so the coarse and fine bucket digits (the top bits
+// of y) need not be stored: a coarse-bucketed record keeps the low B - cb bits of y next to the ext
+// code (<= 40 bits: a u32 plane + a byte plane), a fine-bucketed record the low B - cb - fb bits
+// (<= 32 bits: one u32 plane), and k_count rebuilds the key as cunmix(bucket digits | stored bits).
+// cmix is fmix64's xorshift-multiply chain over B bits: x ^= x >> s with s >= B/2 is its own inverse
+// on B bits, and an odd multiplier is invertible modulo 2^B.
+constexpr uint64_t CMIX_M1 = 0xff51afd7ed558ccdull, CMIX_M2 = 0xc4ceb9fe1a85ec53ull;
+constexpr int CMP_MIN_K = 10, CMP_MAX_K = 21;
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+constexpr uint64_t inv_odd(uint64_t a) {  // a^-1 mod 2^64 (Newton: the correct low bits double per step)
+  uint64_t x = a;
+  for (int i = 0; i < 6; i++) x *= 2 - a * x;
+  return x;
+}
+constexpr uint64_t CMIX_I1 = inv_odd(CMIX_M1), CMIX_I2 = inv_odd(CMIX_M2);
+
+MHM_HD uint64_t cmix(uint64_t x, int B) {
+  const uint64_t m = (1ull << B) - 1;
+  const int s = (B + 1) >> 1;
+  x ^= x >> s;
+  x = (x * CMIX_M1) & m;
+  x ^= x >> s;
+  x = (x * CMIX_M2) & m;
+  x ^= x >> s;
+  return x;
+}
+
+MHM_HD uint64_t cunmix(uint64_t y, int B) {
+  const uint64_t m = (1ull << B) - 1;
+  const int s = (B + 1) >> 1;
+  y ^= y >> s;
+  y = (y * CMIX_I2) & m;
+  y ^= y >> s;
+  y = (y * CMIX_I1) & m;
+  y ^= y >> s;
+  return y;
+}
+
+// Partition hash of a compact key word (2k bits, left-aligned): the mixed key, left-aligned, so that the
+// coarse / fine digits are taken from its top bits exactly as from part_hash.
+MHM_HD uint64_t cpart_hash(uint64_t w, int B) { return cmix(w >> (64 - B), B) << (64 - B); }
+
+MHM_HD bool compact_ok(int k, int nl) { return nl == 1 && k >= CMP_MIN_K && k <= CMP_MAX_K; }
+
 // Reverse the order of the 32 two-bit groups of x.
 MHM_HD uint64_t rev2(uint64_t x) {
   x = __builtin_bswap64(x);

@@ -82,6 +82,7 @@ struct mhmkc {
   mhmkc_config cfg{};
   int k = 0, nl = 1, nlo = 1;
   bool packed = true;
+  bool compact = false;  // compact records (kmer_ops.hpp cmix): 5 B per coarse record, 4 B per fine record
   int cb = 8, fb = 8, hbits = 0;
   uint32_t nb = 256, nf = 256;
   uint32_t own_lo = 0, own_hi = 256;  // owned coarse range [own_lo, own_hi)
@@ -163,7 +164,9 @@ struct mhmkc {
 
   uint32_t owner_lo(int r) const { return (uint32_t)(((uint64_t)r * nb + cfg.n_ranks - 1) / cfg.n_ranks); }
   uint32_t n_owned() const { return own_hi - own_lo; }
-  size_t rec_bytes() const { return 8 * (size_t)nl + (packed ? 0 : 1); }
+  size_t rec_bytes() const { return compact ? 5 : 8 * (size_t)nl + (packed ? 0 : 1); }
+  // compact fine records hold the mixed key's bits below the coarse and fine digits + the ext code
+  int min_fine_bits() const { return compact ? std::max(0, 2 * k - cb - 26) : 0; }
 
   int begin_round() {
     if (finished) return fail(MHMKC_ESTATE, "handle already finished; call mhmkc_reset first");
@@ -179,14 +182,18 @@ struct mhmkc {
     return slabs[n_slabs++];
   }
 
-  int set_planes(DevBuf &buf, uint64_t n, mhm::PlaneSet &ps) {
-    const size_t plane = align_up(std::max<uint64_t>(n, 1) * 8, 256);
-    const size_t extb = packed ? 0 : align_up(std::max<uint64_t>(n, 1), 256);
-    hipError_t e = buf.ensure(plane * nl + extb);
+  // Record planes for n records: NL u64 word planes (+ a byte plane when the ext code is not packed);
+  // compact: a u32 plane (w[0]) + a byte plane for coarse-bucketed records, the u32 plane alone for fine.
+  int set_planes(DevBuf &buf, uint64_t n, mhm::PlaneSet &ps, bool fine = false) {
+    const uint64_t m = std::max<uint64_t>(n, 1);
+    const size_t plane = align_up(m * (compact ? 4 : 8), 256);
+    const size_t extb = (compact ? !fine : !packed) ? align_up(m, 256) : 0;
+    const int np = compact ? 1 : nl;
+    hipError_t e = buf.ensure(plane * np + extb);
     if (e != hipSuccess) return hip_fail(e, "allocating record planes");
     char *b = buf.as<char>();
-    for (int w = 0; w < 4; w++) ps.w[w] = w < nl ? (uint64_t *)(b + plane * w) : nullptr;
-    ps.ext = packed ? nullptr : (uint8_t *)(b + plane * nl);
+    for (int w = 0; w < 4; w++) ps.w[w] = w < np ? (uint64_t *)(b + plane * w) : nullptr;
+    ps.ext = extb ? (uint8_t *)(b + plane * np) : nullptr;
     return MHMKC_OK;
   }
 
@@ -227,6 +234,7 @@ int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
   p.coarse_bits = cb;
   p.n_bins = nb;
   p.hbits = hbits;
+  p.compact = compact;
   p.hist = d_hist.as<unsigned long long>();
   p.cursor = d_cursor.as<unsigned long long>();
   p.err = d_err.as<unsigned int>();
@@ -381,15 +389,23 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
       const Slab *sl = slabs[s];
       const uint64_t a = sl->bases[lo * NSUB], b = sl->bases[hi * NSUB];
       if (b == a) continue;
-      for (int w = 0; w < nl; w++) ncclSend(sl->planes.w[w] + a, b - a, ncclUint64, p, comm, stream);
-      if (!packed) ncclSend(sl->planes.ext + a, b - a, ncclUint8, p, comm, stream);
+      if (compact) {
+        ncclSend((uint32_t *)sl->planes.w[0] + a, b - a, ncclUint32, p, comm, stream);
+      } else {
+        for (int w = 0; w < nl; w++) ncclSend(sl->planes.w[w] + a, b - a, ncclUint64, p, comm, stream);
+      }
+      if (sl->planes.ext) ncclSend(sl->planes.ext + a, b - a, ncclUint8, p, comm, stream);
       sent += (b - a) * rec_bytes();
     }
   }
   for (const Seg &g : rsegs) {
     if (!g.n) continue;
-    for (int w = 0; w < nl; w++) ncclRecv(rps.w[w] + g.off, g.n, ncclUint64, g.peer, comm, stream);
-    if (!packed) ncclRecv(rps.ext + g.off, g.n, ncclUint8, g.peer, comm, stream);
+    if (compact) {
+      ncclRecv((uint32_t *)rps.w[0] + g.off, g.n, ncclUint32, g.peer, comm, stream);
+    } else {
+      for (int w = 0; w < nl; w++) ncclRecv(rps.w[w] + g.off, g.n, ncclUint64, g.peer, comm, stream);
+    }
+    if (rps.ext) ncclRecv(rps.ext + g.off, g.n, ncclUint8, g.peer, comm, stream);
   }
   if ((nr = ncclGroupEnd()) != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupEnd: %s", ncclGetErrorString(nr));
   prof_end();
@@ -449,7 +465,7 @@ int mhmkc::prepare_ctgs() {
   mhm::CtgView cv{d_ctg_bytes.as<uint8_t>(), d_ctg_offs.as<uint64_t>(), d_ctg_depth.as<uint16_t>(),
                   d_ctg_win.as<uint64_t>(), nc, W};
   prof_begin(MHMKC_STAGE_OTHER);
-  e = mhm::ctg_prepare(cv, k, nl, 1, cfg.dmin_thres, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, d_ctg_scratch.p, sb, keys,
+  e = mhm::ctg_prepare(cv, k, nl, compact, 1, cfg.dmin_thres, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, d_ctg_scratch.p, sb, keys,
                        d_ctg_state.as<uint32_t>(), d_ctg_bucket.as<uint32_t>(), &ctg_n, d_err.as<unsigned int>(),
                        stream);
   prof_end();
@@ -488,16 +504,19 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       owned += s.count[i];
     }
   st.owned_records = owned;
+  st.coarse_record_bytes = rec_bytes();
+  st.fine_record_bytes = compact ? 4 : rec_bytes();
   for (uint32_t c = 0; c < no; c++)  // k_count indexes a bucket with 32 bits
     if (per_coarse[c] >= 0xffffffffull)
       return fail(MHMKC_EUNSUPPORTED, "more than 2^32 records in one hash bucket (split the input into batches of ranks)");
 
   // fine bits: aim at ~4 records per LDS table slot per fine bucket
   const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
-  const uint64_t target = (uint64_t)mhm::count_cap(nl) * 4;
+  const uint64_t target = (uint64_t)mhm::count_cap(nl, compact) * 4;
   fb = 4;
   while (fb < 11 && (avg_coarse >> fb) > target) fb++;
   if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
+  fb = std::max(fb, min_fine_bits());
   nf = 1u << fb;
   const uint32_t n_fine = no * nf;
   st.fine_buckets = n_fine;
@@ -508,16 +527,25 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   std::vector<mhm::SRun> runs;
   std::vector<mhm::PlaneSet> ps;
   uint64_t n_chunks = 0;
-  for (size_t s = 0; s < srcs.size(); s++) {
-    ps.push_back(srcs[s].planes);
-    for (uint32_t i = 0; i < no * NSUB; i++) {
-      const uint64_t cnt = srcs[s].count[i];
-      if (!cnt) continue;
-      runs.push_back({srcs[s].start[i], cnt, (uint32_t)s, i / NSUB, (uint32_t)n_chunks, 0});
-      n_chunks += (cnt + T - 1) / T;
-    }
+  uint64_t xcd_start[9] = {0};
+  for (size_t s = 0; s < srcs.size(); s++) ps.push_back(srcs[s].planes);
+  // ordered by XCD class (coarse % 8), then coarse bucket, segment, source (see xcd_chunk)
+  for (uint32_t x = 0; x < 8; x++) {
+    xcd_start[x] = n_chunks;
+    for (uint32_t c = x; c < no; c += 8)
+      for (uint32_t q = 0; q < NSUB; q++)
+        for (size_t s = 0; s < srcs.size(); s++) {
+          const uint32_t i = c * NSUB + q;
+          const uint64_t cnt = srcs[s].count[i];
+          if (!cnt) continue;
+          runs.push_back({srcs[s].start[i], cnt, (uint32_t)s, c, (uint32_t)n_chunks, 0});
+          n_chunks += (cnt + T - 1) / T;
+        }
   }
+  xcd_start[8] = n_chunks;
   if (n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
+  uint64_t xcd_max = 0;
+  for (int x = 0; x < 8; x++) xcd_max = std::max(xcd_max, xcd_start[x + 1] - xcd_start[x]);
   // capped fine layout
   std::vector<uint64_t> cfit(2 * (size_t)no);  // [coarse_base | coarse_fcap]
   uint64_t r2_size = 0;
@@ -563,11 +591,14 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   pp.chunk_run = d_chunk_run;
   pp.n_runs = (uint32_t)runs.size();
   pp.n_chunks = (uint32_t)n_chunks;
+  for (int x = 0; x < 9; x++) pp.xcd_start[x] = (uint32_t)xcd_start[x];
+  pp.grid = (uint32_t)(8 * xcd_max);
   pp.srcs = d_srcs.as<mhm::PlaneSet>();
   pp.k = k;
   pp.coarse_bits = cb;
   pp.fine_bits = fb;
   pp.hbits = hbits;
+  pp.compact = compact;
   pp.fine_hist = d_fine_hist.as<unsigned long long>();
   pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
   pp.err = d_err.as<unsigned int>();
@@ -576,10 +607,14 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.bucket_base = d_fine_base.as<unsigned long long>();
   cp.bucket_end = d_fine_cursor.as<unsigned long long>();
   cp.hbits = hbits;
+  cp.compact = compact;
+  cp.coarse_bits = cb;
+  cp.fine_bits = fb;
+  cp.bucket0 = own_lo << fb;
   cp.n_buckets = n_fine;
   cp.grid = (uint32_t)std::max(0, n_cu);  // one persistent workgroup per CU (k_count needs ~160 KB of LDS)
   cp.k = k;
-  cp.cap = mhm::count_cap(nl);
+  cp.cap = mhm::count_cap(nl, compact);
   if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
   cp.dmin_thres = cfg.dmin_thres;
   cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
@@ -623,11 +658,11 @@ int mhmkc::finish(uint64_t *n_out_ret) {
                            d_fine_cursor.as<unsigned long long>(), n_fine, stream);
       prof_end();
       if (e != hipSuccess) return hip_fail(e, "scan");
-      if ((rc = set_planes(d_r2, owned, r2))) return rc;
+      if ((rc = set_planes(d_r2, owned, r2, true))) return rc;
     } else {
       pp.coarse_base = d_cfit;
       pp.coarse_fcap = d_cfit + no;
-      if ((rc = set_planes(d_r2, r2_size, r2))) return rc;
+      if ((rc = set_planes(d_r2, r2_size, r2, true))) return rc;
     }
     pp.out = r2;
     prof_begin(MHMKC_STAGE_SSCAT);
@@ -771,6 +806,10 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
 #define MHMKC_CB0 8
 #endif
   h->cb = MHMKC_CB0 + extra;
+  // compact records for 10 <= k <= 21 (MHMKC_WIDE_RECORDS=1 keeps the 8-byte records: A/B and tests)
+  const char *wide = getenv("MHMKC_WIDE_RECORDS");
+  h->compact = mhm::compact_ok(k, nl) && 2 * k - h->cb <= 34 && !(wide && atoi(wide));
+  if (h->compact) h->hbits = 0;
   h->nb = 1u << h->cb;
   h->own_lo = h->owner_lo(cfg->rank);
   h->own_hi = h->owner_lo(cfg->rank + 1);

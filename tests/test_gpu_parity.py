@@ -39,7 +39,7 @@ def check_stats(st, oracle_stats=None):
         assert st["purged"] == oracle_stats["purged"]
 
 
-@pytest.mark.parametrize("k", [21, 33, 55, 63, 77, 99, 15, 31, 45, 127])
+@pytest.mark.parametrize("k", [21, 33, 55, 63, 77, 99, 15, 31, 45, 127, 9, 10, 11, 19, 22])
 def test_synthetic_vs_oracle(k):
     b, o = synth_set(2000, 10000, 100 + k)
     ref = O.kcount(b, o, k)
@@ -97,13 +97,16 @@ def test_batches_equal_single(k):
     assert_tables_equal(many, one, "5 batches vs 1")
 
 
-@pytest.mark.parametrize("k", [21, 63])
-def test_forced_overflow_sweeps(k, monkeypatch):
-    """Tiny LDS tables force the multi-sweep path (a closed table overflows whole keys to the next sweep)."""
+@pytest.mark.parametrize("k,wide", [(21, True), (15, False), (17, False), (63, False)])
+def test_forced_overflow_sweeps(k, wide, monkeypatch):
+    """Tiny LDS tables force the multi-sweep path (a closed table overflows whole keys to the next sweep).
+    Compact records (k <= 21) need >= 2k - 34 fine bits, so k = 15, 17 cover them with one fine bucket."""
     b, o = synth_set(3000, 50000, 13)
     exp = oracle_table(b, o, k)
     monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
     monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    if wide:
+        monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
     got, st = hip_table(b, o, k)
     assert st["overflow_sweeps"] > 0
     assert_tables_equal(got, exp, "forced overflow")
@@ -244,13 +247,15 @@ def test_contig_pass_order_kept_across_calls():
     assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, 21), "contigs in 4 calls")
 
 
-@pytest.mark.parametrize("k", [21, 63])
-def test_contig_pass_with_overflow_sweeps(k, monkeypatch):
+@pytest.mark.parametrize("k,wide", [(21, True), (17, False), (63, False)])
+def test_contig_pass_with_overflow_sweeps(k, wide, monkeypatch):
     """Tiny LDS tables: read entries are spread over several sweeps of a bucket; a contig k-mer must meet
     its read entry in whichever sweep holds it, and only count as contig-only after the last sweep."""
     b, o, seqs, depths = ctg_set(seed=91, n_reads=600)
     monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
     monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    if wide:
+        monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
     got, st = ctg_table(b, o, seqs, depths, k)
     assert st["overflow_sweeps"] > 0
     assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, k), "contigs + overflow sweeps")
@@ -280,3 +285,34 @@ def test_analyze_kmers_with_contigs():
     m.analyze_kmers(21, 0, 33, [pr], 2, ctgs, dht)
     assert_tables_equal(dht.table, oracle_ctg_table(b, o, seqs, depths, 21), "analyze_kmers + contigs")
     dht.counter.close()
+
+
+@pytest.mark.parametrize("k", [21, 19])
+def test_compact_overflow_at_min_fine_bits(k, monkeypatch):
+    """Compact records at their smallest fine partition (2k - 34 fine bits at k = 21): ~120 distinct
+    k-mers per fine bucket against 64-slot tables, so most buckets need several sweeps."""
+    b, o = synth_set(60000, 4_000_000, 23)
+    exp = oracle_table(b, o, k)
+    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
+    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    got, st = hip_table(b, o, k)
+    assert st["overflow_sweeps"] > 0
+    assert_tables_equal(got, exp, "compact overflow")
+    check_stats(st)
+
+
+@pytest.mark.parametrize("k", [21, 12])
+def test_compact_equals_wide_records(k, monkeypatch):
+    """The compact (4/5-byte, key rebuilt from the bucket) and 8-byte record layouts give the same table,
+    through the capped and the exact partition paths."""
+    b, o = synth_set(20000, 300000, 31)
+    cmp_t, st_c = hip_table(b, o, k)
+    monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
+    wide_t, st_w = hip_table(b, o, k)
+    assert_tables_equal(cmp_t, wide_t, "compact vs wide")
+    monkeypatch.delenv("MHMKC_WIDE_RECORDS")
+    monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+    exact_t, _ = hip_table(b, o, k)
+    assert_tables_equal(exact_t, wide_t, "compact exact vs wide")
+    for key in ("distinct", "n_out", "purged", "count_sum"):
+        assert st_c[key] == st_w[key], key
