@@ -793,6 +793,11 @@ struct CountLds {
   int cap;         // multiple of 4: slots are probed in groups of 4
 };
 
+#ifndef MHMKC_BOVERLAP
+#define MHMKC_BOVERLAP 1
+#endif
+constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
+
 // Groups a key may probe before its record is deferred to the next sweep of its bucket.
 #ifndef MHMKC_CPROBE
 #define MHMKC_CPROBE 64
@@ -909,6 +914,16 @@ __device__ __forceinline__ uint32_t lds_add(const CountLds<K> &t, int slot, uint
   if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
   if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
   return old;
+}
+
+// lds_add without the old count (ds_add_u32 without return: nothing to wait for), for sweeps of fewer than
+// 0xC000 records, whose counters cannot reach the clamp level (a counter never exceeds the sweep's records).
+template <typename K>
+__device__ __forceinline__ void lds_add_nr(const CountLds<K> &t, int slot, uint32_t e) {
+  atomicAdd(&t.cnt[slot], 1u);
+  const int l = (int)((e >> 3) & 7u), r = (int)(e & 7u);
+  if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
+  if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
 }
 
 // Saturation at the decision level: a 16-bit half that reached 0xC000 is CAS-clamped back to 0x8000.
@@ -1101,12 +1116,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned long long *s_u64 = (unsigned long long *)(t.ext + 4 * t.cap);
   unsigned long long &s_gbase = s_u64[0];
   unsigned long long *s_red = s_u64 + 1;  // [3]
-  unsigned int *s_nmiss = (unsigned int *)(s_u64 + 4);  // [2] miss-list lengths, alternating rounds
+  unsigned int *s_nmiss = (unsigned int *)(s_u64 + 14);  // [3] miss-list lengths of rounds r % 3
   unsigned int &s_ovf = *(unsigned int *)(s_u64 + 5);
   unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
   unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
   // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
   constexpr int MC = miss_cap(NL, CMP);
+  // B_OVERLAP: phase B of round r overlaps phase A of round r + 1, so the miss list is double-buffered
+  constexpr int MCL = B_OVERLAP ? (MC / 2) & ~63 : MC;
   K *s_mkey = (K *)(smem + count_table_bytes(NL, CMP));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, CMP) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
@@ -1187,6 +1204,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     if (tid == 0) {
       s_nmiss[0] = 0;
       s_nmiss[1] = 0;
+      s_nmiss[2] = 0;
       s_ovf = 0;
       s_err = 0;
     }
@@ -1203,8 +1221,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     //      workgroup in a divergent loop.
     if (!first_sweep && n) prefetch(ps, n, 0);  // a re-sweep reads the deferred records
     first_sweep = false;
-    int rnd = 0;
-    for (uint32_t r0 = 0; r0 < n; r0 += RND, rnd++) {
+    const bool cold = n < 0xC000u;  // no counter of this sweep can reach the clamp level (lds_add_nr)
+    int rnd = 0, lr = 0;           // lr = rnd % 3: the round's miss counter
+    for (uint32_t r0 = 0; r0 < n; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
       STAMP(t_r0);
       uint64_t ck[R][NL];
       uint32_t ce[R];
@@ -1237,7 +1256,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         continue;
       }
 #endif
-      unsigned int *nmiss = &s_nmiss[rnd & 1];
+      unsigned int *nmiss = &s_nmiss[lr];
+      K *mkey = s_mkey + (B_OVERLAP ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
+      uint32_t *me = s_me + (B_OVERLAP ? (rnd & 1) * MCL : 0);
       // A. home-group lookups: the first groups of all R records are read in batches of C_BATCH (the
       //    reads of a batch in flight together), then found records are counted, missed ones listed.
       uint32_t old[R], defer = 0, okm = 0;
@@ -1263,10 +1284,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         int r = slot[j];
         if (r < 0) {
           const unsigned int q = atomicAdd(nmiss, 1u);
-          if (q < (unsigned int)MC) {  // handed to phase B
+          if (q < (unsigned int)MCL) {  // handed to phase B
 #pragma unroll
-            for (int w = 0; w < NL; w++) s_mkey[w * MC + q] = (K)ck[j][w];
-            s_me[q] = ce[j];
+            for (int w = 0; w < NL; w++) mkey[w * MCL + q] = (K)ck[j][w];
+            me[q] = ce[j];
             slot[j] = -3;
             continue;
           }
@@ -1277,7 +1298,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           if (r < 0) continue;
         }
 #if !MHMKC_EXP_NOATOM
-        old[j] = lds_add(t, r, ce[j]);
+        if (cold)
+          lds_add_nr(t, r, ce[j]);
+        else
+          old[j] = lds_add(t, r, ce[j]);
 #endif
         okm |= 1u << j;
       }
@@ -1286,6 +1310,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         if (((okm >> j) & 1u) && old[j] >= HOT) lds_clamp(t, slot[j], ce[j]);
       STAMP(t_r2);
       STAMP_ADD(2, t_r2 - t_r1);
+      // the next round's counter: its last readers (phase B two rounds back) are behind the previous barrier
+      if (B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
       __syncthreads();
       STAMP(t_r3);
       STAMP_ADD(3, t_r3 - t_r2);
@@ -1304,20 +1330,23 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #if MHMKC_EXP_NOB
       const unsigned int M = 0;
 #else
-      const unsigned int M = min(*nmiss, (unsigned int)MC);
+      const unsigned int M = min(*nmiss, (unsigned int)MCL);
 #endif
-      if (tid == 0) s_nmiss[(rnd + 1) & 1] = 0;  // the next round's list (the previous one's is done)
+      if (!B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
       for (unsigned int q = tid; q < M; q += C_THREADS) {
         uint64_t key[NL];
 #pragma unroll
-        for (int w = 0; w < NL; w++) key[w] = s_mkey[w * MC + q];
-        const uint32_t e = s_me[q];
+        for (int w = 0; w < NL; w++) key[w] = mkey[w * MCL + q];
+        const uint32_t e = me[q];
         const int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
         K v[4];
         read_group(last, g, v);
         const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
         if (r >= 0) {
-          if (lds_add(t, r, e) >= HOT) lds_clamp(t, r, e);
+          if (cold)
+            lds_add_nr(t, r, e);
+          else if (lds_add(t, r, e) >= HOT)
+            lds_clamp(t, r, e);
         } else if (r == -1) {
           const unsigned int pos = atomicAdd(&s_ovf, 1u);
           store_record<NL, PACKED, CMP>(ps, pos, key, e);
@@ -1325,7 +1354,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           s_err = 1;
         }
       }
-      __syncthreads();
+      // Without B_OVERLAP a barrier closes the round. With it, the next round's phase A starts while
+      // other waves still work off this list: its misses go to the other list buffer and counter, and a
+      // lookup that races an insert of phase B at worst misses and is resolved by its own phase B (slots
+      // are only ever claimed, so the deferral rule of lds_insert holds across the two phases).
+      if (!B_OVERLAP) __syncthreads();
 #if MHMKC_STAMP
       const uint64_t t_r4 = __builtin_amdgcn_s_memtime();
       STAMP_ADD(4, t_r4 - t_r3);
