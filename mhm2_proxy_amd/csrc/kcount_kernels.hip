@@ -419,8 +419,11 @@ __device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const 
 __host__ __device__ constexpr size_t staged_cnt_bytes(uint32_t nb) {
   return scatter_lds_bytes(nb) + (((size_t)nb * 4 + 15) & ~(size_t)15) + 32;
 }
-__host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packed) {
-  return (size_t)nl * T * 8 + (size_t)T * 2 + (packed ? 0 : (size_t)T);
+// Compact records are staged at their stored width: u32 (+ the high byte for SF_C40).
+__host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packed, int sf = SF_WORDS) {
+  return sf == SF_C40   ? (size_t)T * (4 + 1 + 2)
+         : sf == SF_C32 ? (size_t)T * (4 + 2)
+                        : (size_t)nl * T * 8 + (size_t)T * 2 + (packed ? 0 : (size_t)T);
 }
 
 template <int NL, bool PACKED, int W, int SF>
@@ -433,8 +436,10 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
   uint32_t *lstart = (uint32_t *)(smem + scatter_lds_bytes(nb));
   uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - 32);
+  constexpr bool C32 = SF != SF_WORDS;  // compact: low 32 bits in stage32, the high byte (SF_C40) in sext
   uint64_t *stage = (uint64_t *)area;
-  uint16_t *sbin = (uint16_t *)(stage + NL * T);
+  uint32_t *stage32 = (uint32_t *)area;
+  uint16_t *sbin = C32 ? (uint16_t *)(stage32 + T) : (uint16_t *)(stage + NL * T);
   uint8_t *sext = (uint8_t *)(sbin + T);
   uint32_t rank[W];
 #pragma unroll
@@ -464,8 +469,13 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
     if (inf[j] >> 31) {
       const uint32_t d = inf[j] & 0xffffu;
       const uint32_t pos = lstart[d] + rank[j];
+      if (C32) {
+        stage32[pos] = (uint32_t)rk[j][0];
+        if (SF == SF_C40) sext[pos] = (uint8_t)(rk[j][0] >> 32);
+      } else {
 #pragma unroll
-      for (int w = 0; w < NL; w++) stage[w * T + pos] = rk[j][w];
+        for (int w = 0; w < NL; w++) stage[w * T + pos] = rk[j][w];
+      }
       sbin[pos] = (uint16_t)d;
       if (!PACKED) sext[pos] = (uint8_t)((inf[j] >> 16) & 63u);
     }
@@ -487,8 +497,12 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       const unsigned long long dst = goff[d] + (pos - lstart[d]);
       if (lim.cap && dst >= lim.end(d)) continue;
       uint64_t v[NL];
+      if (C32) {
+        v[0] = (uint64_t)stage32[pos] | (SF == SF_C40 ? (uint64_t)sext[pos] << 32 : 0ull);
+      } else {
 #pragma unroll
-      for (int w = 0; w < NL; w++) v[w] = stage[w * T + pos];
+        for (int w = 0; w < NL; w++) v[w] = stage[w * T + pos];
+      }
       store_out<NL, PACKED, SF>(out, dst, v, PACKED ? 0u : sext[pos]);
     }
   }
@@ -1519,7 +1533,7 @@ static hipError_t do_extract_hist(const ExtractParams &p, hipStream_t s) {
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
   constexpr int T = kTile<NL>();
-  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_lds_bytes<NL>(), staged_area_bytes(NL, T, PK))
+  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_lds_bytes<NL>(), staged_area_bytes(NL, T, PK, CMP ? SF_C40 : SF_WORDS))
                               : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
@@ -1539,7 +1553,8 @@ static hipError_t do_part_hist(const PartitionParams &p, hipStream_t s) {
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
   const uint32_t nf = 1u << p.fine_bits;
-  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kTile<NL>(), PK) : scatter_lds_bytes(nf);
+  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kTile<NL>(), PK, CMP ? SF_C32 : SF_WORDS)
+                              : scatter_lds_bytes(nf);
   hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
   k_part_scatter<NL, PK, CMP><<<dim3(p.grid), dim3(E_THREADS), lds, s>>>(p);
