@@ -1235,149 +1235,157 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     //      workgroup in a divergent loop.
     if (!first_sweep && n) prefetch(ps, n, 0);  // a re-sweep reads the deferred records
     first_sweep = false;
-    const bool cold = n < 0xC000u;  // no counter of this sweep can reach the clamp level (lds_add_nr)
-    int rnd = 0, lr = 0;           // lr = rnd % 3: the round's miss counter
-    for (uint32_t r0 = 0; r0 < n; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
-      STAMP(t_r0);
-      uint64_t ck[R][NL];
-      uint32_t ce[R];
+    // a sweep of fewer than 0xC000 records cannot bring a counter to the clamp level: its rounds count
+    // with non-returning adds and carry no clamp check (COLD instantiation of the round loop)
+    auto rounds = [&](auto cold_tag) {
+      constexpr bool COLD = decltype(cold_tag)::value;
+      int rnd = 0, lr = 0;           // lr = rnd % 3: the round's miss counter
+      for (uint32_t r0 = 0; r0 < n; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
+        STAMP(t_r0);
+        uint64_t ck[R][NL];
+        uint32_t ce[R];
 #pragma unroll
-      for (int j = 0; j < R; j++) {
-        const bool valid = r0 + (uint32_t)tid + (uint32_t)j * C_THREADS < n;
+        for (int j = 0; j < R; j++) {
+          const bool valid = r0 + (uint32_t)tid + (uint32_t)j * C_THREADS < n;
 #pragma unroll
-        for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
-        if (PACKED) {
-          ce[j] = valid ? (uint32_t)(ck[j][NL - 1] & low_mask) : NONE;
-          ck[j][NL - 1] &= ~low_mask;
-        } else {
-          ce[j] = valid ? nx[j] : NONE;
+          for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
+          if (PACKED) {
+            ce[j] = valid ? (uint32_t)(ck[j][NL - 1] & low_mask) : NONE;
+            ck[j][NL - 1] &= ~low_mask;
+          } else {
+            ce[j] = valid ? nx[j] : NONE;
+          }
         }
-      }
 #if MHMKC_STAMP
 #pragma unroll
-      for (int j = 0; j < R; j++) asm volatile("" ::"v"(ck[j][0]), "v"(ce[j]));
+        for (int j = 0; j < R; j++) asm volatile("" ::"v"(ck[j][0]), "v"(ce[j]));
 #endif
-      STAMP(t_r1);
-      STAMP_ADD(1, t_r1 - t_r0);
-      if (r0 + RND < n) prefetch(ps, n, r0 + RND);
+        STAMP(t_r1);
+        STAMP_ADD(1, t_r1 - t_r0);
+        if (r0 + RND < n) prefetch(ps, n, r0 + RND);
 #if MHMKC_EXP_LOADONLY
-      {
-        uint32_t acc = 0;
+        {
+          uint32_t acc = 0;
 #pragma unroll
-        for (int j = 0; j < R; j++) acc ^= ce[j] ^ (uint32_t)ck[j][0];
-        if (acc == 0x12345u) s_err = 1;
-        __syncthreads();
-        continue;
-      }
-#endif
-      unsigned int *nmiss = &s_nmiss[lr];
-      K *mkey = s_mkey + (B_OVERLAP ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
-      uint32_t *me = s_me + (B_OVERLAP ? (rnd & 1) * MCL : 0);
-      // A. home-group lookups: the first groups of all R records are read in batches of C_BATCH (the
-      //    reads of a batch in flight together), then found records are counted, missed ones listed.
-      uint32_t old[R], defer = 0, okm = 0;
-      int slot[R], g[R];
-#pragma unroll
-      for (int j0 = 0; j0 < R; j0 += C_BATCH) {
-        K v[C_BATCH][4];
-#pragma unroll
-        for (int j = j0; j < j0 + C_BATCH; j++) {
-          g[j] = (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
-          read_group(last, g[j], v[j - j0]);  // also for an invalid lane: harmless, keeps the batch uniform
-        }
-#pragma unroll
-        for (int j = j0; j < j0 + C_BATCH; j++) slot[j] = examine_group<NL>(t, ck[j], g[j], v[j - j0]);
-      }
-#pragma unroll
-      for (int j = 0; j < R; j++) {
-        old[j] = 0;
-        if (ce[j] == NONE) {
-          slot[j] = -3;
+          for (int j = 0; j < R; j++) acc ^= ce[j] ^ (uint32_t)ck[j][0];
+          if (acc == 0x12345u) s_err = 1;
+          __syncthreads();
           continue;
         }
-        int r = slot[j];
-        if (r < 0) {
-          const unsigned int q = atomicAdd(nmiss, 1u);
-          if (q < (unsigned int)MCL) {  // handed to phase B
+#endif
+        unsigned int *nmiss = &s_nmiss[lr];
+        K *mkey = s_mkey + (B_OVERLAP ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
+        uint32_t *me = s_me + (B_OVERLAP ? (rnd & 1) * MCL : 0);
+        // A. home-group lookups: the first groups of all R records are read in batches of C_BATCH (the
+        //    reads of a batch in flight together), then found records are counted, missed ones listed.
+        uint32_t old[R], defer = 0, okm = 0;
+        int slot[R], g[R];
 #pragma unroll
-            for (int w = 0; w < NL; w++) mkey[w * MCL + q] = (K)ck[j][w];
-            me[q] = ce[j];
+        for (int j0 = 0; j0 < R; j0 += C_BATCH) {
+          K v[C_BATCH][4];
+#pragma unroll
+          for (int j = j0; j < j0 + C_BATCH; j++) {
+            g[j] = (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
+            read_group(last, g[j], v[j - j0]);  // also for an invalid lane: harmless, keeps the batch uniform
+          }
+#pragma unroll
+          for (int j = j0; j < j0 + C_BATCH; j++) slot[j] = examine_group<NL>(t, ck[j], g[j], v[j - j0]);
+        }
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+          old[j] = 0;
+          if (ce[j] == NONE) {
             slot[j] = -3;
             continue;
           }
-          r = lds_insert<NL>(t, ck[j], g[j], r);  // list full (first rounds of a bucket): in place
-          if (r == -1) defer |= 1u << j;
-          if (r == -2) s_err = 1;
-          slot[j] = r;
-          if (r < 0) continue;
-        }
+          int r = slot[j];
+          if (r < 0) {
+            const unsigned int q = atomicAdd(nmiss, 1u);
+            if (q < (unsigned int)MCL) {  // handed to phase B
+#pragma unroll
+              for (int w = 0; w < NL; w++) mkey[w * MCL + q] = (K)ck[j][w];
+              me[q] = ce[j];
+              slot[j] = -3;
+              continue;
+            }
+            r = lds_insert<NL>(t, ck[j], g[j], r);  // list full (first rounds of a bucket): in place
+            if (r == -1) defer |= 1u << j;
+            if (r == -2) s_err = 1;
+            slot[j] = r;
+            if (r < 0) continue;
+          }
 #if !MHMKC_EXP_NOATOM
-        if (cold)
-          lds_add_nr(t, r, ce[j]);
-        else
-          old[j] = lds_add(t, r, ce[j]);
+          if (COLD)
+            lds_add_nr(t, r, ce[j]);
+          else
+            old[j] = lds_add(t, r, ce[j]);
 #endif
-        okm |= 1u << j;
-      }
+          okm |= 1u << j;
+        }
 #pragma unroll
-      for (int j = 0; j < R; j++)
-        if (((okm >> j) & 1u) && old[j] >= HOT) lds_clamp(t, slot[j], ce[j]);
-      STAMP(t_r2);
-      STAMP_ADD(2, t_r2 - t_r1);
-      // the next round's counter: its last readers (phase B two rounds back) are behind the previous barrier
-      if (B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
-      __syncthreads();
-      STAMP(t_r3);
-      STAMP_ADD(3, t_r3 - t_r2);
-      // deferred records go back to the front of the bucket, to positions every lane has consumed
-      // (< r0 + RND), for the next sweep
-      if (defer) {
+        for (int j = 0; j < R; j++)
+          if (!COLD && ((okm >> j) & 1u) && old[j] >= HOT) lds_clamp(t, slot[j], ce[j]);
+        STAMP(t_r2);
+        STAMP_ADD(2, t_r2 - t_r1);
+        // the next round's counter: its last readers (phase B two rounds back) are behind the previous barrier
+        if (B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
+        __syncthreads();
+        STAMP(t_r3);
+        STAMP_ADD(3, t_r3 - t_r2);
+        // deferred records go back to the front of the bucket, to positions every lane has consumed
+        // (< r0 + RND), for the next sweep
+        if (defer) {
 #pragma unroll
-        for (int j = 0; j < R; j++) {
-          if ((defer >> j) & 1u) {
-            const unsigned int pos = atomicAdd(&s_ovf, 1u);
-            store_record<NL, PACKED, CMP>(ps, pos, ck[j], ce[j]);
+          for (int j = 0; j < R; j++) {
+            if ((defer >> j) & 1u) {
+              const unsigned int pos = atomicAdd(&s_ovf, 1u);
+              store_record<NL, PACKED, CMP>(ps, pos, ck[j], ce[j]);
+            }
           }
         }
-      }
-      // B. the miss list, densely
+        // B. the miss list, densely
 #if MHMKC_EXP_NOB
-      const unsigned int M = 0;
+        const unsigned int M = 0;
 #else
-      const unsigned int M = min(*nmiss, (unsigned int)MCL);
+        const unsigned int M = min(*nmiss, (unsigned int)MCL);
 #endif
-      if (!B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
-      for (unsigned int q = tid; q < M; q += C_THREADS) {
-        uint64_t key[NL];
+        if (!B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
+        for (unsigned int q = tid; q < M; q += C_THREADS) {
+          uint64_t key[NL];
 #pragma unroll
-        for (int w = 0; w < NL; w++) key[w] = mkey[w * MCL + q];
-        const uint32_t e = me[q];
-        const int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
-        K v[4];
-        read_group(last, g, v);
-        const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
-        if (r >= 0) {
-          if (cold)
-            lds_add_nr(t, r, e);
-          else if (lds_add(t, r, e) >= HOT)
-            lds_clamp(t, r, e);
-        } else if (r == -1) {
-          const unsigned int pos = atomicAdd(&s_ovf, 1u);
-          store_record<NL, PACKED, CMP>(ps, pos, key, e);
-        } else {
-          s_err = 1;
+          for (int w = 0; w < NL; w++) key[w] = mkey[w * MCL + q];
+          const uint32_t e = me[q];
+          const int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
+          K v[4];
+          read_group(last, g, v);
+          const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
+          if (r >= 0) {
+            if (COLD)
+              lds_add_nr(t, r, e);
+            else if (lds_add(t, r, e) >= HOT)
+              lds_clamp(t, r, e);
+          } else if (r == -1) {
+            const unsigned int pos = atomicAdd(&s_ovf, 1u);
+            store_record<NL, PACKED, CMP>(ps, pos, key, e);
+          } else {
+            s_err = 1;
+          }
         }
-      }
-      // Without B_OVERLAP a barrier closes the round. With it, the next round's phase A starts while
-      // other waves still work off this list: its misses go to the other list buffer and counter, and a
-      // lookup that races an insert of phase B at worst misses and is resolved by its own phase B (slots
-      // are only ever claimed, so the deferral rule of lds_insert holds across the two phases).
-      if (!B_OVERLAP) __syncthreads();
+        // Without B_OVERLAP a barrier closes the round. With it, the next round's phase A starts while
+        // other waves still work off this list: its misses go to the other list buffer and counter, and a
+        // lookup that races an insert of phase B at worst misses and is resolved by its own phase B (slots
+        // are only ever claimed, so the deferral rule of lds_insert holds across the two phases).
+        if (!B_OVERLAP) __syncthreads();
 #if MHMKC_STAMP
-      const uint64_t t_r4 = __builtin_amdgcn_s_memtime();
-      STAMP_ADD(4, t_r4 - t_r3);
+        const uint64_t t_r4 = __builtin_amdgcn_s_memtime();
+        STAMP_ADD(4, t_r4 - t_r3);
 #endif
-    }
+      }
+    };
+    if (n < 0xC000u)
+      rounds(std::true_type{});
+    else
+      rounds(std::false_type{});
     __syncthreads();
     STAMP(t_f0);
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
