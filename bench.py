@@ -181,7 +181,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "k-mers/s (whole node), k=21 150bp reads",
+            "metric": f"k-mers/s (whole node), k={args.k} {args.read_len}bp reads",
             "value": round(value, 1),
             "unit": "k-mers/s",
             "n_gpus": world,

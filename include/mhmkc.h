@@ -83,6 +83,7 @@ typedef struct {
   uint64_t ctg_kmers;      /* distinct contig k-mers of the contig pass (0 without contigs) */
   uint64_t coarse_record_bytes; /* HBM bytes per k-mer record after extraction (5 for compact records) */
   uint64_t fine_record_bytes;   /* HBM bytes per k-mer record after the fine partition (4 when compact) */
+  uint64_t distinct_estimate;   /* sketch estimate of this rank's distinct k-mers (sizes the fine partition) */
   double ms_total;         /* wall time of the last add_reads..finish sequence (device events) */
   double ms_kernel[8];     /* per-stage device time when profiling is on: see MHMKC_STAGE_* */
   uint64_t launches[8];    /* per-stage launch count when profiling is on */

@@ -74,6 +74,7 @@ class MhmkcStats(C.Structure):
         ("ctg_kmers", C.c_uint64),
         ("coarse_record_bytes", C.c_uint64),
         ("fine_record_bytes", C.c_uint64),
+        ("distinct_estimate", C.c_uint64),
         ("ms_total", C.c_double),
         ("ms_kernel", C.c_double * 8),
         ("launches", C.c_uint64 * 8),

@@ -714,6 +714,36 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
     scatter_regs<NL, PACKED, W, SF>(rk, inf, nf, smem, cur, 1, p.out, lim, p.err);
 }
 
+// Distinct-key sketch (HyperLogLog, SKETCH_M registers) over the records of one coarse bucket, from which
+// the host sizes the fine partition (distinct keys per fine bucket vs the LDS table capacity). The key of
+// a record is its words without the ext code and stored hash bits (compact: the stored bits, unique within
+// the coarse bucket); the sketch hash is an fmix64 chain, independent of the partition hash.
+template <int NL, bool PACKED, bool CMP>
+__global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigned int *hll) {
+  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+  __shared__ unsigned int reg[SKETCH_M];
+  for (int i = threadIdx.x; i < SKETCH_M; i += E_THREADS) reg[i] = 0;
+  const SChunk ch = chunk_of<T>(p, blockIdx.x);
+  const PlaneSet src = p.srcs[ch.src];
+  uint64_t rk[W][NL];
+  uint32_t re[W];
+  load_chunk<NL, PACKED, CMP, W>(src, ch, rk, re);
+  __syncthreads();
+  const uint64_t low_mask = CMP ? 63ull : PACKED ? (1ull << (EXT_BITS + p.hbits)) - 1 : 0ull;
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    if (threadIdx.x + j * E_THREADS >= ch.count) continue;
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+    for (int w = 0; w < NL; w++) h = fmix64(h ^ (w == NL - 1 ? rk[j][w] & ~low_mask : rk[j][w]));
+    const uint32_t rho = (uint32_t)__clzll(h | (uint64_t)(SKETCH_M - 1)) + 1;  // first 1 among the top bits
+    atomicMax(&reg[h & (SKETCH_M - 1)], rho);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < SKETCH_M; i += E_THREADS)
+    if (reg[i]) atomicMax(&hll[i], reg[i]);
+}
+
 // capped fine layout
 __global__ void k_init_fine(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap, uint32_t n_coarse,
                             int fine_bits, unsigned long long *base, unsigned long long *cursor) {
@@ -1630,6 +1660,19 @@ hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_
   if (!n_runs) return hipSuccess;
   k_chunk_runs<<<dim3(n_runs), dim3(256), 0, s>>>(runs, chunk_run, tile);
   return hipGetLastError();
+}
+
+template <int NL, bool PK, bool CMP = false>
+static hipError_t do_sketch(const PartitionParams &p, uint32_t n, unsigned int *hll, hipStream_t s) {
+  k_sketch<NL, PK, CMP><<<dim3(n), dim3(E_THREADS), 0, s>>>(p, hll);
+  return hipGetLastError();
+}
+
+hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
+                         hipStream_t s) {
+  if (!n_chunks) return hipSuccess;
+  if (p.compact) return do_sketch<1, true, true>(p, n_chunks, hll, s);
+  MHM_DISPATCH(nl, packed, do_sketch, (p, n_chunks, hll, s));
 }
 
 hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor, uint32_t n,

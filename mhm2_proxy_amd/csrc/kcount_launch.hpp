@@ -196,6 +196,11 @@ hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, h
 hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_run, int tile, hipStream_t s);
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s);
+// HyperLogLog sketch of the distinct keys in chunks [0, n_chunks) of p's chunk table (one coarse bucket):
+// hll[SKETCH_M] registers, max-merged (zero them first).
+constexpr int SKETCH_M = 1024;
+hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
+                         hipStream_t s);
 hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor,
                        uint32_t n, hipStream_t s);
 hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s);

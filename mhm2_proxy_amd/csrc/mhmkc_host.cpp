@@ -8,6 +8,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -96,7 +97,7 @@ struct mhmkc {
   size_t n_slabs = 0;
   DevBuf d_hist, d_cursor, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xcounts;
-  DevBuf d_in_bytes, d_in_offs;
+  DevBuf d_in_bytes, d_in_offs, d_hll;
   // contig pass (add_ctg_kmers): contigs in the PackedRead byte layout, kept on the host until finish
   std::vector<uint8_t> ctg_bytes;
   std::vector<uint64_t> ctg_offs{0}, ctg_win{0};  // byte offsets, counted-window prefix
@@ -201,6 +202,22 @@ struct mhmkc {
   int exchange(std::vector<Source> &srcs);
   int finish(uint64_t *n_out_ret);
 };
+
+// Fine partition target: distinct keys per fine bucket <= FINE_LOAD x LDS table slots.
+constexpr double FINE_LOAD = 0.7;
+
+// HyperLogLog estimate (Flajolet et al. 2007) with the linear-counting correction for small counts.
+static double hll_estimate(const std::vector<uint32_t> &reg) {
+  const double m = (double)reg.size();
+  double sum = 0;
+  int zeros = 0;
+  for (uint32_t r : reg) {
+    sum += std::ldexp(1.0, -(int)r);
+    zeros += r == 0;
+  }
+  const double e = 0.7213 / (1.0 + 1.079 / m) * m * m / sum;
+  return (e <= 2.5 * m && zeros) ? m * std::log(m / zeros) : e;
+}
 
 // ------------------------------------------------------------------------------------------------
 // extract one batch of reads into a coarse-bucketed slab
@@ -510,29 +527,17 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     if (per_coarse[c] >= 0xffffffffull)
       return fail(MHMKC_EUNSUPPORTED, "more than 2^32 records in one hash bucket (split the input into batches of ranks)");
 
-  // fine bits: aim at ~4 records per LDS table slot per fine bucket
-  const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
-  const uint64_t target = (uint64_t)mhm::count_cap(nl, compact) * 4;
-  fb = 4;
-  while (fb < 11 && (avg_coarse >> fb) > target) fb++;
-  if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
-  fb = std::max(fb, min_fine_bits());
-  nf = 1u << fb;
-  const uint32_t n_fine = no * nf;
-  st.fine_buckets = n_fine;
-  if ((rc = prepare_ctgs())) return rc;
-
   // run table: one entry per non-empty (source, segment) span; the device expands it into chunks
   const int T = mhm::tile_bases(nl);
   std::vector<mhm::SRun> runs;
   std::vector<mhm::PlaneSet> ps;
-  uint64_t n_chunks = 0;
+  uint64_t n_chunks = 0, n_c0 = 0;  // n_c0: chunks of the first owned coarse bucket (they come first)
   uint64_t xcd_start[9] = {0};
   for (size_t s = 0; s < srcs.size(); s++) ps.push_back(srcs[s].planes);
   // ordered by XCD class (coarse % 8), then coarse bucket, segment, source (see xcd_chunk)
   for (uint32_t x = 0; x < 8; x++) {
     xcd_start[x] = n_chunks;
-    for (uint32_t c = x; c < no; c += 8)
+    for (uint32_t c = x; c < no; c += 8) {
       for (uint32_t q = 0; q < NSUB; q++)
         for (size_t s = 0; s < srcs.size(); s++) {
           const uint32_t i = c * NSUB + q;
@@ -541,21 +546,13 @@ int mhmkc::finish(uint64_t *n_out_ret) {
           runs.push_back({srcs[s].start[i], cnt, (uint32_t)s, c, (uint32_t)n_chunks, 0});
           n_chunks += (cnt + T - 1) / T;
         }
+      if (c == 0) n_c0 = n_chunks;
+    }
   }
   xcd_start[8] = n_chunks;
   if (n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
   uint64_t xcd_max = 0;
   for (int x = 0; x < 8; x++) xcd_max = std::max(xcd_max, xcd_start[x + 1] - xcd_start[x]);
-  // capped fine layout
-  std::vector<uint64_t> cfit(2 * (size_t)no);  // [coarse_base | coarse_fcap]
-  uint64_t r2_size = 0;
-  for (uint32_t c = 0; c < no; c++) {
-    const uint64_t ex = per_coarse[c] >> fb;
-    const uint64_t fcap = align_up(ex + ex / 4 + 256, 16);
-    cfit[c] = r2_size;
-    cfit[no + c] = fcap;
-    r2_size += fcap << fb;
-  }
   if ((e = d_chunks.ensure(std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun) + 4 * (n_chunks + 1) + 256)) !=
       hipSuccess)
     return hip_fail(e, "chunk table");
@@ -574,6 +571,57 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if (!ps.empty() && (e = hipMemcpyAsync(d_srcs.p, ps.data(), ps.size() * sizeof(mhm::PlaneSet),
                                          hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "source H2D");
+
+  // fine bits: at most FINE_LOAD x the LDS table slots of distinct keys per fine bucket,
+  // with the distinct keys of the first owned coarse bucket estimated by a HyperLogLog sketch (the ratio
+  // of distinct keys to records grows with k and the error rate, so the record count alone misjudges it)
+  const uint32_t cap_slots = (uint32_t)mhm::count_cap(nl, compact);
+  fb = 4;
+  if (n_c0) {
+    mhm::PartitionParams sp{};
+    sp.runs = d_runs;
+    sp.chunk_run = d_chunk_run;
+    sp.n_runs = (uint32_t)runs.size();
+    sp.n_chunks = (uint32_t)n_chunks;
+    sp.srcs = d_srcs.as<mhm::PlaneSet>();
+    sp.k = k;
+    sp.coarse_bits = cb;
+    sp.hbits = hbits;
+    sp.compact = compact;
+    std::vector<uint32_t> reg(mhm::SKETCH_M);
+    prof_begin(MHMKC_STAGE_OTHER);
+    if ((e = d_hll.ensure(4 * mhm::SKETCH_M)) != hipSuccess ||
+        (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_M, stream)) != hipSuccess ||
+        (e = mhm::launch_sketch(sp, (uint32_t)n_c0, d_hll.as<unsigned int>(), nl, packed, stream)) != hipSuccess)
+      return hip_fail(e, "distinct sketch");
+    prof_end();
+    if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * mhm::SKETCH_M, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(stream)) != hipSuccess)
+      return hip_fail(e, "sketch D2H");
+    const double est = hll_estimate(reg);
+    st.distinct_estimate = (uint64_t)(est * no);
+    while (fb < 11 && est / (double)(1u << fb) > FINE_LOAD * cap_slots) fb++;
+  } else {  // no records in the first coarse bucket: ~4 records per slot
+    const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
+    while (fb < 11 && (avg_coarse >> fb) > (uint64_t)cap_slots * 4) fb++;
+  }
+  if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
+  fb = std::max(fb, min_fine_bits());
+  nf = 1u << fb;
+  const uint32_t n_fine = no * nf;
+  st.fine_buckets = n_fine;
+  if ((rc = prepare_ctgs())) return rc;
+
+  // capped fine layout
+  std::vector<uint64_t> cfit(2 * (size_t)no);  // [coarse_base | coarse_fcap]
+  uint64_t r2_size = 0;
+  for (uint32_t c = 0; c < no; c++) {
+    const uint64_t ex = per_coarse[c] >> fb;
+    const uint64_t fcap = align_up(ex + ex / 4 + 256, 16);
+    cfit[c] = r2_size;
+    cfit[no + c] = fcap;
+    r2_size += fcap << fb;
+  }
   if (no && (e = hipMemcpyAsync(d_cfit, cfit.data(), 16 * (size_t)no, hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "layout H2D");
   if ((e = d_fine_hist.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");

@@ -316,3 +316,12 @@ def test_compact_equals_wide_records(k, monkeypatch):
     assert_tables_equal(exact_t, wide_t, "compact exact vs wide")
     for key in ("distinct", "n_out", "purged", "count_sum"):
         assert st_c[key] == st_w[key], key
+
+
+@pytest.mark.parametrize("k", [21, 63])
+def test_distinct_sketch_estimate(k):
+    """The HyperLogLog sketch that sizes the fine partition is within 12 % of the true distinct count."""
+    b, o = synth_set(40000, 2_000_000, 41)
+    _, st = hip_table(b, o, k)
+    assert st["distinct"] > 0
+    assert abs(st["distinct_estimate"] - st["distinct"]) <= 0.12 * st["distinct"], (st["distinct_estimate"], st["distinct"])
