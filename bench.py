@@ -62,6 +62,16 @@ def algorithmic_bytes(stage: str, st: dict, k: int) -> float:
     }.get(stage, 0.0)
 
 
+def survey_model_bytes(st: dict, k: int, n_reads: int, read_len: int) -> float:
+    """SURVEY.md §8(d) B_alg of one step on one GPU: the reference's DRAM-table traffic model (2-bit read
+    stream, one S_slot read + write per occurrence, compacted output), without its capacity-dependent
+    finalize-scan term. It prices the work the reference's hash table does; this design keeps that table
+    in LDS, so the figure is a path-level yardstick, not the HBM bytes moved."""
+    nl = k // 32 + 1
+    s_slot = 8 * nl + 20
+    return n_reads * ((3 * read_len + 7) // 8) + st["occurrences"] * 2 * s_slot + st["n_out"] * (8 * nl + 4)
+
+
 def cpu_baseline(b, o, k, n_reads):
     """The CPU oracle (oracle/kcount_oracle.c, single thread) on the first n_reads reads."""
     sys.path.insert(0, str(ROOT / "tests"))
@@ -201,6 +211,11 @@ def main():
             "stages_ms_per_step": {s: round(v, 3) for s, v in per_step.items()},
             "achieved_alg_GBps_whole_step": round(
                 sum(algorithmic_bytes(s, st, k) for s in per_step) / (elapsed / steps) / 1e9, 1) if st else None,
+            "survey_model": {
+                "bytes_per_step_per_gpu": int(survey_model_bytes(st, k, R, L)),
+                "GBps_per_gpu": round(survey_model_bytes(st, k, R, L) / (elapsed / steps) / 1e9, 1),
+                "frac_of_hbm_peak": round(survey_model_bytes(st, k, R, L) / (elapsed / steps) / 1e9 / HBM_PEAK_GBPS, 4),
+            } if st else None,
             "distinct_per_gpu": st["distinct"] if st else None,
             "n_out_per_gpu": st["n_out"] if st else None,
             "synth_seconds": round(gen_s, 2),
