@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 3
+#define MHMKC_ABI_VERSION 4
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -130,6 +130,31 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_packed_bytes, const uint6
  * SeqBlockInserter::process_seq receives (src/kcount/kcount.cpp:80-86). Host buffers. depth is the
  * per-sequence count (reads: 1). Only depth == 1 (the read pass) is supported in this version. */
 int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *seq_offsets, uint64_t n_seqs, uint16_t depth);
+
+/* Add reads given as FASTQ text: parsed and packed on the device, then counted as mhmkc_add_reads.
+ * Replaces FastqReader::get_next_fq_record (src/fastq.cpp:504-551: 4 lines per record, rtrim, the '@' and
+ * '+' checks, get_fq_name :73-122, equal sequence and quality lengths) + the PackedRead constructor
+ * (src/packed_reads.cpp:73-109: N and IUPAC codes -> 4, quality min(q - qual_offset, 31)) for reads that
+ * reach kcount unchanged (single-end input, or pairs that merge_reads leaves unmerged: pair merging,
+ * src/merge_reads.cpp:237-588, is not part of this library). Where the reference DIEs the call fails:
+ * MHMKC_EINVAL for a malformed record (the message names the first bad record, 0-based),
+ * MHMKC_EBADCHAR for a base outside A C G T N U R Y K M S W B D H V, MHMKC_EUNSUPPORTED for a line
+ * longer than 2045 characters (the reference's fgets buffer, src/fastq.hpp:61, would split it).
+ * Host text of n_bytes bytes (no terminator needed). */
+int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes);
+
+/* Same, with device-resident text (only read during the call). */
+int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes);
+
+/* The PackedReads of the last mhmkc_add_fastq[_device] call on the device: d_bytes[n_bases] in the
+ * PackedRead layout, d_offsets[n_reads + 1]. Valid until the next add_fastq, reset or destroy. Any
+ * pointer may be NULL. */
+int mhmkc_fastq_packed(mhmkc_t h, const uint8_t **d_bytes, const uint64_t **d_offsets, uint64_t *n_reads,
+                       uint64_t *n_bases);
+
+/* Copy the PackedReads of the last mhmkc_add_fastq[_device] call to host arrays (either may be NULL):
+ * bytes[n_bases], offsets[n_reads + 1] (sizes from mhmkc_fastq_packed). */
+int mhmkc_fastq_fetch(mhmkc_t h, uint8_t *bytes, uint64_t *offsets);
 
 /* Add contigs for the contig pass of rounds after the first k (add_ctg_kmers, src/kcount/kcount.cpp:100-138;
  * insert_supermer_from_ctg, src/kcount/kcount_cpu.cpp:356-406). seqs: contig sequences back to back (case

@@ -20,9 +20,10 @@ from .kcount import (  # noqa: F401
     synth_genome,
     synth_reads,
 )
+from ._native import MhmkcError  # noqa: F401
 
 __all__ = [
     "KmerCounter", "KmerCounts", "KmerDHT", "KmerTable", "PackedReads", "analyze_kmers", "comm_id",
     "get_kmer_target_rank", "kmer_from_string", "kmer_to_string", "keys_to_strings", "n_longs_for",
-    "synth_genome", "synth_reads",
+    "synth_genome", "synth_reads", "MhmkcError",
 ]

@@ -35,6 +35,7 @@ ABI_SYMBOLS = [
     "mhmkc_config_init", "mhmkc_create", "mhmkc_destroy", "mhmkc_comm_id", "mhmkc_add_reads",
     "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_add_ctgs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_device_output",
     "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
+    "mhmkc_add_fastq", "mhmkc_add_fastq_device", "mhmkc_fastq_packed", "mhmkc_fastq_fetch",
 ]
 SYNTH_SYMBOLS = ["mhmkc_synth_config_init", "mhmkc_synth_genome", "mhmkc_synth_reads"]
 
@@ -141,6 +142,10 @@ def lib() -> C.CDLL:
     L.mhmkc_add_reads_device.argtypes = [VP, VP, VP, U64, U64]
     L.mhmkc_add_seqs.argtypes = [VP, C.c_char_p, VP, U64, C.c_uint16]
     L.mhmkc_add_ctgs.argtypes = [VP, C.c_char_p, VP, VP, U64]
+    L.mhmkc_add_fastq.argtypes = [VP, C.c_char_p, U64]
+    L.mhmkc_add_fastq_device.argtypes = [VP, VP, U64]
+    L.mhmkc_fastq_packed.argtypes = [VP, P(VP), P(VP), P(U64), P(U64)]
+    L.mhmkc_fastq_fetch.argtypes = [VP, VP, VP]
     L.mhmkc_finish.argtypes = [VP, P(U64)]
     L.mhmkc_fetch.argtypes = [VP, VP, VP, VP, VP]
     L.mhmkc_device_output.argtypes = [VP, P(VP), P(VP), P(VP), P(VP), P(U64)]

@@ -1,0 +1,225 @@
+// FASTQ text -> PackedRead bytes on the device ("ingest to the device stream").
+//
+// Reference: FastqReader::get_next_fq_record (src/fastq.cpp:504-551: four fgets lines per record, rtrim,
+// '@' / '+' checks, get_fq_name :73-122, equal sequence and quality lengths) feeding the PackedRead
+// constructor (src/packed_reads.cpp:73-109: A0 C1 G2 T3, N and the IUPAC codes U R Y K M S W B D H V -> 4,
+// anything else fatal; quality min(q - qual_offset, 31) in bits 3-7).
+//
+// The text is HBM-resident; the pass is byte streaming:
+//   k_fq_count    newlines per 4 KB chunk (16 bytes per lane, SWAR zero-byte test)
+//   scan          chunk bases (rocPRIM)
+//   k_fq_lines    the position of every newline, in order (block scan of the lanes' counts)
+//   k_fq_records  one lane per 4-line record: trims, format checks, sequence length
+//   scan          read offsets (rocPRIM) = the PackedReads CSR layout k_extract_scatter consumes
+//   k_fq_pack     one wave per record: base code | quality << 3
+// Errors are reported as the first failing record (atomicMin of record << 4 | kind, kinds as in
+// kcount_launch.hpp FQ_E_*), which is where the reference DIEs.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_scan.hpp>
+
+#include "kcount_launch.hpp"
+
+namespace mhm {
+
+namespace {
+
+constexpr int FQ_THREADS = 256;
+constexpr int FQ_BYTES = 16;  // per lane
+static_assert(FQ_THREADS * FQ_BYTES == FQ_CHUNK, "chunk = one block");
+
+// 4-bit mask of the '\n' bytes of a little-endian word (exact zero-byte test of w ^ 0x0a0a0a0a)
+__device__ __forceinline__ uint32_t nl4(uint32_t w) {
+  const uint32_t x = w ^ 0x0a0a0a0au;
+  const uint32_t hi = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+  return ((hi >> 7) & 1u) | ((hi >> 14) & 2u) | ((hi >> 21) & 4u) | ((hi >> 28) & 8u);
+}
+
+// 16-bit mask of the newlines among text[pos, pos + 16) (bytes at or past n never match)
+__device__ __forceinline__ uint32_t nl_mask(const char *text, uint64_t pos, uint64_t n) {
+  if (pos + FQ_BYTES <= n && (((uintptr_t)(text + pos)) & 15u) == 0) {
+    const uint4 v = *(const uint4 *)(text + pos);
+    return nl4(v.x) | (nl4(v.y) << 4) | (nl4(v.z) << 8) | (nl4(v.w) << 12);
+  }
+  uint32_t m = 0;
+  for (int i = 0; i < FQ_BYTES; i++)
+    if (pos + i < n && text[pos + i] == '\n') m |= 1u << i;
+  return m;
+}
+
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_count(const char *text, uint64_t n, unsigned long long *chunk) {
+  __shared__ uint32_t s_w[FQ_THREADS / 64];
+  const uint64_t pos = (uint64_t)blockIdx.x * FQ_CHUNK + (uint64_t)threadIdx.x * FQ_BYTES;
+  uint32_t c = __popc(nl_mask(text, pos, n));
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < FQ_THREADS / 64; w++) t += s_w[w];
+    chunk[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_lines(const char *text, uint64_t n,
+                                                          const unsigned long long *chunk_base,
+                                                          unsigned long long *line_end) {
+  __shared__ uint32_t s_w[FQ_THREADS / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t pos = (uint64_t)blockIdx.x * FQ_CHUNK + (uint64_t)threadIdx.x * FQ_BYTES;
+  uint32_t m = nl_mask(text, pos, n);
+  const uint32_t c = __popc(m);
+  uint32_t incl = c;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  uint64_t o = chunk_base[blockIdx.x] + (incl - c);
+  for (int w = 0; w < wid; w++) o += s_w[w];
+  while (m) {
+    const int b = __ffs(m) - 1;
+    m &= m - 1;
+    line_end[o++] = pos + (uint64_t)b;
+  }
+}
+
+__device__ __forceinline__ bool fq_space(unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+
+__device__ __forceinline__ uint64_t rtrim_end(const char *s, uint64_t b, uint64_t e) {
+  while (e > b && fq_space((unsigned char)s[e - 1])) e--;
+  return e;
+}
+
+// get_fq_name's verdict (src/fastq.cpp:73-122) on the trimmed id line [b, e), which starts with '@'
+__device__ bool name_ok(const char *s, uint64_t b, uint64_t e) {
+  const char *h = s + b + 1;
+  const uint64_t len = rtrim_end(s, b + 1, e) - (b + 1);
+  if (len < 3 || h[len - 2] == '/') return true;
+  if (h[len - 2] == 'R') return true;  // HudsonAlpha @pair-R1 / @pair-R2
+  uint64_t tab = len, sp = len;
+  for (uint64_t i = 0; i < len && tab == len; i++) {
+    const char c = h[i];
+    if (c == '\t') tab = i;
+    if (c == ' ' && sp == len) sp = i;
+  }
+  const uint64_t ep = tab < len ? tab : sp;  // first tab, else first space
+  if (ep == len) return true;                // no comment
+  if (ep > 3 && h[ep - 2] == '/' && (h[ep - 1] == '1' || h[ep - 1] == '2')) return true;
+  if (len < ep + 7 || h[ep + 2] != ':' || h[ep + 4] != ':' || h[ep + 6] != ':' || (h[ep + 1] != '1' && h[ep + 1] != '2'))
+    return false;
+  return true;
+}
+
+__device__ __forceinline__ void fq_fail(unsigned long long *err, uint64_t r, int kind) {
+  atomicMin(err, ((unsigned long long)r << 4) | (unsigned long long)kind);
+}
+
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_records(const char *text, const unsigned long long *line_end,
+                                                            uint64_t n_rec, unsigned long long *len,
+                                                            unsigned long long *err) {
+  const uint64_t r = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x;
+  if (r > n_rec) return;
+  if (r == n_rec) {  // the scan's last element: offs[n_rec] = total
+    len[r] = 0;
+    return;
+  }
+  uint64_t lb[4], le[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t j = 4 * r + i;
+    lb[i] = j ? line_end[j - 1] + 1 : 0;
+    le[i] = line_end[j];
+  }
+  len[r] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (le[i] - lb[i] > FQ_MAX_LINE) return fq_fail(err, r, FQ_E_LONG);
+  const uint64_t ide = rtrim_end(text, lb[0], le[0]);
+  if (ide == lb[0] || text[lb[0]] != '@') return fq_fail(err, r, FQ_E_ID);
+  if (le[2] == lb[2] || text[lb[2]] != '+') return fq_fail(err, r, FQ_E_PLUS);
+  if (!name_ok(text, lb[0], ide)) return fq_fail(err, r, FQ_E_NAME);
+  const uint64_t L = rtrim_end(text, lb[1], le[1]) - lb[1];
+  if (L != rtrim_end(text, lb[3], le[3]) - lb[3]) return fq_fail(err, r, FQ_E_LEN);
+  len[r] = L;
+}
+
+// PackedRead base code (packed_reads.cpp:87-105), -1 for a fatal character
+__device__ __forceinline__ int base_code(unsigned char c) {
+  const uint32_t i = (uint32_t)c - 'A';
+  if (i >= 26) return -1;
+  if (i == 0) return 0;
+  if (i == 'C' - 'A') return 1;
+  if (i == 'G' - 'A') return 2;
+  if (i == 'T' - 'A') return 3;
+  constexpr uint32_t four = (1u << ('N' - 'A')) | (1u << ('U' - 'A')) | (1u << ('R' - 'A')) | (1u << ('Y' - 'A')) |
+                            (1u << ('K' - 'A')) | (1u << ('M' - 'A')) | (1u << ('S' - 'A')) | (1u << ('W' - 'A')) |
+                            (1u << ('B' - 'A')) | (1u << ('D' - 'A')) | (1u << ('H' - 'A')) | (1u << ('V' - 'A'));
+  return ((four >> i) & 1u) ? 4 : -1;
+}
+
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_pack(const char *text, const unsigned long long *line_end,
+                                                         uint64_t n_rec, const unsigned long long *offs,
+                                                         int qual_offset, uint8_t *out, unsigned long long *err) {
+  const uint64_t r = (uint64_t)blockIdx.x * (FQ_THREADS / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n_rec) return;
+  const uint64_t sb = line_end[4 * r] + 1, qb = line_end[4 * r + 2] + 1;
+  const uint64_t o = offs[r], L = offs[r + 1] - o;
+  bool bad = false;
+  for (uint64_t i = lane; i < L; i += 64) {
+    const int c = base_code((unsigned char)text[sb + i]);
+    int q = (int)(signed char)text[qb + i] - qual_offset;
+    q = q < 31 ? q : 31;
+    bad |= c < 0;
+    out[o + i] = (uint8_t)((c & 7) | (uint8_t)((unsigned)(unsigned char)q << 3));
+  }
+  if (__ballot(bad) && lane == 0) fq_fail(err, r, FQ_E_CHAR);
+}
+
+}  // namespace
+
+size_t fq_scan_tmp_bytes(uint64_t n_items) {
+  size_t a = 0;
+  (void)rocprim::exclusive_scan(nullptr, a, (const unsigned long long *)nullptr, (unsigned long long *)nullptr, 0ull,
+                                (size_t)n_items, rocprim::plus<unsigned long long>());
+  return a;
+}
+
+hipError_t fq_scan(void *tmp, size_t tmp_bytes, const unsigned long long *in, unsigned long long *out,
+                   uint64_t n_items, hipStream_t s) {
+  return rocprim::exclusive_scan(tmp, tmp_bytes, in, out, 0ull, (size_t)n_items, rocprim::plus<unsigned long long>(), s);
+}
+
+hipError_t launch_fq_count(const char *text, uint64_t n, unsigned long long *chunk, hipStream_t s) {
+  const uint64_t nch = (n + FQ_CHUNK - 1) / FQ_CHUNK;
+  if (nch) hipLaunchKernelGGL(k_fq_count, dim3((uint32_t)nch), dim3(FQ_THREADS), 0, s, text, n, chunk);
+  return hipGetLastError();
+}
+
+hipError_t launch_fq_lines(const char *text, uint64_t n, const unsigned long long *chunk_base,
+                           unsigned long long *line_end, hipStream_t s) {
+  const uint64_t nch = (n + FQ_CHUNK - 1) / FQ_CHUNK;
+  if (nch) hipLaunchKernelGGL(k_fq_lines, dim3((uint32_t)nch), dim3(FQ_THREADS), 0, s, text, n, chunk_base, line_end);
+  return hipGetLastError();
+}
+
+hipError_t launch_fq_records(const char *text, const unsigned long long *line_end, uint64_t n_rec,
+                             unsigned long long *len, unsigned long long *err, hipStream_t s) {
+  const uint64_t nb = (n_rec + 1 + FQ_THREADS - 1) / FQ_THREADS;
+  hipLaunchKernelGGL(k_fq_records, dim3((uint32_t)nb), dim3(FQ_THREADS), 0, s, text, line_end, n_rec, len, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_fq_pack(const char *text, const unsigned long long *line_end, uint64_t n_rec,
+                          const unsigned long long *offs, int qual_offset, uint8_t *out, unsigned long long *err,
+                          hipStream_t s) {
+  const uint64_t nb = (n_rec + FQ_THREADS / 64 - 1) / (FQ_THREADS / 64);
+  if (nb)
+    hipLaunchKernelGGL(k_fq_pack, dim3((uint32_t)nb), dim3(FQ_THREADS), 0, s, text, line_end, n_rec, offs,
+                       qual_offset, out, err);
+  return hipGetLastError();
+}
+
+}  // namespace mhm

@@ -205,4 +205,27 @@ hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, u
                        uint32_t n, hipStream_t s);
 hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s);
 
+// FASTQ ingest (fastq.hip): text -> PackedRead bytes. FQ_CHUNK bytes of text per count / lines block.
+constexpr int FQ_CHUNK = 4096;
+// longest line (without its newline) that the reference's fgets buffer reads whole (BUF_SIZE 2047,
+// src/fastq.hpp:61)
+constexpr uint64_t FQ_MAX_LINE = 2045;
+// error kinds, in the order the reference checks them (src/fastq.cpp:525-547, packed_reads.cpp:104)
+enum { FQ_E_ID = 1, FQ_E_PLUS = 2, FQ_E_NAME = 3, FQ_E_LEN = 4, FQ_E_LONG = 5, FQ_E_CHAR = 6, FQ_E_TRUNC = 7 };
+size_t fq_scan_tmp_bytes(uint64_t n_items);
+hipError_t fq_scan(void *tmp, size_t tmp_bytes, const unsigned long long *in, unsigned long long *out,
+                   uint64_t n_items, hipStream_t s);
+// newlines per FQ_CHUNK chunk -> chunk[ceil(n / FQ_CHUNK)]
+hipError_t launch_fq_count(const char *text, uint64_t n, unsigned long long *chunk, hipStream_t s);
+// position of every newline, in order, from the scanned chunk counts
+hipError_t launch_fq_lines(const char *text, uint64_t n, const unsigned long long *chunk_base,
+                           unsigned long long *line_end, hipStream_t s);
+// per record: sequence length (len[n_rec] = 0 for the scan) and format checks (err: atomicMin of
+// record << 4 | FQ_E_*)
+hipError_t launch_fq_records(const char *text, const unsigned long long *line_end, uint64_t n_rec,
+                             unsigned long long *len, unsigned long long *err, hipStream_t s);
+hipError_t launch_fq_pack(const char *text, const unsigned long long *line_end, uint64_t n_rec,
+                          const unsigned long long *offs, int qual_offset, uint8_t *out, unsigned long long *err,
+                          hipStream_t s);
+
 }  // namespace mhm

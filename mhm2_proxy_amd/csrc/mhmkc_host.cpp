@@ -98,6 +98,11 @@ struct mhmkc {
   DevBuf d_hist, d_cursor, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xcounts;
   DevBuf d_in_bytes, d_in_offs, d_hll;
+  // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
+  // the packed reads of the last batch, first error
+  DevBuf d_fq_text, d_fq_chunk, d_fq_lines, d_fq_len, d_fq_tmp, d_fq_bytes, d_fq_offs, d_fq_err;
+  uint64_t fq_reads = 0, fq_bases = 0;
+  int add_fastq(const char *d_text, uint64_t n);
   // contig pass (add_ctg_kmers): contigs in the PackedRead byte layout, kept on the host until finish
   std::vector<uint8_t> ctg_bytes;
   std::vector<uint64_t> ctg_offs{0}, ctg_win{0};  // byte offsets, counted-window prefix
@@ -914,7 +919,9 @@ void mhmkc_destroy(mhmkc_t h) {
   DevBuf *bufs[] = {&h->d_hist,     &h->d_cursor,    &h->d_tiles,     &h->d_err,       &h->d_stats,
                     &h->d_fine_hist, &h->d_fine_base, &h->d_fine_cursor, &h->d_chunks,  &h->d_srcs,
                     &h->d_r2,       &h->d_out_keys,  &h->d_out_counts, &h->d_out_left, &h->d_out_right,
-                    &h->d_out_cursor, &h->d_recv,    &h->d_xcounts,   &h->d_in_bytes,  &h->d_in_offs};
+                    &h->d_out_cursor, &h->d_recv,    &h->d_xcounts,   &h->d_in_bytes,  &h->d_in_offs,
+                    &h->d_hll,       &h->d_fq_text,   &h->d_fq_chunk,  &h->d_fq_lines,  &h->d_fq_len,
+                    &h->d_fq_tmp,    &h->d_fq_bytes,  &h->d_fq_offs,   &h->d_fq_err};
   for (DevBuf *b : bufs) b->release();
   DevBuf *cbufs[] = {&h->d_ctg_bytes, &h->d_ctg_offs, &h->d_ctg_win,   &h->d_ctg_depth, &h->d_ctg_scratch,
                      &h->d_ctg_state, &h->d_ctg_bucket, &h->d_ctg_done, &h->d_ctg_keys[0], &h->d_ctg_keys[1],
@@ -936,6 +943,86 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_
   if (!h) return MHMKC_EINVAL;
   if (n_reads && (!d_bytes || !d_offs)) return h->fail(MHMKC_EINVAL, "null device buffer");
   return h->add_device(d_bytes, d_offs, n_reads, n_bases, h->cfg.qual_cutoff);
+}
+
+// FASTQ text on the device -> PackedReads in d_fq_bytes / d_fq_offs -> add_device (fastq.hip).
+int mhmkc::add_fastq(const char *d_text, uint64_t n) {
+  int rc = begin_round();
+  if (rc) return rc;
+  fq_reads = fq_bases = 0;
+  if (n == 0) return MHMKC_OK;
+  hipError_t e;
+  const uint64_t nch = (n + mhm::FQ_CHUNK - 1) / mhm::FQ_CHUNK;
+  if ((e = d_fq_chunk.ensure((nch + 1) * 16)) != hipSuccess) return hip_fail(e, "fastq chunk counts");
+  unsigned long long *cnt = d_fq_chunk.as<unsigned long long>(), *cbase = cnt + nch + 1;
+  size_t tmp_bytes = mhm::fq_scan_tmp_bytes(nch + 1);
+  if ((e = d_fq_tmp.ensure(tmp_bytes)) != hipSuccess) return hip_fail(e, "fastq scan scratch");
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = hipMemsetAsync(cnt + nch, 0, 8, stream);
+  if (e == hipSuccess) e = mhm::launch_fq_count(d_text, n, cnt, stream);
+  if (e == hipSuccess) e = mhm::fq_scan(d_fq_tmp.p, tmp_bytes, cnt, cbase, nch + 1, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "fastq newline count");
+  unsigned long long newlines = 0;
+  char last = 0;
+  if ((e = hipMemcpyAsync(&newlines, cbase + nch, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess)
+    return hip_fail(e, "fastq newline count D2H");
+  // fgets returns a last line without its newline
+  const uint64_t lines = newlines + (last != '\n' ? 1 : 0);
+  const uint64_t R = lines / 4;
+  if ((e = d_fq_lines.ensure(std::max<uint64_t>(lines, 1) * 8)) != hipSuccess) return hip_fail(e, "fastq lines");
+  if ((e = d_fq_len.ensure((R + 1) * 8)) != hipSuccess || (e = d_fq_offs.ensure((R + 1) * 8)) != hipSuccess ||
+      (e = d_fq_err.ensure(8)) != hipSuccess)
+    return hip_fail(e, "fastq records");
+  const size_t tmp2 = mhm::fq_scan_tmp_bytes(R + 1);
+  if (tmp2 > tmp_bytes) {
+    if ((e = d_fq_tmp.ensure(tmp2)) != hipSuccess) return hip_fail(e, "fastq scan scratch");
+    tmp_bytes = tmp2;
+  }
+  unsigned long long *lend = d_fq_lines.as<unsigned long long>(), *len = d_fq_len.as<unsigned long long>();
+  unsigned long long *offs = d_fq_offs.as<unsigned long long>(), *err_d = d_fq_err.as<unsigned long long>();
+  const unsigned long long n_end = n;
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = mhm::launch_fq_lines(d_text, n, cbase, lend, stream);
+  if (e == hipSuccess && last != '\n') e = hipMemcpyAsync(lend + lines - 1, &n_end, 8, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(err_d, 0xff, 8, stream);
+  if (e == hipSuccess) e = mhm::launch_fq_records(d_text, lend, R, len, err_d, stream);
+  if (e == hipSuccess) e = mhm::fq_scan(d_fq_tmp.p, tmp_bytes, len, offs, R + 1, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "fastq records");
+  unsigned long long n_bases = 0;
+  if ((e = hipMemcpyAsync(&n_bases, offs + R, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess)
+    return hip_fail(e, "fastq records D2H");
+  if ((e = d_fq_bytes.ensure(std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess) return hip_fail(e, "fastq bytes");
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = mhm::launch_fq_pack(d_text, lend, R, offs, cfg.qual_offset, d_fq_bytes.as<uint8_t>(), err_d, stream);
+  prof_end();
+  unsigned long long first_err = ~0ull;
+  if (e == hipSuccess) e = hipMemcpyAsync(&first_err, err_d, 8, hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return hip_fail(e, "fastq pack");
+  if (lines % 4) first_err = std::min<unsigned long long>(first_err, ((unsigned long long)R << 4) | mhm::FQ_E_TRUNC);
+  if (first_err != ~0ull) {
+    const unsigned long long rec = first_err >> 4;
+    switch ((int)(first_err & 15)) {
+      case mhm::FQ_E_ID: return fail(MHMKC_EINVAL, "invalid FASTQ record %llu: expected read name (@)", rec);
+      case mhm::FQ_E_PLUS: return fail(MHMKC_EINVAL, "invalid FASTQ record %llu: expected '+'", rec);
+      case mhm::FQ_E_NAME: return fail(MHMKC_EINVAL, "invalid FASTQ record %llu: incorrect name format", rec);
+      case mhm::FQ_E_LEN:
+        return fail(MHMKC_EINVAL, "invalid FASTQ record %llu: sequence length != quals length", rec);
+      case mhm::FQ_E_LONG:
+        return fail(MHMKC_EUNSUPPORTED, "FASTQ record %llu: line longer than %llu characters", rec,
+                    (unsigned long long)mhm::FQ_MAX_LINE);
+      case mhm::FQ_E_CHAR: return fail(MHMKC_EBADCHAR, "FASTQ record %llu: illegal base character", rec);
+      default: return fail(MHMKC_EINVAL, "FASTQ text ends inside record %llu", rec);
+    }
+  }
+  fq_reads = R;
+  fq_bases = n_bases;
+  return add_device(d_fq_bytes.as<uint8_t>(), d_fq_offs.as<uint64_t>(), R, n_bases, cfg.qual_cutoff);
 }
 
 static int add_host(mhmkc_t h, const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut) {
@@ -973,6 +1060,48 @@ int mhmkc_add_reads(mhmkc_t h, const uint8_t *bytes, const uint64_t *offs, uint6
   int rc = check_offsets(h, offs, n_reads);
   if (rc) return rc;
   return add_host(h, bytes, offs, n_reads, h->cfg.qual_cutoff);
+}
+
+int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes) {
+  if (!h) return MHMKC_EINVAL;
+  if (n_bytes && !d_text) return h->fail(MHMKC_EINVAL, "null device buffer");
+  return h->add_fastq(d_text, n_bytes);
+}
+
+int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes) {
+  if (!h) return MHMKC_EINVAL;
+  if (n_bytes && !text) return h->fail(MHMKC_EINVAL, "null host buffer");
+  hipError_t e;
+  if ((e = h->d_fq_text.ensure(n_bytes + 16)) != hipSuccess) return h->hip_fail(e, "fastq staging");
+  if (n_bytes && (e = hipMemcpyAsync(h->d_fq_text.p, text, n_bytes, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+    return h->hip_fail(e, "fastq H2D");
+  int rc = h->add_fastq(h->d_fq_text.as<char>(), n_bytes);
+  if (rc == MHMKC_OK && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return h->hip_fail(e, "add_fastq");
+  return rc;
+}
+
+int mhmkc_fastq_packed(mhmkc_t h, const uint8_t **d_bytes, const uint64_t **d_offsets, uint64_t *n_reads,
+                       uint64_t *n_bases) {
+  if (!h) return MHMKC_EINVAL;
+  if (d_bytes) *d_bytes = h->d_fq_bytes.as<uint8_t>();
+  if (d_offsets) *d_offsets = h->d_fq_offs.as<uint64_t>();
+  if (n_reads) *n_reads = h->fq_reads;
+  if (n_bases) *n_bases = h->fq_bases;
+  return MHMKC_OK;
+}
+
+int mhmkc_fastq_fetch(mhmkc_t h, uint8_t *bytes, uint64_t *offsets) {
+  if (!h) return MHMKC_EINVAL;
+  hipError_t e = hipSuccess;
+  if (bytes && h->fq_bases) e = hipMemcpyAsync(bytes, h->d_fq_bytes.p, h->fq_bases, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && offsets) {
+    if (h->d_fq_offs.p && h->fq_reads)
+      e = hipMemcpyAsync(offsets, h->d_fq_offs.p, (h->fq_reads + 1) * 8, hipMemcpyDeviceToHost, h->stream);
+    else
+      offsets[0] = 0;
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fastq fetch");
 }
 
 int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *offs, uint64_t n_seqs, uint16_t depth) {
@@ -1093,6 +1222,7 @@ int mhmkc_reset(mhmkc_t h) {
   h->ctg_win.assign(1, 0);
   h->ctg_depth.clear();
   h->ctg_n = 0;
+  h->fq_reads = h->fq_bases = 0;
   h->finished = false;
   h->began = false;
   h->n_out = 0;

@@ -285,6 +285,26 @@ class KmerCounter:
         n_reads = int(offsets_t.numel()) - 1
         self.add_packed_reads_device(bytes_t.data_ptr(), offsets_t.data_ptr(), n_reads, int(bytes_t.numel()))
 
+    def add_fastq(self, text) -> None:
+        """FASTQ text (bytes or str), parsed and packed on the device, then counted: FastqReader +
+        PackedRead construction (src/fastq.cpp:504-551, src/packed_reads.cpp:73-109) for reads that reach
+        kcount unmerged. Malformed input raises MhmkcError where the reference DIEs."""
+        blob = text.encode("ascii") if isinstance(text, str) else bytes(text)
+        self._check(N.lib().mhmkc_add_fastq(self._h, blob, len(blob)))
+
+    def add_fastq_tensor(self, text_t) -> None:
+        """FASTQ text already in HBM (a uint8 torch tensor on the counter's device)."""
+        self._check(N.lib().mhmkc_add_fastq_device(self._h, text_t.data_ptr(), int(text_t.numel())))
+
+    def fastq_packed(self) -> tuple[np.ndarray, np.ndarray]:
+        """The PackedReads (bytes, offsets) of the last add_fastq call, copied to the host."""
+        n_reads, n_bases = C.c_uint64(), C.c_uint64()
+        self._check(N.lib().mhmkc_fastq_packed(self._h, None, None, C.byref(n_reads), C.byref(n_bases)))
+        b = np.empty(int(n_bases.value), dtype=np.uint8)
+        o = np.empty(int(n_reads.value) + 1, dtype=np.uint64)
+        self._check(N.lib().mhmkc_fastq_fetch(self._h, b.ctypes.data, o.ctypes.data))
+        return b, o
+
     def add_reads(self, reads: PackedReads) -> None:
         self.add_packed_reads(reads.packed_bytes, reads.offsets)
 

@@ -715,3 +715,94 @@ void orc_table_free(orc_table *t) {
 void orc_kmer_hash_many(const uint64_t *keys, uint64_t n, int n_longs, uint64_t *out) {
   for (uint64_t i = 0; i < n; i++) out[i] = orc_kmer_hash(keys + i * n_longs, n_longs);
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * FASTQ ingest: FastqReader::get_next_fq_record (src/fastq.cpp:504-551) with
+ * rtrim (:67-71) and get_fq_name (:73-122), then the PackedRead constructor (src/packed_reads.cpp:73-109).
+ * Records are read 4 lines at a time with fgets into a BUF_SIZE = 2047 buffer (src/fastq.hpp:61): a line
+ * longer than 2045 characters would be split by fgets and is reported as unsupported here.
+ * Error kinds (the first failing record, in file order; within a record in this order), all a DIE in the
+ * reference: 1 id line without '@' (:539), 2 third line without '+' (:540), 3 name format (:542),
+ * 4 sequence / quality length mismatch (:545), 5 line too long, 6 illegal base (packed_reads.cpp:104),
+ * 7 file ends inside a record (:525). rtrim of an all-whitespace line is undefined behaviour in the
+ * reference (size_t underflow); here it yields the empty string. */
+
+static int fq_isspace(unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+
+static uint64_t fq_rtrim(const char *s, uint64_t b, uint64_t e) { /* :67-71 */
+  while (e > b && fq_isspace((unsigned char)s[e - 1])) e--;
+  return e;
+}
+
+/* get_fq_name's verdict on the rtrimmed id line [b, e) (which starts with '@') */
+static int fq_name_ok(const char *s, uint64_t b, uint64_t e) {
+  const char *h = s + b + 1; /* header.erase(0, 1) */
+  const uint64_t len = fq_rtrim(s, b + 1, e) - (b + 1);
+  if (len >= 3 && h[len - 2] != '/') {
+    if (h[len - 2] == 'R') return 1; /* HudsonAlpha -R1 / -R2 */
+    uint64_t end_pos = len;
+    for (uint64_t i = 0; i < len; i++)
+      if (h[i] == '\t') { end_pos = i; break; }
+    if (end_pos == len) {
+      for (uint64_t i = 0; i < len; i++)
+        if (h[i] == ' ') { end_pos = i; break; }
+      if (end_pos == len) return 1; /* no comment */
+    }
+    if (end_pos > 3 && h[end_pos - 2] == '/' && (h[end_pos - 1] == '1' || h[end_pos - 1] == '2')) return 1;
+    if (len < end_pos + 7 || h[end_pos + 2] != ':' || h[end_pos + 4] != ':' || h[end_pos + 6] != ':' ||
+        (h[end_pos + 1] != '1' && h[end_pos + 1] != '2'))
+      return 0;
+  }
+  return 1;
+}
+
+static int fq_code(char c) { /* PackedRead::PackedRead switch, packed_reads.cpp:87-105 */
+  switch (c) {
+    case 'A': return 0;
+    case 'C': return 1;
+    case 'G': return 2;
+    case 'T': return 3;
+    case 'N': case 'U': case 'R': case 'Y': case 'K': case 'M': case 'S': case 'W': case 'B': case 'D':
+    case 'H': case 'V': return 4;
+  }
+  return -1;
+}
+
+/* Packs every record of text[0, n). Returns the number of records, or -kind on error with *err_rec = the
+ * failing record. out needs room for n bytes, offs for n / 6 + 2 entries. */
+int64_t orc_fastq_pack(const char *text, uint64_t n, int qual_offset, uint8_t *out, uint64_t *offs,
+                       uint64_t *err_rec) {
+  uint64_t pos = 0, r = 0, nb = 0;
+  offs[0] = 0;
+  while (pos < n) {
+    uint64_t lb[4], le[4];
+    for (int i = 0; i < 4; i++) {
+      if (pos >= n) { *err_rec = r; return -7; }
+      const char *nl = memchr(text + pos, '\n', n - pos);
+      const uint64_t end = nl ? (uint64_t)(nl - text) : n;
+      lb[i] = pos;
+      le[i] = end;
+      pos = end + 1;
+    }
+    for (int i = 0; i < 4; i++)
+      if (le[i] - lb[i] > 2045) { *err_rec = r; return -5; }
+    const uint64_t ide = fq_rtrim(text, lb[0], le[0]);
+    const uint64_t se = fq_rtrim(text, lb[1], le[1]);
+    const uint64_t qe = fq_rtrim(text, lb[3], le[3]);
+    if (ide == lb[0] || text[lb[0]] != '@') { *err_rec = r; return -1; }
+    if (le[2] == lb[2] || text[lb[2]] != '+') { *err_rec = r; return -2; }
+    if (!fq_name_ok(text, lb[0], ide)) { *err_rec = r; return -3; }
+    const uint64_t L = se - lb[1];
+    if (L != qe - lb[3]) { *err_rec = r; return -4; }
+    for (uint64_t i = 0; i < L; i++) {
+      const int c = fq_code(text[lb[1] + i]);
+      if (c < 0) { *err_rec = r; return -6; }
+      int q = (int)(signed char)text[lb[3] + i] - qual_offset;
+      if (q > 31) q = 31;
+      out[nb + i] = (uint8_t)(c | (uint8_t)((unsigned char)q << 3));
+    }
+    nb += L;
+    offs[++r] = nb;
+  }
+  return (int64_t)r;
+}

@@ -160,3 +160,42 @@ def read_table_file(path: Path, k: int) -> m.KmerTable:
             right.append(ord(r))
     return m.KmerTable(k, np.array(keys, dtype=np.uint64).reshape(-1, nl), np.array(counts, dtype=np.uint16),
                        np.array(left, dtype=np.uint8), np.array(right, dtype=np.uint8))
+
+
+NAME_STYLES = ("illumina18", "slash", "hudson", "tab", "plain", "slash_comment")
+
+
+def fastq_text(packed_bytes, offsets, *, seed: int = 0, crlf_every: int = 0, trailing_ws: bool = False,
+               iupac: bool = False, final_newline: bool = True, qual_offset: int = 33) -> bytes:
+    """FASTQ text of packed reads, in every read-name style get_fq_name accepts (src/fastq.cpp:73-122),
+    optionally with CRLF lines, trailing whitespace and IUPAC codes for N (all of which pack back to the
+    same PackedRead bytes)."""
+    rng = np.random.default_rng(seed)
+    b = np.asarray(packed_bytes, dtype=np.uint8)
+    codes = np.frombuffer(b"ACGTN", dtype=np.uint8)
+    seq_all = codes[np.minimum(b & 7, 4)].copy()
+    if iupac:
+        amb = np.frombuffer(b"NURYKMSWBDHV", dtype=np.uint8)
+        isn = seq_all == ord("N")
+        seq_all[isn] = amb[rng.integers(0, len(amb), size=int(isn.sum()))]
+    qual_all = ((b >> 3) + qual_offset).astype(np.uint8)
+    out = []
+    n = len(offsets) - 1
+    for i in range(n):
+        lo, hi = int(offsets[i]), int(offsets[i + 1])
+        style = NAME_STYLES[(i + seed) % len(NAME_STYLES)]
+        mate = 1 + (i & 1)
+        name = {"illumina18": f"@M0:{i}:FC:1:{i % 97}:{i % 13}:{i} {mate}:N:0:ACGT",
+                "slash": f"@read{i}/{mate}", "hudson": f"@pair{i}-R{mate}",
+                "tab": f"@read{i}/{mate}\textra", "plain": f"@r{i}",
+                "slash_comment": f"@read{i}/{mate} comment here"}[style]
+        eol = "\r\n" if crlf_every and i % crlf_every == 0 else "\n"
+        ws = "  \t" if trailing_ws and i % 3 == 0 else ""
+        out.append(f"{name}{ws}{eol}".encode())
+        out.append(seq_all[lo:hi].tobytes() + ws.encode() + eol.encode())
+        out.append(f"+{eol}".encode())
+        out.append(qual_all[lo:hi].tobytes() + eol.encode())
+    t = b"".join(out)
+    if not final_newline and t.endswith(b"\n"):
+        t = t[:-2] if t.endswith(b"\r\n") else t[:-1]
+    return t

@@ -52,6 +52,8 @@ def oracle() -> C.CDLL:
         L.orc_extract.restype = C.c_int64
         L.orc_count_records.argtypes = [VP, VP, U64, I, I, C.c_double]
         L.orc_count_records.restype = VP
+        L.orc_fastq_pack.argtypes = [C.c_char_p, U64, I, VP, VP, VP]
+        L.orc_fastq_pack.restype = C.c_int64
         L.orc_table_size.argtypes = [VP]
         L.orc_table_size.restype = U64
         L.orc_table_fetch.argtypes = [VP, VP, VP, VP, VP]
@@ -190,3 +192,26 @@ def minimizer_hash_fast(longs, k: int, m: int) -> int:
 def target_rank(longs, k: int, rank_n: int) -> int:
     a = np.ascontiguousarray(longs, dtype=np.uint64)
     return int(oracle().orc_kmer_target_rank(a.ctypes.data, k, a.size, rank_n))
+
+
+FQ_KINDS = {1: "id", 2: "plus", 3: "name", 4: "len", 5: "long", 6: "char", 7: "trunc"}
+
+
+def fastq_pack(text: bytes, qual_offset: int = 33):
+    """FASTQ text -> (PackedRead bytes, offsets), or raises FastqError(kind, record) where the reference
+    DIEs (orc_fastq_pack: FastqReader::get_next_fq_record + PackedRead ctor)."""
+    n = len(text)
+    out = np.empty(max(n, 1), dtype=np.uint8)
+    offs = np.empty(n // 6 + 2, dtype=np.uint64)
+    err = np.zeros(1, dtype=np.uint64)
+    r = oracle().orc_fastq_pack(text, n, qual_offset, out.ctypes.data, offs.ctypes.data, err.ctypes.data)
+    if r < 0:
+        raise FastqError(FQ_KINDS[-r], int(err[0]))
+    return out[: int(offs[r])].copy(), offs[: r + 1].copy()
+
+
+class FastqError(ValueError):
+    def __init__(self, kind: str, record: int):
+        super().__init__(f"{kind} at record {record}")
+        self.kind = kind
+        self.record = record
