@@ -11,7 +11,7 @@
 //   k_fq_lines    the position of every newline, in order (block scan of the lanes' counts)
 //   k_fq_records  one lane per 4-line record: trims, format checks, sequence length
 //   scan          read offsets (rocPRIM) = the PackedReads CSR layout k_extract_scatter consumes
-//   k_fq_pack     one wave per record: base code | quality << 3
+//   k_fq_pack     one 16-lane group per record: base code | quality << 3
 // Errors are reported as the first failing record (atomicMin of record << 4 | kind, kinds as in
 // kcount_launch.hpp FQ_E_*), which is where the reference DIEs.
 #include <hip/hip_runtime.h>
@@ -92,17 +92,24 @@ __device__ __forceinline__ uint64_t rtrim_end(const char *s, uint64_t b, uint64_
   return e;
 }
 
-// get_fq_name's verdict (src/fastq.cpp:73-122) on the trimmed id line [b, e), which starts with '@'
+// get_fq_name's verdict (src/fastq.cpp:73-122) on the trimmed id line [b, e), which starts with '@'.
+// The header is scanned 16 bytes at a time (16 independent loads, then the tests) so that a lane waits for
+// one memory round trip per 16 characters instead of one per character.
 __device__ bool name_ok(const char *s, uint64_t b, uint64_t e) {
   const char *h = s + b + 1;
   const uint64_t len = rtrim_end(s, b + 1, e) - (b + 1);
   if (len < 3 || h[len - 2] == '/') return true;
   if (h[len - 2] == 'R') return true;  // HudsonAlpha @pair-R1 / @pair-R2
   uint64_t tab = len, sp = len;
-  for (uint64_t i = 0; i < len && tab == len; i++) {
-    const char c = h[i];
-    if (c == '\t') tab = i;
-    if (c == ' ' && sp == len) sp = i;
+  for (uint64_t i0 = 0; i0 < len && tab == len; i0 += 16) {
+    char v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) v[j] = i0 + j < len ? h[i0 + j] : 'x';
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      if (v[j] == '\t' && tab == len) tab = i0 + j;
+      if (v[j] == ' ' && sp == len) sp = i0 + j;
+    }
   }
   const uint64_t ep = tab < len ? tab : sp;  // first tab, else first space
   if (ep == len) return true;                // no comment
@@ -136,12 +143,17 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_records(const char *text, con
 #pragma unroll
   for (int i = 0; i < 4; i++)
     if (le[i] - lb[i] > FQ_MAX_LINE) return fq_fail(err, r, FQ_E_LONG);
-  const uint64_t ide = rtrim_end(text, lb[0], le[0]);
-  if (ide == lb[0] || text[lb[0]] != '@') return fq_fail(err, r, FQ_E_ID);
-  if (le[2] == lb[2] || text[lb[2]] != '+') return fq_fail(err, r, FQ_E_PLUS);
+  // the characters every record needs, loaded together (one memory round trip): first of the id and '+'
+  // lines, last of the id, sequence and quality lines (trailing whitespace is rare: trimmed further only then)
+  const unsigned char c_id = le[0] > lb[0] ? text[lb[0]] : 0, c_plus = le[2] > lb[2] ? text[lb[2]] : 0;
+  const unsigned char e_id = le[0] > lb[0] ? text[le[0] - 1] : 'x';
+  const unsigned char e_seq = le[1] > lb[1] ? text[le[1] - 1] : 'x', e_q = le[3] > lb[3] ? text[le[3] - 1] : 'x';
+  const uint64_t ide = fq_space(e_id) ? rtrim_end(text, lb[0], le[0] - 1) : le[0];
+  if (ide == lb[0] || c_id != '@') return fq_fail(err, r, FQ_E_ID);
+  if (c_plus != '+') return fq_fail(err, r, FQ_E_PLUS);
   if (!name_ok(text, lb[0], ide)) return fq_fail(err, r, FQ_E_NAME);
-  const uint64_t L = rtrim_end(text, lb[1], le[1]) - lb[1];
-  if (L != rtrim_end(text, lb[3], le[3]) - lb[3]) return fq_fail(err, r, FQ_E_LEN);
+  const uint64_t L = (fq_space(e_seq) ? rtrim_end(text, lb[1], le[1] - 1) : le[1]) - lb[1];
+  if (L != (fq_space(e_q) ? rtrim_end(text, lb[3], le[3] - 1) : le[3]) - lb[3]) return fq_fail(err, r, FQ_E_LEN);
   len[r] = L;
 }
 
@@ -159,23 +171,62 @@ __device__ __forceinline__ int base_code(unsigned char c) {
   return ((four >> i) & 1u) ? 4 : -1;
 }
 
+// One 16-lane group per record. A pass covers 256 bases: lane t packs the 4-byte runs t, t + 16, t + 32,
+// t + 48, each read as two aligned dwords joined with alignbyte (the text lines start at any byte), so a
+// lane issues up to 16 independent dword loads per pass. (Unaligned dwordx4 loads and stores, which
+// gfx950's unaligned-access mode allows, measured slower: 4.6 vs 3.2 ms at C2.) A dword that starts
+// inside the text is read whole: allocations are at least 4-byte granular.
+constexpr int FQ_GROUP = 16;
+__device__ __forceinline__ uint32_t load4(const char *text, uint32_t a) {
+  const uintptr_t p = (uintptr_t)(text + a);  // aligned in the address space, not relative to text
+  const uint32_t *w = (const uint32_t *)(p & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(p & 3u);
+  const uint32_t v0 = w[0];
+  if (sh == 0) return v0;
+  return __builtin_amdgcn_alignbyte(w[1], v0, sh);  // v_alignbyte_b32: ({w1, v0} >> 8 * sh)
+}
 __global__ __launch_bounds__(FQ_THREADS) void k_fq_pack(const char *text, const unsigned long long *line_end,
                                                          uint64_t n_rec, const unsigned long long *offs,
                                                          int qual_offset, uint8_t *out, unsigned long long *err) {
-  const uint64_t r = (uint64_t)blockIdx.x * (FQ_THREADS / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (r >= n_rec) return;
-  const uint64_t sb = line_end[4 * r] + 1, qb = line_end[4 * r + 2] + 1;
-  const uint64_t o = offs[r], L = offs[r + 1] - o;
+  const uint64_t r = (uint64_t)blockIdx.x * (FQ_THREADS / FQ_GROUP) + (threadIdx.x / FQ_GROUP);
+  const int gl = threadIdx.x % FQ_GROUP;
   bool bad = false;
-  for (uint64_t i = lane; i < L; i += 64) {
-    const int c = base_code((unsigned char)text[sb + i]);
-    int q = (int)(signed char)text[qb + i] - qual_offset;
-    q = q < 31 ? q : 31;
-    bad |= c < 0;
-    out[o + i] = (uint8_t)((c & 7) | (uint8_t)((unsigned)(unsigned char)q << 3));
+  if (r < n_rec) {
+    // 32-bit offsets inside a record (lines are at most FQ_MAX_LINE long): one 64-bit base per stream
+    const char *sp = text + line_end[4 * r] + 1, *qp = text + line_end[4 * r + 2] + 1;
+    const uint64_t o = offs[r];
+    uint8_t *dst = out + o;
+    const uint32_t L = (uint32_t)(offs[r + 1] - o);
+    for (uint32_t p0 = 0; p0 < L; p0 += 4 * FQ_GROUP * 4) {
+      uint32_t vs[4], vq[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t i = p0 + 4 * (gl + FQ_GROUP * u);
+        vs[u] = i < L ? load4(sp, i) : 0x41414141u;  // 'AAAA' past the end
+        vq[u] = i < L ? load4(qp, i) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t i = p0 + 4 * (gl + FQ_GROUP * u);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const bool in = i + j < L;
+          const int c = base_code(in ? (unsigned char)(vs[u] >> (8 * j)) : 'A');
+          int q = (int)(signed char)(vq[u] >> (8 * j)) - qual_offset;
+          q = q < 31 ? q : 31;
+          bad |= c < 0;
+          if (in) dst[i + j] = (uint8_t)((c & 7) | (uint8_t)((unsigned)(unsigned char)q << 3));
+        }
+      }
+    }
   }
-  if (__ballot(bad) && lane == 0) fq_fail(err, r, FQ_E_CHAR);
+  // groups of a wave hold consecutive records: the lowest bad record of the wave is reported (atomicMin)
+  const uint64_t bal = __ballot(bad);
+  if (bal && (threadIdx.x & 63) == 0) {
+    const int first_lane = __ffsll((long long)bal) - 1;
+    fq_fail(err, (uint64_t)blockIdx.x * (FQ_THREADS / FQ_GROUP) + ((threadIdx.x & ~63) + first_lane) / FQ_GROUP,
+            FQ_E_CHAR);
+  }
 }
 
 }  // namespace
@@ -215,7 +266,7 @@ hipError_t launch_fq_records(const char *text, const unsigned long long *line_en
 hipError_t launch_fq_pack(const char *text, const unsigned long long *line_end, uint64_t n_rec,
                           const unsigned long long *offs, int qual_offset, uint8_t *out, unsigned long long *err,
                           hipStream_t s) {
-  const uint64_t nb = (n_rec + FQ_THREADS / 64 - 1) / (FQ_THREADS / 64);
+  const uint64_t nb = (n_rec + FQ_THREADS / FQ_GROUP - 1) / (FQ_THREADS / FQ_GROUP);
   if (nb)
     hipLaunchKernelGGL(k_fq_pack, dim3((uint32_t)nb), dim3(FQ_THREADS), 0, s, text, line_end, n_rec, offs,
                        qual_offset, out, err);
