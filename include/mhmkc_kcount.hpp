@@ -165,6 +165,11 @@ class PackedReads {
     }
     offsets_.push_back(bytes_.size());
   }
+  // the reads packed on the device by mhmkc_add_fastq (HashTableInserter::fastq_packed_reads)
+  void assign(std::vector<uint8_t> bytes, std::vector<uint64_t> offsets) {
+    bytes_ = std::move(bytes);
+    offsets_ = std::move(offsets);
+  }
   int get_qual_offset() const { return qual_offset_; }
   int64_t get_local_num_reads() const { return (int64_t)offsets_.size() - 1; }
   const uint8_t *bytes() const { return bytes_.data(); }
@@ -240,6 +245,20 @@ class HashTableInserter {
   void add_packed_reads(const PackedReads &pr) {
     check(mhmkc_add_reads(h_, pr.bytes(), pr.offsets(), (uint64_t)pr.get_local_num_reads()), h_, "mhmkc_add_reads");
   }
+  // FASTQ text parsed and packed on the device (FastqReader + PackedRead, src/fastq.cpp:504-551,
+  // src/packed_reads.cpp:73-109), then counted; malformed input DIEs as the reference does
+  void add_fastq(const std::string &text) {
+    check(mhmkc_add_fastq(h_, text.data(), text.size()), h_, "mhmkc_add_fastq");
+  }
+  // the PackedReads of the last add_fastq, copied back (for a host that keeps them, as main.cpp does)
+  void fastq_packed_reads(PackedReads &pr) const {
+    uint64_t n_reads = 0, n_bases = 0;
+    check(mhmkc_fastq_packed(h_, nullptr, nullptr, &n_reads, &n_bases), h_, "mhmkc_fastq_packed");
+    std::vector<uint8_t> b(n_bases);
+    std::vector<uint64_t> o(n_reads + 1);
+    check(mhmkc_fastq_fetch(h_, b.data(), o.data()), h_, "mhmkc_fastq_fetch");
+    pr.assign(std::move(b), std::move(o));
+  }
   void flush_inserts() {
     if (seq_offs_.size() > 1) {
       check(mhmkc_add_seqs(h_, seq_buf_.data(), seq_offs_.data(), seq_offs_.size() - 1, 1), h_, "mhmkc_add_seqs");
@@ -297,6 +316,7 @@ class KmerDHT {
   void add_supermer(const std::string &seq, kmer_count_t count) { ht_inserter.insert_supermer(seq, count); }
   void init_ctg_kmers(int max_elems) { ht_inserter.init_ctg_kmers(max_elems); }  // kmer_dht.cpp:169-172
   void add_packed_reads(const PackedReads &pr) { ht_inserter.add_packed_reads(pr); }
+  void add_fastq(const std::string &text) { ht_inserter.add_fastq(text); }
   void flush_updates() { ht_inserter.flush_inserts(); }
   void finish_updates() { ht_inserter.insert_into_local_hashtable(local_kmers); }
   KmerCounts *get_local_kmer_counts(const Kmer<MAX_K> &kmer) {

@@ -5,9 +5,11 @@
 //   adapter_test reads <k> <seqqual.txt>  analyze_kmers over PackedReads
 //   adapter_test seqs  <k> <seqqual.txt>  SeqBlockInserter::process_seq over lowercase-masked strings
 //   adapter_test ctgs  <k> <seqqual.txt> <ctgs.txt>  analyze_kmers with a Contigs list ("SEQ DEPTH" lines)
+//   adapter_test fastq <k> <reads.fq>     FASTQ text through KmerDHT::add_fastq (device parse + pack)
 #include <algorithm>
 #include <fstream>
 #include <iostream>
+#include <iterator>
 #include <sstream>
 
 #include "mhmkc_kcount.hpp"
@@ -21,7 +23,7 @@ int run(const std::string &mode, int k, const std::string &path, const std::stri
   std::string line;
   PackedReads pr(33);
   std::vector<std::pair<std::string, std::string>> reads;
-  while (std::getline(in, line)) {
+  while (mode != "fastq" && std::getline(in, line)) {
     std::istringstream ss(line);
     std::string s, q;
     ss >> s >> q;
@@ -41,7 +43,16 @@ int run(const std::string &mode, int k, const std::string &path, const std::stri
       ctgs.push_back(c);
     }
   }
-  if (mode == "reads" || mode == "ctgs") {
+  if (mode == "fastq") {
+    std::ifstream fq(path, std::ios::binary);
+    std::string text((std::istreambuf_iterator<char>(fq)), std::istreambuf_iterator<char>());
+    dht.add_fastq(text);
+    PackedReads back(33);
+    dht.inserter().fastq_packed_reads(back);
+    std::cerr << "fastq reads " << back.get_local_num_reads() << "\n";
+    dht.flush_updates();
+    dht.finish_updates();
+  } else if (mode == "reads" || mode == "ctgs") {
     std::vector<PackedReads *> list{&pr};
     analyze_kmers<MAX_K>(k, 0, 33, list, 2, ctgs, dht, false);
   } else {

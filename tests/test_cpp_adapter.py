@@ -66,3 +66,25 @@ def test_adapter_contig_pass(k, tmp_path):
     out = subprocess.run([str(exe), "ctgs", str(k), str(reads), str(ctgs)], capture_output=True, text=True, check=True)
     exp = sorted(oracle_ctg_table(b, o, seqs, depths, k).lines())
     assert out.stdout.splitlines() == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [21, 63])
+def test_adapter_fastq(k, tmp_path):
+    """KmerDHT::add_fastq (FASTQ text -> device parse + pack -> count) equals the oracle's count of the oracle's
+    pack of the same text."""
+    import sys
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    from common import fastq_text, oracle_table, synth_set
+
+    exe = build(tmp_path)
+    b, o = synth_set(3000, 30000, 130 + k)
+    text = fastq_text(b, o, crlf_every=4, trailing_ws=True, iupac=True, seed=k)
+    fq = tmp_path / "reads.fq"
+    fq.write_bytes(text)
+    out = subprocess.run([str(exe), "fastq", str(k), str(fq)], capture_output=True, text=True, check=True)
+    assert "fastq reads 3000" in out.stderr
+    pb, po = O.fastq_pack(text)
+    assert out.stdout.splitlines() == sorted(oracle_table(pb, po, k).lines())
