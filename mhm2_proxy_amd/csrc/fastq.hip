@@ -171,11 +171,15 @@ __device__ __forceinline__ int base_code(unsigned char c) {
   return ((four >> i) & 1u) ? 4 : -1;
 }
 
-// One 16-lane group per record. A pass covers 256 bases: lane t packs the 4-byte runs t, t + 16, t + 32,
-// t + 48, each read as two aligned dwords joined with alignbyte (the text lines start at any byte), so a
-// lane issues up to 16 independent dword loads per pass. (Unaligned dwordx4 loads and stores, which
-// gfx950's unaligned-access mode allows, measured slower: 4.6 vs 3.2 ms at C2.) A dword that starts
-// inside the text is read whole: allocations are at least 4-byte granular.
+// One 16-lane group per record. The group walks the record in runs of 64 bases: lane t owns output
+// dword d = 16 * run + t. It reads bases [4d, 4d + 4) of the sequence and quality lines as two aligned
+// dwords joined with v_alignbyte (the text lines start at any byte), packs them into W_d, and writes the
+// ALIGNED output dword that holds record bytes [4d - s, 4d + 4 - s), s = the record's output misalignment:
+// the high s bytes of W_{d-1} (the next lower lane, row_shr:1 DPP; lane 0 takes the previous run's lane 15)
+// and the low 4 - s bytes of W_d. Only the record's first and last dwords, which it shares with its
+// neighbours, are written bytewise. (Unaligned dwordx4 loads and stores, which gfx950's unaligned-access
+// mode allows, measured slower: 4.6 ms vs 3.2 ms for byte stores at C2.) A dword that starts inside the
+// text is read whole: allocations are at least 4-byte granular.
 constexpr int FQ_GROUP = 16;
 __device__ __forceinline__ uint32_t load4(const char *text, uint32_t a) {
   const uintptr_t p = (uintptr_t)(text + a);  // aligned in the address space, not relative to text
@@ -185,39 +189,68 @@ __device__ __forceinline__ uint32_t load4(const char *text, uint32_t a) {
   if (sh == 0) return v0;
   return __builtin_amdgcn_alignbyte(w[1], v0, sh);  // v_alignbyte_b32: ({w1, v0} >> 8 * sh)
 }
+__device__ __forceinline__ uint32_t pack4(uint32_t vs, uint32_t vq, int n_valid, int qual_offset, bool &bad) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const bool in = j < n_valid;
+    const int c = base_code(in ? (unsigned char)(vs >> (8 * j)) : 'A');
+    int q = (int)(signed char)(vq >> (8 * j)) - qual_offset;
+    q = q < 31 ? q : 31;
+    bad |= c < 0;
+    const uint32_t byte = (uint32_t)(uint8_t)((c & 7) | (uint8_t)((unsigned)(unsigned char)q << 3));
+    w |= in ? byte << (8 * j) : 0u;
+  }
+  return w;
+}
 __global__ __launch_bounds__(FQ_THREADS) void k_fq_pack(const char *text, const unsigned long long *line_end,
                                                          uint64_t n_rec, const unsigned long long *offs,
                                                          int qual_offset, uint8_t *out, unsigned long long *err) {
   const uint64_t r = (uint64_t)blockIdx.x * (FQ_THREADS / FQ_GROUP) + (threadIdx.x / FQ_GROUP);
   const int gl = threadIdx.x % FQ_GROUP;
+  const int last_of_group = (threadIdx.x & 63 & ~(FQ_GROUP - 1)) + FQ_GROUP - 1;
   bool bad = false;
-  if (r < n_rec) {
+  // every lane of the wave takes part in the cross-lane moves: no early exit
+  const bool live = r < n_rec;
+  const char *sp = text, *qp = text;
+  uint8_t *dst = out;
+  int L = 0;
+  if (live) {
     // 32-bit offsets inside a record (lines are at most FQ_MAX_LINE long): one 64-bit base per stream
-    const char *sp = text + line_end[4 * r] + 1, *qp = text + line_end[4 * r + 2] + 1;
+    sp = text + line_end[4 * r] + 1;
+    qp = text + line_end[4 * r + 2] + 1;
     const uint64_t o = offs[r];
-    uint8_t *dst = out + o;
-    const uint32_t L = (uint32_t)(offs[r + 1] - o);
-    for (uint32_t p0 = 0; p0 < L; p0 += 4 * FQ_GROUP * 4) {
-      uint32_t vs[4], vq[4];
+    dst = out + o;
+    L = (int)(offs[r + 1] - o);
+  }
+  const int s = (int)((uintptr_t)dst & 3u);
+  uint32_t *const a0 = (uint32_t *)((uintptr_t)dst - (uintptr_t)s);  // aligned; dword d covers [4d - s, 4d + 4 - s)
+  // the group's runs: while the run's first aligned dword starts inside the record (uniform per wave: the
+  // longest record of the wave's groups decides, idle groups run with L = 0)
+  int wave_L = L;
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t i = p0 + 4 * (gl + FQ_GROUP * u);
-        vs[u] = i < L ? load4(sp, i) : 0x41414141u;  // 'AAAA' past the end
-        vq[u] = i < L ? load4(qp, i) : 0u;
-      }
+  for (int d = 16; d < 64; d <<= 1) wave_L = max(wave_L, __shfl_xor(wave_L, d, 64));
+  uint32_t carry = 0;  // W_{-1} of the next run's lane 0
+  // (hoisting the loads of 4 runs ahead of their use measured slower: 3.38 vs 3.09 ms at C2)
+  for (int base = 0; 4 * base - 3 < wave_L; base += FQ_GROUP) {
+    const int d = base + gl, i = 4 * d;
+    uint32_t vs = 0x41414141u, vq = 0;
+    if (i < L) {
+      vs = load4(sp, (uint32_t)i);
+      vq = load4(qp, (uint32_t)i);
+    }
+    const uint32_t w = pack4(vs, vq, min(4, L - i), qual_offset, bad);
+    // W_{d-1}: row_shr:1 within the 16-lane row; lane 0 of the row keeps 'old' = carry
+    const uint32_t wm = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)w, 0x111, 0xf, 0xf, false);
+    carry = (uint32_t)__shfl((int)w, last_of_group, 64);
+    const uint32_t ow = s ? __builtin_amdgcn_alignbyte(w, wm, 4 - s) : w;
+    const int x0 = i - s;  // record byte of the output dword's first byte
+    if (x0 >= 0 && x0 + 4 <= L) {
+      a0[d] = ow;
+    } else if (x0 < L && x0 + 4 > 0) {  // the record's first or last dword: only its own bytes
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t i = p0 + 4 * (gl + FQ_GROUP * u);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const bool in = i + j < L;
-          const int c = base_code(in ? (unsigned char)(vs[u] >> (8 * j)) : 'A');
-          int q = (int)(signed char)(vq[u] >> (8 * j)) - qual_offset;
-          q = q < 31 ? q : 31;
-          bad |= c < 0;
-          if (in) dst[i + j] = (uint8_t)((c & 7) | (uint8_t)((unsigned)(unsigned char)q << 3));
-        }
-      }
+      for (int j = 0; j < 4; j++)
+        if (x0 + j >= 0 && x0 + j < L) ((uint8_t *)(a0 + d))[j] = (uint8_t)(ow >> (8 * j));
     }
   }
   // groups of a wave hold consecutive records: the lowest bad record of the wave is reported (atomicMin)
