@@ -189,7 +189,25 @@ __device__ __forceinline__ uint32_t load4(const char *text, uint32_t a) {
   if (sh == 0) return v0;
   return __builtin_amdgcn_alignbyte(w[1], v0, sh);  // v_alignbyte_b32: ({w1, v0} >> 8 * sh)
 }
+// exact per-byte zero test: bit 7 of each byte of the result is set iff that byte of x is 0
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
 __device__ __forceinline__ uint32_t pack4(uint32_t vs, uint32_t vq, int n_valid, int qual_offset, bool &bad) {
+  // SWAR fast path: four A/C/G/T bases with qualities in [qual_offset, 0x7f]
+  const uint32_t acgt = zero_bytes(vs ^ 0x41414141u) | zero_bytes(vs ^ 0x43434343u) | zero_bytes(vs ^ 0x47474747u) |
+                        zero_bytes(vs ^ 0x54545454u);
+  const uint32_t qo = (uint32_t)qual_offset * 0x01010101u;
+  const bool q_ok = (vq & 0x80808080u) == 0 && (((vq | 0x80808080u) - qo) & 0x80808080u) == 0x80808080u;
+  if (n_valid >= 4 && acgt == 0x80808080u && q_ok) {
+    uint32_t code = (vs >> 1) & 0x03030303u;  // A 0, C 1, G 3, T 2
+    code ^= (code >> 1) & 0x01010101u;        // G 2, T 3
+    uint32_t x = vq - qo;                     // q - offset per byte, no borrows
+    uint32_t over = x & 0x60606060u;          // q - offset >= 32 (< 0x80): bit 5 or 6
+    over = ((over | (over >> 1)) >> 5) & 0x01010101u;
+    x = (x & ~(over * 0xffu)) | (over * 31u);  // min(q - offset, 31)
+    return code | (x << 3);
+  }
   uint32_t w = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
