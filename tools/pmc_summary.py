@@ -10,7 +10,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(lambda: collections.defaultdict(set))
 for f in sorted(glob.glob(f"gpurun_out/{tag}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mhm::", "")
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("mhm::", "")
         if name.startswith("__amd"):
             continue
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
