@@ -246,3 +246,32 @@ def test_gpu_fastq_device_text_large():
         st = cnt.stats()
     assert (go == o).all() and (gb == b).all()
     assert st["occurrences"] == st["count_sum"] == 400_000 * (150 - K - 1)
+
+
+@pytest.mark.gpu
+def test_gpu_fastq_ragged_reads():
+    """Reads of every length 0..150 (empty records are undefined behaviour in the reference's rtrim; both
+    sides read them as empty), all-N and low-quality reads: every output misalignment and partial dword of
+    k_fq_pack, against the oracle, then counted."""
+    import mhm2_proxy_amd as m
+    b, o = c.edge_case_set(seed=31, n=3000)
+    t = c.fastq_text(b, o, seed=3, crlf_every=7, iupac=True)
+    pb, po = O.fastq_pack(t)
+    assert (po == o).all() and (pb == b).all()
+    with m.KmerCounter(K, device=0) as cnt:
+        cnt.add_fastq(t)
+        gb, go = cnt.fastq_packed()
+        cnt.finish()
+        got = cnt.fetch().sorted()
+    assert (go == po).all() and (gb == pb).all()
+    keys, counts, left, right = O.kcount(pb, po, K).fetch()
+    assert (got.keys == keys).all() and (got.counts == counts).all()
+    assert (got.left == left).all() and (got.right == right).all()
+
+
+def test_oracle_fastq_ragged_reads():
+    b, o = c.edge_case_set(seed=31, n=600)
+    t = c.fastq_text(b, o, seed=3, crlf_every=7, iupac=True)
+    pb, po = O.fastq_pack(t)
+    lb, lo = literal_pack(t)
+    assert (po == o).all() and (pb == b).all() and (lo == o).all() and (lb == b).all()
