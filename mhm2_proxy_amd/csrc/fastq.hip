@@ -8,8 +8,9 @@
 // The text is HBM-resident; the pass is byte streaming:
 //   k_fq_count    newlines per 4 KB chunk (16 bytes per lane, SWAR zero-byte test)
 //   scan          chunk bases (rocPRIM)
-//   k_fq_lines    the position of every newline, in order (block scan of the lanes' counts)
-//   k_fq_records  one lane per 4-line record: trims, format checks, sequence length
+//   k_fq_lines    every newline, in order (block scan of the lanes' counts), as one word: position,
+//                 trailing whitespace of the line, first character of the next line
+//   k_fq_records  one lane per 4-line record: format checks and sequence length from the line words
 //   scan          read offsets (rocPRIM) = the PackedReads CSR layout k_extract_scatter consumes
 //   k_fq_pack     one 16-lane group per record: base code | quality << 3
 // Errors are reported as the first failing record (atomicMin of record << 4 | kind, kinds as in
@@ -61,13 +62,43 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_count(const char *text, uint6
   }
 }
 
+__device__ __forceinline__ bool fq_space(unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
+
+// 16 bytes of text from pos (zero past n), with the newline mask
+__device__ __forceinline__ uint32_t load16(const char *text, uint64_t pos, uint64_t n, uint32_t (&v)[4]) {
+  if (pos + FQ_BYTES <= n && (((uintptr_t)(text + pos)) & 15u) == 0) {
+    const uint4 q = *(const uint4 *)(text + pos);
+    v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (pos + 4 * i + j < n) x |= (uint32_t)(unsigned char)text[pos + 4 * i + j] << (8 * j);
+      v[i] = x;
+    }
+  }
+  uint32_t m = nl4(v[0]) | (nl4(v[1]) << 4) | (nl4(v[2]) << 8) | (nl4(v[3]) << 12);
+  if (pos + FQ_BYTES > n) m &= n > pos ? (1u << (n - pos)) - 1u : 0u;  // zero bytes past n are not newlines
+  return m;
+}
+__device__ __forceinline__ unsigned char byte_of(const uint32_t (&v)[4], int i) {
+  return (unsigned char)(v[i >> 2] >> (8 * (i & 3)));
+}
+
+// Per newline (line j ends at it), one word: its position (bits 0-39), the number of trailing whitespace
+// characters of line j (rtrim, src/fastq.cpp:67-71; bits 40-55) and the first character of line j + 1 (the
+// newline itself when that line is empty, 0 at the end of the text; bits 56-63). k_fq_records checks
+// records from these words instead of re-reading the text for them.
 __global__ __launch_bounds__(FQ_THREADS) void k_fq_lines(const char *text, uint64_t n,
                                                           const unsigned long long *chunk_base,
                                                           unsigned long long *line_end) {
   __shared__ uint32_t s_w[FQ_THREADS / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t pos = (uint64_t)blockIdx.x * FQ_CHUNK + (uint64_t)threadIdx.x * FQ_BYTES;
-  uint32_t m = nl_mask(text, pos, n);
+  uint32_t v[4];
+  uint32_t m = load16(text, pos, n, v);
   const uint32_t c = __popc(m);
   uint32_t incl = c;
   for (int d = 1; d < 64; d <<= 1) {
@@ -78,14 +109,31 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_lines(const char *text, uint6
   __syncthreads();
   uint64_t o = chunk_base[blockIdx.x] + (incl - c);
   for (int w = 0; w < wid; w++) o += s_w[w];
+  // the neighbouring lanes' edge bytes (the byte before this lane's 16 and the byte after them), so that
+  // only the wave's edge lanes go to memory for them
+  const uint32_t prev_w = __shfl_up(v[3], 1, 64), next_w = __shfl_down(v[0], 1, 64);
   while (m) {
     const int b = __ffs(m) - 1;
     m &= m - 1;
-    line_end[o++] = pos + (uint64_t)b;
+    const uint64_t p = pos + (uint64_t)b;
+    const unsigned nf = b < FQ_BYTES - 1 ? byte_of(v, b + 1)
+                    : lane < 63       ? (unsigned char)next_w
+                                      : (p + 1 < n ? (unsigned char)text[p + 1] : 0);
+    // trailing whitespace of the line that ends at p: back from p - 1 to the previous newline or the start
+    uint32_t t = 0;
+    int64_t q = (int64_t)p - 1;
+    while (q >= 0 && t < 0xffffu) {
+      const unsigned char ch = q >= (int64_t)pos                      ? byte_of(v, (int)(q - (int64_t)pos))
+                               : (q == (int64_t)pos - 1 && lane > 0) ? (unsigned char)(prev_w >> 24)
+                                                                      : (unsigned char)text[q];
+      if (ch == '\n' || !fq_space(ch)) break;
+      t++;
+      q--;
+    }
+    line_end[o] = p | ((uint64_t)t << FQ_LE_BITS) | ((uint64_t)nf << 56);
+    o++;
   }
 }
-
-__device__ __forceinline__ bool fq_space(unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r'); }
 
 __device__ __forceinline__ uint64_t rtrim_end(const char *s, uint64_t b, uint64_t e) {
   while (e > b && fq_space((unsigned char)s[e - 1])) e--;
@@ -123,37 +171,37 @@ __device__ __forceinline__ void fq_fail(unsigned long long *err, uint64_t r, int
   atomicMin(err, ((unsigned long long)r << 4) | (unsigned long long)kind);
 }
 
-__global__ __launch_bounds__(FQ_THREADS) void k_fq_records(const char *text, const unsigned long long *line_end,
-                                                            uint64_t n_rec, unsigned long long *len,
-                                                            unsigned long long *err) {
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_records(const char *text, uint64_t n,
+                                                            const unsigned long long *line_end, uint64_t n_rec,
+                                                            unsigned long long *len, unsigned long long *err) {
   const uint64_t r = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x;
   if (r > n_rec) return;
   if (r == n_rec) {  // the scan's last element: offs[n_rec] = total
     len[r] = 0;
     return;
   }
-  uint64_t lb[4], le[4];
+  uint64_t lw[5], lb[4], le[4], te[4];
+#pragma unroll
+  for (int i = 0; i < 5; i++) lw[i] = (4 * r + i) ? line_end[4 * r + i - 1] : 0;  // lw[i]: the word ending line 4r+i-1
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const uint64_t j = 4 * r + i;
-    lb[i] = j ? line_end[j - 1] + 1 : 0;
-    le[i] = line_end[j];
+    lb[i] = (4 * r + i) ? (lw[i] & FQ_LE_MASK) + 1 : 0;
+    le[i] = lw[i + 1] & FQ_LE_MASK;
+    // a last line without a newline (end = n, set by the host) has no metadata of its own
+    te[i] = le[i] == n ? rtrim_end(text, lb[i], le[i]) : le[i] - ((lw[i + 1] >> FQ_LE_BITS) & 0xffffu);
   }
   len[r] = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++)
     if (le[i] - lb[i] > FQ_MAX_LINE) return fq_fail(err, r, FQ_E_LONG);
-  // the characters every record needs, loaded together (one memory round trip): first of the id and '+'
-  // lines, last of the id, sequence and quality lines (trailing whitespace is rare: trimmed further only then)
-  const unsigned char c_id = le[0] > lb[0] ? text[lb[0]] : 0, c_plus = le[2] > lb[2] ? text[lb[2]] : 0;
-  const unsigned char e_id = le[0] > lb[0] ? text[le[0] - 1] : 'x';
-  const unsigned char e_seq = le[1] > lb[1] ? text[le[1] - 1] : 'x', e_q = le[3] > lb[3] ? text[le[3] - 1] : 'x';
-  const uint64_t ide = fq_space(e_id) ? rtrim_end(text, lb[0], le[0] - 1) : le[0];
-  if (ide == lb[0] || c_id != '@') return fq_fail(err, r, FQ_E_ID);
-  if (c_plus != '+') return fq_fail(err, r, FQ_E_PLUS);
-  if (!name_ok(text, lb[0], ide)) return fq_fail(err, r, FQ_E_NAME);
-  const uint64_t L = (fq_space(e_seq) ? rtrim_end(text, lb[1], le[1] - 1) : le[1]) - lb[1];
-  if (L != (fq_space(e_q) ? rtrim_end(text, lb[3], le[3] - 1) : le[3]) - lb[3]) return fq_fail(err, r, FQ_E_LEN);
+  // first characters of the id and '+' lines (the following newline when a line is empty)
+  const unsigned char c_id = r ? (unsigned char)(lw[0] >> 56) : (n ? (unsigned char)text[0] : 0);
+  const unsigned char c_plus = (unsigned char)(lw[2] >> 56);
+  if (te[0] == lb[0] || c_id != '@') return fq_fail(err, r, FQ_E_ID);
+  if (le[2] == lb[2] || c_plus != '+') return fq_fail(err, r, FQ_E_PLUS);
+  if (!name_ok(text, lb[0], te[0])) return fq_fail(err, r, FQ_E_NAME);
+  const uint64_t L = te[1] - lb[1];
+  if (L != te[3] - lb[3]) return fq_fail(err, r, FQ_E_LEN);
   len[r] = L;
 }
 
@@ -235,8 +283,8 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pack(const char *text, const 
   int L = 0;
   if (live) {
     // 32-bit offsets inside a record (lines are at most FQ_MAX_LINE long): one 64-bit base per stream
-    sp = text + line_end[4 * r] + 1;
-    qp = text + line_end[4 * r + 2] + 1;
+    sp = text + (line_end[4 * r] & FQ_LE_MASK) + 1;
+    qp = text + (line_end[4 * r + 2] & FQ_LE_MASK) + 1;
     const uint64_t o = offs[r];
     dst = out + o;
     L = (int)(offs[r + 1] - o);
@@ -307,10 +355,10 @@ hipError_t launch_fq_lines(const char *text, uint64_t n, const unsigned long lon
   return hipGetLastError();
 }
 
-hipError_t launch_fq_records(const char *text, const unsigned long long *line_end, uint64_t n_rec,
+hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_rec,
                              unsigned long long *len, unsigned long long *err, hipStream_t s) {
   const uint64_t nb = (n_rec + 1 + FQ_THREADS - 1) / FQ_THREADS;
-  hipLaunchKernelGGL(k_fq_records, dim3((uint32_t)nb), dim3(FQ_THREADS), 0, s, text, line_end, n_rec, len, err);
+  hipLaunchKernelGGL(k_fq_records, dim3((uint32_t)nb), dim3(FQ_THREADS), 0, s, text, n, line_end, n_rec, len, err);
   return hipGetLastError();
 }
 

@@ -217,12 +217,15 @@ hipError_t fq_scan(void *tmp, size_t tmp_bytes, const unsigned long long *in, un
                    uint64_t n_items, hipStream_t s);
 // newlines per FQ_CHUNK chunk -> chunk[ceil(n / FQ_CHUNK)]
 hipError_t launch_fq_count(const char *text, uint64_t n, unsigned long long *chunk, hipStream_t s);
-// position of every newline, in order, from the scanned chunk counts
+// every newline, in order, from the scanned chunk counts, as one word per line: position (bits 0-39),
+// trailing whitespace count of the line it ends (bits 40-55), first character of the next line (56-63)
+constexpr int FQ_LE_BITS = 40;
+constexpr uint64_t FQ_LE_MASK = (1ull << FQ_LE_BITS) - 1;
 hipError_t launch_fq_lines(const char *text, uint64_t n, const unsigned long long *chunk_base,
                            unsigned long long *line_end, hipStream_t s);
 // per record: sequence length (len[n_rec] = 0 for the scan) and format checks (err: atomicMin of
 // record << 4 | FQ_E_*)
-hipError_t launch_fq_records(const char *text, const unsigned long long *line_end, uint64_t n_rec,
+hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_rec,
                              unsigned long long *len, unsigned long long *err, hipStream_t s);
 hipError_t launch_fq_pack(const char *text, const unsigned long long *line_end, uint64_t n_rec,
                           const unsigned long long *offs, int qual_offset, uint8_t *out, unsigned long long *err,

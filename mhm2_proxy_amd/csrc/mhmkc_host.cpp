@@ -951,6 +951,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n) {
   if (rc) return rc;
   fq_reads = fq_bases = 0;
   if (n == 0) return MHMKC_OK;
+  if (n > mhm::FQ_LE_MASK) return fail(MHMKC_EINVAL, "FASTQ text larger than 2^40 bytes in one call");
   hipError_t e;
   const uint64_t nch = (n + mhm::FQ_CHUNK - 1) / mhm::FQ_CHUNK;
   if ((e = d_fq_chunk.ensure((nch + 1) * 16)) != hipSuccess) return hip_fail(e, "fastq chunk counts");
@@ -988,7 +989,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n) {
   e = mhm::launch_fq_lines(d_text, n, cbase, lend, stream);
   if (e == hipSuccess && last != '\n') e = hipMemcpyAsync(lend + lines - 1, &n_end, 8, hipMemcpyHostToDevice, stream);
   if (e == hipSuccess) e = hipMemsetAsync(err_d, 0xff, 8, stream);
-  if (e == hipSuccess) e = mhm::launch_fq_records(d_text, lend, R, len, err_d, stream);
+  if (e == hipSuccess) e = mhm::launch_fq_records(d_text, n, lend, R, len, err_d, stream);
   if (e == hipSuccess) e = mhm::fq_scan(d_fq_tmp.p, tmp_bytes, len, offs, R + 1, stream);
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "fastq records");
