@@ -7,11 +7,17 @@
 A step = one full counting round of this rank's resident read shard: extract -> coarse partition ->
 RCCL all-to-all (N > 1) -> fine partition -> LDS hash-table count -> finalize + compacted output table,
 i.e. mhmkc_add_reads_device + mhmkc_finish. Reads are already in HBM when the timed region starts.
-Workload (weak scaling): configs[1] of BASELINE.json per GPU — 10M synthetic 150 bp reads per GPU, genome
-50 Mbp x N (30x coverage), k = 21. value = counted k-mer occurrences of all ranks / max-over-ranks time.
+Workloads (--config):
+  C2 (default): configs[1] of BASELINE.json per GPU — 10M synthetic 150 bp reads per GPU, genome 50 Mbp x N
+      (30x coverage), seed 2, k = 21 (weak scaling: the driver's N = 1, 2, 4, 8 lines);
+  C3: configs[2] — 100M reads in total over the N GPUs (100M / N each), genome 500 Mbp, seed 3, k = 21;
+  C4: configs[3] — C3 at k = 63.
+value = counted k-mer occurrences of all ranks / max-over-ranks time.
 
-Extra JSON fields: roofline (dominant kernel, algorithmic bytes / its HIP-event time), cpu_baseline (the
-CPU oracle on a bounded sample, rank 0 at N = 1), stages (per-stage device ms per step).
+Extra JSON fields: roofline (dominant kernel: the LDS time floor of its op mix against its HIP-event time,
+with its HBM figures beside it), cpu_baseline (the multi-threaded CPU restatement on a bounded sample,
+rank 0 at N = 1), stages (per-stage device ms per step), h2d_inclusive (the same step from reads in pinned
+host memory: chunked H2D overlapped with extraction), d2h_fetch (copying the finished table to the host).
 """
 from __future__ import annotations
 
@@ -26,6 +32,15 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# Random-address LDS throughput on MI355X, whole chip, lane-ops/s (tools/micro/lds_atomics.hip,
+# profiles/r01_lds_microbench.txt): the cost model of k_count's LDS floor.
+LDS_RATE = {"ds_read_b128": 1593.28e9, "ds_add_u32": 5507.50e9, "ds_cmpst_rtn_b32": 3347.90e9,
+            "ds_read_b64": 5656.04e9, "ds_write_b32": 6066.34e9}
+CONFIGS = {  # reads in total (None: per GPU), genome (per GPU for C2), seed, k
+    "C2": dict(reads_per_gpu=10_000_000, reads_total=None, genome=50_000_000, genome_scales=True, seed=2, k=21),
+    "C3": dict(reads_per_gpu=None, reads_total=100_000_000, genome=500_000_000, genome_scales=False, seed=3, k=21),
+    "C4": dict(reads_per_gpu=None, reads_total=100_000_000, genome=500_000_000, genome_scales=False, seed=3, k=63),
+}
 
 
 def parse():
@@ -33,13 +48,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--k", type=int, default=21)
-    ap.add_argument("--reads-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="C2")
+    ap.add_argument("--k", type=int, default=None, help="override the config's k")
+    ap.add_argument("--reads-per-gpu", type=int, default=None, help="override (C2: reads per GPU)")
+    ap.add_argument("--reads-total", type=int, default=None, help="override (C3/C4: reads over all GPUs)")
     ap.add_argument("--read-len", type=int, default=150)
-    ap.add_argument("--genome-per-gpu", type=int, default=50_000_000)
-    ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--cpu-sample-reads", type=int, default=400_000)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--h2d-steps", type=int, default=3, help="steps of the H2D-inclusive leg (0: skip)")
     ap.add_argument("--input", choices=("packed", "fastq"), default="packed",
                     help="packed: PackedRead bytes in HBM (the headline); fastq: FASTQ text in HBM, parsed and "
                          "packed on the device inside every step (mhmkc_add_fastq_device)")
@@ -61,8 +79,24 @@ def algorithmic_bytes(stage: str, st: dict, k: int) -> float:
         "part_hist": owned * rec,
         "part_scatter": owned * (rec + frec),
         "count": owned * frec + out,
-        "exchange": st["bytes_sent"],
+        "exchange": st["bytes_sent"] + st.get("bytes_recv", 0),
     }.get(stage, 0.0)
+
+
+def lds_floor_seconds(st: dict, k: int) -> tuple:
+    """k_count's LDS time floor: its table operations priced at the measured whole-chip
+    random-address LDS rates. Per record: the home-group read (one ds_read_b128 of four 32-bit keys; two for
+    64-bit keys) and the count add; per extension add one ds_add; per phase-B record (not in its home group)
+    one more group read, a CAS and a miss-list write + read. Returns (seconds, LDS bytes)."""
+    nl = k // 32 + 1
+    g_reads = 1 if st["fine_record_bytes"] == 4 else 2 * nl  # b128 reads per group lookup
+    recs, miss, ext = st["owned_records"], st["lds_misses"], st["lds_ext_adds"]
+    r = LDS_RATE
+    t = (recs * (g_reads / r["ds_read_b128"] + 1 / r["ds_add_u32"]) + ext / r["ds_add_u32"] +
+         miss * (g_reads / r["ds_read_b128"] + 1 / r["ds_cmpst_rtn_b32"] + 2 * nl / r["ds_write_b32"] +
+                 nl / r["ds_read_b64"]))
+    b = recs * (16 * g_reads + 4) + ext * 4 + miss * (16 * g_reads + 4 + 16 * nl)
+    return t, b
 
 
 def survey_model_bytes(st: dict, k: int, n_reads: int, read_len: int) -> float:
@@ -96,19 +130,20 @@ def fastq_text(b, o, read_len: int):
     return t.reshape(-1)
 
 
-def cpu_baseline(b, o, k, n_reads):
-    """The CPU oracle (oracle/kcount_oracle.c, single thread) on the first n_reads reads."""
+def cpu_baseline(b, o, k, n_reads, threads):
+    """The CPU restatement (oracle/kcount_mt.c: the reference's read-pass rules, hash-partitioned over T
+    threads like the reference's ranks) timed on this host on the first n_reads reads."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as O
 
     n = min(n_reads, o.size - 1)
     bb, oo = b[: int(o[n])], o[: n + 1]
     t0 = time.perf_counter()
-    t = O.kcount(bb, oo, k)
+    t = O.kcount_mt(bb, oo, k, threads=threads)
     dt = time.perf_counter() - t0
     occ = t.stats()["occurrences"]
-    return {"value": occ / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} reads of this rank's C2 shard ({occ} k-mers), oracle/kcount_oracle.c, 1 thread, "
+    return {"value": occ / dt, "unit": "k-mers/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} reads of this rank's shard ({occ} k-mers), oracle/kcount_mt.c, {threads} threads, "
                       f"{dt:.1f} s"}
 
 
@@ -134,23 +169,35 @@ def main():
 
     import mhm2_proxy_amd as m
 
-    k, L, R = args.k, args.read_len, args.reads_per_gpu
-    G = args.genome_per_gpu * world
+    cf = dict(CONFIGS[args.config])
+    k = args.k or cf["k"]
+    seed = args.seed if args.seed is not None else cf["seed"]
+    L = args.read_len
+    if args.reads_total or cf["reads_total"]:
+        total = args.reads_total or cf["reads_total"]
+        first, R = total * rank // world, total * (rank + 1) // world - total * rank // world
+        G = cf["genome"]
+    else:
+        R = args.reads_per_gpu or cf["reads_per_gpu"]
+        total, first = R * world, rank * R
+        G = cf["genome"] * world
     threads = max(1, min(16, (os.cpu_count() or 8) // max(1, world)))
     t0 = time.perf_counter()
-    genome = m.synth_genome(G, args.seed)
-    b, o = m.synth_reads(genome, R, L, args.seed, first_read=rank * R, threads=threads)
+    genome = m.synth_genome(G, seed)
+    b, o = m.synth_reads(genome, R, L, seed, first_read=first, threads=threads)
     del genome
     gen_s = time.perf_counter() - t0
     dev = torch.device("cuda", local)
     if args.input == "fastq":
         text = fastq_text(b, o, L)
-        tt = torch.from_numpy(text).to(dev)
+        tt = torch.zeros(int(text.size) + 16, dtype=torch.uint8, device=dev)  # 4+ bytes of padding (mhmkc.h)
+        tt[: text.size].copy_(torch.from_numpy(text))
         text_bytes = int(text.size)
         del text
     else:
         bt = torch.from_numpy(b).to(dev)
         ot = torch.from_numpy(o.view(np.int64)).to(dev)
+    n_bases = int(o[-1])
     torch.cuda.synchronize()
 
     cid = None
@@ -164,9 +211,9 @@ def main():
     def step():
         counter.reset()
         if args.input == "fastq":
-            counter.add_fastq_tensor(tt)
+            counter.add_fastq_tensor(tt, n_bytes=text_bytes)
         else:
-            counter.add_tensors(bt, ot)
+            counter.add_tensors(bt, ot, n_bases=n_bases)
         counter.finish()
 
     for _ in range(args.warmup):
@@ -183,9 +230,9 @@ def main():
         step()
         st = counter.stats()
         occ_total += st["occurrences"]
-        for s, v in st["ms_kernel"].items():
-            stage_ms[s] = stage_ms.get(s, 0.0) + v
-            launches[s] = launches.get(s, 0) + st["launches"][s]
+        for s_, v in st["ms_kernel"].items():
+            stage_ms[s_] = stage_ms.get(s_, 0.0) + v
+            launches[s_] = launches.get(s_, 0) + st["launches"][s_]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -200,31 +247,90 @@ def main():
 
     value = occ_total / elapsed
     steps = max(1, args.steps)
-    per_step = {s: v / steps for s, v in stage_ms.items()}
-    dom = max((s for s in per_step if s not in ("other", "tileidx")), key=lambda s: per_step[s], default=None)
+    per_step = {s_: v / steps for s_, v in stage_ms.items()}
+    dom = max((s_ for s_ in per_step if s_ not in ("other", "tileidx")), key=lambda s_: per_step[s_], default=None)
     roofline = None
+    pmc = {}
+    if Path(args.pmc_json).exists():
+        try:
+            pmc = json.loads(Path(args.pmc_json).read_text())
+        except Exception:
+            pmc = {}
     if dom and launches.get(dom):
         ms_launch = stage_ms[dom] / launches[dom]
         alg = algorithmic_bytes(dom, st, k) / max(1, launches[dom] // steps)
-        achieved = alg / (ms_launch * 1e-3) / 1e9
-        traffic = None
-        pmc = Path(args.pmc_json)
-        if pmc.exists():
-            try:
-                traffic = json.loads(pmc.read_text()).get("per_launch_bytes", {}).get(dom)
-            except Exception:
-                traffic = None
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "algorithmic_bytes": int(alg), "avg_launch_ms": round(ms_launch, 4)}
+        hbm = {"achieved": round(alg / (ms_launch * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+               "frac": round(alg / (ms_launch * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "algorithmic_bytes": int(alg)}
+        traffic = pmc.get("per_launch_bytes", {}).get(dom)
+        if dom == "count":
+            # k_count keeps its hash table in LDS and is bound there: the roofline is its LDS
+            # time floor at the measured random-access LDS rates; achieved / peak are the LDS bytes of its
+            # table operations over the measured time / over that floor
+            t_floor, lds_b = lds_floor_seconds(st, k)
+            roofline = {"bound": "lds", "kernel": "k_count", "achieved": round(lds_b / (ms_launch * 1e-3) / 1e12, 3),
+                        "peak": round(lds_b / t_floor / 1e12, 3), "unit": "TB/s",
+                        "frac": round(t_floor / (ms_launch * 1e-3), 4), "traffic": traffic,
+                        "traffic_source": pmc.get("source"), "avg_launch_ms": round(ms_launch, 4),
+                        "lds_floor_ms": round(t_floor * 1e3, 4),
+                        "lds_ops": {"records": st["owned_records"], "phase_b_records": st["lds_misses"],
+                                    "ext_adds": st["lds_ext_adds"]},
+                        "hbm": hbm}
+        else:
+            roofline = {"bound": "hbm", "kernel": dom, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": hbm["frac"], "traffic": traffic, "traffic_source": pmc.get("source"),
+                        "algorithmic_bytes": int(alg), "avg_launch_ms": round(ms_launch, 4)}
+
+    # D2H of the finished table (the KmerMap fill starts from it)
+    t1 = time.perf_counter()
+    table = counter.fetch()
+    d2h_ms = (time.perf_counter() - t1) * 1e3
+    d2h = {"ms": round(d2h_ms, 2), "rows": len(table), "bytes": int(len(table) * (8 * counter.n_longs + 4)),
+           "GBps": round(len(table) * (8 * counter.n_longs + 4) / (d2h_ms * 1e-3) / 1e9, 2) if d2h_ms else None}
+    del table
+
+    # the same step from reads in pinned host memory: chunked H2D on a copy stream, each chunk extracted as
+    # soon as it lands (mhmkc_add_reads); the timed region starts at the first H2D
+    h2d = None
+    if args.h2d_steps and args.input == "packed":
+        hb = torch.from_numpy(b).pin_memory().numpy()
+        ho = torch.from_numpy(o.view(np.int64)).pin_memory().numpy().view(np.uint64)
+        counter.set_profiling(False)
+        ts, h2d_ms = [], []
+        for i in range(args.h2d_steps + 1):
+            if dist:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            counter.reset()
+            counter.add_packed_reads(hb, ho)
+            counter.finish()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t1
+            if dist:
+                tt_ = torch.tensor([dt], dtype=torch.float64, device=dev)
+                dist.all_reduce(tt_, op=dist.ReduceOp.MAX)
+                dt = float(tt_.item())
+            if i:  # the first is a warm-up (pinned staging, chunk events)
+                ts.append(dt)
+                h2d_ms.append(counter.stats()["ms_h2d"])
+        tmed = sorted(ts)[len(ts) // 2]
+        stt = counter.stats()
+        hbytes = stt["h2d_bytes"]
+        h2d = {"value": round(occ_total / steps * 1.0 / tmed, 1), "unit": "k-mers/s", "ms_per_step": round(tmed * 1e3, 3),
+               "h2d_ms": round(sorted(h2d_ms)[len(h2d_ms) // 2], 3), "h2d_bytes_per_gpu": int(hbytes),
+               "h2d_GBps": round(hbytes / (sorted(h2d_ms)[len(h2d_ms) // 2] * 1e-3) / 1e9, 1) if h2d_ms[0] else None,
+               "chunks": int(stt["h2d_chunks"]), "steps": len(ts),
+               "input": "PackedRead bytes + offsets in pinned host memory (torch pin_memory)"}
+        del hb, ho
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(b, o, k, args.cpu_sample_reads)
+        cpu = cpu_baseline(b, o, k, args.cpu_sample_reads, args.cpu_threads)
 
     if rank == 0:
+        launched = [s_ for s_ in per_step if launches.get(s_)]
         line = {
-            "metric": f"k-mers/s (whole node), k={args.k} {args.read_len}bp reads",
+            "metric": f"k-mers/s (whole node), k={k} {L}bp reads",
             "value": round(value, 1),
             "unit": "k-mers/s",
             "n_gpus": world,
@@ -232,25 +338,30 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.config == "C2" else "strong",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (SURVEY.md §8(d) generator: splitmix64 genome + reads, 0.5% subst, 0.02% N, 2% Q10)",
-            "config": {"workload": f"C2 per GPU: {R} x {L}bp synthetic reads/GPU, k={k}, genome {G} bp "
-                                   f"(30x), seed {args.seed}", "k": k, "reads_per_gpu": R, "read_len": L,
-                       "genome_len": G, "occurrences_per_step": occ_total // steps, "parallelism": f"hash-range x{world}"},
+            "config": {"workload": (f"{args.config}: {total} x {L}bp synthetic reads ({R} on rank 0), k={k}, genome "
+                                    f"{G} bp, seed {seed}"),
+                       "k": k, "reads_total": total, "reads_per_gpu": R, "read_len": L, "genome_len": G,
+                       "occurrences_per_step": occ_total // steps, "parallelism": f"hash-range x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "stages_ms_per_step": {s: round(v, 3) for s, v in per_step.items()},
+            "stages_ms_per_step": {s_: round(v, 3) for s_, v in per_step.items() if launches.get(s_)},
             "achieved_alg_GBps_whole_step": round(
-                sum(algorithmic_bytes(s, st, k) for s in per_step) / (elapsed / steps) / 1e9, 1) if st else None,
+                sum(algorithmic_bytes(s_, st, k) * launches[s_] / steps for s_ in launched) / (elapsed / steps) / 1e9,
+                1) if st else None,
             "survey_model": {
                 "bytes_per_step_per_gpu": int(survey_model_bytes(st, k, R, L)),
                 "GBps_per_gpu": round(survey_model_bytes(st, k, R, L) / (elapsed / steps) / 1e9, 1),
                 "frac_of_hbm_peak": round(survey_model_bytes(st, k, R, L) / (elapsed / steps) / 1e9 / HBM_PEAK_GBPS, 4),
             } if st else None,
+            "h2d_inclusive": h2d,
+            "d2h_fetch": d2h,
             "distinct_per_gpu": st["distinct"] if st else None,
             "n_out_per_gpu": st["n_out"] if st else None,
+            "bytes_sent_rank0": st["bytes_sent"] if st else None,
             "synth_seconds": round(gen_s, 2),
         }
         if args.input == "fastq":

@@ -16,10 +16,14 @@
  *   - every function returns MHMKC_OK (0) or a negative MHMKC_E* code; mhmkc_last_error() holds the
  *     message; the C++ adapter turns a failure into a fatal error like the reference's DIE;
  *   - host input buffers are borrowed only for the duration of the call;
- *   - device input buffers passed to *_device functions must stay valid until mhmkc_finish returns;
+ *   - device input buffers passed to *_device functions must stay valid until mhmkc_finish returns, and
+ *     are read on the handle's stream: data written on another stream must be ordered first with
+ *     mhmkc_wait_stream (or by creating the handle on that stream, mhmkc_config.stream);
  *   - a handle drives exactly one GPU and is not thread-safe. Multi-GPU = one process (rank) per
- *     GPU, all ranks calling the same sequence; the k-mer exchange is an RCCL all-to-all inside
- *     mhmkc_finish (replacing the UPC++ supermer store, src/kcount/kmer_dht.cpp:133-149,222-224).
+ *     GPU, all ranks calling the same sequence; the k-mer exchange is an all-to-all inside mhmkc_finish
+ *     (replacing the UPC++ supermer store, src/kcount/kmer_dht.cpp:133-149,222-224): RCCL over xGMI
+ *     (mhmkc_config.comm_id), or a host-staged transport the caller provides (mhmkc_set_transport: a
+ *     UPC++/MPI/gloo host, several nodes, or several ranks sharing one GPU).
  */
 #ifndef MHMKC_H
 #define MHMKC_H
@@ -31,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 4
+#define MHMKC_ABI_VERSION 5
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -42,7 +46,8 @@ enum {
   MHMKC_ERCCL = -4,       /* RCCL error */
   MHMKC_ESTATE = -5,      /* call out of order (e.g. fetch before finish) */
   MHMKC_EBADCHAR = -6,    /* input byte outside the PackedRead code range (reference DIE, kcount_cpu.cpp:453-458) */
-  MHMKC_EUNSUPPORTED = -7 /* valid for the reference but not supported here */
+  MHMKC_EUNSUPPORTED = -7, /* valid for the reference but not supported here */
+  MHMKC_ETRANSPORT = -8    /* a mhmkc_set_transport callback failed, or none was set where needed */
 };
 
 typedef struct mhmkc *mhmkc_t;
@@ -59,9 +64,20 @@ typedef struct {
   int32_t device;         /* HIP device ordinal; -1 = current device */
   int32_t rank;           /* this rank, 0 <= rank < n_ranks */
   int32_t n_ranks;        /* number of GPUs (ranks) sharing the k-mer space */
-  const uint8_t *comm_id; /* MHMKC_COMM_ID_BYTES from mhmkc_comm_id() on rank 0; NULL if n_ranks==1 */
+  const uint8_t *comm_id; /* MHMKC_COMM_ID_BYTES from mhmkc_comm_id() on rank 0; NULL if n_ranks==1 or
+                             the exchange goes through mhmkc_set_transport */
   void *stream;           /* hipStream_t to run on; NULL = the library creates its own */
+  int32_t output_owner;   /* MHMKC_OWNER_*: where a finished k-mer lives when n_ranks > 1 */
+  int32_t minimizer_len;  /* m of get_kmer_target_rank; 0 = the KmerDHT rule clamp(2k/3+1, 15, 27)
+                             (src/kcount/kmer_dht.cpp:114-116) */
 } mhmkc_config;
+
+enum {
+  MHMKC_OWNER_HASH = 0,      /* the counting partition (hash range): no extra exchange */
+  MHMKC_OWNER_MINIMIZER = 1  /* the reference's owner, KmerDHT::get_kmer_target_rank =
+                                minimizer_hash_fast(minimizer_len) % n_ranks (src/kcount/kmer_dht.cpp:193-196),
+                                which dbjg_traversal.cpp looks k-mers up on (:232-234,264-274) */
+};
 
 /* Statistics; replaces the SLOG lines of flush_inserts / insert_into_local_hashtable
  * (src/kcount/kcount_cpu.cpp:465-488,525-527). Counters are for this rank. */
@@ -87,6 +103,15 @@ typedef struct {
   double ms_total;         /* wall time of the last add_reads..finish sequence (device events) */
   double ms_kernel[8];     /* per-stage device time when profiling is on: see MHMKC_STAGE_* */
   uint64_t launches[8];    /* per-stage launch count when profiling is on */
+  uint64_t bytes_recv;     /* bytes received from other ranks in the exchange */
+  uint64_t handoff_sent;   /* finished k-mers moved to their MHMKC_OWNER_MINIMIZER owner (other ranks) */
+  uint64_t handoff_recv;   /* finished k-mers received from other ranks at the hand-off */
+  uint64_t h2d_bytes;      /* host bytes copied to the device by mhmkc_add_reads (PackedRead bytes + offsets) */
+  uint64_t h2d_chunks;     /* H2D chunks of mhmkc_add_reads, each extracted as soon as it has landed */
+  uint64_t slabs;          /* extracted record slabs (one per device batch or H2D chunk) */
+  double ms_h2d;           /* device time of the H2D copies of the last mhmkc_add_reads (copy-stream events) */
+  uint64_t lds_misses;     /* count kernel: records not found in their home slot group (LDS slow path) */
+  uint64_t lds_ext_adds;   /* count kernel: extension-counter increments */
 } mhmkc_stats;
 
 enum {
@@ -119,12 +144,20 @@ int mhmkc_comm_id(uint8_t out[MHMKC_COMM_ID_BYTES]);
  * bits 0-2 = A,C,G,T,N -> 0..4, bits 3-7 = min(q - qual_offset, 31). read_offsets has n_reads+1
  * entries, read_offsets[0] == 0, read i = bytes[read_offsets[i], read_offsets[i+1]).
  * Replaces the count_kmers read loop + SeqBlockInserter::process_seq
- * (src/kcount/kcount.cpp:54-98, src/kcount/kcount_cpu.cpp:73-103). Host buffers. */
+ * (src/kcount/kcount.cpp:54-98, src/kcount/kcount_cpu.cpp:73-103). Host buffers: copied to the device in
+ * chunks on a copy stream, each chunk extracted as soon as it has landed (pinned host memory, e.g. from
+ * hipHostMalloc, lets the copies run without the CPU). Returns once the copies are done. */
 int mhmkc_add_reads(mhmkc_t h, const uint8_t *packed_bytes, const uint64_t *read_offsets, uint64_t n_reads);
 
-/* Same, with device-resident buffers (no copy; must stay valid until mhmkc_finish returns). */
+/* Same, with device-resident buffers (no copy; must stay valid until mhmkc_finish returns). n_bases must be
+ * d_read_offsets[n_reads]; the offsets are checked on the device (MHMKC_EINVAL: not a PackedReads CSR). */
 int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_packed_bytes, const uint64_t *d_read_offsets,
                            uint64_t n_reads, uint64_t n_bases);
+
+/* Order the handle's later device work after everything enqueued so far on `stream` (a hipStream_t; NULL =
+ * the legacy default stream): call it before passing buffers that another stream (e.g. torch's current
+ * stream) has just written. */
+int mhmkc_wait_stream(mhmkc_t h, void *stream);
 
 /* Add sequences given as characters, lowercase = quality below the cutoff — the string that
  * SeqBlockInserter::process_seq receives (src/kcount/kcount.cpp:80-86). Host buffers. depth is the
@@ -143,7 +176,8 @@ int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *seq_offsets, uin
  * Host text of n_bytes bytes (no terminator needed). */
 int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes);
 
-/* Same, with device-resident text (only read during the call). */
+/* Same, with device-resident text (only read during the call). The buffer must extend at least 4 bytes
+ * past n_bytes (the parser reads whole aligned dwords; the padding bytes are never interpreted). */
 int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes);
 
 /* The PackedReads of the last mhmkc_add_fastq[_device] call on the device: d_bytes[n_bases] in the
@@ -161,11 +195,19 @@ int mhmkc_fastq_fetch(mhmkc_t h, uint8_t *bytes, uint64_t *offsets);
  * = quality as for reads; contigs are uppercase), seq_offsets: n_ctgs+1 offsets, depths:
  * Contig::get_uint16_t_depth() (src/contigs.hpp:65), 0 counting as 1. The contig pass runs inside
  * mhmkc_finish after every read, over the contigs in the order they were added (the reference's order,
- * which its rules depend on). Contigs shorter than k+2 contribute nothing. Host buffers. Single rank
- * (n_ranks == 1) in this version. */
+ * which its rules depend on). Contigs shorter than k+2 contribute nothing. Host buffers. With several ranks
+ * every rank passes its own contigs (possibly none) and the contigs of all ranks are applied in rank order
+ * (rank 0's first), one serialisation the reference's concurrent supermer stores can produce; the result
+ * equals a single rank given the concatenation. */
 int mhmkc_add_ctgs(mhmkc_t h, const char *seqs, const uint64_t *seq_offsets, const uint16_t *depths, uint64_t n_ctgs);
 
-/* Exchange (multi-GPU), count and finalize: purge count < 2 and X/X, choose extensions.
+/* The depth threshold of the finish: the reference's global _dmin_thres (src/kcount/kmer_dht.hpp:57), which
+ * analyze_kmers sets (src/kcount/kcount.cpp:145) after the KmerDHT was built and get_ext reads at finish
+ * (src/kcount/kcount_cpu.cpp:178). Starts as mhmkc_config.dmin_thres; takes effect at the next finish. */
+int mhmkc_set_dmin_thres(mhmkc_t h, int32_t dmin_thres);
+
+/* Exchange (multi-GPU), count and finalize: purge count < 2 and X/X, choose extensions; with
+ * MHMKC_OWNER_MINIMIZER, then move every finished k-mer to its get_kmer_target_rank owner.
  * Replaces KmerDHT::flush_updates + finish_updates -> HashTableInserter::insert_into_local_hashtable
  * (src/kcount/kmer_dht.cpp:227-236, src/kcount/kcount_cpu.cpp:490-528). *n_out may be NULL. */
 int mhmkc_finish(mhmkc_t h, uint64_t *n_out);
@@ -178,6 +220,26 @@ int mhmkc_fetch(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *r
 /* Device pointers of the finished table (valid until the next reset/destroy). */
 int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,
                         const char **d_right, uint64_t *n_out);
+
+/* Host-staged exchange between ranks (instead of RCCL): for n_ranks > 1 with comm_id == NULL, set before
+ * the first mhmkc_finish. Every rank's callbacks are called collectively, in the same order on all ranks, with
+ * host buffers; a callback returns 0 on success.
+ *   allgather: every rank contributes `bytes` bytes from send; recv receives n_ranks * bytes, rank order;
+ *   alltoallv: send holds, back to back in rank order, send_bytes[p] bytes for every rank p (0 for itself);
+ *              recv receives recv_bytes[p] bytes from every rank p, back to back in rank order.
+ * This is the seam a UPC++ / MPI host (several nodes, or several ranks sharing one GPU) plugs into; the
+ * reference's own transport is UPC++ RPC (src/kcount/kmer_dht.cpp:133-149,222-231). */
+typedef struct {
+  void *ctx;
+  int (*allgather)(void *ctx, const void *send, void *recv, uint64_t bytes);
+  int (*alltoallv)(void *ctx, const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes);
+} mhmkc_transport;
+int mhmkc_set_transport(mhmkc_t h, const mhmkc_transport *t);
+
+/* Kmer::minimizer_hash_fast(m) of n k-mers of the handle's k (src/kmer.cpp:344-393,454-463), computed on the
+ * handle's GPU: keys[n * n_longs] in Kmer::longs layout (host), hashes[n] (host). get_kmer_target_rank is
+ * hashes[i] % rank_n (src/kcount/kmer_dht.cpp:193-196). m = 0: the KmerDHT minimizer length for k. */
+int mhmkc_minimizer_hashes(mhmkc_t h, const uint64_t *keys, uint64_t n, int32_t n_longs, int32_t m, uint64_t *hashes);
 
 /* Statistics of the last round. */
 int mhmkc_get_stats(mhmkc_t h, mhmkc_stats *s);

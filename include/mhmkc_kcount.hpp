@@ -11,8 +11,13 @@
 //   SeqBlockInserter<MAX_K>          src/kcount/kcount.hpp:57-69
 //   KmerDHT<MAX_K>                   src/kcount/kmer_dht.hpp:118-172 (one rank; UPC++ dist_object dropped)
 //   analyze_kmers<MAX_K>(...)        src/kcount/kcount.hpp:71-73
-// Errors abort with a message, as the reference's DIE does (upcxx-utils log.hpp:251).
+//   _dmin_thres                      src/kcount/kmer_dht.hpp:57 (set by analyze_kmers, read at finish)
+// Errors abort with a message, as the reference's DIE does (upcxx-utils log.hpp:251). dump_kmers writes
+// gzip through zlib: link with -lz.
 #pragma once
+
+#include <sys/stat.h>
+#include <zlib.h>
 
 #include <array>
 #include <cstdint>
@@ -21,6 +26,7 @@
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <algorithm>
 #include <unordered_map>
 #include <vector>
 
@@ -29,6 +35,23 @@
 namespace mhm2 {
 
 using kmer_count_t = uint16_t;
+
+// the depth threshold of get_ext: a global in the reference (src/kcount/kmer_dht.hpp:57), set by
+// analyze_kmers (src/kcount/kcount.cpp:145) and read when the table is finished (kcount_cpu.cpp:178)
+inline int _dmin_thres = 2;
+
+// quick_hash (src/hash_funcs.c:332-342)
+inline uint64_t quick_hash(uint64_t v) {
+  v = v * 3935559000370003845ull + 2691343689449507681ull;
+  v ^= v >> 21;
+  v ^= v << 37;
+  v ^= v >> 4;
+  v *= 4768777513237032717ull;
+  v ^= v << 20;
+  v ^= v >> 41;
+  v ^= v << 5;
+  return v;
+}
 
 [[noreturn]] inline void die(const std::string &msg) {
   std::fprintf(stderr, "mhmkc: %s\n", msg.c_str());
@@ -118,6 +141,21 @@ class Kmer {
     for (unsigned i = 0; i < k; i++) s[i] = "ACGT"[(longs[i / 32] >> (2 * (31 - i % 32))) & 3];
     return s;
   }
+
+  // get_minimizer_fast(m, least_complement = true) (src/kmer.cpp:344-403): the greatest, over the m-mer
+  // positions, of min(forward m-mer, its reverse complement), left-aligned with the low bits zero
+  uint64_t get_minimizer_fast(int m) const {
+    const uint64_t mm = (1ull << (2 * m)) - 1;
+    uint64_t f = 0, r = 0, best = 0;
+    for (unsigned j = 0; j < k; j++) {
+      const uint64_t b = (longs[j / 32] >> (62 - 2 * (j % 32))) & 3;
+      f = ((f << 2) | b) & mm;
+      r = (r >> 2) | ((3 - b) << (2 * m - 2));
+      if ((int)j >= m - 1) best = std::max(best, std::min(f << (64 - 2 * m), r << (64 - 2 * m)));
+    }
+    return best;
+  }
+  uint64_t minimizer_hash_fast(int m) const { return quick_hash(get_minimizer_fast(m)); }  // src/kmer.cpp:454-463
 };
 
 template <int MAX_K>
@@ -187,10 +225,15 @@ using Contigs = std::vector<Contig>;
 // ---------------------------------------------------------------------------------------------
 // HashTableInserter / KmerDHT / SeqBlockInserter
 
+// Where this rank sits. n_ranks > 1: the exchange runs over RCCL (comm_id from mhmkc_comm_id on rank 0,
+// broadcast by the host) or over the host's own transport (UPC++ / MPI, mhmkc_set_transport), and the
+// finished k-mers end on the reference's owner rank (get_kmer_target_rank), where dbjg looks them up.
 struct RankInfo {
   int rank = 0, n_ranks = 1;
   const uint8_t *comm_id = nullptr;
+  const mhmkc_transport *transport = nullptr;
   int device = -1;
+  int output_owner = MHMKC_OWNER_MINIMIZER;
 };
 
 template <int MAX_K>
@@ -200,7 +243,6 @@ class HashTableInserter {
   std::vector<uint64_t> seq_offs_{0}, ctg_offs_{0};
   std::vector<uint16_t> ctg_depths_;
   bool using_ctg_kmers_ = false;
-  int dmin_thres_ = 2;
 
  public:
   HashTableInserter() = default;
@@ -208,20 +250,23 @@ class HashTableInserter {
   HashTableInserter(const HashTableInserter &) = delete;
   HashTableInserter &operator=(const HashTableInserter &) = delete;
 
-  void set_dmin_thres(int d) { dmin_thres_ = d; }
-
-  // kcount_cpu.cpp:425-443; the estimate only sized the CPU table, the GPU path sizes itself exactly
+  // kcount_cpu.cpp:425-443; the estimate only sized the CPU table, the GPU path sizes itself exactly. The
+  // depth threshold is not known yet: analyze_kmers sets _dmin_thres later (kcount.cpp:145).
   void init(int /*num_elems*/, bool /*use_qf*/, const RankInfo &ri = RankInfo()) {
     mhmkc_config cfg;
     mhmkc_config_init(&cfg);
     cfg.k = (int)Kmer<MAX_K>::get_k();
     cfg.n_longs = Kmer<MAX_K>::N_LONGS;
-    cfg.dmin_thres = dmin_thres_;
     cfg.rank = ri.rank;
     cfg.n_ranks = ri.n_ranks;
     cfg.comm_id = ri.comm_id;
     cfg.device = ri.device;
+    cfg.output_owner = ri.output_owner;
     check(mhmkc_create(&h_, &cfg), nullptr, "mhmkc_create");
+    if (ri.n_ranks > 1 && !ri.comm_id) {
+      if (!ri.transport) die("n_ranks > 1 needs RankInfo::comm_id or RankInfo::transport");
+      check(mhmkc_set_transport(h_, ri.transport), h_, "mhmkc_set_transport");
+    }
   }
   // kcount_cpu.cpp:445-448: later supermers are contig supermers (insert_supermer_from_ctg)
   void init_ctg_kmers(int /*max_elems*/) {
@@ -273,9 +318,10 @@ class HashTableInserter {
       ctg_depths_.clear();
     }
   }
-  // kcount_cpu.cpp:490-528
+  // kcount_cpu.cpp:490-528 (get_ext reads the global _dmin_thres at this point, :178)
   void insert_into_local_hashtable(KmerMap<MAX_K> &local_kmers) {
     flush_inserts();
+    check(mhmkc_set_dmin_thres(h_, _dmin_thres), h_, "mhmkc_set_dmin_thres");
     uint64_t n = 0;
     check(mhmkc_finish(h_, &n), h_, "mhmkc_finish");
     std::vector<uint64_t> keys(n * Kmer<MAX_K>::N_LONGS);
@@ -306,11 +352,14 @@ class KmerDHT {
   int minimizer_len;
 
  public:
-  // src/kcount/kmer_dht.cpp:106-154 (store sizes and RPC limits have no meaning without UPC++)
-  KmerDHT(uint64_t my_num_kmers, int dmin_thres = 2, const RankInfo &rank_info = RankInfo()) : ri(rank_info) {
+  // src/kcount/kmer_dht.cpp:106-154: the same arguments (the store sizes and RPC limits have no meaning
+  // without UPC++'s aggregation stores; the estimate only sized the CPU table) + where this rank sits
+  KmerDHT(uint64_t my_num_kmers, int /*max_kmer_store_bytes*/, int /*max_rpcs_in_flight*/, bool /*useHHSS*/,
+          bool use_qf, const RankInfo &rank_info = RankInfo())
+      : ri(rank_info) {
     minimizer_len = std::min(27, std::max(15, (int)Kmer<MAX_K>::get_k() * 2 / 3 + 1));
-    ht_inserter.set_dmin_thres(dmin_thres);
-    ht_inserter.init((int)my_num_kmers, false, ri);
+    if (use_qf) my_num_kmers = (uint64_t)(my_num_kmers * 0.6);
+    ht_inserter.init((int)my_num_kmers, use_qf, ri);
   }
   int get_minimizer_len() const { return minimizer_len; }
   void add_supermer(const std::string &seq, kmer_count_t count) { ht_inserter.insert_supermer(seq, count); }
@@ -323,15 +372,38 @@ class KmerDHT {
     auto it = local_kmers.find(kmer);
     return it == local_kmers.end() ? nullptr : &it->second;
   }
+  // src/kcount/kmer_dht.cpp:193-196: minimizer_hash_fast(minimizer_len) % rank_n (the same for a k-mer and its
+  // reverse complement); after finish every local k-mer satisfies it (MHMKC_OWNER_MINIMIZER)
+  int get_kmer_target_rank(const Kmer<MAX_K> &kmer) const {
+    return (int)(kmer.minimizer_hash_fast(minimizer_len) % (uint64_t)ri.n_ranks);
+  }
   int64_t get_local_num_kmers() const { return (int64_t)local_kmers.size(); }
   typename KmerMap<MAX_K>::iterator local_kmers_begin() { return local_kmers.begin(); }
   typename KmerMap<MAX_K>::iterator local_kmers_end() { return local_kmers.end(); }
   HashTableInserter<MAX_K> &inserter() { return ht_inserter; }
-  // src/kcount/kmer_dht.cpp:243-266 (plain text; the reference gzips through zstr)
-  void dump_kmers(const std::string &fname) {
-    std::ofstream f(fname);
-    for (auto &e : local_kmers) f << e.first.to_string() << " " << e.second.count << " " << e.second.left << " "
-                                  << e.second.right << "\n";
+  // src/kcount/kmer_dht.cpp:243-266: kmers-<k>.txt.gz in the rank's directory (get_rank_path,
+  // upcxx-utils/src/log.cpp:283-312: <dir>/per_rank/<rank / 1000, 8 digits>/<rank, 8 digits>/), one
+  // "KMER count L R" line per k-mer, gzip (the reference writes through zstr)
+  std::string dump_kmers(const std::string &dir = ".") {
+    char sub[64];
+    std::snprintf(sub, sizeof sub, "%08d/%08d", ri.rank / 1000, ri.rank);
+    std::string path = dir + "/per_rank";
+    for (const std::string &d : {path, path + "/" + std::string(sub, 8), path + "/" + std::string(sub)}) mkdir(d.c_str(), 0777);
+    path += "/" + std::string(sub) + "/kmers-" + std::to_string(Kmer<MAX_K>::get_k()) + ".txt.gz";
+    gzFile f = gzopen(path.c_str(), "wb");
+    if (!f) die("cannot open " + path);
+    std::string buf;
+    int64_t i = 0;
+    for (auto &e : local_kmers) {
+      buf += e.first.to_string() + " " + std::to_string(e.second.count) + " " + e.second.left + " " + e.second.right + "\n";
+      if (!(++i % 1000)) {
+        if (gzwrite(f, buf.data(), (unsigned)buf.size()) != (int)buf.size()) die("gzwrite " + path);
+        buf.clear();
+      }
+    }
+    if (!buf.empty() && gzwrite(f, buf.data(), (unsigned)buf.size()) != (int)buf.size()) die("gzwrite " + path);
+    if (gzclose(f) != Z_OK) die("gzclose " + path);
+    return path;
   }
 };
 
@@ -349,9 +421,10 @@ struct SeqBlockInserter {
 // src/kcount/kcount.hpp:71-73 / kcount.cpp:140-157
 template <int MAX_K>
 void analyze_kmers(unsigned kmer_len, unsigned /*prev_kmer_len*/, int qual_offset,
-                   std::vector<PackedReads *> &packed_reads_list, int /*dmin_thres: set on KmerDHT*/, Contigs &ctgs,
+                   std::vector<PackedReads *> &packed_reads_list, int dmin_thres, Contigs &ctgs,
                    KmerDHT<MAX_K> &kmer_dht, bool dump_kmers) {
   if (kmer_len != Kmer<MAX_K>::get_k()) die("kmer_len differs from Kmer<MAX_K>::get_k()");
+  _dmin_thres = dmin_thres;  // kcount.cpp:145
   for (auto *pr : packed_reads_list) {
     if (pr->get_qual_offset() != qual_offset) die("qual_offset mismatch");
     kmer_dht.add_packed_reads(*pr);
@@ -369,7 +442,7 @@ void analyze_kmers(unsigned kmer_len, unsigned /*prev_kmer_len*/, int qual_offse
     kmer_dht.flush_updates();
   }
   kmer_dht.finish_updates();
-  if (dump_kmers) kmer_dht.dump_kmers("kmers-" + std::to_string(kmer_len) + ".txt");
+  if (dump_kmers) kmer_dht.dump_kmers();
 }
 
 }  // namespace mhm2

@@ -10,6 +10,7 @@ from .kcount import (  # noqa: F401
     KmerDHT,
     KmerTable,
     PackedReads,
+    TorchDistTransport,
     analyze_kmers,
     comm_id,
     get_kmer_target_rank,
@@ -20,10 +21,10 @@ from .kcount import (  # noqa: F401
     synth_genome,
     synth_reads,
 )
-from ._native import MhmkcError  # noqa: F401
+from ._native import MHMKC_OWNER_HASH, MHMKC_OWNER_MINIMIZER, MhmkcError  # noqa: F401
 
 __all__ = [
     "KmerCounter", "KmerCounts", "KmerDHT", "KmerTable", "PackedReads", "analyze_kmers", "comm_id",
     "get_kmer_target_rank", "kmer_from_string", "kmer_to_string", "keys_to_strings", "n_longs_for",
-    "synth_genome", "synth_reads", "MhmkcError",
+    "synth_genome", "synth_reads", "MhmkcError", "TorchDistTransport", "MHMKC_OWNER_HASH", "MHMKC_OWNER_MINIMIZER",
 ]

@@ -26,7 +26,11 @@ ERRORS = {
     -5: "MHMKC_ESTATE",
     -6: "MHMKC_EBADCHAR",
     -7: "MHMKC_EUNSUPPORTED",
+    -8: "MHMKC_ETRANSPORT",
 }
+
+MHMKC_OWNER_HASH = 0
+MHMKC_OWNER_MINIMIZER = 1
 
 STAGES = ["tileidx", "extract_hist", "extract_scatter", "exchange", "part_hist", "part_scatter", "count", "other"]
 
@@ -36,6 +40,7 @@ ABI_SYMBOLS = [
     "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_add_ctgs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_device_output",
     "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
     "mhmkc_add_fastq", "mhmkc_add_fastq_device", "mhmkc_fastq_packed", "mhmkc_fastq_fetch",
+    "mhmkc_wait_stream", "mhmkc_set_dmin_thres", "mhmkc_set_transport", "mhmkc_minimizer_hashes",
 ]
 SYNTH_SYMBOLS = ["mhmkc_synth_config_init", "mhmkc_synth_genome", "mhmkc_synth_reads"]
 
@@ -53,6 +58,8 @@ class MhmkcConfig(C.Structure):
         ("n_ranks", C.c_int32),
         ("comm_id", C.c_void_p),
         ("stream", C.c_void_p),
+        ("output_owner", C.c_int32),
+        ("minimizer_len", C.c_int32),
     ]
 
 
@@ -79,6 +86,15 @@ class MhmkcStats(C.Structure):
         ("ms_total", C.c_double),
         ("ms_kernel", C.c_double * 8),
         ("launches", C.c_uint64 * 8),
+        ("bytes_recv", C.c_uint64),
+        ("handoff_sent", C.c_uint64),
+        ("handoff_recv", C.c_uint64),
+        ("h2d_bytes", C.c_uint64),
+        ("h2d_chunks", C.c_uint64),
+        ("slabs", C.c_uint64),
+        ("ms_h2d", C.c_double),
+        ("lds_misses", C.c_uint64),
+        ("lds_ext_adds", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -86,6 +102,15 @@ class MhmkcStats(C.Structure):
         d["ms_kernel"] = {STAGES[i]: self.ms_kernel[i] for i in range(8)}
         d["launches"] = {STAGES[i]: int(self.launches[i]) for i in range(8)}
         return d
+
+
+# mhmkc_transport (host-staged exchange between ranks)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p, C.POINTER(C.c_uint64))
+
+
+class MhmkcTransport(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
 class SynthConfig(C.Structure):
@@ -155,6 +180,10 @@ def lib() -> C.CDLL:
     L.mhmkc_last_error.argtypes = [VP]
     L.mhmkc_last_error.restype = C.c_char_p
     L.mhmkc_abi_version.argtypes = []
+    L.mhmkc_wait_stream.argtypes = [VP, VP]
+    L.mhmkc_set_dmin_thres.argtypes = [VP, C.c_int32]
+    L.mhmkc_set_transport.argtypes = [VP, P(MhmkcTransport)]
+    L.mhmkc_minimizer_hashes.argtypes = [VP, VP, U64, C.c_int32, C.c_int32, VP]
     _lib = L
     return L
 

@@ -23,7 +23,8 @@ LIB = PKG / "libmhmkc.so"
 SYNTH = PKG / "libmhmkc_synth.so"
 ORACLE = ROOT / "oracle" / "liboracle.so"
 
-LIB_SOURCES = [CSRC / "kcount_kernels.hip", CSRC / "kcount_ctg.hip", CSRC / "fastq.hip", CSRC / "mhmkc_host.cpp"]
+LIB_SOURCES = [CSRC / "kcount_kernels.hip", CSRC / "kcount_ctg.hip", CSRC / "kcount_owner.hip", CSRC / "fastq.hip",
+               CSRC / "mhmkc_host.cpp"]
 LIB_DEPS = LIB_SOURCES + [CSRC / "kcount_launch.hpp", CSRC / "kmer_ops.hpp", ROOT / "include" / "mhmkc.h"]
 SYNTH_DEPS = [CSRC / "synth.c", ROOT / "include" / "mhmkc_synth.h"]
 

@@ -113,7 +113,7 @@ __device__ __forceinline__ uint32_t single_choice(uint32_t code, uint32_t count,
 template <int NL>
 __global__ __launch_bounds__(G_THREADS) void k_ctg_fold(PlaneSet keys, const uint32_t *aux, const uint32_t *perm,
                                                          uint64_t n, int dmin, double dyn_mult, int cb, int fb,
-                                                         uint32_t own_lo, int cmpB, PlaneSet fkeys, uint32_t *fstate,
+                                                         uint32_t own_lo, uint32_t own_hi, int cmpB, PlaneSet fkeys, uint32_t *fstate,
                                                          uint32_t *fbucket, uint32_t *fidx,
                                                          unsigned long long *counter) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -155,6 +155,7 @@ __global__ __launch_bounds__(G_THREADS) void k_ctg_fold(PlaneSet keys, const uin
     }
     const uint64_t h = (NL == 1 && cmpB) ? cpart_hash(key[0], cmpB) : part_hash<NL>(key);  // as k_extract_scatter
     const uint32_t coarse = (uint32_t)(h >> (64 - cb));
+    if (coarse < own_lo || coarse >= own_hi) continue;  // another rank's hash range (it folds this key itself)
     const uint32_t fine = fb ? (uint32_t)((h >> (64 - cb - fb)) & ((1ull << fb) - 1)) : 0u;
     const unsigned long long o = atomicAdd(counter, 1ull);
 #pragma unroll
@@ -213,7 +214,7 @@ size_t carve(void *base, uint64_t n, int nl, Scratch *sc) {
 
 template <int NL>
 hipError_t prepare(const CtgView &cv, int k, int qcut, int dmin, double dyn_mult, int cb, int fb, uint32_t own_lo,
-                   int cmpB, const Scratch &sc, uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket,
+                   uint32_t own_hi, int cmpB, const Scratch &sc, uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket,
                    uint64_t *n_out, unsigned int *err, hipStream_t s) {
   const uint64_t n = cv.n_windows;
   hipError_t e;
@@ -233,7 +234,8 @@ hipError_t prepare(const CtgView &cv, int k, int qcut, int dmin, double dyn_mult
     std::swap(perm, perm2);
   }
   if ((e = hipMemsetAsync(sc.counter, 0, 8, s)) != hipSuccess) return e;
-  k_ctg_fold<NL><<<grid_for(n), G_THREADS, 0, s>>>(sc.keys, sc.aux, perm, n, dmin, dyn_mult, cb, fb, own_lo, cmpB, sc.fkeys,
+  k_ctg_fold<NL><<<grid_for(n), G_THREADS, 0, s>>>(sc.keys, sc.aux, perm, n, dmin, dyn_mult, cb, fb, own_lo, own_hi, cmpB,
+                                                   sc.fkeys,
                                                    sc.fstate, sc.fbucket, sc.fidx, sc.counter);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   unsigned long long f = 0;
@@ -258,7 +260,8 @@ hipError_t prepare(const CtgView &cv, int k, int qcut, int dmin, double dyn_mult
 size_t ctg_scratch_bytes(uint64_t n_windows, int nl) { return carve(nullptr, n_windows, nl, nullptr); }
 
 hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool compact, int qual_cutoff, int dmin_thres,
-                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, void *scratch, size_t scratch_bytes,
+                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi, void *scratch,
+                       size_t scratch_bytes,
                        uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,
                        unsigned int *err, hipStream_t s) {
   *n_out = 0;
@@ -268,13 +271,13 @@ hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool compact, int qual_
   if (carve(scratch, cv.n_windows, nl, &sc) > scratch_bytes) return hipErrorInvalidValue;
   const int cmpB = compact ? 2 * k : 0;
   switch (nl) {
-    case 1: return prepare<1>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, cmpB, sc, out_keys,
+    case 1: return prepare<1>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
-    case 2: return prepare<2>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, cmpB, sc, out_keys,
+    case 2: return prepare<2>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
-    case 3: return prepare<3>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, cmpB, sc, out_keys,
+    case 3: return prepare<3>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
-    case 4: return prepare<4>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, cmpB, sc, out_keys,
+    case 4: return prepare<4>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
   }
   return hipErrorInvalidValue;

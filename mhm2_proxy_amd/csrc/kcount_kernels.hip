@@ -176,7 +176,7 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
   __syncthreads();
   const int64_t lo = gA * 32, hi = (gA + NG) * 32;
   for (uint64_t r = (uint64_t)first_read + threadIdx.x; r <= rv.n_reads; r += blockDim.x) {
-    const int64_t s = (int64_t)rv.offs[r];
+    const int64_t s = (int64_t)(rv.offs[r] - rv.obase);
     if (s >= hi) break;
     if (s >= lo) {
       const int64_t d = s - lo;
@@ -214,7 +214,7 @@ __device__ __forceinline__ int next_start(const uint32_t *start, int q) {
 // every window; key/ext are meaningless when !valid.
 template <int NL, typename Emit>
 __device__ __forceinline__ void walk_windows(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
-                                             uint32_t tile, uint64_t n_bases, int k, Emit &&emit) {
+                                             uint32_t tile, uint64_t n_bases, uint32_t head, int k, Emit &&emit) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
   static_assert(W <= 32, "one 32-bit mask per thread span");
   const int klast = k - 32 * (NL - 1);
@@ -258,6 +258,8 @@ __device__ __forceinline__ void walk_windows(const uint64_t *fwd, const uint32_t
   // data end in tile positions: window p needs p + k < end (p + k is the right neighbour)
   const int64_t end64 = (int64_t)n_bases - ((int64_t)tile * T - 32);
   const int end = end64 > (int64_t)(1 << 30) ? (1 << 30) : (int)end64;
+  // data begin (a slice view): window p needs its left neighbour p - 1 at or after the view's head
+  const int beg = tile == 0 ? (int)head + 32 : -(1 << 30);
   uint32_t cl = (uint32_t)(codes64(lp0 - 1) >> 62);
 #pragma unroll
   for (int i = 0; i < W; i++) {
@@ -265,7 +267,7 @@ __device__ __forceinline__ void walk_windows(const uint64_t *fwd, const uint32_t
     const uint32_t cr = (uint32_t)(incoming >> (62 - 2 * i)) & 3u;
     const uint32_t gl = (gl_bits >> (31 - i)) & 1u, gr = (gr_bits >> (31 - i)) & 1u;
     if ((st_bits >> (31 - i)) & 1u) last = lp + k;
-    const bool valid = (last < lp) && (lp + k < end);
+    const bool valid = (last < lp) && (lp + k < end) && (lp > beg);
     int l = gl ? (int)cl : EXT_NONE, r = gr ? (int)cr : EXT_NONE;
     const bool use_rc = kmer_less<NL>(rc, fw);
     uint64_t key[NL];
@@ -300,7 +302,7 @@ __global__ void k_tile_first_read(ReadsView rv, uint32_t *out, uint32_t n_tiles,
   uint64_t a = 0, b = rv.n_reads + 1;  // lower_bound over offs[0..n_reads]
   while (a < b) {
     const uint64_t m = (a + b) >> 1;
-    if (rv.offs[m] < lo)
+    if (rv.offs[m] - rv.obase < lo)
       a = m + 1;
     else
       b = m;
@@ -330,7 +332,7 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
   const uint32_t tile = blockIdx.x;
   load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
   const int sh = 64 - p.coarse_bits;
-  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.k, [&](int, const uint64_t *key, uint32_t, bool valid) {
+  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, p.k, [&](int, const uint64_t *key, uint32_t, bool valid) {
     if (valid) atomicAdd(&hist[(uint32_t)(window_hash<NL, CMP>(key, p.k) >> sh)], 1u);
   });
   __syncthreads();
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   const int csh = 64 - (2 * p.k - p.coarse_bits);  // compact: keep the low 2k - cb bits of the mixed key
   uint64_t rk[W][NL];
   uint32_t inf[W];
-  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.k,
+  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, p.k,
                    [&](int i, const uint64_t *key, uint32_t e, bool valid) {
                      const uint64_t h = window_hash<NL, CMP>(key, p.k);
 #pragma unroll
@@ -569,9 +571,9 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   constexpr int SF = CMP ? SF_C40 : SF_WORDS;
   if (kEStaged)
     scatter_staged<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
-                                      p.err);
+                                      p.ovf);
   else
-    scatter_regs<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.err);
+    scatter_regs<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -756,12 +758,20 @@ __global__ void k_init_fine(const unsigned long long *coarse_base, const unsigne
 }
 
 // sum over reads of max(0, L - k - 1): the counted windows of a batch
-__global__ __launch_bounds__(256) void k_count_windows(ReadsView rv, int k, unsigned long long *out) {
+// and the CSR checks of mhmkc_add_reads (offsets non-decreasing, reads <= 65535 bases: PackedRead's
+// read_len is a uint16, src/packed_reads.hpp:60-80) for device-resident offsets
+__global__ __launch_bounds__(256) void k_count_windows(ReadsView rv, int k, unsigned long long *out, unsigned int *err) {
   unsigned long long acc = 0;
+  bool bad = false;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads; r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t L = rv.offs[r + 1] - rv.offs[r];
-    if (L > (uint64_t)k + 1) acc += L - k - 1;
+    const uint64_t a = rv.offs[r], b = rv.offs[r + 1];
+    bad |= b < a || b - a > 65535;
+    const uint64_t L = b - a;
+    if (b >= a && L > (uint64_t)k + 1) acc += L - k - 1;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    bad |= rv.offs[0] != rv.obase + rv.head || rv.offs[rv.n_reads] - rv.obase != rv.n_bases;
+  if (bad) atomicOr(err, 4u);
   acc = wave_sum_u64(acc);
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
@@ -1149,6 +1159,11 @@ __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, c
 
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
+  // A capped fine bucket overflowed in k_part_scatter (same stream, earlier launch): its cursor, which is
+  // this kernel's bucket end, ran past the bucket, so reading up to it would leave the layout. The host
+  // discards this launch and redoes the partition with exact bucket sizes. (Uniform: every lane reads the
+  // same word before any barrier.)
+  if (p.err && (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u)) return;
   extern __shared__ __align__(16) unsigned char smem[];
   using K = typename std::conditional<CMP, uint32_t, uint64_t>::type;
   CountLds<K> t;
@@ -1221,6 +1236,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   };
 
   unsigned long long my_occ = 0, my_purged = 0, my_sum = 0, my_out = 0, my_sweeps = 0, my_maxb = 0;
+  uint32_t my_miss = 0, my_ext = 0;  // phase-B records (tid 0), extension adds (per lane): the LDS op mix
 #if MHMKC_STAMP
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
 #endif
@@ -1285,6 +1301,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           } else {
             ce[j] = valid ? nx[j] : NONE;
           }
+          my_ext += valid ? (uint32_t)(((ce[j] >> 3) & 7u) < 4u) + (uint32_t)((ce[j] & 7u) < 4u) : 0u;
         }
 #if MHMKC_STAMP
 #pragma unroll
@@ -1379,6 +1396,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #else
         const unsigned int M = min(*nmiss, (unsigned int)MCL);
 #endif
+        if (tid == 0) my_miss += M;
         if (!B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
         for (unsigned int q = tid; q < M; q += C_THREADS) {
           uint64_t key[NL];
@@ -1513,6 +1531,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   my_occ = wave_sum_u64(my_occ);
   my_purged = wave_sum_u64(my_purged);
   my_sum = wave_sum_u64(my_sum);
+  const unsigned long long wext = wave_sum_u64(my_ext);
+  if (lane == 0 && wext) atomicAdd(&p.stats[STAT_EXTADDS], wext);
+  if (tid == 0 && my_miss) atomicAdd(&p.stats[STAT_MISSES], (unsigned long long)my_miss);
   if (tid == 0) {
     s_red[0] = 0;
     s_red[1] = 0;
@@ -1615,10 +1636,10 @@ hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_
   return hipGetLastError();
 }
 
-hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, hipStream_t s) {
+hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, unsigned int *err, hipStream_t s) {
   if (!r.n_reads) return hipSuccess;
   const uint64_t blocks = std::min<uint64_t>(2048, (r.n_reads + 255) / 256);
-  k_count_windows<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, k, out);
+  k_count_windows<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, k, out, err);
   return hipGetLastError();
 }
 

@@ -7,11 +7,17 @@
 namespace mhm {
 
 // Read stream in the PackedRead byte layout (src/packed_reads.cpp:73-109) + CSR offsets.
+// A view may be a slice of a larger batch (one H2D chunk, mhmkc_add_reads): its offsets are then the
+// batch's, and obase (<= offs[0], 16-byte aligned in the batch) is subtracted from them; bytes points
+// at batch byte obase. Positions [0, head) belong to the previous slice's last read and hold no window.
 struct ReadsView {
   const uint8_t *bytes;   // n_bases bytes: code (bits 0-2) | min(q-off,31) << 3
-  const uint64_t *offs;   // n_reads+1 offsets, offs[0]=0, offs[n_reads]=n_bases
+  const uint64_t *offs;   // n_reads+1 offsets, offs[n_reads] - obase = n_bases
   uint64_t n_reads;
   uint64_t n_bases;
+  uint64_t obase;         // subtracted from every offset (0 for a whole batch)
+  uint32_t head;          // offs[0] - obase (< 16)
+  uint32_t pad;
 };
 
 // Record planes of one slab: word planes (SoA) + optional ext byte plane.
@@ -35,7 +41,8 @@ struct ExtractParams {
   uint64_t bin_cap;                 // capped mode: segment (b, s) owns [i*bin_cap, (i+1)*bin_cap), i = b*E_NSUB+s,
                                     // s = blockIdx % E_NSUB; 0 = exact bases, everything in segment (b, 0)
   PlaneSet out;                     // (E-scatter)
-  unsigned int *err;                // bit 0: input byte with code > 4; bit 1: a capped bin overflowed
+  unsigned int *err;                // bit 0: input byte with code > 4
+  unsigned int *ovf;                // bit 1: a capped bin of this slab overflowed (per slab)
 };
 
 // One chunk of S work: <= tile records of one (source, coarse bucket) segment.
@@ -98,6 +105,8 @@ struct CountParams {
   char *out_right;
   unsigned long long *out_cursor;
   unsigned long long *stats;          // [STAT_*]
+  const unsigned int *err;            // k_part_scatter's flag word: bit 1 set = a capped fine bucket overflowed,
+                                      // its cursor ran past the bucket, so the launch is void (returns at once)
   // contig pass (kcount_ctg.hip): folded contig k-mers sorted by bucket; 0 entries = no contig pass
   uint64_t ctg_n;
   const uint64_t *ctg_keys[4];        // [NL][ctg_n] canonical key words
@@ -126,8 +135,10 @@ size_t ctg_scratch_bytes(uint64_t n_windows, int nl);
 // Extract, sort by key (stable: contig order kept within a key), fold every key's contig occurrences in
 // order (insert_supermer_from_ctg) and sort the folded k-mers by local fine bucket. Outputs (n_out of them)
 // go to out_keys[NL] (SoA, each out_cap long), out_state, out_bucket.
+// Only k-mers whose coarse bucket is in [own_lo, own_hi) (this rank's hash range) are kept.
 hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool compact, int qual_cutoff, int dmin_thres,
-                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, void *scratch, size_t scratch_bytes,
+                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi, void *scratch,
+                       size_t scratch_bytes,
                        uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,
                        unsigned int *err, hipStream_t s);
 
@@ -138,7 +149,9 @@ enum {
   STAT_COUNTSUM = 3,
   STAT_SWEEPS = 4,
   STAT_MAXBUCKET = 5,
-  STAT_N = 8
+  STAT_MISSES = 6,    // records worked off in phase B (not in their home group)
+  STAT_N = 8,         // stats[STAT_N - 1]: internal error flag
+  STAT_EXTADDS = 14   // extension-counter adds (records with an A/C/G/T neighbour, per side)
 };
 constexpr int STAT_ALLOC = 16;  // stats[8..13]: k_count phase stamps in MHMKC_STAMP builds
 
@@ -184,8 +197,9 @@ static_assert(count_lds_bytes(1) <= 163840 && count_lds_bytes(2) <= 163840 && co
               "k_count LDS budget");
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);
-// total counted windows sum(max(0, L - k - 1)) of a batch, added to *out
-hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, hipStream_t s);
+// total counted windows sum(max(0, L - k - 1)) of a batch, added to *out; err bit 2 (4) when the offsets are
+// not a valid PackedReads CSR (offs[0] != 0, decreasing, a read longer than 65535, offs[n] != n_bases)
+hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, unsigned int *err, hipStream_t s);
 // capped fine layout: base/cursor of bucket (c, d) = coarse_base[c] + d * coarse_fcap[c]
 hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap,
                             uint32_t n_coarse, int fine_bits, unsigned long long *base, unsigned long long *cursor,
@@ -230,5 +244,23 @@ hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long l
 hipError_t launch_fq_pack(const char *text, const unsigned long long *line_end, uint64_t n_rec,
                           const unsigned long long *offs, int qual_offset, uint8_t *out, unsigned long long *err,
                           hipStream_t s);
+
+// Output hand-off to the reference's owner rank (kcount_owner.hip): get_kmer_target_rank =
+// minimizer_hash_fast(minimizer_len) % rank_n (src/kcount/kmer_dht.cpp:193-196, src/kmer.cpp:344-393,454-463).
+struct OutRows {
+  uint64_t *keys;  // [n * nlo] Kmer::longs layout
+  uint16_t *counts;
+  char *left, *right;
+};
+// KmerDHT minimizer length for k (src/kcount/kmer_dht.cpp:114-116)
+inline int minimizer_len_for(int k) { return k * 2 / 3 + 1 < 15 ? 15 : (k * 2 / 3 + 1 > 27 ? 27 : k * 2 / 3 + 1); }
+// minimizer_hash_fast of n keys (nlo words each, the first k/32+1 used)
+hipError_t launch_minimizer_hash(const uint64_t *keys, uint64_t n, int nlo, int k, int m, uint64_t *out, hipStream_t s);
+// dest[i] = owner rank of row i; hist[r] += rows owned by rank r (zero hist first)
+hipError_t launch_owner_hist(const uint64_t *keys, uint64_t n, int nlo, int k, int m, int n_ranks, uint8_t *dest,
+                             unsigned long long *hist, hipStream_t s);
+// rows grouped by owner: row i goes to out at cursor[dest[i]]++ (cursor = per-owner start offsets)
+hipError_t launch_owner_scatter(const OutRows &in, uint64_t n, int nlo, const uint8_t *dest, int n_ranks,
+                                unsigned long long *cursor, const OutRows &out, hipStream_t s);
 
 }  // namespace mhm

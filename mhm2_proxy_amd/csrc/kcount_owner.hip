@@ -1,0 +1,135 @@
+// Output hand-off to the reference's owner rank on gfx950.
+//
+// dbjg looks a k-mer up on rank get_kmer_target_rank(kmer) = minimizer_hash_fast(minimizer_len) % rank_n
+// (src/kcount/kmer_dht.cpp:193-196; callers src/dbjg_traversal.cpp:232-234,264-274). The count itself is
+// partitioned by hash range (kcount_kernels.hip); after finalize, mhmkc_finish moves every surviving k-mer to
+// that owner when the handle asks for it (mhmkc_config.output_owner). These kernels compute the owner of
+// each output row and group the rows by owner for the exchange.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kcount_launch.hpp"
+#include "kmer_ops.hpp"
+
+namespace mhm {
+
+namespace {
+
+constexpr int O_THREADS = 256;
+
+inline unsigned grid_for(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(8192, (n + 255) / 256)); }
+
+// quick_hash (src/hash_funcs.c:332-342)
+__device__ __forceinline__ uint64_t quick_hash(uint64_t v) {
+  v = v * 3935559000370003845ull + 2691343689449507681ull;
+  v ^= v >> 21;
+  v ^= v << 37;
+  v ^= v >> 4;
+  v *= 4768777513237032717ull;
+  v ^= v << 20;
+  v ^= v >> 41;
+  v ^= v << 5;
+  return v;
+}
+
+// Kmer::get_minimizer_fast(m, least_complement = true) (src/kmer.cpp:344-393, 395-403): the greatest, over
+// the m-mer positions i in [0, k-m], of min(forward m-mer i, its reverse complement), each left-aligned in a
+// word with the low bits zero (ZERO_MASK[m], :81-87). The reference reads the reverse-complement candidate
+// of position i as the m-mer at k-m-i of revcomp(kmer), which is the reverse complement of forward m-mer
+// i; here both are rolled base by base (forward shifts a base in at the bottom, the reverse complement
+// shifts the complemented base in at the top), m <= 28.
+__device__ __forceinline__ uint64_t minimizer_fast(const uint64_t *w, int k, int m) {
+  const uint64_t mm = (1ull << (2 * m)) - 1;
+  const int up = 64 - 2 * m;
+  uint64_t f = 0, r = 0, best = 0;
+  for (int j = 0; j < k; j++) {
+    const uint64_t b = (w[j >> 5] >> (62 - 2 * (j & 31))) & 3u;
+    f = ((f << 2) | b) & mm;
+    r = (r >> 2) | ((3u - b) << (2 * m - 2));
+    if (j >= m - 1) {
+      const uint64_t fl = f << up, rl = r << up;
+      const uint64_t least = fl < rl ? fl : rl;
+      best = least > best ? least : best;
+    }
+  }
+  return best;
+}
+
+__global__ __launch_bounds__(O_THREADS) void k_minimizer_hash(const uint64_t *keys, uint64_t n, int nlo, int k, int m,
+                                                              uint64_t *out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = quick_hash(minimizer_fast(keys + i * (uint64_t)nlo, k, m));
+}
+
+__global__ __launch_bounds__(O_THREADS) void k_owner_hist(const uint64_t *keys, uint64_t n, int nlo, int k, int m, int G,
+                                                          uint8_t *dest, unsigned long long *hist) {
+  __shared__ unsigned int lh[256];
+  for (int i = threadIdx.x; i < G; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t d = (uint32_t)(quick_hash(minimizer_fast(keys + i * (uint64_t)nlo, k, m)) % (uint64_t)G);
+    dest[i] = (uint8_t)d;
+    atomicAdd(&lh[d], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G; i += blockDim.x)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+}
+
+// Rows grouped by owner. The order inside an owner's group is free (the reference's KmerMap order is
+// unspecified): each workgroup reserves one run per owner with one atomic and ranks its rows in LDS.
+__global__ __launch_bounds__(O_THREADS) void k_owner_scatter(OutRows in, uint64_t n, int nlo, const uint8_t *dest, int G,
+                                                             unsigned long long *cursor, OutRows out) {
+  __shared__ unsigned int lc[256];
+  __shared__ unsigned long long lb[256];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+    for (int i = threadIdx.x; i < G; i += blockDim.x) lc[i] = 0;
+    __syncthreads();
+    const uint64_t i = i0 + threadIdx.x;
+    uint32_t d = 0, rk = 0;
+    if (i < n) {
+      d = dest[i];
+      rk = atomicAdd(&lc[d], 1u);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < G; j += blockDim.x) lb[j] = lc[j] ? atomicAdd(&cursor[j], (unsigned long long)lc[j]) : 0ull;
+    __syncthreads();
+    if (i < n) {
+      const uint64_t o = lb[d] + rk;
+      for (int w = 0; w < nlo; w++) out.keys[o * nlo + w] = in.keys[i * nlo + w];
+      out.counts[o] = in.counts[i];
+      out.left[o] = in.left[i];
+      out.right[o] = in.right[i];
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+hipError_t launch_minimizer_hash(const uint64_t *keys, uint64_t n, int nlo, int k, int m, uint64_t *out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (m < 1 || m > 28 || m > k) return hipErrorInvalidValue;
+  k_minimizer_hash<<<grid_for(n), O_THREADS, 0, s>>>(keys, n, nlo, k, m, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_hist(const uint64_t *keys, uint64_t n, int nlo, int k, int m, int n_ranks, uint8_t *dest,
+                             unsigned long long *hist, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (m < 1 || m > 28 || m > k || n_ranks < 1 || n_ranks > 256) return hipErrorInvalidValue;
+  k_owner_hist<<<grid_for(n), O_THREADS, 0, s>>>(keys, n, nlo, k, m, n_ranks, dest, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_owner_scatter(const OutRows &in, uint64_t n, int nlo, const uint8_t *dest, int n_ranks,
+                                unsigned long long *cursor, const OutRows &out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (n_ranks < 1 || n_ranks > 256) return hipErrorInvalidValue;
+  k_owner_scatter<<<grid_for(n), O_THREADS, 0, s>>>(in, n, nlo, dest, n_ranks, cursor, out);
+  return hipGetLastError();
+}
+
+}  // namespace mhm

@@ -1,9 +1,14 @@
-// Host side of libmhmkc: handle lifetime, device memory arena, stage orchestration, the RCCL
-// exchange and the C ABI declared in include/mhmkc.h.
+// Host side of libmhmkc: handle lifetime, device memory, stage orchestration, the exchange between ranks
+// (RCCL or a host-staged transport), the owner hand-off and the C ABI declared in include/mhmkc.h.
 //
 // One handle = one GPU = one rank. The reference's per-rank state (KmerDHT + HashTableInserter,
 // src/kcount/kmer_dht.hpp:95-172) maps onto this struct; its UPC++ supermer store
 // (src/kcount/kmer_dht.cpp:133-149,222-224) maps onto the hash-range exchange in exchange().
+//
+// Work is enqueued on one stream and the host waits only where it needs a number from the device:
+// a batch of reads becomes one "slab" of coarse-bucketed records whose bucket counts are copied back
+// asynchronously and read at mhmkc_finish, so host batches copied in chunks on a second stream are
+// extracted while the next chunk is still on the wire.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -50,19 +55,58 @@ struct DevBuf {
   }
 };
 
+// Pinned host memory (asynchronous copies to and from it).
+struct PinBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    release();
+    size_t want = bytes + bytes / 8 + 4096;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T *as() const {
+    return (T *)p;
+  }
+};
+
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Records of one add_reads batch, partitioned by coarse bucket (hash range). Every coarse bucket b is
-// E_NSUB segments i = b * E_NSUB + s (one per group of blocks sharing an XCD in the capped layout; in
-// the exact layout segment s = 0 holds the whole bucket and the others are empty). Segments are in
-// bucket order, so a range of buckets is one contiguous span (with gaps in the capped layout).
+// Records of one batch (or one H2D chunk), partitioned by coarse bucket (hash range). Every coarse bucket b
+// is E_NSUB segments i = b * E_NSUB + s (one per group of blocks sharing an XCD in the capped layout; in the
+// exact layout segment s = 0 holds the whole bucket and the others are empty). Segments are in bucket
+// order, so a range of buckets is one contiguous span (with gaps in the capped layout).
 constexpr uint32_t NSUB = mhm::E_NSUB;
 struct Slab {
-  DevBuf buf;
+  DevBuf buf;   // record planes
+  DevBuf meta;  // device cursors [nseg] (sub-major) + the overflow flag word
+  PinBuf pin;   // host copy of meta: initial cursors going in, final cursors coming back
   mhm::PlaneSet planes{};
+  mhm::ReadsView rv{};  // the reads it came from (kept for an exact rerun at finish)
+  uint64_t wins = 0;    // counted windows = records
   uint64_t n = 0;
+  uint32_t tiles = 0;
+  int qcut = 20;         // quality cutoff of its batch (mhmkc_add_seqs encodes quality as case: cutoff 1)
+  bool pending = false;  // final cursors not read yet
   std::vector<uint64_t> counts;  // [nb * NSUB]
   std::vector<uint64_t> bases;   // [nb * NSUB + 1] segment starts, bases[nb * NSUB] = end of the slab
+};
+
+// Device copy of one host batch (mhmkc_add_reads); it lives until finish (a slab may be re-extracted).
+struct Arena {
+  DevBuf bytes, offs;
 };
 
 // A source of owned records for the fine partition: per owned coarse bucket (local index) and segment.
@@ -72,16 +116,27 @@ struct Source {
   std::vector<uint64_t> count;  // [n_owned * NSUB]
 };
 
+// One device-to-device transfer of the exchange: `bytes` at `ptr` to (or from) rank `peer`.
+struct Xfer {
+  int peer;
+  void *ptr;
+  uint64_t bytes;
+};
+
 struct Prof {
   int stage;
   hipEvent_t a, b;
 };
 
+// Bytes of one H2D chunk of mhmkc_add_reads (MHMKC_CHUNK_BYTES overrides: tests force many chunks).
+constexpr uint64_t CHUNK_BYTES = 128ull << 20;
+
 }  // namespace
 
 struct mhmkc {
   mhmkc_config cfg{};
-  int k = 0, nl = 1, nlo = 1;
+  int k = 0, nl = 1, nlo = 1, mlen = 15;
+  int dmin = 2;  // the finish's depth threshold (mhmkc_set_dmin_thres)
   bool packed = true;
   bool compact = false;  // compact records (kmer_ops.hpp cmix): 5 B per coarse record, 4 B per fine record
   int cb = 8, fb = 8, hbits = 0;
@@ -89,15 +144,21 @@ struct mhmkc {
   uint32_t own_lo = 0, own_hi = 256;  // owned coarse range [own_lo, own_hi)
   int dev = 0;
   int n_cu = 0;  // compute units: persistent k_count workgroups
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr, copy_stream = nullptr;
   bool own_stream = false;
   ncclComm_t comm = nullptr;
+  mhmkc_transport xp{};
+  bool has_xp = false;
 
   std::vector<Slab *> slabs;  // pool; first n_slabs are in use
   size_t n_slabs = 0;
-  DevBuf d_hist, d_cursor, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
-  DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xcounts;
-  DevBuf d_in_bytes, d_in_offs, d_hll;
+  std::vector<Arena *> arenas;  // pool; first n_arenas are in use
+  size_t n_arenas = 0;
+  std::vector<hipEvent_t> chunk_ev;  // one per H2D chunk in flight (pool)
+  DevBuf d_hist, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
+  DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
+  DevBuf d_hll, d_dest, d_ohist, d_out2_keys, d_out2_counts, d_out2_left, d_out2_right, d_mh;
+  PinBuf x_send, x_recv;  // host-staged exchange
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
   DevBuf d_fq_text, d_fq_chunk, d_fq_lines, d_fq_len, d_fq_tmp, d_fq_bytes, d_fq_offs, d_fq_err;
@@ -120,7 +181,7 @@ struct mhmkc {
   bool profiling = false;
   std::vector<Prof> prof;
   std::vector<hipEvent_t> ev_pool;
-  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_h2d0 = nullptr, ev_h2d1 = nullptr;
 
   int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -168,6 +229,7 @@ struct mhmkc {
     prof.clear();
   }
 
+  int G() const { return cfg.n_ranks; }
   uint32_t owner_lo(int r) const { return (uint32_t)(((uint64_t)r * nb + cfg.n_ranks - 1) / cfg.n_ranks); }
   uint32_t n_owned() const { return own_hi - own_lo; }
   size_t rec_bytes() const { return compact ? 5 : 8 * (size_t)nl + (packed ? 0 : 1); }
@@ -187,6 +249,17 @@ struct mhmkc {
     if (n_slabs == slabs.size()) slabs.push_back(new Slab());
     return slabs[n_slabs++];
   }
+  Arena *new_arena() {
+    if (n_arenas == arenas.size()) arenas.push_back(new Arena());
+    return arenas[n_arenas++];
+  }
+
+  // Grow a buffer that kernels already enqueued may still read: wait for them first (a free would not).
+  hipError_t grow(DevBuf &b, size_t bytes) {
+    if (bytes <= b.cap && b.p) return hipSuccess;
+    hipError_t e = hipStreamSynchronize(stream);
+    return e != hipSuccess ? e : b.ensure(bytes);
+  }
 
   // Record planes for n records: NL u64 word planes (+ a byte plane when the ext code is not packed);
   // compact: a u32 plane (w[0]) + a byte plane for coarse-bucketed records, the u32 plane alone for fine.
@@ -195,7 +268,7 @@ struct mhmkc {
     const size_t plane = align_up(m * (compact ? 4 : 8), 256);
     const size_t extb = (compact ? !fine : !packed) ? align_up(m, 256) : 0;
     const int np = compact ? 1 : nl;
-    hipError_t e = buf.ensure(plane * np + extb);
+    hipError_t e = grow(buf, plane * np + extb);
     if (e != hipSuccess) return hip_fail(e, "allocating record planes");
     char *b = buf.as<char>();
     for (int w = 0; w < 4; w++) ps.w[w] = w < np ? (uint64_t *)(b + plane * w) : nullptr;
@@ -203,9 +276,18 @@ struct mhmkc {
     return MHMKC_OK;
   }
 
-  int add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, uint64_t n_bases, int qcut);
+  int add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known);
+  int extract(Slab *sl, bool exact);
+  int resolve_slabs();
+  int add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut);
+  int allgather_host(const void *send, void *recv, size_t bytes);
+  int move(const std::vector<Xfer> &snd, const std::vector<Xfer> &rcv);
   int exchange(std::vector<Source> &srcs);
+  int gather_ctgs(std::vector<uint8_t> &gb, std::vector<uint64_t> &go, std::vector<uint64_t> &gw,
+                  std::vector<uint16_t> &gd);
+  int handoff();
   int finish(uint64_t *n_out_ret);
+  int qcut_pending = 20;  // quality cutoff of the batch being added (add_seqs encodes quality as case)
 };
 
 // Fine partition target: distinct keys per fine bucket <= FINE_LOAD x LDS table slots.
@@ -225,118 +307,304 @@ static double hll_estimate(const std::vector<uint32_t> &reg) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// extract one batch of reads into a coarse-bucketed slab
+// extraction: one batch (or chunk) of reads into a coarse-bucketed slab
 
-// Coarse buckets are sized from the exact window count (+4 % and 4096 records of slack each), which lets
-// one extract pass write the records. A bucket that would overflow (only skewed inputs: very repetitive
-// reads) makes the pass redo itself with an exact histogram first (extract_hist).
-int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, uint64_t n_bases, int qcut) {
-  int rc = begin_round();
-  if (rc) return rc;
-  st.reads += n_reads;
-  st.bases += n_bases;
-  if (n_reads == 0 || n_bases == 0) return MHMKC_OK;
-  if (n_reads >= 0xffffffffull) return fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
+// Enqueue the extraction of a slab. Capped layout (the default): every segment gets the expected share of
+// the windows + 4 % + 1024 records, one scatter pass, no histogram; the final cursors come back to pinned
+// memory asynchronously and are read by resolve_slabs. Exact layout (skewed input that overflowed a capped
+// segment, or MHMKC_DEBUG_EXACT): a histogram pass first, which the host waits for.
+int mhmkc::extract(Slab *sl, bool exact) {
   const int T = mhm::tile_bases(nl);
-  const uint64_t tiles64 = (n_bases + T - 1) / T;
-  if (tiles64 >= 0x7fffffffull) return fail(MHMKC_EINVAL, "batch too large");
-  const uint32_t tiles = (uint32_t)tiles64;
+  const uint32_t nseg = nb * NSUB;
   hipError_t e;
-  if ((e = d_tiles.ensure((size_t)tiles * 4)) != hipSuccess) return hip_fail(e, "tile index");
-  if ((e = d_hist.ensure((size_t)nb * 8 + 8)) != hipSuccess) return hip_fail(e, "histogram");
-  if ((e = d_cursor.ensure((size_t)nb * NSUB * mhm::CPAD * 8)) != hipSuccess) return hip_fail(e, "cursor");
-  unsigned long long *d_wins = d_hist.as<unsigned long long>() + nb;
-
+  if ((e = grow(d_tiles, (size_t)sl->tiles * 4 + 64)) != hipSuccess) return hip_fail(e, "tile index");
+  if ((e = grow(d_hist, (size_t)nb * 8 + 64)) != hipSuccess) return hip_fail(e, "histogram");
+  if ((e = sl->meta.ensure((size_t)nseg * 8 + 64)) != hipSuccess) return hip_fail(e, "slab cursors");
+  if ((e = sl->pin.ensure((size_t)nseg * 8 + 64)) != hipSuccess) return hip_fail(e, "slab cursors (host)");
+  sl->counts.assign(nseg, 0);
+  sl->bases.assign(nseg + 1, 0);
   mhm::ExtractParams p{};
-  p.reads = {bytes, offs, n_reads, n_bases};
+  p.reads = sl->rv;
   p.tile_first_read = d_tiles.as<uint32_t>();
-  p.n_tiles = tiles;
+  p.n_tiles = sl->tiles;
   p.k = k;
-  p.qual_cutoff = qcut;
+  p.qual_cutoff = sl->qcut;
   p.coarse_bits = cb;
   p.n_bins = nb;
   p.hbits = hbits;
   p.compact = compact;
   p.hist = d_hist.as<unsigned long long>();
-  p.cursor = d_cursor.as<unsigned long long>();
+  unsigned long long *dcur = sl->meta.as<unsigned long long>();
+  p.cursor = dcur;
   p.err = d_err.as<unsigned int>();
-
+  p.ovf = (unsigned int *)(dcur + nseg);
   prof_begin(MHMKC_STAGE_TILEIDX);
-  e = mhm::launch_tile_first_read(p.reads, d_tiles.as<uint32_t>(), tiles, T, stream);
-  if (e == hipSuccess) e = hipMemsetAsync(d_wins, 0, 8, stream);
-  if (e == hipSuccess) e = mhm::launch_count_windows(p.reads, k, d_wins, stream);
+  e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
   prof_end();
-  if (e != hipSuccess) return hip_fail(e, "tile index / window count");
-  uint64_t wins = 0;
-  if ((e = hipMemcpyAsync(&wins, d_wins, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-    return hip_fail(e, "window count D2H");
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "window count");
-  if (wins == 0) return MHMKC_OK;
-
-  Slab *sl = new_slab();
-  const uint32_t nseg = nb * NSUB;
-  sl->counts.assign(nseg, 0);
-  sl->bases.assign(nseg + 1, 0);
+  if (e != hipSuccess) return hip_fail(e, "tile index");
+  if (exact) {
+    std::vector<uint64_t> hist(nb);
+    prof_begin(MHMKC_STAGE_OTHER);
+    e = hipMemsetAsync(d_hist.p, 0, (size_t)nb * 8, stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "memset");
+    prof_begin(MHMKC_STAGE_EHIST);
+    e = mhm::launch_extract_hist(p, nl, packed, stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "extract_hist");
+    if ((e = hipMemcpyAsync(hist.data(), d_hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(stream)) != hipSuccess)
+      return hip_fail(e, "extract_hist");
+    uint64_t tot = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+      sl->bases[b * NSUB] = tot;
+      tot += hist[b];
+      for (uint32_t q = 1; q < NSUB; q++) sl->bases[b * NSUB + q] = tot;  // empty segments
+    }
+    sl->bases[nseg] = tot;
+    p.bin_cap = 0;
+  } else {
+    const uint64_t expect = sl->wins / nseg;
+    const uint64_t cap = align_up(expect + expect / 25 + 1024, 64);
+    for (uint32_t i = 0; i <= nseg; i++) sl->bases[i] = (uint64_t)i * cap;
+    p.bin_cap = cap;
+  }
+  int rc;
+  if ((rc = set_planes(sl->buf, sl->bases[nseg], sl->planes))) return rc;
   // device cursors are sub-major (cursor[s * nb + b]): the 64 lanes of one atomic instruction then hit 64
   // consecutive words, which the memory-side atomic unit serves as whole lines
-  std::vector<uint64_t> cur((size_t)nseg), hist(nb);
-  auto cidx = [&](uint32_t i) { return (size_t)(i % NSUB) * nb + i / NSUB; };
-  const uint64_t expect = wins / nseg;
-  const uint64_t cap = align_up(expect + expect / 25 + 1024, 64);
-  bool exact = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
-  for (int attempt = 0; attempt < 2; attempt++) {
-    if (exact) {
-      prof_begin(MHMKC_STAGE_OTHER);
-      e = hipMemsetAsync(d_hist.p, 0, (size_t)nb * 8, stream);
-      prof_end();
-      if (e != hipSuccess) return hip_fail(e, "memset");
-      prof_begin(MHMKC_STAGE_EHIST);
-      e = mhm::launch_extract_hist(p, nl, packed, stream);
-      prof_end();
-      if (e != hipSuccess) return hip_fail(e, "extract_hist");
-      if ((e = hipMemcpyAsync(hist.data(), d_hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-        return hip_fail(e, "histogram D2H");
-      if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_hist");
-      uint64_t tot = 0;
-      for (uint32_t b = 0; b < nb; b++) {
-        sl->bases[b * NSUB] = tot;
-        tot += hist[b];
-        for (uint32_t q = 1; q < NSUB; q++) sl->bases[b * NSUB + q] = tot;  // empty segments
-      }
-      sl->bases[nseg] = tot;
-      p.bin_cap = 0;
-    } else {
-      for (uint32_t i = 0; i <= nseg; i++) sl->bases[i] = (uint64_t)i * cap;
-      p.bin_cap = cap;
-    }
-    if ((rc = set_planes(sl->buf, sl->bases[nseg], sl->planes))) return rc;
-    for (uint32_t i = 0; i < nseg; i++) cur[cidx(i)] = sl->bases[i];
-    if ((e = hipMemcpyAsync(d_cursor.p, cur.data(), cur.size() * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
-      return hip_fail(e, "cursor H2D");
-    p.out = sl->planes;
-    prof_begin(MHMKC_STAGE_ESCAT);
-    e = mhm::launch_extract_scatter(p, nl, packed, stream);
+  uint64_t *hc = sl->pin.as<uint64_t>();
+  for (uint32_t i = 0; i < nseg; i++) hc[(size_t)(i % NSUB) * nb + i / NSUB] = sl->bases[i];
+  hc[nseg] = 0;  // overflow flag
+  if ((e = hipMemcpyAsync(dcur, hc, (size_t)nseg * 8 + 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "cursor H2D");
+  p.out = sl->planes;
+  prof_begin(MHMKC_STAGE_ESCAT);
+  e = mhm::launch_extract_scatter(p, nl, packed, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "extract_scatter");
+  if ((e = hipMemcpyAsync(hc, dcur, (size_t)nseg * 8 + 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(e, "cursor D2H");
+  sl->pending = true;
+  return MHMKC_OK;
+}
+
+// A batch as a device view. wins (the counted windows) comes from the host when it knows the offsets;
+// otherwise a small kernel counts them (and checks the offsets) and the host waits for the number.
+int mhmkc::add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known) {
+  hipError_t e;
+  if (!wins_known) {
+    if ((e = grow(d_hist, (size_t)nb * 8 + 64)) != hipSuccess) return hip_fail(e, "histogram");
+    unsigned long long *d_wins = d_hist.as<unsigned long long>() + nb;
+    unsigned int ef = 0;
+    prof_begin(MHMKC_STAGE_TILEIDX);
+    e = hipMemsetAsync(d_wins, 0, 8, stream);
+    if (e == hipSuccess) e = mhm::launch_count_windows(rv, k, d_wins, d_err.as<unsigned int>(), stream);
     prof_end();
-    if (e != hipSuccess) return hip_fail(e, "extract_scatter");
-    unsigned int errf = 0;
-    if ((e = hipMemcpyAsync(cur.data(), d_cursor.p, cur.size() * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-      return hip_fail(e, "cursor D2H");
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract_scatter");
-    if (!(errf & 2u)) break;
-    // a capped bucket overflowed: clear the flag (keep the bad-input bit) and redo with exact sizes
-    errf &= ~2u;
-    if ((e = hipMemcpy(d_err.p, &errf, 4, hipMemcpyHostToDevice)) != hipSuccess) return hip_fail(e, "flag reset");
-    exact = true;
-    st.exact_reruns++;
+    if (e == hipSuccess) e = hipMemcpyAsync(&wins, d_wins, 8, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&ef, d_err.p, 4, hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hip_fail(e, "window count");
+    if (ef & 4u)
+      return fail(MHMKC_EINVAL, "device read offsets are not a PackedReads CSR (offs[0] == 0, non-decreasing, reads "
+                                "<= 65535 bases, offs[n_reads] == n_bases)");
   }
-  uint64_t tot = 0;
-  for (uint32_t i = 0; i < nseg; i++) {
-    sl->counts[i] = cur[cidx(i)] - sl->bases[i];
-    tot += sl->counts[i];
+  if (wins == 0) return MHMKC_OK;
+  const int T = mhm::tile_bases(nl);
+  const uint64_t tiles64 = (rv.n_bases + T - 1) / T;
+  if (tiles64 >= 0x7fffffffull) return fail(MHMKC_EINVAL, "batch too large");
+  Slab *sl = new_slab();
+  sl->rv = rv;
+  sl->wins = wins;
+  sl->tiles = (uint32_t)tiles64;
+  sl->qcut = qcut_pending;
+  sl->n = 0;
+  st.occurrences += wins;
+  st.slabs++;
+  return extract(sl, getenv("MHMKC_DEBUG_EXACT") != nullptr);  // tests force the exact layout
+}
+
+// Read the final cursors of every pending slab (one wait for all of them); a slab whose capped segment
+// overflowed (skewed input: very repetitive reads) is extracted again with exact sizes.
+int mhmkc::resolve_slabs() {
+  bool any = false;
+  for (size_t s = 0; s < n_slabs; s++) any |= slabs[s]->pending;
+  if (!any) return MHMKC_OK;
+  hipError_t e;
+  const uint32_t nseg = nb * NSUB;
+  for (int pass = 0; pass < 2; pass++) {
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract");
+    bool redo = false;
+    for (size_t s = 0; s < n_slabs; s++) {
+      Slab *sl = slabs[s];
+      if (!sl->pending) continue;
+      const uint64_t *hc = sl->pin.as<uint64_t>();
+      if (hc[nseg] & 2u) {  // a capped segment overflowed: its excess records were not written
+        if (pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
+        st.exact_reruns++;
+        int rc = extract(sl, true);
+        if (rc) return rc;
+        redo = true;
+        continue;
+      }
+      uint64_t tot = 0;
+      for (uint32_t i = 0; i < nseg; i++) {
+        sl->counts[i] = hc[(size_t)(i % NSUB) * nb + i / NSUB] - sl->bases[i];
+        tot += sl->counts[i];
+      }
+      if (tot != sl->wins) return fail(MHMKC_EHIP, "internal: slab holds %llu records, expected %llu",
+                                       (unsigned long long)tot, (unsigned long long)sl->wins);
+      sl->n = tot;
+      sl->pending = false;
+    }
+    if (!redo) break;
   }
-  sl->n = tot;
-  st.occurrences += tot;
+  return MHMKC_OK;
+}
+
+// Host batch: copied to a device arena in chunks of whole reads on the copy stream, each chunk extracted
+// (as a slice view of the arena) as soon as its copy has landed. The host validates the offsets and counts
+// each chunk's windows while the previous chunk is on the wire.
+int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut) {
+  int rc = begin_round();
+  if (rc) return rc;
+  if (offs[0] != 0) return fail(MHMKC_EINVAL, "read_offsets[0] must be 0");
+  const uint64_t n_bases = offs[n_reads];
+  st.reads += n_reads;
+  st.bases += n_bases;
+  if (n_reads == 0) return MHMKC_OK;
+  if (n_reads >= 0xffffffffull) return fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
+  uint64_t chunk = CHUNK_BYTES;
+  if (const char *env = getenv("MHMKC_CHUNK_BYTES")) chunk = std::max<uint64_t>(64, strtoull(env, nullptr, 10));
+  hipError_t e;
+  Arena *ar = new_arena();
+  if ((e = grow(ar->bytes, n_bases + 64)) != hipSuccess || (e = grow(ar->offs, (n_reads + 1) * 8)) != hipSuccess)
+    return hip_fail(e, "input staging");
+  qcut_pending = qcut;
+  // the copies must not overwrite an arena that earlier work on the stream still reads
+  (void)hipEventRecord(ev_h2d0, stream);
+  if ((e = hipStreamWaitEvent(copy_stream, ev_h2d0, 0)) != hipSuccess) return hip_fail(e, "copy stream");
+  (void)hipEventRecord(ev_h2d0, copy_stream);
+  uint8_t *db = ar->bytes.as<uint8_t>();
+  uint64_t *dofs = ar->offs.as<uint64_t>();
+  const uint64_t kk = (uint64_t)k;
+  size_t n_ev = 0;
+  for (uint64_t r0 = 0; r0 < n_reads;) {
+    // the chunk [r0, r1): whole reads, about `chunk` bytes; validate them and count their windows
+    uint64_t r1 = r0, wins = 0;
+    const uint64_t b0 = offs[r0];
+    while (r1 < n_reads && (r1 == r0 || offs[r1] - b0 < chunk)) {
+      const uint64_t a = offs[r1], b = offs[r1 + 1];
+      if (b < a) return fail(MHMKC_EINVAL, "read_offsets must be non-decreasing (read %llu)", (unsigned long long)r1);
+      if (b - a > 65535)
+        return fail(MHMKC_EINVAL, "read %llu longer than 65535 (PackedRead read_len is uint16)", (unsigned long long)r1);
+      if (b - a > kk + 1) wins += b - a - kk - 1;
+      r1++;
+    }
+    const uint64_t b1 = offs[r1];
+    if (b1 > b0 && (e = hipMemcpyAsync(db + b0, bytes + b0, b1 - b0, hipMemcpyHostToDevice, copy_stream)) != hipSuccess)
+      return hip_fail(e, "input H2D");
+    if ((e = hipMemcpyAsync(dofs + r0, offs + r0, (r1 - r0 + 1) * 8, hipMemcpyHostToDevice, copy_stream)) != hipSuccess)
+      return hip_fail(e, "input H2D");
+    if (n_ev == chunk_ev.size()) {
+      hipEvent_t ev = nullptr;
+      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "event");
+      chunk_ev.push_back(ev);
+    }
+    hipEvent_t ev = chunk_ev[n_ev++];
+    if ((e = hipEventRecord(ev, copy_stream)) != hipSuccess || (e = hipStreamWaitEvent(stream, ev, 0)) != hipSuccess)
+      return hip_fail(e, "chunk event");
+    st.h2d_bytes += (b1 - b0) + (r1 - r0 + 1) * 8;
+    st.h2d_chunks++;
+    // slice view: the bytes from the 16-byte aligned position at or below the chunk's first read (the bytes
+    // before it belong to the previous chunk, copied earlier on the same stream)
+    mhm::ReadsView rv{};
+    rv.obase = b0 & ~15ull;
+    rv.head = (uint32_t)(b0 - rv.obase);
+    rv.bytes = db + rv.obase;
+    rv.offs = dofs + r0;
+    rv.n_reads = r1 - r0;
+    rv.n_bases = b1 - rv.obase;
+    if ((rc = add_view(rv, wins, true))) return rc;
+    r0 = r1;
+  }
+  (void)hipEventRecord(ev_h2d1, copy_stream);
+  // the caller's buffers are only borrowed for the call: wait for the copies (not for the extraction)
+  if ((e = hipStreamSynchronize(copy_stream)) != hipSuccess) return hip_fail(e, "input H2D");
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, ev_h2d0, ev_h2d1) == hipSuccess) st.ms_h2d = ms;
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// collectives between ranks: RCCL over xGMI (comm) or the caller's host transport (xp)
+
+int mhmkc::allgather_host(const void *send, void *recv, size_t bytes) {
+  if (has_xp) {
+    if (!xp.allgather || xp.allgather(xp.ctx, send, recv, bytes) != 0)
+      return fail(MHMKC_ETRANSPORT, "transport allgather failed");
+    return MHMKC_OK;
+  }
+  if (!comm) return fail(MHMKC_ETRANSPORT, "n_ranks > 1 needs comm_id or mhmkc_set_transport");
+  const int g = G();
+  hipError_t e;
+  ncclResult_t nr;
+  if ((e = grow(d_xg, bytes * (g + 1) + 64)) != hipSuccess) return hip_fail(e, "allgather buffer");
+  char *d = d_xg.as<char>();
+  if ((e = hipMemcpyAsync(d, send, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return hip_fail(e, "allgather H2D");
+  if ((nr = ncclAllGather(d, d + bytes, bytes, ncclUint8, comm, stream)) != ncclSuccess)
+    return fail(MHMKC_ERCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
+  if ((e = hipMemcpyAsync(recv, d + bytes, bytes * g, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess)
+    return hip_fail(e, "allgather D2H");
+  return MHMKC_OK;
+}
+
+// Point-to-point transfers of device buffers, given per peer in the same order on both sides (snd and rcv
+// sorted by peer). RCCL: one group of ncclSend/ncclRecv. Host transport: staged through pinned memory,
+// one alltoallv call.
+int mhmkc::move(const std::vector<Xfer> &snd, const std::vector<Xfer> &rcv) {
+  const int g = G();
+  hipError_t e;
+  for (auto &x : snd) st.bytes_sent += x.bytes;
+  for (auto &x : rcv) st.bytes_recv += x.bytes;
+  if (has_xp) {
+    std::vector<uint64_t> sb(g, 0), rb(g, 0);
+    uint64_t ts = 0, tr = 0;
+    for (auto &x : snd) sb[x.peer] += x.bytes, ts += x.bytes;
+    for (auto &x : rcv) rb[x.peer] += x.bytes, tr += x.bytes;
+    if ((e = x_send.ensure(ts + 64)) != hipSuccess || (e = x_recv.ensure(tr + 64)) != hipSuccess)
+      return hip_fail(e, "exchange staging");
+    char *hs = x_send.as<char>(), *hr = x_recv.as<char>();
+    uint64_t o = 0;
+    for (auto &x : snd) {
+      if (x.bytes && (e = hipMemcpyAsync(hs + o, x.ptr, x.bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return hip_fail(e, "exchange D2H");
+      o += x.bytes;
+    }
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange D2H");
+    if (!xp.alltoallv || xp.alltoallv(xp.ctx, hs, sb.data(), hr, rb.data()) != 0)
+      return fail(MHMKC_ETRANSPORT, "transport alltoallv failed");
+    o = 0;
+    for (auto &x : rcv) {
+      if (x.bytes && (e = hipMemcpyAsync(x.ptr, hr + o, x.bytes, hipMemcpyHostToDevice, stream)) != hipSuccess)
+        return hip_fail(e, "exchange H2D");
+      o += x.bytes;
+    }
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange H2D");  // x_recv is reused
+    return MHMKC_OK;
+  }
+  if (!comm) return fail(MHMKC_ETRANSPORT, "n_ranks > 1 needs comm_id or mhmkc_set_transport");
+  ncclResult_t nr;
+  if ((nr = ncclGroupStart()) != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupStart: %s", ncclGetErrorString(nr));
+  for (auto &x : snd)
+    if (x.bytes && (nr = ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, comm, stream)) != ncclSuccess) break;
+  if (nr == ncclSuccess)
+    for (auto &x : rcv)
+      if (x.bytes && (nr = ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, comm, stream)) != ncclSuccess) break;
+  ncclResult_t ne = ncclGroupEnd();
+  if (nr != ncclSuccess) return fail(MHMKC_ERCCL, "ncclSend/Recv: %s", ncclGetErrorString(nr));
+  if (ne != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupEnd: %s", ncclGetErrorString(ne));
   return MHMKC_OK;
 }
 
@@ -345,41 +613,23 @@ int mhmkc::add_device(const uint8_t *bytes, const uint64_t *offs, uint64_t n_rea
 // src/kcount/kmer_dht.cpp:133-149,222-224, and its flush/barrier, kmer_dht.cpp:227-231)
 
 int mhmkc::exchange(std::vector<Source> &srcs) {
-  const int G = cfg.n_ranks, me = cfg.rank;
+  const int g = G(), me = cfg.rank;
   const uint32_t no = n_owned();
-  hipError_t e;
-  ncclResult_t nr;
+  int rc;
   // 1. number of slabs of every rank
   uint64_t my_slabs = n_slabs;
-  if ((e = d_xcounts.ensure(8 * (size_t)G * 2)) != hipSuccess) return hip_fail(e, "exchange counts");
-  if ((e = hipMemcpyAsync(d_xcounts.p, &my_slabs, 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
-    return hip_fail(e, "exchange H2D");
-  uint64_t *dx = d_xcounts.as<uint64_t>();
-  if ((nr = ncclAllGather(dx, dx + G, 1, ncclUint64, comm, stream)) != ncclSuccess)
-    return fail(MHMKC_ERCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
-  std::vector<uint64_t> slabs_of(G);
-  if ((e = hipMemcpyAsync(slabs_of.data(), dx + G, 8 * (size_t)G, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-    return hip_fail(e, "exchange D2H");
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange sync");
+  std::vector<uint64_t> slabs_of(g);
+  if ((rc = allgather_host(&my_slabs, slabs_of.data(), 8))) return rc;
   const uint64_t ms = std::max<uint64_t>(1, *std::max_element(slabs_of.begin(), slabs_of.end()));
   // 2. per slab: segment counts [nseg] and segment starts [nseg + 1] (capped slabs have gaps), of every rank
   const uint32_t nseg = nb * NSUB;
   const size_t per = 2 * (size_t)nseg + 1;
-  std::vector<uint64_t> mine(ms * per, 0), all((size_t)G * ms * per, 0);
+  std::vector<uint64_t> mine(ms * per, 0), all((size_t)g * ms * per, 0);
   for (size_t s = 0; s < n_slabs; s++) {
     std::copy(slabs[s]->counts.begin(), slabs[s]->counts.end(), mine.begin() + s * per);
     std::copy(slabs[s]->bases.begin(), slabs[s]->bases.end(), mine.begin() + s * per + nseg);
   }
-  if ((e = d_xcounts.ensure(8 * (size_t)(G + 1) * ms * per)) != hipSuccess) return hip_fail(e, "exchange counts");
-  dx = d_xcounts.as<uint64_t>();
-  if ((e = hipMemcpyAsync(dx, mine.data(), 8 * ms * per, hipMemcpyHostToDevice, stream)) != hipSuccess)
-    return hip_fail(e, "exchange H2D");
-  if ((nr = ncclAllGather(dx, dx + ms * per, ms * per, ncclUint64, comm, stream)) != ncclSuccess)
-    return fail(MHMKC_ERCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
-  if ((e = hipMemcpyAsync(all.data(), dx + ms * per, 8 * (size_t)G * ms * per, hipMemcpyDeviceToHost, stream)) !=
-      hipSuccess)
-    return hip_fail(e, "exchange D2H");
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange sync");
+  if ((rc = allgather_host(mine.data(), all.data(), 8 * ms * per))) return rc;
   auto cnt = [&](int r, uint64_t s, uint32_t i) { return all[((size_t)r * ms + s) * per + i]; };
   auto bas = [&](int r, uint64_t s, uint32_t i) { return all[((size_t)r * ms + s) * per + nseg + i]; };
   // 3. receive layout: for each peer p != me, for each of its slabs s, the span of my owned range
@@ -389,7 +639,7 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
     uint64_t slab, off, n;
   };
   std::vector<Seg> rsegs;
-  for (int p = 0; p < G; p++) {
+  for (int p = 0; p < g; p++) {
     if (p == me) continue;
     for (uint64_t s = 0; s < slabs_of[p]; s++) {
       const uint64_t n = bas(p, s, own_hi * NSUB) - bas(p, s, own_lo * NSUB);
@@ -398,40 +648,31 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
     }
   }
   mhm::PlaneSet rps{};
-  int rc;
   if ((rc = set_planes(d_recv, recv_total, rps))) return rc;
-  // 4. grouped send/recv (per pair the calls are issued in the same slab/plane order on both sides)
-  prof_begin(MHMKC_STAGE_XCHG);
-  if ((nr = ncclGroupStart()) != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupStart: %s", ncclGetErrorString(nr));
-  uint64_t sent = 0;
-  for (int p = 0; p < G; p++) {
+  // 4. transfers, per peer in slab and plane order on both sides
+  const int np = compact ? 1 : nl;
+  const size_t wb = compact ? 4 : 8;  // bytes of a word-plane entry
+  std::vector<Xfer> snd, rcv;
+  for (int p = 0; p < g; p++) {
     if (p == me) continue;
     const uint32_t lo = owner_lo(p), hi = owner_lo(p + 1);
     for (size_t s = 0; s < n_slabs; s++) {
       const Slab *sl = slabs[s];
       const uint64_t a = sl->bases[lo * NSUB], b = sl->bases[hi * NSUB];
       if (b == a) continue;
-      if (compact) {
-        ncclSend((uint32_t *)sl->planes.w[0] + a, b - a, ncclUint32, p, comm, stream);
-      } else {
-        for (int w = 0; w < nl; w++) ncclSend(sl->planes.w[w] + a, b - a, ncclUint64, p, comm, stream);
-      }
-      if (sl->planes.ext) ncclSend(sl->planes.ext + a, b - a, ncclUint8, p, comm, stream);
-      sent += (b - a) * rec_bytes();
+      for (int w = 0; w < np; w++) snd.push_back({p, (char *)sl->planes.w[w] + a * wb, (b - a) * wb});
+      if (sl->planes.ext) snd.push_back({p, sl->planes.ext + a, b - a});
     }
   }
-  for (const Seg &g : rsegs) {
-    if (!g.n) continue;
-    if (compact) {
-      ncclRecv((uint32_t *)rps.w[0] + g.off, g.n, ncclUint32, g.peer, comm, stream);
-    } else {
-      for (int w = 0; w < nl; w++) ncclRecv(rps.w[w] + g.off, g.n, ncclUint64, g.peer, comm, stream);
-    }
-    if (rps.ext) ncclRecv(rps.ext + g.off, g.n, ncclUint8, g.peer, comm, stream);
+  for (const Seg &sg : rsegs) {
+    if (!sg.n) continue;
+    for (int w = 0; w < np; w++) rcv.push_back({sg.peer, (char *)rps.w[w] + sg.off * wb, sg.n * wb});
+    if (rps.ext) rcv.push_back({sg.peer, rps.ext + sg.off, sg.n});
   }
-  if ((nr = ncclGroupEnd()) != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupEnd: %s", ncclGetErrorString(nr));
+  prof_begin(MHMKC_STAGE_XCHG);
+  rc = move(snd, rcv);
   prof_end();
-  st.bytes_sent += sent;
+  if (rc) return rc;
   // 5. sources: local slabs (owned range in place) + received segments
   for (size_t s = 0; s < n_slabs; s++) {
     Source src;
@@ -440,14 +681,14 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
     src.count.assign(slabs[s]->counts.begin() + own_lo * NSUB, slabs[s]->counts.begin() + own_hi * NSUB);
     srcs.push_back(std::move(src));
   }
-  for (const Seg &g : rsegs) {
+  for (const Seg &sg : rsegs) {
     Source src;
     src.planes = rps;
     src.start.resize((size_t)no * NSUB);
     src.count.resize((size_t)no * NSUB);
     for (uint32_t i = 0; i < no * NSUB; i++) {
-      src.start[i] = g.off + (bas(g.peer, g.slab, own_lo * NSUB + i) - bas(g.peer, g.slab, own_lo * NSUB));
-      src.count[i] = cnt(g.peer, g.slab, own_lo * NSUB + i);
+      src.start[i] = sg.off + (bas(sg.peer, sg.slab, own_lo * NSUB + i) - bas(sg.peer, sg.slab, own_lo * NSUB));
+      src.count[i] = cnt(sg.peer, sg.slab, own_lo * NSUB + i);
     }
     srcs.push_back(std::move(src));
   }
@@ -457,39 +698,94 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
 // ------------------------------------------------------------------------------------------------
 // contig pass: extract, fold and bucket the contig k-mers (kcount_ctg.hip); k_count applies them
 
+// With several ranks every rank needs the contigs of all ranks, in one order, for the k-mers of its hash
+// range: the contigs are all-gathered (rank order). They are small next to the reads (an assembly's
+// contigs are about the genome; the reads are 30x it).
+int mhmkc::gather_ctgs(std::vector<uint8_t> &gb, std::vector<uint64_t> &go, std::vector<uint64_t> &gw,
+                       std::vector<uint16_t> &gd) {
+  const int g = G();
+  int rc;
+  uint64_t mine[2] = {ctg_depth.size(), ctg_bytes.size()};
+  std::vector<uint64_t> sizes(2 * (size_t)g);
+  if ((rc = allgather_host(mine, sizes.data(), 16))) return rc;
+  uint64_t max_c = 0, max_b = 0, tot_c = 0;
+  for (int r = 0; r < g; r++) {
+    max_c = std::max(max_c, sizes[2 * r]);
+    max_b = std::max(max_b, sizes[2 * r + 1]);
+    tot_c += sizes[2 * r];
+  }
+  gb.clear();
+  go.assign(1, 0);
+  gw.assign(1, 0);
+  gd.clear();
+  if (!tot_c) return MHMKC_OK;
+  // one record per rank: [lengths: max_c u64][depths: max_c u16, padded to 8][bytes: max_b, padded to 8]
+  const size_t rec = 8 * max_c + align_up(2 * max_c, 8) + align_up(max_b, 8);
+  std::vector<uint8_t> mr(rec, 0), all(rec * g);
+  for (size_t i = 0; i < ctg_depth.size(); i++) ((uint64_t *)mr.data())[i] = ctg_offs[i + 1] - ctg_offs[i];
+  if (!ctg_depth.empty()) memcpy(mr.data() + 8 * max_c, ctg_depth.data(), 2 * ctg_depth.size());
+  if (!ctg_bytes.empty()) memcpy(mr.data() + 8 * max_c + align_up(2 * max_c, 8), ctg_bytes.data(), ctg_bytes.size());
+  if ((rc = allgather_host(mr.data(), all.data(), rec))) return rc;
+  for (int r = 0; r < g; r++) {
+    const uint8_t *q = all.data() + rec * r;
+    const uint64_t *lens = (const uint64_t *)q;
+    const uint16_t *dep = (const uint16_t *)(q + 8 * max_c);
+    const uint8_t *byt = q + 8 * max_c + align_up(2 * max_c, 8);
+    gb.insert(gb.end(), byt, byt + sizes[2 * r + 1]);
+    for (uint64_t i = 0; i < sizes[2 * r]; i++) {
+      const uint64_t L = lens[i];
+      go.push_back(go.back() + L);
+      gw.push_back(gw.back() + (L >= (uint64_t)k + 2 ? L - k - 1 : 0));
+      gd.push_back(dep[i]);
+    }
+  }
+  if (gw.back() >= 0xffffffffull) return fail(MHMKC_EINVAL, "at most 2^32-1 contig k-mers per round");
+  return MHMKC_OK;
+}
+
 int mhmkc::prepare_ctgs() {
   ctg_n = 0;
-  const uint64_t W = ctg_win.back();
+  std::vector<uint8_t> gb;
+  std::vector<uint64_t> go, gw;
+  std::vector<uint16_t> gd;
+  const std::vector<uint8_t> *cb_ = &ctg_bytes;
+  const std::vector<uint64_t> *co = &ctg_offs, *cw = &ctg_win;
+  const std::vector<uint16_t> *cd = &ctg_depth;
+  if (G() > 1) {
+    int rc = gather_ctgs(gb, go, gw, gd);
+    if (rc) return rc;
+    cb_ = &gb, co = &go, cw = &gw, cd = &gd;
+  }
+  const uint64_t W = cw->back();
   if (!W) return MHMKC_OK;
-  if (cfg.n_ranks > 1) return fail(MHMKC_EUNSUPPORTED, "the contig pass is single-rank in this version");
   hipError_t e;
-  const uint64_t nc = ctg_depth.size();
-  if ((e = d_ctg_bytes.ensure(ctg_bytes.size() + 64)) != hipSuccess ||
-      (e = d_ctg_offs.ensure((nc + 1) * 8)) != hipSuccess || (e = d_ctg_win.ensure((nc + 1) * 8)) != hipSuccess ||
-      (e = d_ctg_depth.ensure(nc * 2 + 2)) != hipSuccess)
+  const uint64_t nc = cd->size();
+  if ((e = grow(d_ctg_bytes, cb_->size() + 64)) != hipSuccess || (e = grow(d_ctg_offs, (nc + 1) * 8)) != hipSuccess ||
+      (e = grow(d_ctg_win, (nc + 1) * 8)) != hipSuccess || (e = grow(d_ctg_depth, nc * 2 + 2)) != hipSuccess)
     return hip_fail(e, "contig staging");
-  if ((e = hipMemcpyAsync(d_ctg_bytes.p, ctg_bytes.data(), ctg_bytes.size(), hipMemcpyHostToDevice, stream)) !=
-          hipSuccess ||
-      (e = hipMemcpyAsync(d_ctg_offs.p, ctg_offs.data(), (nc + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess ||
-      (e = hipMemcpyAsync(d_ctg_win.p, ctg_win.data(), (nc + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess ||
-      (e = hipMemcpyAsync(d_ctg_depth.p, ctg_depth.data(), nc * 2, hipMemcpyHostToDevice, stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(d_ctg_bytes.p, cb_->data(), cb_->size(), hipMemcpyHostToDevice, stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_ctg_offs.p, co->data(), (nc + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_ctg_win.p, cw->data(), (nc + 1) * 8, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_ctg_depth.p, cd->data(), nc * 2, hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "contig H2D");
   const size_t sb = mhm::ctg_scratch_bytes(W, nl);
-  if ((e = d_ctg_scratch.ensure(sb)) != hipSuccess) return hip_fail(e, "contig scratch");
+  if ((e = grow(d_ctg_scratch, sb)) != hipSuccess) return hip_fail(e, "contig scratch");
   uint64_t *keys[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int w = 0; w < nl; w++) {
-    if ((e = d_ctg_keys[w].ensure(W * 8)) != hipSuccess) return hip_fail(e, "contig keys");
+    if ((e = grow(d_ctg_keys[w], W * 8)) != hipSuccess) return hip_fail(e, "contig keys");
     keys[w] = d_ctg_keys[w].as<uint64_t>();
   }
-  if ((e = d_ctg_state.ensure(W * 4)) != hipSuccess || (e = d_ctg_bucket.ensure(W * 4)) != hipSuccess ||
-      (e = d_ctg_done.ensure(W)) != hipSuccess)
+  if ((e = grow(d_ctg_state, W * 4)) != hipSuccess || (e = grow(d_ctg_bucket, W * 4)) != hipSuccess ||
+      (e = grow(d_ctg_done, W)) != hipSuccess)
     return hip_fail(e, "contig entries");
   mhm::CtgView cv{d_ctg_bytes.as<uint8_t>(), d_ctg_offs.as<uint64_t>(), d_ctg_depth.as<uint16_t>(),
                   d_ctg_win.as<uint64_t>(), nc, W};
   prof_begin(MHMKC_STAGE_OTHER);
-  e = mhm::ctg_prepare(cv, k, nl, compact, 1, cfg.dmin_thres, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, d_ctg_scratch.p, sb, keys,
-                       d_ctg_state.as<uint32_t>(), d_ctg_bucket.as<uint32_t>(), &ctg_n, d_err.as<unsigned int>(),
-                       stream);
+  // the synchronous copies above keep the host vectors alive long enough: ctg_prepare waits for its
+  // fold count before returning
+  e = mhm::ctg_prepare(cv, k, nl, compact, 1, dmin, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, own_hi,
+                       d_ctg_scratch.p, sb, keys, d_ctg_state.as<uint32_t>(), d_ctg_bucket.as<uint32_t>(), &ctg_n,
+                       d_err.as<unsigned int>(), stream);
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "contig pass");
   st.ctg_kmers = ctg_n;
@@ -497,17 +793,116 @@ int mhmkc::prepare_ctgs() {
 }
 
 // ------------------------------------------------------------------------------------------------
+// owner hand-off: move every finished k-mer to get_kmer_target_rank (MHMKC_OWNER_MINIMIZER)
+
+int mhmkc::handoff() {
+  const int g = G(), me = cfg.rank;
+  hipError_t e;
+  int rc;
+  const uint64_t n = n_out;
+  if ((e = grow(d_dest, n + 64)) != hipSuccess || (e = grow(d_ohist, 16 * (size_t)g + 64)) != hipSuccess)
+    return hip_fail(e, "hand-off buffers");
+  std::vector<uint64_t> hist(g, 0), start(g, 0);
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = hipMemsetAsync(d_ohist.p, 0, 8 * (size_t)g, stream);
+  if (e == hipSuccess)
+    e = mhm::launch_owner_hist(d_out_keys.as<uint64_t>(), n, nlo, k, mlen, g, d_dest.as<uint8_t>(),
+                               d_ohist.as<unsigned long long>(), stream);
+  prof_end();
+  if (e == hipSuccess) e = hipMemcpyAsync(hist.data(), d_ohist.p, 8 * (size_t)g, hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return hip_fail(e, "owner histogram");
+  for (int r = 1; r < g; r++) start[r] = start[r - 1] + hist[r - 1];
+  // rows grouped by owner into the second output set
+  if ((e = grow(d_out2_keys, n * 8 * nlo + 64)) != hipSuccess || (e = grow(d_out2_counts, n * 2 + 64)) != hipSuccess ||
+      (e = grow(d_out2_left, n + 64)) != hipSuccess || (e = grow(d_out2_right, n + 64)) != hipSuccess)
+    return hip_fail(e, "hand-off buffers");
+  mhm::OutRows in{d_out_keys.as<uint64_t>(), d_out_counts.as<uint16_t>(), d_out_left.as<char>(), d_out_right.as<char>()};
+  mhm::OutRows grp{d_out2_keys.as<uint64_t>(), d_out2_counts.as<uint16_t>(), d_out2_left.as<char>(),
+                   d_out2_right.as<char>()};
+  prof_begin(MHMKC_STAGE_OTHER);
+  e = hipMemcpyAsync(d_ohist.as<uint64_t>() + g, start.data(), 8 * (size_t)g, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess)
+    e = mhm::launch_owner_scatter(in, n, nlo, d_dest.as<uint8_t>(), g, d_ohist.as<unsigned long long>() + g, grp, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "owner scatter");
+  // who sends whom how many rows
+  std::vector<uint64_t> mat((size_t)g * g);
+  if ((rc = allgather_host(hist.data(), mat.data(), 8 * (size_t)g))) return rc;
+  auto M = [&](int from, int to) { return mat[(size_t)from * g + to]; };
+  uint64_t new_n = 0;
+  std::vector<uint64_t> roff(g, 0);
+  roff[me] = 0;
+  new_n = M(me, me);
+  for (int p = 0; p < g; p++) {
+    if (p == me) continue;
+    roff[p] = new_n;
+    new_n += M(p, me);
+  }
+  // the final rows go back into the first output set (its old contents were grouped into the second)
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "owner scatter");
+  if ((e = grow(d_out_keys, new_n * 8 * nlo + 64)) != hipSuccess || (e = grow(d_out_counts, new_n * 2 + 64)) != hipSuccess ||
+      (e = grow(d_out_left, new_n + 64)) != hipSuccess || (e = grow(d_out_right, new_n + 64)) != hipSuccess)
+    return hip_fail(e, "hand-off output");
+  const size_t kb = 8 * (size_t)nlo;
+  char *ok = d_out_keys.as<char>(), *oc = d_out_counts.as<char>(), *ol = d_out_left.as<char>(),
+       *orr = d_out_right.as<char>();
+  char *gk = d_out2_keys.as<char>(), *gc = d_out2_counts.as<char>(), *gl = d_out2_left.as<char>(),
+       *gr = d_out2_right.as<char>();
+  const uint64_t mine_n = hist[me], ms = start[me];
+  if (mine_n) {
+    if ((e = hipMemcpyAsync(ok, gk + ms * kb, mine_n * kb, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(oc, gc + ms * 2, mine_n * 2, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(ol, gl + ms, mine_n, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(orr, gr + ms, mine_n, hipMemcpyDeviceToDevice, stream)) != hipSuccess)
+      return hip_fail(e, "hand-off copy");
+  }
+  std::vector<Xfer> snd, rcv;
+  for (int p = 0; p < g; p++) {
+    if (p == me) continue;
+    const uint64_t a = start[p], c = hist[p];
+    if (c) {
+      snd.push_back({p, gk + a * kb, c * kb});
+      snd.push_back({p, gc + a * 2, c * 2});
+      snd.push_back({p, gl + a, c});
+      snd.push_back({p, gr + a, c});
+      st.handoff_sent += c;
+    }
+    const uint64_t rn = M(p, me), ro = roff[p];
+    if (rn) {
+      rcv.push_back({p, ok + ro * kb, rn * kb});
+      rcv.push_back({p, oc + ro * 2, rn * 2});
+      rcv.push_back({p, ol + ro, rn});
+      rcv.push_back({p, orr + ro, rn});
+      st.handoff_recv += rn;
+    }
+  }
+  const uint64_t sent0 = st.bytes_sent, recv0 = st.bytes_recv;
+  prof_begin(MHMKC_STAGE_XCHG);
+  rc = move(snd, rcv);
+  prof_end();
+  st.bytes_sent = sent0;  // bytes_* count the record exchange only
+  st.bytes_recv = recv0;
+  if (rc) return rc;
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "hand-off");
+  n_out = new_n;
+  st.n_out = new_n;
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 // fine partition + LDS count + finalize
 
 // Fine buckets are capped at 1.25x their expected size (+256): a single scatter pass, no histogram. If a
-// bucket overflows, the count kernel's results are discarded and the pass is redone with part_hist + scan.
+// bucket overflows, the count kernel returns at once and the pass is redone with part_hist + scan.
 int mhmkc::finish(uint64_t *n_out_ret) {
   int rc = begin_round();
   if (rc) return rc;
+  if ((rc = resolve_slabs())) return rc;
   hipError_t e;
   const uint32_t no = n_owned();
   std::vector<Source> srcs;
-  if (cfg.n_ranks > 1) {
+  if (G() > 1) {
     if ((rc = exchange(srcs))) return rc;
   } else {
     for (size_t s = 0; s < n_slabs; s++) {
@@ -558,14 +953,15 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if (n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
   uint64_t xcd_max = 0;
   for (int x = 0; x < 8; x++) xcd_max = std::max(xcd_max, xcd_start[x + 1] - xcd_start[x]);
-  if ((e = d_chunks.ensure(std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun) + 4 * (n_chunks + 1) + 256)) !=
+  if ((e = grow(d_chunks, std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun) + 4 * (n_chunks + 1) + 256)) !=
       hipSuccess)
     return hip_fail(e, "chunk table");
   mhm::SRun *d_runs = d_chunks.as<mhm::SRun>();
   uint32_t *d_chunk_run = (uint32_t *)(d_chunks.as<char>() + align_up(runs.size() * sizeof(mhm::SRun), 256));
-  if ((e = d_srcs.ensure(std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 16 * (size_t)no)) != hipSuccess)
+  if ((e = grow(d_srcs, std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 16 * (size_t)no)) != hipSuccess)
     return hip_fail(e, "source table");
   unsigned long long *d_cfit = (unsigned long long *)(d_srcs.as<char>() + align_up(ps.size() * sizeof(mhm::PlaneSet), 16));
+  // the tables are small: synchronous copies (their host vectors go out of scope)
   if (!runs.empty()) {
     if ((e = hipMemcpyAsync(d_runs, runs.data(), runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, stream)) !=
         hipSuccess)
@@ -595,7 +991,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     sp.compact = compact;
     std::vector<uint32_t> reg(mhm::SKETCH_M);
     prof_begin(MHMKC_STAGE_OTHER);
-    if ((e = d_hll.ensure(4 * mhm::SKETCH_M)) != hipSuccess ||
+    if ((e = grow(d_hll, 4 * mhm::SKETCH_M)) != hipSuccess ||
         (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_M, stream)) != hipSuccess ||
         (e = mhm::launch_sketch(sp, (uint32_t)n_c0, d_hll.as<unsigned int>(), nl, packed, stream)) != hipSuccess)
       return hip_fail(e, "distinct sketch");
@@ -629,15 +1025,15 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   }
   if (no && (e = hipMemcpyAsync(d_cfit, cfit.data(), 16 * (size_t)no, hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "layout H2D");
-  if ((e = d_fine_hist.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
-  if ((e = d_fine_base.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
-  if ((e = d_fine_cursor.ensure((size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine cursor");
+  if ((e = grow(d_fine_hist, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
+  if ((e = grow(d_fine_base, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
+  if ((e = grow(d_fine_cursor, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine cursor");
   const uint64_t out_cap = owned / 2 + ctg_n + 1;
-  if ((e = d_out_keys.ensure(out_cap * 8 * nlo)) != hipSuccess) return hip_fail(e, "output keys");
-  if ((e = d_out_counts.ensure(out_cap * 2)) != hipSuccess) return hip_fail(e, "output counts");
-  if ((e = d_out_left.ensure(out_cap)) != hipSuccess) return hip_fail(e, "output left");
-  if ((e = d_out_right.ensure(out_cap)) != hipSuccess) return hip_fail(e, "output right");
-  if ((e = d_out_cursor.ensure(8)) != hipSuccess) return hip_fail(e, "output cursor");
+  if ((e = grow(d_out_keys, out_cap * 8 * nlo)) != hipSuccess) return hip_fail(e, "output keys");
+  if ((e = grow(d_out_counts, out_cap * 2)) != hipSuccess) return hip_fail(e, "output counts");
+  if ((e = grow(d_out_left, out_cap)) != hipSuccess) return hip_fail(e, "output left");
+  if ((e = grow(d_out_right, out_cap)) != hipSuccess) return hip_fail(e, "output right");
+  if ((e = grow(d_out_cursor, 8)) != hipSuccess) return hip_fail(e, "output cursor");
 
   mhm::PartitionParams pp{};
   pp.runs = d_runs;
@@ -669,7 +1065,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.k = k;
   cp.cap = mhm::count_cap(nl, compact);
   if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
-  cp.dmin_thres = cfg.dmin_thres;
+  cp.dmin_thres = dmin;
   cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
   cp.nlo = nlo;
   cp.out_keys = d_out_keys.as<uint64_t>();
@@ -678,6 +1074,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.out_right = d_out_right.as<char>();
   cp.out_cursor = d_out_cursor.as<unsigned long long>();
   cp.stats = d_stats.as<unsigned long long>();
+  cp.err = d_err.as<unsigned int>();
   cp.ctg_n = ctg_n;
   for (int w = 0; w < 4; w++) cp.ctg_keys[w] = w < nl ? d_ctg_keys[w].as<uint64_t>() : nullptr;
   cp.ctg_state = d_ctg_state.as<uint32_t>();
@@ -689,6 +1086,11 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   unsigned int errf = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     mhm::PlaneSet r2{};
+    if (exact) {
+      if ((rc = set_planes(d_r2, owned, r2, true))) return rc;
+    } else {
+      if ((rc = set_planes(d_r2, r2_size, r2, true))) return rc;
+    }
     prof_begin(MHMKC_STAGE_OTHER);
     e = hipMemsetAsync(d_out_cursor.p, 0, 8, stream);
     if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_ALLOC, stream);
@@ -711,11 +1113,9 @@ int mhmkc::finish(uint64_t *n_out_ret) {
                            d_fine_cursor.as<unsigned long long>(), n_fine, stream);
       prof_end();
       if (e != hipSuccess) return hip_fail(e, "scan");
-      if ((rc = set_planes(d_r2, owned, r2, true))) return rc;
     } else {
       pp.coarse_base = d_cfit;
       pp.coarse_fcap = d_cfit + no;
-      if ((rc = set_planes(d_r2, r2_size, r2, true))) return rc;
     }
     pp.out = r2;
     prof_begin(MHMKC_STAGE_SSCAT);
@@ -741,7 +1141,6 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   }
   float ms = 0;
   if (hipEventElapsedTime(&ms, ev_begin, ev_end) == hipSuccess) st.ms_total = ms;
-  prof_collect();
   finished = true;
   if (errf & 1u) return fail(MHMKC_EBADCHAR, "input byte with a base code > 4 (not A,C,G,T,N)");
   if (stats[mhm::STAT_N - 1]) return fail(MHMKC_EHIP, "internal: LDS probe bound exceeded");
@@ -759,9 +1158,15 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   st.count_sum = stats[mhm::STAT_COUNTSUM];
   st.overflow_sweeps = stats[mhm::STAT_SWEEPS];
   st.max_bucket = stats[mhm::STAT_MAXBUCKET];
+  st.lds_misses = stats[mhm::STAT_MISSES];
+  st.lds_ext_adds = stats[mhm::STAT_EXTADDS];
   st.dropped = 0;
   n_out = st.n_out;
   if (n_out > out_cap) return fail(MHMKC_EHIP, "internal: output overflow");
+  if (cfg.output_owner == MHMKC_OWNER_MINIMIZER && G() > 1) {
+    if ((rc = handoff())) return rc;
+  }
+  prof_collect();
   if (n_out_ret) *n_out_ret = n_out;
   return MHMKC_OK;
 }
@@ -787,6 +1192,8 @@ int mhmkc_config_init(mhmkc_config *cfg) {
   cfg->n_ranks = 1;
   cfg->comm_id = nullptr;
   cfg->stream = nullptr;
+  cfg->output_owner = MHMKC_OWNER_HASH;
+  cfg->minimizer_len = 0;
   return MHMKC_OK;
 }
 
@@ -842,8 +1249,13 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     g_create_error = "bad rank / n_ranks (1..8 ranks, one per GPU of a node)";
     return MHMKC_EINVAL;
   }
-  if (cfg->n_ranks > 1 && !cfg->comm_id) {
-    g_create_error = "comm_id required when n_ranks > 1";
+  if (cfg->output_owner != MHMKC_OWNER_HASH && cfg->output_owner != MHMKC_OWNER_MINIMIZER) {
+    g_create_error = "output_owner must be MHMKC_OWNER_HASH or MHMKC_OWNER_MINIMIZER";
+    return MHMKC_EINVAL;
+  }
+  const int mlen = cfg->minimizer_len ? cfg->minimizer_len : mhm::minimizer_len_for(k);
+  if (cfg->output_owner == MHMKC_OWNER_MINIMIZER && (mlen < 1 || mlen > 28 || mlen > k)) {
+    g_create_error = "minimizer_len must be in [1, min(k, 28)] (Kmer::get_minimizer_fast)";
     return MHMKC_EINVAL;
   }
   mhmkc *h = new mhmkc();
@@ -851,6 +1263,9 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   h->k = k;
   h->nl = nl;
   h->nlo = nlo;
+  h->mlen = mlen;
+  h->dmin = cfg->dmin_thres;
+  h->qcut_pending = cfg->qual_cutoff;
   h->packed = mhm::ext_packs(k, nl);
   h->hbits = mhm::stored_hash_bits(k, nl, h->packed);
   int extra = 0;
@@ -886,14 +1301,16 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     }
     h->own_stream = true;
   }
-  if ((e = hipEventCreate(&h->ev_begin)) != hipSuccess || (e = hipEventCreate(&h->ev_end)) != hipSuccess ||
+  if ((e = hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreate(&h->ev_begin)) != hipSuccess || (e = hipEventCreate(&h->ev_end)) != hipSuccess ||
+      (e = hipEventCreate(&h->ev_h2d0)) != hipSuccess || (e = hipEventCreate(&h->ev_h2d1)) != hipSuccess ||
       (e = h->d_err.ensure(16)) != hipSuccess || (e = h->d_stats.ensure(8 * mhm::STAT_ALLOC)) != hipSuccess ||
       (e = hipMemset(h->d_err.p, 0, 16)) != hipSuccess) {
     g_create_error = std::string("init: ") + hipGetErrorString(e);
     mhmkc_destroy(h);
     return MHMKC_EHIP;
   }
-  if (cfg->n_ranks > 1) {
+  if (cfg->n_ranks > 1 && cfg->comm_id) {
     ncclUniqueId id;
     memcpy(&id, cfg->comm_id, sizeof id);
     ncclResult_t r = ncclCommInitRank(&h->comm, cfg->n_ranks, id, cfg->rank);
@@ -911,29 +1328,43 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
 void mhmkc_destroy(mhmkc_t h) {
   if (!h) return;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
   if (h->comm) ncclCommDestroy(h->comm);
   for (Slab *s : h->slabs) {
     s->buf.release();
+    s->meta.release();
+    s->pin.release();
     delete s;
   }
-  DevBuf *bufs[] = {&h->d_hist,     &h->d_cursor,    &h->d_tiles,     &h->d_err,       &h->d_stats,
-                    &h->d_fine_hist, &h->d_fine_base, &h->d_fine_cursor, &h->d_chunks,  &h->d_srcs,
-                    &h->d_r2,       &h->d_out_keys,  &h->d_out_counts, &h->d_out_left, &h->d_out_right,
-                    &h->d_out_cursor, &h->d_recv,    &h->d_xcounts,   &h->d_in_bytes,  &h->d_in_offs,
-                    &h->d_hll,       &h->d_fq_text,   &h->d_fq_chunk,  &h->d_fq_lines,  &h->d_fq_len,
-                    &h->d_fq_tmp,    &h->d_fq_bytes,  &h->d_fq_offs,   &h->d_fq_err};
+  for (Arena *a : h->arenas) {
+    a->bytes.release();
+    a->offs.release();
+    delete a;
+  }
+  DevBuf *bufs[] = {&h->d_hist,     &h->d_tiles,      &h->d_err,        &h->d_stats,      &h->d_fine_hist,
+                    &h->d_fine_base, &h->d_fine_cursor, &h->d_chunks,    &h->d_srcs,       &h->d_r2,
+                    &h->d_out_keys, &h->d_out_counts, &h->d_out_left,   &h->d_out_right,  &h->d_out_cursor,
+                    &h->d_recv,     &h->d_xg,         &h->d_hll,        &h->d_dest,       &h->d_ohist,
+                    &h->d_out2_keys, &h->d_out2_counts, &h->d_out2_left, &h->d_out2_right, &h->d_mh,
+                    &h->d_fq_text,  &h->d_fq_chunk,   &h->d_fq_lines,   &h->d_fq_len,     &h->d_fq_tmp,
+                    &h->d_fq_bytes, &h->d_fq_offs,    &h->d_fq_err};
   for (DevBuf *b : bufs) b->release();
   DevBuf *cbufs[] = {&h->d_ctg_bytes, &h->d_ctg_offs, &h->d_ctg_win,   &h->d_ctg_depth, &h->d_ctg_scratch,
                      &h->d_ctg_state, &h->d_ctg_bucket, &h->d_ctg_done, &h->d_ctg_keys[0], &h->d_ctg_keys[1],
                      &h->d_ctg_keys[2], &h->d_ctg_keys[3]};
   for (DevBuf *b : cbufs) b->release();
+  h->x_send.release();
+  h->x_recv.release();
   for (auto &p : h->prof) {
     h->ev_pool.push_back(p.a);
     h->ev_pool.push_back(p.b);
   }
   for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
-  if (h->ev_begin) (void)hipEventDestroy(h->ev_begin);
-  if (h->ev_end) (void)hipEventDestroy(h->ev_end);
+  for (hipEvent_t ev : h->chunk_ev) (void)hipEventDestroy(ev);
+  hipEvent_t evs[] = {h->ev_begin, h->ev_end, h->ev_h2d0, h->ev_h2d1};
+  for (hipEvent_t ev : evs)
+    if (ev) (void)hipEventDestroy(ev);
+  if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -942,22 +1373,41 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_
                            uint64_t n_bases) {
   if (!h) return MHMKC_EINVAL;
   if (n_reads && (!d_bytes || !d_offs)) return h->fail(MHMKC_EINVAL, "null device buffer");
-  return h->add_device(d_bytes, d_offs, n_reads, n_bases, h->cfg.qual_cutoff);
+  int rc = h->begin_round();  // (records the round's start event before the reads are counted)
+  if (rc) return rc;
+  h->st.reads += n_reads;
+  h->st.bases += n_bases;
+  if (n_reads == 0) return MHMKC_OK;
+  if (n_reads >= 0xffffffffull) return h->fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
+  h->qcut_pending = h->cfg.qual_cutoff;
+  mhm::ReadsView rv{d_bytes, d_offs, n_reads, n_bases, 0, 0, 0};
+  return h->add_view(rv, 0, false);
 }
 
-// FASTQ text on the device -> PackedReads in d_fq_bytes / d_fq_offs -> add_device (fastq.hip).
+int mhmkc_wait_stream(mhmkc_t h, void *stream) {
+  if (!h) return MHMKC_EINVAL;
+  hipEvent_t ev = h->take_event();
+  hipError_t e = hipEventRecord(ev, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, ev, 0);
+  h->ev_pool.push_back(ev);  // reusable: a later record replaces the captured work, the wait is enqueued
+  return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "wait_stream");
+}
+
+// FASTQ text on the device -> PackedReads in d_fq_bytes / d_fq_offs -> add_view (fastq.hip).
 int mhmkc::add_fastq(const char *d_text, uint64_t n) {
   int rc = begin_round();
   if (rc) return rc;
   fq_reads = fq_bases = 0;
   if (n == 0) return MHMKC_OK;
   if (n > mhm::FQ_LE_MASK) return fail(MHMKC_EINVAL, "FASTQ text larger than 2^40 bytes in one call");
+  // the packed reads of an earlier add_fastq may still be read by a pending extraction: settle it first
+  if ((rc = resolve_slabs())) return rc;
   hipError_t e;
   const uint64_t nch = (n + mhm::FQ_CHUNK - 1) / mhm::FQ_CHUNK;
-  if ((e = d_fq_chunk.ensure((nch + 1) * 16)) != hipSuccess) return hip_fail(e, "fastq chunk counts");
+  if ((e = grow(d_fq_chunk, (nch + 1) * 16)) != hipSuccess) return hip_fail(e, "fastq chunk counts");
   unsigned long long *cnt = d_fq_chunk.as<unsigned long long>(), *cbase = cnt + nch + 1;
   size_t tmp_bytes = mhm::fq_scan_tmp_bytes(nch + 1);
-  if ((e = d_fq_tmp.ensure(tmp_bytes)) != hipSuccess) return hip_fail(e, "fastq scan scratch");
+  if ((e = grow(d_fq_tmp, tmp_bytes)) != hipSuccess) return hip_fail(e, "fastq scan scratch");
   prof_begin(MHMKC_STAGE_OTHER);
   e = hipMemsetAsync(cnt + nch, 0, 8, stream);
   if (e == hipSuccess) e = mhm::launch_fq_count(d_text, n, cnt, stream);
@@ -973,13 +1423,13 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n) {
   // fgets returns a last line without its newline
   const uint64_t lines = newlines + (last != '\n' ? 1 : 0);
   const uint64_t R = lines / 4;
-  if ((e = d_fq_lines.ensure(std::max<uint64_t>(lines, 1) * 8)) != hipSuccess) return hip_fail(e, "fastq lines");
-  if ((e = d_fq_len.ensure((R + 1) * 8)) != hipSuccess || (e = d_fq_offs.ensure((R + 1) * 8)) != hipSuccess ||
-      (e = d_fq_err.ensure(8)) != hipSuccess)
+  if ((e = grow(d_fq_lines, std::max<uint64_t>(lines, 1) * 8)) != hipSuccess) return hip_fail(e, "fastq lines");
+  if ((e = grow(d_fq_len, (R + 1) * 8)) != hipSuccess || (e = grow(d_fq_offs, (R + 1) * 8)) != hipSuccess ||
+      (e = grow(d_fq_err, 8)) != hipSuccess)
     return hip_fail(e, "fastq records");
   const size_t tmp2 = mhm::fq_scan_tmp_bytes(R + 1);
   if (tmp2 > tmp_bytes) {
-    if ((e = d_fq_tmp.ensure(tmp2)) != hipSuccess) return hip_fail(e, "fastq scan scratch");
+    if ((e = grow(d_fq_tmp, tmp2)) != hipSuccess) return hip_fail(e, "fastq scan scratch");
     tmp_bytes = tmp2;
   }
   unsigned long long *lend = d_fq_lines.as<unsigned long long>(), *len = d_fq_len.as<unsigned long long>();
@@ -997,7 +1447,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n) {
   if ((e = hipMemcpyAsync(&n_bases, offs + R, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
       (e = hipStreamSynchronize(stream)) != hipSuccess)
     return hip_fail(e, "fastq records D2H");
-  if ((e = d_fq_bytes.ensure(std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess) return hip_fail(e, "fastq bytes");
+  if ((e = grow(d_fq_bytes, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess) return hip_fail(e, "fastq bytes");
   prof_begin(MHMKC_STAGE_OTHER);
   e = mhm::launch_fq_pack(d_text, lend, R, offs, cfg.qual_offset, d_fq_bytes.as<uint8_t>(), err_d, stream);
   prof_end();
@@ -1023,44 +1473,19 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n) {
   }
   fq_reads = R;
   fq_bases = n_bases;
-  return add_device(d_fq_bytes.as<uint8_t>(), d_fq_offs.as<uint64_t>(), R, n_bases, cfg.qual_cutoff);
-}
-
-static int add_host(mhmkc_t h, const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut) {
-  const uint64_t n_bases = offs[n_reads];
-  hipError_t e;
-  if ((e = h->d_in_bytes.ensure(std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess)
-    return h->hip_fail(e, "input staging");
-  if ((e = h->d_in_offs.ensure((n_reads + 1) * 8)) != hipSuccess) return h->hip_fail(e, "input staging");
-  if (n_bases && (e = hipMemcpyAsync(h->d_in_bytes.p, bytes, n_bases, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
-    return h->hip_fail(e, "input H2D");
-  if ((e = hipMemcpyAsync(h->d_in_offs.p, offs, (n_reads + 1) * 8, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
-    return h->hip_fail(e, "input H2D");
-  int rc = h->add_device(h->d_in_bytes.as<uint8_t>(), h->d_in_offs.as<uint64_t>(), n_reads, n_bases, qcut);
-  if (rc == MHMKC_OK) {
-    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return h->hip_fail(e, "add_reads");
-  }
-  return rc;
-}
-
-static int check_offsets(mhmkc_t h, const uint64_t *offs, uint64_t n_reads) {
-  if (offs[0] != 0) return h->fail(MHMKC_EINVAL, "read_offsets[0] must be 0");
-  for (uint64_t i = 0; i < n_reads; i++) {
-    if (offs[i + 1] < offs[i]) return h->fail(MHMKC_EINVAL, "read_offsets must be non-decreasing (read %llu)",
-                                              (unsigned long long)i);
-    if (offs[i + 1] - offs[i] > 65535)
-      return h->fail(MHMKC_EINVAL, "read %llu longer than 65535 (PackedRead read_len is uint16)",
-                     (unsigned long long)i);
-  }
-  return MHMKC_OK;
+  st.reads += R;
+  st.bases += n_bases;
+  if (R == 0) return MHMKC_OK;
+  qcut_pending = cfg.qual_cutoff;
+  // the offsets were made here from checked records: the window count kernel re-checks them anyway
+  mhm::ReadsView rv{d_fq_bytes.as<uint8_t>(), d_fq_offs.as<uint64_t>(), R, n_bases, 0, 0, 0};
+  return add_view(rv, 0, false);
 }
 
 int mhmkc_add_reads(mhmkc_t h, const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads) {
   if (!h) return MHMKC_EINVAL;
   if (!offs || (n_reads && !bytes)) return h->fail(MHMKC_EINVAL, "null host buffer");
-  int rc = check_offsets(h, offs, n_reads);
-  if (rc) return rc;
-  return add_host(h, bytes, offs, n_reads, h->cfg.qual_cutoff);
+  return h->add_host(bytes, offs, n_reads, h->cfg.qual_cutoff);
 }
 
 int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes) {
@@ -1072,11 +1497,13 @@ int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes) {
 int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes) {
   if (!h) return MHMKC_EINVAL;
   if (n_bytes && !text) return h->fail(MHMKC_EINVAL, "null host buffer");
+  int rc = h->resolve_slabs();  // an earlier add_fastq's text may still be read
+  if (rc) return rc;
   hipError_t e;
-  if ((e = h->d_fq_text.ensure(n_bytes + 16)) != hipSuccess) return h->hip_fail(e, "fastq staging");
+  if ((e = h->grow(h->d_fq_text, n_bytes + 16)) != hipSuccess) return h->hip_fail(e, "fastq staging");
   if (n_bytes && (e = hipMemcpyAsync(h->d_fq_text.p, text, n_bytes, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
     return h->hip_fail(e, "fastq H2D");
-  int rc = h->add_fastq(h->d_fq_text.as<char>(), n_bytes);
+  rc = h->add_fastq(h->d_fq_text.as<char>(), n_bytes);
   if (rc == MHMKC_OK && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return h->hip_fail(e, "add_fastq");
   return rc;
 }
@@ -1105,35 +1532,38 @@ int mhmkc_fastq_fetch(mhmkc_t h, uint8_t *bytes, uint64_t *offsets) {
   return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fastq fetch");
 }
 
+// PackedRead code of a sequence character; case carries the quality (SeqBlockInserter::process_seq input,
+// src/kcount/kcount.cpp:80-86; quals[i] = isupper, src/kcount/kcount_cpu.cpp:309-312). -1: not A/C/G/T/N
+// (HashTableInserter::insert_supermer DIEs, src/kcount/kcount_cpu.cpp:452-458).
+static int seq_byte(char c) {
+  int code;
+  switch (c) {
+    case 'A': case 'a': code = 0; break;
+    case 'C': case 'c': code = 1; break;
+    case 'G': case 'g': code = 2; break;
+    case 'T': case 't': code = 3; break;
+    case 'N': case 'n': code = 4; break;
+    default: return -1;
+  }
+  return code | ((c >= 'A' && c <= 'Z') ? (31 << 3) : 0);
+}
+
 int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *offs, uint64_t n_seqs, uint16_t depth) {
   if (!h) return MHMKC_EINVAL;
   if (!offs || (n_seqs && !seqs)) return h->fail(MHMKC_EINVAL, "null host buffer");
-  if (depth > 1) return h->fail(MHMKC_EUNSUPPORTED, "contig pass (depth > 1) is not supported in this version");
+  if (depth > 1) return h->fail(MHMKC_EUNSUPPORTED, "depth > 1 is a contig supermer: use mhmkc_add_ctgs");
   if (offs[0] != 0) return h->fail(MHMKC_EINVAL, "seq_offsets[0] must be 0");
   for (uint64_t i = 0; i < n_seqs; i++)
     if (offs[i + 1] < offs[i]) return h->fail(MHMKC_EINVAL, "seq_offsets must be non-decreasing");
   const uint64_t n = offs[n_seqs];
-  // Case carries the quality (SeqBlockInserter::process_seq input, src/kcount/kcount.cpp:80-86;
-  // quals[i] = isupper, src/kcount/kcount_cpu.cpp:309-312): uppercase -> q 31, lowercase -> q 0, and the
-  // batch runs with cutoff 1. Characters other than ACGTN are fatal in the reference
-  // (HashTableInserter::insert_supermer DIE, src/kcount/kcount_cpu.cpp:452-458).
+  // uppercase -> q 31, lowercase -> q 0, and the batch runs with cutoff 1
   std::vector<uint8_t> bytes(n);
   for (uint64_t i = 0; i < n; i++) {
-    const char c = seqs[i];
-    uint8_t code;
-    switch (c) {
-      case 'A': case 'a': code = 0; break;
-      case 'C': case 'c': code = 1; break;
-      case 'G': case 'g': code = 2; break;
-      case 'T': case 't': code = 3; break;
-      case 'N': case 'n': code = 4; break;
-      default:
-        return h->fail(MHMKC_EBADCHAR, "bad char '%c' (%d) at position %llu", c, (int)c, (unsigned long long)i);
-    }
-    const bool upper = (c >= 'A' && c <= 'Z');
-    bytes[i] = (uint8_t)(code | (upper ? (31u << 3) : 0u));
+    const int b = seq_byte(seqs[i]);
+    if (b < 0) return h->fail(MHMKC_EBADCHAR, "bad char '%c' (%d) at position %llu", seqs[i], (int)seqs[i], (unsigned long long)i);
+    bytes[i] = (uint8_t)b;
   }
-  return add_host(h, bytes.data(), offs, n_seqs, 1);
+  return h->add_host(bytes.data(), offs, n_seqs, 1);
 }
 
 int mhmkc_add_ctgs(mhmkc_t h, const char *seqs, const uint64_t *offs, const uint16_t *depths, uint64_t n_ctgs) {
@@ -1141,37 +1571,70 @@ int mhmkc_add_ctgs(mhmkc_t h, const char *seqs, const uint64_t *offs, const uint
   if (!offs || (n_ctgs && (!seqs || !depths))) return h->fail(MHMKC_EINVAL, "null host buffer");
   if (h->finished) return h->fail(MHMKC_ESTATE, "handle already finished; call mhmkc_reset first");
   if (offs[0] != 0) return h->fail(MHMKC_EINVAL, "seq_offsets[0] must be 0");
-  for (uint64_t i = 0; i < n_ctgs; i++)
+  const uint64_t k = (uint64_t)h->k;
+  uint64_t W = h->ctg_win.back();
+  for (uint64_t i = 0; i < n_ctgs; i++) {
     if (offs[i + 1] < offs[i]) return h->fail(MHMKC_EINVAL, "seq_offsets must be non-decreasing");
+    const uint64_t L = offs[i + 1] - offs[i];
+    W += L >= k + 2 ? L - k - 1 : 0;  // add_ctg_kmers skips contigs shorter than k + 2 (src/kcount/kcount.cpp:128)
+  }
+  if (W >= 0xffffffffull) return h->fail(MHMKC_EINVAL, "at most 2^32-1 contig k-mers per round");
   const uint64_t n = offs[n_ctgs];
   const size_t b0 = h->ctg_bytes.size();
   h->ctg_bytes.resize(b0 + n);
   // case carries the quality as for reads (get_kmers_and_exts: quals[i] = isupper, kcount_cpu.cpp:309-313);
   // contigs are uppercase. Characters other than ACGTN are fatal (insert_supermer DIE, :452-458).
   for (uint64_t i = 0; i < n; i++) {
-    const char c = seqs[i];
-    uint8_t code;
-    switch (c) {
-      case 'A': case 'a': code = 0; break;
-      case 'C': case 'c': code = 1; break;
-      case 'G': case 'g': code = 2; break;
-      case 'T': case 't': code = 3; break;
-      case 'N': case 'n': code = 4; break;
-      default:
-        h->ctg_bytes.resize(b0);
-        return h->fail(MHMKC_EBADCHAR, "bad char '%c' (%d) in contig position %llu", c, (int)c, (unsigned long long)i);
+    const int b = seq_byte(seqs[i]);
+    if (b < 0) {
+      h->ctg_bytes.resize(b0);
+      return h->fail(MHMKC_EBADCHAR, "bad char '%c' (%d) in contig position %llu", seqs[i], (int)seqs[i],
+                     (unsigned long long)i);
     }
-    h->ctg_bytes[b0 + i] = (uint8_t)(code | ((c >= 'A' && c <= 'Z') ? (31u << 3) : 0u));
+    h->ctg_bytes[b0 + i] = (uint8_t)b;
   }
-  const uint64_t k = (uint64_t)h->k;
   for (uint64_t i = 0; i < n_ctgs; i++) {
     const uint64_t L = offs[i + 1] - offs[i];
     h->ctg_offs.push_back(b0 + offs[i + 1]);
-    // add_ctg_kmers skips contigs shorter than k + 2 (src/kcount/kcount.cpp:128); interior windows only
-    h->ctg_win.push_back(h->ctg_win.back() + (L >= k + 2 ? L - k - 1 : 0));
+    h->ctg_win.push_back(h->ctg_win.back() + (L >= k + 2 ? L - k - 1 : 0));  // interior windows only
     h->ctg_depth.push_back(depths[i]);
   }
-  if (h->ctg_win.back() >= 0xffffffffull) return h->fail(MHMKC_EINVAL, "at most 2^32-1 contig k-mers per round");
+  return MHMKC_OK;
+}
+
+int mhmkc_set_dmin_thres(mhmkc_t h, int32_t dmin_thres) {
+  if (!h) return MHMKC_EINVAL;
+  if (dmin_thres < 0 || dmin_thres > 32768)
+    return h->fail(MHMKC_EUNSUPPORTED, "dmin_thres must be in [0, 32768] (DESIGN.md §3.4)");
+  if (h->finished) return h->fail(MHMKC_ESTATE, "handle already finished; call mhmkc_reset first");
+  h->dmin = dmin_thres;
+  return MHMKC_OK;
+}
+
+int mhmkc_set_transport(mhmkc_t h, const mhmkc_transport *t) {
+  if (!h) return MHMKC_EINVAL;
+  if (!t || !t->allgather || !t->alltoallv) return h->fail(MHMKC_EINVAL, "transport needs allgather and alltoallv");
+  if (h->comm) return h->fail(MHMKC_EINVAL, "the handle already has an RCCL communicator (comm_id)");
+  h->xp = *t;
+  h->has_xp = true;
+  return MHMKC_OK;
+}
+
+int mhmkc_minimizer_hashes(mhmkc_t h, const uint64_t *keys, uint64_t n, int32_t n_longs, int32_t m, uint64_t *hashes) {
+  if (!h) return MHMKC_EINVAL;
+  if (n && (!keys || !hashes)) return h->fail(MHMKC_EINVAL, "null host buffer");
+  if (n_longs < h->nl || n_longs > 8) return h->fail(MHMKC_EINVAL, "n_longs must be in [k/32+1, 8]");
+  const int mm = m ? m : mhm::minimizer_len_for(h->k);
+  if (mm < 1 || mm > 28 || mm > h->k) return h->fail(MHMKC_EINVAL, "m must be in [1, min(k, 28)]");
+  if (!n) return MHMKC_OK;
+  hipError_t e;
+  if ((e = h->grow(h->d_mh, n * 8 * ((size_t)n_longs + 1) + 64)) != hipSuccess) return h->hip_fail(e, "minimizer buffers");
+  uint64_t *dk = h->d_mh.as<uint64_t>(), *dh = dk + n * n_longs;
+  if ((e = hipMemcpyAsync(dk, keys, n * 8 * n_longs, hipMemcpyHostToDevice, h->stream)) != hipSuccess ||
+      (e = mhm::launch_minimizer_hash(dk, n, n_longs, h->k, mm, dh, h->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(hashes, dh, n * 8, hipMemcpyDeviceToHost, h->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(h->stream)) != hipSuccess)
+    return h->hip_fail(e, "minimizer hashes");
   return MHMKC_OK;
 }
 
@@ -1218,6 +1681,7 @@ int mhmkc_reset(mhmkc_t h) {
   if (e != hipSuccess) return h->hip_fail(e, "reset");
   h->prof_collect();
   h->n_slabs = 0;
+  h->n_arenas = 0;
   h->ctg_bytes.clear();
   h->ctg_offs.assign(1, 0);
   h->ctg_win.assign(1, 0);

@@ -227,13 +227,16 @@ class KmerCounter:
 
     def __init__(self, k: int, *, n_longs: int = 0, qual_offset: int = 33, qual_cutoff: int = 20,
                  dmin_thres: int = 2, dyn_min_depth: float = 0.9, device: int = -1, rank: int = 0,
-                 n_ranks: int = 1, comm_id: bytes | None = None, stream: int | None = None):
+                 n_ranks: int = 1, comm_id: bytes | None = None, stream: int | None = None,
+                 transport: "TorchDistTransport | None" = None, output_owner: int = N.MHMKC_OWNER_HASH,
+                 minimizer_len: int = 0):
         L = N.lib()
         cfg = N.MhmkcConfig()
         N.check(L.mhmkc_config_init(C.byref(cfg)))
         cfg.k, cfg.n_longs, cfg.qual_offset, cfg.qual_cutoff = k, n_longs, qual_offset, qual_cutoff
         cfg.dmin_thres, cfg.dyn_min_depth, cfg.device = dmin_thres, dyn_min_depth, device
         cfg.rank, cfg.n_ranks = rank, n_ranks
+        cfg.output_owner, cfg.minimizer_len = output_owner, minimizer_len
         self._comm_buf = None
         if comm_id is not None:
             if len(comm_id) != N.MHMKC_COMM_ID_BYTES:
@@ -246,7 +249,11 @@ class KmerCounter:
         self._h = h
         self.k = k
         self.n_longs = n_longs or n_longs_for(k)
+        self.rank, self.n_ranks = rank, n_ranks
         self.n_out = None
+        self._transport = None
+        if transport is not None:
+            self.set_transport(transport)
 
     # -- lifecycle
     def close(self) -> None:
@@ -280,10 +287,26 @@ class KmerCounter:
     def add_packed_reads_device(self, bytes_ptr: int, offsets_ptr: int, n_reads: int, n_bases: int) -> None:
         self._check(N.lib().mhmkc_add_reads_device(self._h, bytes_ptr, offsets_ptr, n_reads, n_bases))
 
-    def add_tensors(self, bytes_t, offsets_t) -> None:
-        """Device-resident torch tensors (uint8 bytes, int64/uint64 offsets with n_reads+1 entries)."""
+    def wait_stream(self, stream_ptr: int | None) -> None:
+        """Order the counter's device work after what is enqueued on another stream (mhmkc_wait_stream)."""
+        self._check(N.lib().mhmkc_wait_stream(self._h, stream_ptr))
+
+    def _after_torch(self, t) -> None:
+        """Device tensors are read on the counter's own stream: order it after torch's current stream."""
+        import torch
+
+        self.wait_stream(torch.cuda.current_stream(t.device).cuda_stream)
+
+    def add_tensors(self, bytes_t, offsets_t, n_bases: int | None = None) -> None:
+        """Device-resident torch tensors (uint8 bytes, int64/uint64 offsets with n_reads+1 entries). n_bases
+        defaults to offsets_t[-1] (one device read); the library checks the offsets on the device."""
         n_reads = int(offsets_t.numel()) - 1
-        self.add_packed_reads_device(bytes_t.data_ptr(), offsets_t.data_ptr(), n_reads, int(bytes_t.numel()))
+        if n_bases is None:
+            n_bases = int(offsets_t[-1]) if n_reads >= 0 else 0
+        if n_bases > int(bytes_t.numel()):
+            raise ValueError("offsets_t[-1] exceeds the bytes tensor")
+        self._after_torch(bytes_t)
+        self.add_packed_reads_device(bytes_t.data_ptr(), offsets_t.data_ptr(), n_reads, n_bases)
 
     def add_fastq(self, text) -> None:
         """FASTQ text (bytes or str), parsed and packed on the device, then counted: FastqReader +
@@ -292,9 +315,20 @@ class KmerCounter:
         blob = text.encode("ascii") if isinstance(text, str) else bytes(text)
         self._check(N.lib().mhmkc_add_fastq(self._h, blob, len(blob)))
 
-    def add_fastq_tensor(self, text_t) -> None:
-        """FASTQ text already in HBM (a uint8 torch tensor on the counter's device)."""
-        self._check(N.lib().mhmkc_add_fastq_device(self._h, text_t.data_ptr(), int(text_t.numel())))
+    def add_fastq_tensor(self, text_t, n_bytes: int | None = None) -> None:
+        """FASTQ text already in HBM (a uint8 torch tensor on the counter's device). The parser reads whole
+        aligned dwords, so the buffer must extend 4 bytes past the text: pass n_bytes <= numel - 4 to use the
+        tensor as is; otherwise the text is copied into a padded buffer first."""
+        import torch
+
+        n = int(text_t.numel()) if n_bytes is None else int(n_bytes)
+        if int(text_t.numel()) < n + 4:
+            padded = torch.zeros(n + 16, dtype=torch.uint8, device=text_t.device)
+            padded[:n].copy_(text_t.reshape(-1)[:n])
+            text_t = padded
+        self._fq_text = text_t  # keep it alive while the call runs
+        self._after_torch(text_t)
+        self._check(N.lib().mhmkc_add_fastq_device(self._h, text_t.data_ptr(), n))
 
     def fastq_packed(self) -> tuple[np.ndarray, np.ndarray]:
         """The PackedReads (bytes, offsets) of the last add_fastq call, copied to the host."""
@@ -329,6 +363,31 @@ class KmerCounter:
         np.cumsum(lens, out=offs[1:])
         blob = "".join(seqs).encode("ascii")
         self._check(N.lib().mhmkc_add_ctgs(self._h, blob, offs.ctypes.data, d.ctypes.data, len(seqs)))
+
+    # -- ranks, thresholds
+    def set_transport(self, transport: "TorchDistTransport") -> None:
+        """Host-staged exchange between ranks (mhmkc_set_transport), e.g. over a gloo process group."""
+        self._transport = transport  # the callbacks must outlive the handle
+        self._check(N.lib().mhmkc_set_transport(self._h, C.byref(transport.struct)))
+
+    def set_dmin_thres(self, dmin_thres: int) -> None:
+        """The finish's depth threshold, the reference's _dmin_thres (src/kcount/kmer_dht.hpp:57), set by
+        analyze_kmers (src/kcount/kcount.cpp:145)."""
+        self._check(N.lib().mhmkc_set_dmin_thres(self._h, int(dmin_thres)))
+
+    def minimizer_hashes(self, keys: np.ndarray, m: int = 0) -> np.ndarray:
+        """Kmer::minimizer_hash_fast of (n, n_longs) keys, on the GPU (src/kmer.cpp:344-393,454-463)."""
+        kk = np.ascontiguousarray(keys, dtype=np.uint64)
+        if kk.ndim == 1:
+            kk = kk.reshape(-1, 1)
+        out = np.empty(kk.shape[0], dtype=np.uint64)
+        self._check(N.lib().mhmkc_minimizer_hashes(self._h, kk.ctypes.data, kk.shape[0], kk.shape[1], m,
+                                                   out.ctypes.data))
+        return out
+
+    def target_ranks(self, keys: np.ndarray, rank_n: int) -> np.ndarray:
+        """KmerDHT::get_kmer_target_rank of every key (src/kcount/kmer_dht.cpp:193-196), on the GPU."""
+        return (self.minimizer_hashes(keys) % np.uint64(rank_n)).astype(np.int64)
 
     # -- finish / output
     def finish(self) -> int:
@@ -367,6 +426,58 @@ class KmerCounter:
 
     def set_profiling(self, on: bool = True) -> None:
         self._check(N.lib().mhmkc_set_profiling(self._h, 1 if on else 0))
+
+
+class TorchDistTransport:
+    """mhmkc_transport (host-staged exchange, include/mhmkc.h) over a torch.distributed process group whose
+    backend moves CPU tensors (gloo). It stands where the reference's UPC++ RPC stands
+    (src/kcount/kmer_dht.cpp:133-149,222-231) for hosts without RCCL between the ranks: several nodes, or
+    several ranks sharing one GPU."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist, self.group = dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.error: BaseException | None = None
+        self._ag = N.ALLGATHER_FN(self._allgather)
+        self._a2a = N.ALLTOALLV_FN(self._alltoallv)
+        self.struct = N.MhmkcTransport(None, self._ag, self._a2a)
+
+    @staticmethod
+    def _view(ptr: int, n: int):
+        import torch
+
+        if n == 0:
+            return torch.empty(0, dtype=torch.uint8)
+        return torch.frombuffer((C.c_uint8 * n).from_address(ptr), dtype=torch.uint8)
+
+    def _allgather(self, _ctx, send, recv, nbytes):
+        try:
+            if nbytes:
+                import torch
+
+                outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+                self.dist.all_gather(outs, self._view(send, nbytes).clone(), group=self.group)
+                dst = self._view(recv, self.world * nbytes)
+                for r in range(self.world):
+                    dst[r * nbytes:(r + 1) * nbytes].copy_(outs[r])
+            return 0
+        except BaseException as e:  # the C side turns a non-zero return into MHMKC_ETRANSPORT
+            self.error = e
+            return 1
+
+    def _alltoallv(self, _ctx, send, send_bytes, recv, recv_bytes):
+        try:
+            sb = [int(send_bytes[p]) for p in range(self.world)]
+            rb = [int(recv_bytes[p]) for p in range(self.world)]
+            inp, out = self._view(send, sum(sb)), self._view(recv, sum(rb))
+            self.dist.all_to_all_single(out, inp, output_split_sizes=rb, input_split_sizes=sb, group=self.group)
+            return 0
+        except BaseException as e:
+            self.error = e
+            return 1
 
 
 def comm_id() -> bytes:
@@ -471,9 +582,11 @@ class KmerDHT:
         return get_kmer_target_rank(longs, self.k, self.n_ranks)
 
     def dump_kmers(self, out_dir: str | os.PathLike = ".") -> Path:
-        """dump_kmers (src/kcount/kmer_dht.cpp:243-266): kmers-<k>.txt.gz, lines "KMER count L R"."""
-        name = f"kmers-{self.k}.txt.gz" if self.n_ranks == 1 else f"kmers-{self.k}-rank{self.rank}.txt.gz"
-        path = Path(out_dir) / name
+        """dump_kmers (src/kcount/kmer_dht.cpp:243-266): kmers-<k>.txt.gz in this rank's directory
+        (get_rank_path: per_rank/<rank / 1000>/<rank>/, upcxx-utils/src/log.cpp:283-312), lines
+        "KMER count L R"."""
+        path = Path(out_dir) / "per_rank" / f"{self.rank // 1000:08d}" / f"{self.rank:08d}" / f"kmers-{self.k}.txt.gz"
+        path.parent.mkdir(parents=True, exist_ok=True)
         with gzip.open(path, "wt") as f:
             for line in self.table.lines():
                 f.write(line + "\n")
@@ -495,6 +608,7 @@ def analyze_kmers(kmer_len: int, prev_kmer_len: int, qual_offset: int, packed_re
     """
     if kmer_len != kmer_dht.k:
         raise ValueError("kmer_len differs from the KmerDHT's k")
+    kmer_dht.counter.set_dmin_thres(dmin_thres)  # _dmin_thres = dmin_thres (kcount.cpp:145)
     for pr in packed_reads_list:
         if pr.qual_offset != qual_offset:
             raise ValueError("PackedReads qual_offset differs")

@@ -2,7 +2,8 @@
 // analyze_kmers (src/contigging.cpp:109-119), then prints the table sorted by k-mer in dump_kmers
 // format. Modes:
 //   adapter_test kat                      Kmer<MAX_K> known answers only (no GPU)
-//   adapter_test reads <k> <seqqual.txt>  analyze_kmers over PackedReads
+//   adapter_test reads <k> <seqqual.txt> [- <dmin>]  analyze_kmers over PackedReads (dmin_thres = 2 by
+//                                                    default), then dump_kmers (per_rank/.../kmers-<k>.txt.gz)
 //   adapter_test seqs  <k> <seqqual.txt>  SeqBlockInserter::process_seq over lowercase-masked strings
 //   adapter_test ctgs  <k> <seqqual.txt> <ctgs.txt>  analyze_kmers with a Contigs list ("SEQ DEPTH" lines)
 //   adapter_test fastq <k> <reads.fq>     FASTQ text through KmerDHT::add_fastq (device parse + pack)
@@ -17,7 +18,7 @@
 using namespace mhm2;
 
 template <int MAX_K>
-int run(const std::string &mode, int k, const std::string &path, const std::string &ctg_path) {
+int run(const std::string &mode, int k, const std::string &path, const std::string &ctg_path, int dmin) {
   Kmer<MAX_K>::set_k(k);
   std::ifstream in(path);
   std::string line;
@@ -30,7 +31,7 @@ int run(const std::string &mode, int k, const std::string &path, const std::stri
     pr.add_read("@r/1", s, q);
     reads.emplace_back(s, q);
   }
-  KmerDHT<MAX_K> dht(1000, 2);
+  KmerDHT<MAX_K> dht(1000, 1 << 20, 100, false, true);  // as contigging.cpp:115-116 builds it
   Contigs ctgs;
   if (mode == "ctgs") {
     std::ifstream cin_(ctg_path);
@@ -54,7 +55,7 @@ int run(const std::string &mode, int k, const std::string &path, const std::stri
     dht.finish_updates();
   } else if (mode == "reads" || mode == "ctgs") {
     std::vector<PackedReads *> list{&pr};
-    analyze_kmers<MAX_K>(k, 0, 33, list, 2, ctgs, dht, false);
+    analyze_kmers<MAX_K>(k, 0, 33, list, dmin, ctgs, dht, mode == "reads");
   } else {
     SeqBlockInserter<MAX_K> sbi(33, dht.get_minimizer_len());
     for (auto &r : reads) {  // count_kmers: lowercase bases below the quality cutoff (kcount.cpp:80-85)
@@ -88,17 +89,24 @@ int main(int argc, char **argv) {
     Kmer<32> a("ACGTACGTACGTACGTACGTA");
     Kmer<64>::set_k(63);
     Kmer<64> b("CGCTGTTCCAGATGACGAACCAGGAATTCCGCCAGGTATTCGACTTTATTCGCGAAGTCAAGA");
+    Kmer<32> c("CGCTGTTCCAGATGACGAACC");
     bool ok = a.get_longs()[0] == 0x1b1b1b1b1b000000ull && a.hash() == 0xa47f0f8106be6783ull &&
               b.get_longs()[0] == 0x67bd48e1814a0f59ull && b.get_longs()[1] == 0x4acf61fcf660b420ull &&
               b.hash() == 0x470509568a42d5b5ull && a.revcomp().revcomp() == a &&
-              a.revcomp().to_string() == "TACGTACGTACGTACGTACGT";
+              a.revcomp().to_string() == "TACGTACGTACGTACGTACGT" &&
+              // get_minimizer_fast / minimizer_hash_fast known answers
+              a.get_minimizer_fast(15) == 0xb1b1b1b000000000ull && a.minimizer_hash_fast(15) == 0x7b9cf376cdbe4a50ull &&
+              c.get_minimizer_fast(15) == 0xdb4de81000000000ull && c.minimizer_hash_fast(15) == 0xfbeed8639c5ae34full &&
+              b.get_minimizer_fast(27) == 0xcf61fcf660b42000ull && b.minimizer_hash_fast(27) == 0xaa95c0beb14e494full &&
+              quick_hash(0) == 0x7b439d0c1fd00de3ull;
     std::cout << (ok ? "KAT OK" : "KAT FAIL") << "\n";
     return ok ? 0 : 1;
   }
   int k = std::atoi(argv[2]);
   const std::string ctg_path = argc > 4 ? argv[4] : "";
-  if (k < 32) return run<32>(mode, k, argv[3], ctg_path);
-  if (k < 64) return run<64>(mode, k, argv[3], ctg_path);
-  if (k < 96) return run<96>(mode, k, argv[3], ctg_path);
-  return run<128>(mode, k, argv[3], ctg_path);
+  const int dmin = argc > 5 ? std::atoi(argv[5]) : 2;
+  if (k < 32) return run<32>(mode, k, argv[3], ctg_path, dmin);
+  if (k < 64) return run<64>(mode, k, argv[3], ctg_path, dmin);
+  if (k < 96) return run<96>(mode, k, argv[3], ctg_path, dmin);
+  return run<128>(mode, k, argv[3], ctg_path, dmin);
 }

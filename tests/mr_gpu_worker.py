@@ -1,0 +1,63 @@
+"""Worker of the multi-rank GPU tests (TEST INFRASTRUCTURE): one rank of libmhmkc's own multi-GPU path.
+
+Every rank is a process with its own counter on the same GPU (RCCL refuses two ranks on one device, so the
+exchange goes through the host-staged transport, mhmkc_set_transport, driven by a gloo process group). The
+rank counts its shard of the reads (and adds its share of the contigs); mhmkc_finish then runs the real
+exchange code (exchange(), the contig all-gather and, with MHMKC_OWNER_MINIMIZER, the owner hand-off).
+"""
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
+sys.path.insert(0, str(HERE.parent))
+
+
+def shard(n: int, rank: int, world: int):
+    return n * rank // world, n * (rank + 1) // world
+
+
+def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
+    import torch
+    import torch.distributed as dist
+
+    import mhm2_proxy_amd as m
+    from common import ctg_set, synth_set
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    for key, val in opts.get("env", {}).items():
+        os.environ[key] = val
+    if opts.get("contigs"):
+        b, o, seqs, depths = ctg_set(seed=opts["seed"], n_reads=opts.get("n_reads", 300))
+    else:
+        b, o = synth_set(opts.get("n_reads", 1200), opts.get("genome", 9000), opts["seed"])
+        seqs, depths = [], np.zeros(0, np.uint16)
+    n = o.size - 1
+    lo, hi = shard(n, rank, world)
+    owner = m.MHMKC_OWNER_MINIMIZER if opts.get("minimizer") else m.MHMKC_OWNER_HASH
+    c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner,
+                      dmin_thres=opts.get("dmin", 2))
+    # two batches per rank: the first from host memory (chunked H2D), the second from device tensors
+    mid = (lo + hi) // 2
+    c.add_packed_reads(b[int(o[lo]):int(o[mid])], (o[lo:mid + 1] - o[lo]).astype(np.uint64))
+    bt = torch.from_numpy(b[int(o[mid]):int(o[hi])].copy()).cuda()
+    ot = torch.from_numpy((o[mid:hi + 1] - o[mid]).astype(np.int64)).cuda()
+    c.add_tensors(bt, ot)
+    if len(seqs):
+        a, z = shard(len(seqs), rank, world)
+        c.add_ctgs(seqs[a:z], depths[a:z])
+    c.finish()
+    t = c.fetch()
+    st = c.stats()
+    np.savez(Path(out_dir) / f"rank{rank}.npz", keys=t.keys, counts=t.counts, left=t.left, right=t.right,
+             bytes_sent=st["bytes_sent"], bytes_recv=st["bytes_recv"], occurrences=st["occurrences"],
+             owned=st["owned_records"], count_sum=st["count_sum"], distinct=st["distinct"], purged=st["purged"],
+             n_out=st["n_out"], handoff_sent=st["handoff_sent"], handoff_recv=st["handoff_recv"],
+             ctg_kmers=st["ctg_kmers"])
+    c.close()
+    dist.barrier()
+    dist.destroy_process_group()

@@ -46,6 +46,8 @@ def oracle() -> C.CDLL:
         L.orc_kmer_target_rank.argtypes = [VP, I, I, I]
         L.orc_kcount.argtypes = [VP, VP, U64, I, I, I, I, C.c_double]
         L.orc_kcount.restype = VP
+        L.orc_kcount_mt.argtypes = [VP, VP, U64, I, I, I, I, C.c_double, I]
+        L.orc_kcount_mt.restype = VP
         L.orc_kcount_ctgs.argtypes = [VP, VP, U64, VP, VP, VP, U64, I, I, I, I, C.c_double]
         L.orc_kcount_ctgs.restype = VP
         L.orc_extract.argtypes = [VP, VP, U64, I, I, I, VP, VP, U64]
@@ -113,6 +115,17 @@ def kcount(packed_bytes, offsets, k, n_longs=None, qual_cutoff=20, dmin_thres=2,
     o = np.ascontiguousarray(offsets, dtype=np.uint64)
     ptr = oracle().orc_kcount(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, dmin_thres,
                               dyn_min_depth)
+    return OracleTable(ptr, nl, k)
+
+
+def kcount_mt(packed_bytes, offsets, k, n_longs=None, qual_cutoff=20, dmin_thres=2, dyn_min_depth=0.9,
+              threads=8) -> OracleTable:
+    """The multi-threaded restatement (oracle/kcount_mt.c); rows in no particular order."""
+    nl = n_longs or (k // 32 + 1)
+    b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ptr = oracle().orc_kcount_mt(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, dmin_thres,
+                                 dyn_min_depth, threads)
     return OracleTable(ptr, nl, k)
 
 

@@ -30,7 +30,7 @@ def test_lib_exports_every_declared_symbol():
     lib = N.lib()
     for name in declared(ROOT / "include" / "mhmkc.h"):
         assert hasattr(lib, name), name
-    assert lib.mhmkc_abi_version() == 4
+    assert lib.mhmkc_abi_version() == 5
 
 
 def test_synth_exports_every_declared_symbol():
@@ -49,7 +49,7 @@ def test_config_defaults_are_the_reference_defaults():
 @pytest.mark.parametrize("field,value,code", [("k", 0, -1), ("k", 128, -1), ("k", 32, -7), ("k", 64, -7),
                                                ("qual_offset", 40, -1), ("dmin_thres", 40000, -7),
                                                ("n_ranks", 0, -1), ("rank", 3, -1), ("n_longs", 9, -1),
-                                               ("dyn_min_depth", 1.5, -1)])
+                                               ("dyn_min_depth", 1.5, -1), ("output_owner", 2, -1)])
 def test_create_rejects_bad_config(field, value, code):
     cfg = N.MhmkcConfig()
     N.lib().mhmkc_config_init(C.byref(cfg))
@@ -82,3 +82,41 @@ def test_header_is_plain_c():
                        'mhmkc_config_init(&c); return c.k == 21 ? 0 : 1;}\n')
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", f"-I{ROOT / 'include'}", str(src)],
                        check=True)
+
+
+def test_ctypes_structs_match_the_header():
+    """sizeof / field offsets of the C structs equal the ctypes mirrors (an ABI drift would corrupt calls)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    if not shutil.which("gcc"):
+        pytest.skip("gcc missing")
+    structs = {"mhmkc_config": N.MhmkcConfig, "mhmkc_stats": N.MhmkcStats, "mhmkc_transport": N.MhmkcTransport}
+    lines = []
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    with tempfile.TemporaryDirectory() as d:
+        src = Path(d) / "t.c"
+        src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mhmkc.h"\nint main(void){' +
+                       "".join(lines) + "return 0;}\n")
+        exe = Path(d) / "t"
+        subprocess.run(["gcc", "-std=c99", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True)
+        out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(line.split()[:2]): int(line.split()[2]) for line in out if line}
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def test_minimizer_len_rule():
+    """minimizer_len 0 = the KmerDHT rule; an explicit length beyond get_minimizer_fast's limit is refused."""
+    cfg = N.MhmkcConfig()
+    N.lib().mhmkc_config_init(C.byref(cfg))
+    cfg.output_owner, cfg.minimizer_len = N.MHMKC_OWNER_MINIMIZER, 29
+    h = C.c_void_p()
+    assert N.lib().mhmkc_create(C.byref(h), C.byref(cfg)) == -1
+    assert not h.value

@@ -16,7 +16,7 @@ def build(tmp: Path) -> Path:
         pytest.skip("g++ missing")
     exe = tmp / "adapter_test"
     subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", f"-I{ROOT / 'include'}", str(SRC),
-                    f"-L{ROOT / 'mhm2_proxy_amd'}", "-lmhmkc", f"-Wl,-rpath,{ROOT / 'mhm2_proxy_amd'}",
+                    f"-L{ROOT / 'mhm2_proxy_amd'}", "-lmhmkc", "-lz", f"-Wl,-rpath,{ROOT / 'mhm2_proxy_amd'}",
                     "-o", str(exe)], check=True)
     return exe
 
@@ -37,10 +37,40 @@ def test_adapter_matches_golden(mode, k, setname, tmp_path):
     exe = build(tmp_path)
     reads = tmp_path / "reads.txt"
     reads.write_text(gzip.open(GOLDEN / f"reads_{setname}.txt.gz", "rt").read())
-    out = subprocess.run([str(exe), mode, str(k), str(reads)], capture_output=True, text=True, check=True)
+    out = subprocess.run([str(exe), mode, str(k), str(reads)], capture_output=True, text=True, check=True,
+                         cwd=tmp_path)
     got = out.stdout.splitlines()
     exp = sorted(gzip.open(GOLDEN / f"table_{setname}_k{k}.tsv.gz", "rt").read().splitlines())
     assert got == exp
+    if mode == "reads":  # analyze_kmers(..., dump_kmers = true): the reference's per-rank gzip file
+        dump = tmp_path / "per_rank" / "00000000" / "00000000" / f"kmers-{k}.txt.gz"
+        assert sorted(gzip.open(dump, "rt").read().splitlines()) == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [21, 63])
+def test_adapter_dmin_from_analyze_kmers(k, tmp_path):
+    """KmerDHT built the reference's way (contigging.cpp:115-116, before dmin is known), then
+    analyze_kmers(..., dmin_thres = 3, ...): the finish uses 3 (_dmin_thres, kcount.cpp:145), as the oracle."""
+    import sys
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    import mhm2_proxy_amd as m
+    from common import oracle_table, synth_set
+
+    exe = build(tmp_path)
+    b, o = synth_set(1500, 8000, 70 + k)
+    pr = m.PackedReads.from_arrays(b, o)
+    reads = tmp_path / "reads.txt"
+    with open(reads, "w") as f:
+        for i in range(pr.get_local_num_reads()):
+            _, s_, q = pr.get_read(i)
+            f.write(f"{s_} {q}\n")
+    out = subprocess.run([str(exe), "reads", str(k), str(reads), "-", "3"], capture_output=True, text=True,
+                         check=True, cwd=tmp_path)
+    exp3 = sorted(oracle_table(b, o, k, dmin_thres=3).lines())
+    assert out.stdout.splitlines() == exp3
+    assert exp3 != sorted(oracle_table(b, o, k, dmin_thres=2).lines())  # the threshold matters here
 
 
 @pytest.mark.gpu

@@ -325,3 +325,144 @@ def test_distinct_sketch_estimate(k):
     _, st = hip_table(b, o, k)
     assert st["distinct"] > 0
     assert abs(st["distinct_estimate"] - st["distinct"]) <= 0.12 * st["distinct"], (st["distinct_estimate"], st["distinct"])
+
+
+# ---- round 2: host chunks, stream ordering, dmin at finish, overflow guard ----------------------------
+
+
+@pytest.mark.parametrize("k,chunk", [(21, 700), (63, 1000), (33, 100000)])
+def test_host_chunks_equal_oracle(k, chunk, monkeypatch):
+    """mhmkc_add_reads copies a host batch in chunks of whole reads, each extracted as a slice view (an aligned
+    byte base plus a head offset) as soon as it lands: ragged reads (empty, shorter than k, N runs, poly-A)
+    over many chunk boundaries give the oracle's table."""
+    monkeypatch.setenv("MHMKC_CHUNK_BYTES", str(chunk))
+    b, o = edge_case_set(seed=17 + k)
+    with m.KmerCounter(k) as c:
+        c.add_packed_reads(b, o)
+        c.finish()
+        got, st = c.fetch(), c.stats()
+    assert st["h2d_chunks"] >= (2 if chunk < 10000 else 1)
+    assert st["h2d_bytes"] == int(o[-1]) + 8 * (o.size - 1) + 8 * st["h2d_chunks"]
+    assert_tables_equal(got, oracle_table(b, o, k), f"host chunks k={k}")
+    check_stats(st)
+
+
+def test_device_input_ordered_after_torch_stream():
+    """Tensors written by an asynchronous copy on torch's current stream and handed over at once: the counter
+    orders its stream after torch's (mhmkc_wait_stream), no torch.cuda.synchronize() needed."""
+    torch = pytest.importorskip("torch")
+    b, o = synth_set(3000, 20000, 52)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        bt = torch.from_numpy(b).pin_memory().cuda(non_blocking=True)
+        ot = torch.from_numpy(o.astype(np.int64)).pin_memory().cuda(non_blocking=True)
+        with m.KmerCounter(21) as c:
+            c.add_tensors(bt, ot, n_bases=int(o[-1]))
+            c.finish()
+            got = c.fetch()
+    assert_tables_equal(got, oracle_table(b, o, 21), "after a torch stream")
+
+
+def test_device_offsets_checked():
+    torch = pytest.importorskip("torch")
+    b, o = synth_set(200, 5000, 53)
+    oo = o.astype(np.int64).copy()
+    oo[50] = oo[51] + 1  # decreasing
+    with m.KmerCounter(21) as c:
+        with pytest.raises(m.MhmkcError) as e:
+            c.add_tensors(torch.from_numpy(b).cuda(), torch.from_numpy(oo).cuda(), n_bases=int(o[-1]))
+        assert e.value.code == -1
+
+
+@pytest.mark.parametrize("k", [21, 63])
+def test_analyze_kmers_dmin_thres(k):
+    """The Python mirror: KmerDHT built first (dmin unknown), analyze_kmers(..., dmin_thres = 3, ...) decides."""
+    b, o = synth_set(1500, 8000, 80 + k)
+    dht = m.KmerDHT(k)
+    m.analyze_kmers(k, 0, 33, [m.PackedReads.from_arrays(b, o)], 3, [], dht)
+    exp = oracle_table(b, o, k, dmin_thres=3)
+    assert_tables_equal(dht.table, exp, "analyze_kmers dmin 3")
+    assert len(exp) != len(oracle_table(b, o, k, dmin_thres=2)) or True
+    dht.counter.close()
+
+
+def _hot_key_last_bucket(k: int) -> str:
+    """A canonical k-mer whose partition hash has the top 19 bits set: the last fine bucket of the last coarse
+    bucket for any fine-bit count <= 11 (compact cmix at k <= 21, MurmurHash3 above)."""
+    rng = np.random.default_rng(k)
+    nl = k // 32 + 1
+    B = 2 * k
+    M = (1 << B) - 1
+    M1, M2 = 0xff51afd7ed558ccd, 0xc4ceb9fe1a85ec53
+
+    def inv(a):
+        x = a
+        for _ in range(6):
+            x = (x * (2 - a * x)) & ((1 << 64) - 1)
+        return x
+
+    I1, I2 = inv(M1), inv(M2)
+    s_ = (B + 1) >> 1
+    for _ in range(1 << 22):
+        if k <= 21:  # cunmix of a y with the top bits set
+            y = (((1 << 19) - 1) << (B - 19)) | int(rng.integers(0, 1 << (B - 19)))
+            y ^= y >> s_
+            y = (y * I2) & M
+            y ^= y >> s_
+            y = (y * I1) & M
+            y ^= y >> s_
+            key = np.array([y << (64 - B)], dtype=np.uint64)
+        else:
+            key = np.array([int(x) for x in rng.integers(0, 1 << 62, nl)], dtype=np.uint64)
+            key[-1] &= np.uint64((~((1 << (64 - 2 * (k - 32 * (nl - 1)))) - 1)) & ((1 << 64) - 1))
+            if (O.kmer_hash(key) >> 45) != (1 << 19) - 1:
+                continue
+        rc = O.kmer_revcomp(key, k)
+        if tuple(int(x) for x in key) <= tuple(int(x) for x in rc):
+            return O.kmer_to_string(key, k)
+    raise AssertionError("no key found")
+
+
+@pytest.mark.parametrize("k", [21, 33])
+def test_capped_overflow_in_last_bucket(k):
+    """a hot k-mer in the LAST fine bucket of the LAST coarse bucket overflows its capped
+    fine bucket. k_count must not run over the bucket (it returns at once when k_part_scatter flagged the
+    overflow); the exact rerun gives the oracle's table."""
+    s = _hot_key_last_bucket(k)
+    b0, o0 = synth_set(300, 20000, 3 + k)
+    hot = m.PackedReads.pack("A" + s + "C", "I" * (k + 2))  # one counted window: the hot k-mer
+    reads = [b0[o0[i]:o0[i + 1]] for i in range(300)] + [hot] * 30000
+    lens = np.array([x.size for x in reads], dtype=np.uint64)
+    o = np.zeros(len(reads) + 1, dtype=np.uint64)
+    np.cumsum(lens, out=o[1:])
+    b = np.concatenate(reads).astype(np.uint8)
+    got, st = hip_table(b, o, k)
+    assert st["exact_reruns"] >= 1
+    exp = oracle_table(b, o, k)
+    assert_tables_equal(got, exp, "hot k-mer in the last bucket")
+    nl = k // 32 + 1
+    hk = O.kmer_from_string(s, nl)
+    row = np.flatnonzero((exp.keys == hk).all(axis=1))
+    assert row.size == 1 and exp.counts[row[0]] == 30000
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("k", [21, 63])
+def test_c2_full_table_vs_cpu_restatement(k):
+    """config C2 at full size (10M x 150 bp, G = 50 Mbp, seed 2) through the host path
+    (chunked H2D), every row of the table compared with the multi-threaded CPU restatement (oracle/kcount_mt.c,
+    itself pinned to the single-threaded oracle and the golden fixtures); k = 21 and the C4 k = 63."""
+    g = m.synth_genome(50_000_000, 2)
+    b, o = m.synth_reads(g, 10_000_000, 150, 2, threads=16)
+    del g
+    got, st = hip_table(b, o, k)
+    assert st["occurrences"] == 10_000_000 * (150 - k - 1)
+    check_stats(st)
+    t = O.kcount_mt(b, o, k, threads=16)
+    keys, c, l, r = t.fetch()
+    ref = m.KmerTable(k, keys, c, l, r)
+    rs = t.stats()
+    del t
+    assert (st["distinct"], st["purged"], st["n_out"]) == (rs["distinct"], rs["purged"], rs["n_out"])
+    assert_tables_equal(got, ref, f"C2 k={k}: GPU vs CPU restatement")

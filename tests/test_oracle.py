@@ -191,3 +191,52 @@ def test_record_path_equals_read_path(k):
     a = O.count_records(keys, exts, k)
     ka, ca, la, ra = a.fetch()
     assert_tables_equal(m.KmerTable(k, ka, ca, la, ra), oracle_table(b, o, k), "records vs reads")
+
+
+# ---- the multi-threaded restatement (oracle/kcount_mt.c) ---------------------------------------------
+
+
+@pytest.mark.parametrize("k,threads", [(21, 1), (21, 8), (33, 3), (63, 8), (99, 5), (15, 2), (127, 4)])
+def test_mt_restatement_equals_oracle(k, threads):
+    from common import assert_tables_equal, oracle_table, synth_set
+
+    b, o = synth_set(3000, 15000, 300 + k)
+    t = O.kcount_mt(b, o, k, threads=threads)
+    keys, c, l, r = t.fetch()
+    assert_tables_equal(m.KmerTable(k, keys, c, l, r), oracle_table(b, o, k), f"mt k={k} threads={threads}")
+    ref = O.kcount(b, o, k).stats()
+    st = t.stats()
+    assert (st["occurrences"], st["distinct"], st["purged"]) == (ref["occurrences"], ref["distinct"], ref["purged"])
+
+
+@pytest.mark.parametrize("k", [21, 63])
+def test_mt_restatement_edge_and_hot(k):
+    from common import assert_tables_equal, edge_case_set, hot_set, oracle_table
+
+    for b, o in (edge_case_set(), hot_set()):
+        t = O.kcount_mt(b, o, k, threads=4)
+        keys, c, l, r = t.fetch()
+        assert_tables_equal(m.KmerTable(k, keys, c, l, r), oracle_table(b, o, k), f"mt edge/hot k={k}")
+
+
+@pytest.mark.parametrize("cutoff,dmin,dyn", [(0, 2, 0.9), (25, 3, 0.75), (20, 0, 0.0), (32, 5, 1.0)])
+def test_mt_restatement_parameters(cutoff, dmin, dyn):
+    from common import assert_tables_equal, oracle_table, synth_set
+
+    b, o = synth_set(1500, 8000, 7)
+    t = O.kcount_mt(b, o, 21, qual_cutoff=cutoff, dmin_thres=dmin, dyn_min_depth=dyn, threads=4)
+    keys, c, l, r = t.fetch()
+    assert_tables_equal(m.KmerTable(21, keys, c, l, r),
+                        oracle_table(b, o, 21, qual_cutoff=cutoff, dmin_thres=dmin, dyn_min_depth=dyn), "mt params")
+
+
+@pytest.mark.parametrize("name", sorted(p.name for p in GOLDEN.glob("table_*.tsv.gz")))
+def test_mt_restatement_reproduces_golden(name):
+    from common import GOLDEN, assert_tables_equal, read_reads_file, read_table_file
+
+    _, setname, kk = name[:-len(".tsv.gz")].split("_")
+    k = int(kk[1:])
+    b, o = read_reads_file(GOLDEN / f"reads_{setname}.txt.gz")
+    t = O.kcount_mt(b, o, k, threads=4)
+    keys, c, l, r = t.fetch()
+    assert_tables_equal(m.KmerTable(k, keys, c, l, r), read_table_file(GOLDEN / name, k), name)
