@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--reads-total", type=int, default=None, help="override (C3/C4: reads over all GPUs)")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
+    ap.add_argument("--cpu-sample-reads", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--h2d-steps", type=int, default=3, help="steps of the H2D-inclusive leg (0: skip)")
