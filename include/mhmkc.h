@@ -111,7 +111,8 @@ typedef struct {
   uint64_t slabs;          /* extracted record slabs (one per device batch or H2D chunk) */
   double ms_h2d;           /* device time of the H2D copies of the last mhmkc_add_reads (copy-stream events) */
   uint64_t lds_misses;     /* count kernel: records not found in their home slot group (LDS slow path) */
-  uint64_t lds_ext_adds;   /* count kernel: extension-counter increments */
+  uint64_t lds_ext_adds;   /* count kernel: extension-counter increments (from the sampled first coarse bucket,
+                              scaled to all records) */
 } mhmkc_stats;
 
 enum {

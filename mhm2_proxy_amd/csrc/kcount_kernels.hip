@@ -720,10 +720,14 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
 // the host sizes the fine partition (distinct keys per fine bucket vs the LDS table capacity). The key of
 // a record is its words without the ext code and stored hash bits (compact: the stored bits, unique within
 // the coarse bucket); the sketch hash is an fmix64 chain, independent of the partition hash.
+// It also counts the extension adds of these records (the LDS op mix of k_count, reported in the stats as
+// a sample of the whole).
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigned int *hll) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
   __shared__ unsigned int reg[SKETCH_M];
+  __shared__ unsigned int s_ext;
+  if (threadIdx.x == 0) s_ext = 0;
   for (int i = threadIdx.x; i < SKETCH_M; i += E_THREADS) reg[i] = 0;
   const SChunk ch = chunk_of<T>(p, blockIdx.x);
   const PlaneSet src = p.srcs[ch.src];
@@ -732,18 +736,22 @@ __global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigne
   load_chunk<NL, PACKED, CMP, W>(src, ch, rk, re);
   __syncthreads();
   const uint64_t low_mask = CMP ? 63ull : PACKED ? (1ull << (EXT_BITS + p.hbits)) - 1 : 0ull;
+  uint32_t ext_adds = 0;
 #pragma unroll
   for (int j = 0; j < W; j++) {
     if (threadIdx.x + j * E_THREADS >= ch.count) continue;
+    ext_adds += (uint32_t)(((re[j] >> 3) & 7u) < 4u) + (uint32_t)((re[j] & 7u) < 4u);
     uint64_t h = 0x9E3779B97F4A7C15ull;
 #pragma unroll
     for (int w = 0; w < NL; w++) h = fmix64(h ^ (w == NL - 1 ? rk[j][w] & ~low_mask : rk[j][w]));
     const uint32_t rho = (uint32_t)__clzll(h | (uint64_t)(SKETCH_M - 1)) + 1;  // first 1 among the top bits
     atomicMax(&reg[h & (SKETCH_M - 1)], rho);
   }
+  atomicAdd(&s_ext, ext_adds);
   __syncthreads();
   for (int i = threadIdx.x; i < SKETCH_M; i += E_THREADS)
     if (reg[i]) atomicMax(&hll[i], reg[i]);
+  if (threadIdx.x == 0 && s_ext) atomicAdd(&hll[SKETCH_M], s_ext);  // (one add per workgroup)
 }
 
 // capped fine layout
@@ -1236,10 +1244,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   };
 
   unsigned long long my_occ = 0, my_purged = 0, my_sum = 0, my_out = 0, my_sweeps = 0, my_maxb = 0;
-  uint32_t my_miss = 0, my_ext = 0;  // phase-B records (tid 0), extension adds (per lane): the LDS op mix
+  unsigned long long &s_missacc = s_u64[4];  // phase-B records of this workgroup (the LDS op mix, stats)
 #if MHMKC_STAMP
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
 #endif
+  if (tid == 0) s_missacc = 0;  // (the first sweep's clear ends with a barrier)
   uint32_t b = blockIdx.x;
   PlaneSet ps;
   uint32_t n;
@@ -1301,7 +1310,6 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           } else {
             ce[j] = valid ? nx[j] : NONE;
           }
-          my_ext += valid ? (uint32_t)(((ce[j] >> 3) & 7u) < 4u) + (uint32_t)((ce[j] & 7u) < 4u) : 0u;
         }
 #if MHMKC_STAMP
 #pragma unroll
@@ -1396,7 +1404,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #else
         const unsigned int M = min(*nmiss, (unsigned int)MCL);
 #endif
-        if (tid == 0) my_miss += M;
+        if (tid == 0) s_missacc += M;
         if (!B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
         for (unsigned int q = tid; q < M; q += C_THREADS) {
           uint64_t key[NL];
@@ -1531,9 +1539,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   my_occ = wave_sum_u64(my_occ);
   my_purged = wave_sum_u64(my_purged);
   my_sum = wave_sum_u64(my_sum);
-  const unsigned long long wext = wave_sum_u64(my_ext);
-  if (lane == 0 && wext) atomicAdd(&p.stats[STAT_EXTADDS], wext);
-  if (tid == 0 && my_miss) atomicAdd(&p.stats[STAT_MISSES], (unsigned long long)my_miss);
+  if (tid == 0 && s_missacc) atomicAdd(&p.stats[STAT_MISSES], s_missacc);
   if (tid == 0) {
     s_red[0] = 0;
     s_red[1] = 0;

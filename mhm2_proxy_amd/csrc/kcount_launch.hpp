@@ -151,7 +151,6 @@ enum {
   STAT_MAXBUCKET = 5,
   STAT_MISSES = 6,    // records worked off in phase B (not in their home group)
   STAT_N = 8,         // stats[STAT_N - 1]: internal error flag
-  STAT_EXTADDS = 14   // extension-counter adds (records with an A/C/G/T neighbour, per side)
 };
 constexpr int STAT_ALLOC = 16;  // stats[8..13]: k_count phase stamps in MHMKC_STAMP builds
 
@@ -211,7 +210,7 @@ hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 // HyperLogLog sketch of the distinct keys in chunks [0, n_chunks) of p's chunk table (one coarse bucket):
-// hll[SKETCH_M] registers, max-merged (zero them first).
+// hll[SKETCH_M] registers, max-merged, and hll[SKETCH_M] += the records' extension adds (zero them first).
 constexpr int SKETCH_M = 1024;
 hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
                          hipStream_t s);

@@ -989,16 +989,19 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     sp.coarse_bits = cb;
     sp.hbits = hbits;
     sp.compact = compact;
-    std::vector<uint32_t> reg(mhm::SKETCH_M);
+    std::vector<uint32_t> reg(mhm::SKETCH_M + 1);
     prof_begin(MHMKC_STAGE_OTHER);
-    if ((e = grow(d_hll, 4 * mhm::SKETCH_M)) != hipSuccess ||
-        (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_M, stream)) != hipSuccess ||
+    if ((e = grow(d_hll, 4 * mhm::SKETCH_M + 64)) != hipSuccess ||
+        (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_M + 4, stream)) != hipSuccess ||
         (e = mhm::launch_sketch(sp, (uint32_t)n_c0, d_hll.as<unsigned int>(), nl, packed, stream)) != hipSuccess)
       return hip_fail(e, "distinct sketch");
     prof_end();
-    if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * mhm::SKETCH_M, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+    if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * mhm::SKETCH_M + 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipStreamSynchronize(stream)) != hipSuccess)
       return hip_fail(e, "sketch D2H");
+    // extension adds of the sampled coarse bucket, scaled to all owned records (the LDS op mix, stats only)
+    if (per_coarse[0]) st.lds_ext_adds = (uint64_t)((double)reg[mhm::SKETCH_M] * (double)owned / (double)per_coarse[0]);
+    reg.resize(mhm::SKETCH_M);
     const double est = hll_estimate(reg);
     st.distinct_estimate = (uint64_t)(est * no);
     while (fb < 11 && est / (double)(1u << fb) > FINE_LOAD * cap_slots) fb++;
@@ -1159,7 +1162,6 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   st.overflow_sweeps = stats[mhm::STAT_SWEEPS];
   st.max_bucket = stats[mhm::STAT_MAXBUCKET];
   st.lds_misses = stats[mhm::STAT_MISSES];
-  st.lds_ext_adds = stats[mhm::STAT_EXTADDS];
   st.dropped = 0;
   n_out = st.n_out;
   if (n_out > out_cap) return fail(MHMKC_EHIP, "internal: output overflow");
