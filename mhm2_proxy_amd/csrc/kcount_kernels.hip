@@ -43,6 +43,10 @@ template <typename T>
 __device__ __forceinline__ T gload(const T *p) {
   return *(const __attribute__((address_space(1))) T *)p;
 }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 gload4(const uint32_t *p) {  // one 16-byte global load (p 16-byte aligned)
+  return *(const __attribute__((address_space(1))) u32x4 *)p;
+}
 
 // All LDS is carved from the one dynamic region at 16-byte aligned offsets (cdna_hip_programming.md
 // Guideline 17): fwd[NG] u64 | good[NG] u32 | start[NG] u32 | rest.
@@ -793,8 +797,9 @@ __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, uns
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint32_t per = (n + 1023) / 1024;
   const uint32_t lo = min((uint32_t)tid * per, n), hi = min(lo + per, n);
+  // bucket bases are kept multiples of 4 records (k_count's compact rounds load 4 records per lane)
   unsigned long long s = 0;
-  for (uint32_t i = lo; i < hi; i++) s += in[i];
+  for (uint32_t i = lo; i < hi; i++) s += (in[i] + 3) & ~3ull;
   unsigned long long x = s;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -816,7 +821,7 @@ __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, uns
   for (uint32_t i = lo; i < hi; i++) {
     base[i] = run;
     cursor[i] = run;
-    run += in[i];
+    run += (in[i] + 3) & ~3ull;
   }
 }
 
@@ -847,6 +852,15 @@ __device__ __forceinline__ uint32_t slot_hash(const uint64_t *key) {
   return (uint32_t)(h >> 32);
 }
 
+// Home group of a compact key. The stored bits of a compact record are bits of the bijectively mixed k-mer
+// (kmer_ops.hpp cmix) below the bucket digits, already uniform: the group is their top 16 bits scaled to the
+// group count with one full-rate 24-bit multiply (the generic slot_hash + fastrange cost three quarter-rate
+// multiplies, in a kernel whose VALU issue is its limit). kshl = 26 - stored bits: the key word holds them in
+// bits [6, 32 - kshl).
+__device__ __forceinline__ int cmp_group(uint32_t key, int kshl, uint32_t ng) {
+  return (int)(__umul24((key << kshl) >> 16, ng) >> 16);
+}
+
 template <typename K>  // key word type: uint64_t, or uint32_t for compact records
 struct CountLds {
   K *keys;         // [NL][cap]
@@ -859,6 +873,11 @@ struct CountLds {
 #define MHMKC_BOVERLAP 1
 #endif
 constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
+
+// Two-pass finalize (list the slots with count >= 2, then decide them densely); 0 = one pass over all slots.
+#ifndef MHMKC_FIN2
+#define MHMKC_FIN2 1
+#endif
 
 // Groups a key may probe before its record is deferred to the next sweep of its bucket.
 #ifndef MHMKC_CPROBE
@@ -978,14 +997,38 @@ __device__ __forceinline__ uint32_t lds_add(const CountLds<K> &t, int slot, uint
   return old;
 }
 
-// lds_add without the old count (ds_add_u32 without return: nothing to wait for), for sweeps of fewer than
-// 0xC000 records, whose counters cannot reach the clamp level (a counter never exceeds the sweep's records).
+// The update of a cold sweep (fewer than 0xC000 records: no counter can reach the clamp level, a counter
+// never exceeds the sweep's records). Two non-returning adds and no branch: the count is not kept but
+// derived at the end, count = left A + C + G + T + left-none, where left-none (a neighbour that is not a
+// countable base) is counted in the count word (< 0xC000 there); a right-none add goes to a dummy word of
+// the wave. slot_count() reads it back; ctg_apply stores an explicit count as 0x80000000 | count.
+#ifndef MHMKC_COLD2
+#define MHMKC_COLD2 1
+#endif
+constexpr bool kCold2 = MHMKC_COLD2 != 0;
 template <typename K>
-__device__ __forceinline__ void lds_add_nr(const CountLds<K> &t, int slot, uint32_t e) {
+__device__ __forceinline__ void lds_add_nr(const CountLds<K> &t, int slot, uint32_t e, uint32_t *dummy) {
+  const uint32_t l = (e >> 3) & 7u, r = e & 7u;
+  if (kCold2) {
+    uint32_t *lw = l < 4u ? &t.ext[(l >> 1) * t.cap + slot] : &t.cnt[slot];
+    atomicAdd(lw, (l & 1u) ? 0x10000u : 1u);
+    uint32_t *rw = r < 4u ? &t.ext[(2 + (r >> 1)) * t.cap + slot] : dummy;
+    atomicAdd(rw, (r & 1u) ? 0x10000u : 1u);
+    return;
+  }
   atomicAdd(&t.cnt[slot], 1u);
-  const int l = (int)((e >> 3) & 7u), r = (int)(e & 7u);
   if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
   if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
+}
+
+// The count of an occupied slot (see lds_add_nr for the cold-sweep encoding).
+template <typename K>
+__device__ __forceinline__ uint32_t slot_count(const CountLds<K> &t, int slot, bool cold) {
+  const uint32_t c = t.cnt[slot];
+  if (!kCold2 || !cold) return c;
+  if (c >> 31) return c & 0x7fffffffu;
+  const uint32_t e0 = t.ext[slot], e1 = t.ext[t.cap + slot];
+  return c + (e0 & 0xffffu) + (e0 >> 16) + (e1 & 0xffffu) + (e1 >> 16);
 }
 
 // Saturation at the decision level: a 16-bit half that reached 0xC000 is CAS-clamped back to 0x8000.
@@ -1033,9 +1076,8 @@ __device__ __forceinline__ void lds_clamp(const CountLds<K> &t, int slot, uint32
 // count < 2 -> purged; left/right = get_ext(count) (kcount_cpu.cpp:173-182, with the exact double
 // expression of the dynamic threshold); both 'X' -> purged.
 template <typename K>
-__device__ __forceinline__ bool slot_survives(const CountLds<K> &t, int slot, const CountParams &p, uint16_t &c16,
-                                              char &L, char &R) {
-  const uint32_t c32 = t.cnt[slot];
+__device__ __forceinline__ bool slot_survives(const CountLds<K> &t, int slot, const CountParams &p, uint32_t c32,
+                                              uint16_t &c16, char &L, char &R) {
   const uint32_t c = c32 > 65535u ? 65535u : c32;
   c16 = (uint16_t)c;
   if (c < 2) return false;
@@ -1055,7 +1097,7 @@ __device__ __forceinline__ bool slot_survives(const CountLds<K> &t, int slot, co
 // bucket's last sweep has run (deferred keys are counted in a later sweep), and is finalized here
 // directly (insert_into_local_hashtable, kcount_cpu.cpp:503-522).
 template <int NL, bool CMP, typename K>
-__device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b, bool last_sweep,
+__device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b, bool last_sweep, bool cold,
                           unsigned long long *s_range) {
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -1091,7 +1133,8 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
       const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
       tkey[0] = (cmix(key[0] >> (64 - B), B) & ((1ull << rb) - 1)) << EXT_BITS;
     }
-    int g = (int)__umulhi(slot_hash<NL>(tkey), (uint32_t)ng);
+    int g = CMP ? cmp_group((uint32_t)tkey[0], 26 - (2 * p.k - p.coarse_bits - p.fine_bits), (uint32_t)ng)
+                : (int)__umulhi(slot_hash<NL>(tkey), (uint32_t)ng);
     int slot = -1;
     for (int pr = 0; pr < C_PROBE; pr++) {  // find only: a key in the table is within its probe window
       K v[4];
@@ -1105,7 +1148,8 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
       g = (g + 1 == ng) ? 0 : g + 1;
     }
     if (slot >= 0) {
-      const uint32_t rc = t.cnt[slot] > 65535u ? 65535u : t.cnt[slot];
+      const uint32_t c32 = slot_count(t, slot, cold);
+      const uint32_t rc = c32 > 65535u ? 65535u : c32;
       bool keep = false;
       if (rc >= 2) {
         const int thr = dyn_threshold(rc, p.dyn_mult, p.dmin_thres);
@@ -1120,7 +1164,7 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
         uint32_t ew[4] = {0, 0, 0, 0};
         if (l < 4) ew[l >> 1] |= h << ((l & 1u) * 16);
         if (r < 4) ew[2 + (r >> 1)] |= h << ((r & 1u) * 16);
-        t.cnt[slot] = c;
+        t.cnt[slot] = (kCold2 && cold) ? 0x80000000u | c : c;  // an explicit count (slot_count)
 #pragma unroll
         for (int i = 0; i < 4; i++) t.ext[i * t.cap + slot] = ew[i];
       }
@@ -1208,6 +1252,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
   const int ng = t.cap >> 2;
   const K *last = t.keys + (NL - 1) * t.cap;
+  const int kshl = CMP ? 26 - (2 * p.k - p.coarse_bits - p.fine_bits) : 0;  // cmp_group
 
   // Persistent workgroups: workgroup w counts buckets w, w + G, w + 2G, ... (G = grid size). The first
   // round of the next bucket is loaded while the current one is finalized, so no bucket starts with an
@@ -1216,7 +1261,22 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // and split into key / ext only when the round starts, so the loads stay in flight (see load_chunk).
   uint64_t nk[R][NL];
   uint32_t nx[R];
+  // Compact records: a lane takes 4 consecutive records of the round with one 16-byte load (bucket bases are
+  // multiples of 4 records: capped fine buckets are multiples of 16, the exact scan rounds them up), so one
+  // address per 4 records; lanes past the end re-read the last aligned quad (inside the bucket's region).
+  static_assert(!CMP || R == 4, "compact rounds take one 16-byte load of 4 records per lane");
   auto prefetch = [&](const PlaneSet &src, uint32_t cnt, uint32_t first) {
+    if constexpr (CMP) {
+      const uint32_t q = first + 4u * (uint32_t)tid, qmax = (cnt - 1) & ~3u;
+      const u32x4 v = gload4((const uint32_t *)src.w[0] + (q < qmax ? q : qmax));
+      nk[0][0] = v.x;
+      nk[1][0] = v.y;
+      nk[2][0] = v.z;
+      nk[3][0] = v.w;
+#pragma unroll
+      for (int j = 0; j < R; j++) nx[j] = 0;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < R; j++) {
       const uint32_t i = first + (uint32_t)tid + (uint32_t)j * C_THREADS;
@@ -1248,7 +1308,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #if MHMKC_STAMP
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
 #endif
-  if (tid == 0) s_missacc = 0;  // (the first sweep's clear ends with a barrier)
+  if (tid == 0) {  // (the first sweep's clear ends with a barrier)
+    s_missacc = 0;
+    s_u64[3] = 0;  // finalize's counters (MHMKC_FIN2)
+  }
   uint32_t b = blockIdx.x;
   PlaneSet ps;
   uint32_t n;
@@ -1301,7 +1364,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         uint32_t ce[R];
 #pragma unroll
         for (int j = 0; j < R; j++) {
-          const bool valid = r0 + (uint32_t)tid + (uint32_t)j * C_THREADS < n;
+          const bool valid = (CMP ? r0 + 4u * (uint32_t)tid + (uint32_t)j : r0 + (uint32_t)tid + (uint32_t)j * C_THREADS) < n;
 #pragma unroll
           for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
           if (PACKED) {
@@ -1340,7 +1403,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           K v[C_BATCH][4];
 #pragma unroll
           for (int j = j0; j < j0 + C_BATCH; j++) {
-            g[j] = (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
+            g[j] = CMP ? cmp_group((uint32_t)ck[j][0], kshl, (uint32_t)ng)
+                       : (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
             read_group(last, g[j], v[j - j0]);  // also for an invalid lane: harmless, keeps the batch uniform
           }
 #pragma unroll
@@ -1371,7 +1435,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           }
 #if !MHMKC_EXP_NOATOM
           if (COLD)
-            lds_add_nr(t, r, ce[j]);
+            lds_add_nr(t, r, ce[j], &s_wave[wid]);
           else
             old[j] = lds_add(t, r, ce[j]);
 #endif
@@ -1411,13 +1475,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
           for (int w = 0; w < NL; w++) key[w] = mkey[w * MCL + q];
           const uint32_t e = me[q];
-          const int g = (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
+          const int g = CMP ? cmp_group((uint32_t)key[0], kshl, (uint32_t)ng)
+                            : (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
           K v[4];
           read_group(last, g, v);
           const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
           if (r >= 0) {
             if (COLD)
-              lds_add_nr(t, r, e);
+              lds_add_nr(t, r, e, &s_wave[wid]);
             else if (lds_add(t, r, e) >= HOT)
               lds_clamp(t, r, e);
           } else if (r == -1) {
@@ -1438,7 +1503,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #endif
       }
     };
-    if (n < 0xC000u)
+    // (s_wave holds the dummy words of the cold adds until finalize overwrites it after a barrier)
+    const bool cold = n < 0xC000u;
+    if (cold)
       rounds(std::true_type{});
     else
       rounds(std::false_type{});
@@ -1446,12 +1513,83 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP(t_f0);
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
-    if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, s_red);
+    if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
     if (last_sweep && b_next < p.n_buckets) {
       bucket(b_next, ps_next, nb_next);
       if (nb_next) prefetch(ps_next, nb_next, 0);
     }
 
+#if MHMKC_FIN2
+    // finalize in two passes. 1: occupancy and count of every slot; the slots with count >= 2 (the only ones
+    // that can survive) are listed in the miss-list space (free: phase B of the last round ended before the
+    // barrier above). 2: the listed slots, dense over the lanes, get get_ext and the X/X purge. (One pass
+    // took every lane through the whole decision for each of its 6 slots whether or not it was occupied.)
+    uint16_t *flist = (uint16_t *)s_mkey;
+    unsigned int *s_fin = (unsigned int *)(s_u64 + 3);  // [0] listed slots, [1] survivors (zeroed between buckets)
+    uint32_t occ = 0;
+    unsigned long long sum = 0;
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+      const int slot = tid + j * C_THREADS;
+      if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != (K)KEY_EMPTY) {
+        occ++;
+        const uint32_t c32 = slot_count(t, slot, cold);
+        sum += c32;
+        if (c32 >= 2) flist[atomicAdd(&s_fin[0], 1u)] = (uint16_t)slot;
+      }
+    }
+    __syncthreads();
+    const uint32_t n_list = s_fin[0];
+    uint32_t surv_mask = 0, spos[SPT];
+    uint16_t c16[SPT], fslot[SPT];
+    char L[SPT], R_[SPT];
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+      const uint32_t i = (uint32_t)tid + (uint32_t)j * C_THREADS;
+      spos[j] = 0;
+      fslot[j] = 0;
+      if (i < n_list) {
+        const int slot = flist[i];
+        fslot[j] = (uint16_t)slot;
+#if !MHMKC_EXP_NOFIN
+        if (slot_survives(t, slot, p, slot_count(t, slot, cold), c16[j], L[j], R_[j])) {
+          surv_mask |= 1u << j;
+          spos[j] = atomicAdd(&s_fin[1], 1u);
+        }
+#endif
+      }
+    }
+    const uint32_t mine = __popc(surv_mask);
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t acc = s_fin[1];
+      s_gbase = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      my_out += acc;
+      s_fin[0] = 0;
+      s_fin[1] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+      if ((surv_mask >> j) & 1u) {
+        const int slot = fslot[j];
+        const unsigned long long g = s_gbase + spos[j];
+        uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
+        if (CMP) {  // key = cunmix(global fine bucket digits | stored bits)
+          const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
+          const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          ok[0] = cunmix(y, B) << (64 - B);
+        } else {
+#pragma unroll
+          for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
+        }
+        for (int w = NL; w < p.nlo; w++) ok[w] = 0;
+        p.out_counts[g] = c16[j];
+        p.out_left[g] = L[j];
+        p.out_right[g] = R_[j];
+      }
+    }
+#else
     // finalize in one pass: decisions in registers, wave-prefix offsets, one global reservation
     uint32_t occ = 0, surv_mask = 0;
     unsigned long long sum = 0;
@@ -1464,9 +1602,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       L[j] = R_[j] = 0;
       if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != (K)KEY_EMPTY) {
         occ++;
-        sum += t.cnt[slot];
+        const uint32_t c32 = slot_count(t, slot, cold);
+        sum += c32;
 #if !MHMKC_EXP_NOFIN
-        if (slot_survives(t, slot, p, c16[j], L[j], R_[j])) surv_mask |= 1u << j;
+        if (slot_survives(t, slot, p, c32, c16[j], L[j], R_[j])) surv_mask |= 1u << j;
 #endif
       }
     }
@@ -1511,8 +1650,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         g++;
       }
     }
+#endif
     my_occ += occ;
-    my_purged += occ - mine;
+    my_purged += occ;  // minus the survivors, in 64 bits: with two passes a lane's survivors are not its slots
+    my_purged -= mine;
     my_sum += sum;
     __syncthreads();
     STAMP(t_f1);

@@ -1089,8 +1089,8 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   unsigned int errf = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     mhm::PlaneSet r2{};
-    if (exact) {
-      if ((rc = set_planes(d_r2, owned, r2, true))) return rc;
+    if (exact) {  // (k_scan rounds every bucket up to a multiple of 4 records)
+      if ((rc = set_planes(d_r2, owned + 3 * (uint64_t)n_fine + 4, r2, true))) return rc;
     } else {
       if ((rc = set_planes(d_r2, r2_size, r2, true))) return rc;
     }
