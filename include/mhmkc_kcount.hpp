@@ -234,6 +234,7 @@ struct RankInfo {
   const mhmkc_transport *transport = nullptr;
   int device = -1;
   int output_owner = MHMKC_OWNER_MINIMIZER;
+  bool table_only = false;  // no counter: the KmerDHT only holds a table given to load_table (no GPU used)
 };
 
 template <int MAX_K>
@@ -253,6 +254,7 @@ class HashTableInserter {
   // kcount_cpu.cpp:425-443; the estimate only sized the CPU table, the GPU path sizes itself exactly. The
   // depth threshold is not known yet: analyze_kmers sets _dmin_thres later (kcount.cpp:145).
   void init(int /*num_elems*/, bool /*use_qf*/, const RankInfo &ri = RankInfo()) {
+    if (ri.table_only) return;
     mhmkc_config cfg;
     mhmkc_config_init(&cfg);
     cfg.k = (int)Kmer<MAX_K>::get_k();
@@ -368,6 +370,17 @@ class KmerDHT {
   void add_fastq(const std::string &text) { ht_inserter.add_fastq(text); }
   void flush_updates() { ht_inserter.flush_inserts(); }
   void finish_updates() { ht_inserter.insert_into_local_hashtable(local_kmers); }
+  // fill the local KmerMap from a finished table in mhmkc_fetch's layout (n_longs = N_LONGS words per key)
+  void load_table(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n) {
+    local_kmers.reserve(local_kmers.size() + n);
+    for (uint64_t i = 0; i < n; i++) {
+      KmerCounts kc;
+      kc.count = counts[i];
+      kc.left = left[i];
+      kc.right = right[i];
+      local_kmers.emplace(Kmer<MAX_K>(&keys[i * Kmer<MAX_K>::N_LONGS]), kc);
+    }
+  }
   KmerCounts *get_local_kmer_counts(const Kmer<MAX_K> &kmer) {
     auto it = local_kmers.find(kmer);
     return it == local_kmers.end() ? nullptr : &it->second;
