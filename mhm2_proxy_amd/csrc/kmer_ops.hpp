@@ -101,7 +101,7 @@ MHM_HD uint64_t part_hash(const uint64_t *w) {
 
 // ------------------------------------------------------------------------------------------------
 // Compact records (one key word, 10 <= k <= 21). The partition hash of a compact key is
-// a bijection y = cmix(x) of its B = 2k key bits x, so the coarse and fine bucket digits (the top bits
+// a bijection y = cmix(x) of its B = 2k key bits x (20 <= B <= 42), so the coarse and fine bucket digits (the top bits
 // of y) need not be stored: a coarse-bucketed record keeps the low B - cb bits of y next to the ext
 // code (<= 40 bits: a u32 plane + a byte plane), a fine-bucketed record the low B - cb - fb bits
 // (<= 32 bits: one u32 plane), and k_count rebuilds the key as cunmix(bucket digits | stored bits).
@@ -119,7 +119,28 @@ constexpr uint64_t inv_odd(uint64_t a) {  // a^-1 mod 2^64 (Newton: the correct 
 }
 constexpr uint64_t CMIX_I1 = inv_odd(CMIX_M1), CMIX_I2 = inv_odd(CMIX_M2);
 
+#ifndef MHMKC_FEISTEL
+#define MHMKC_FEISTEL 1
+#endif
+// MHMKC_FEISTEL (default): a 4-round Feistel network on the two halves of the B key bits (a = B/2 low bits,
+// b = B - a <= 21 high bits; a Feistel round is invertible whatever its round function). The round function
+// takes bits [11, 11 + n) of the low 32 bits of a 24 x 24-bit product: one full-rate v_mul_u32_u24, where the
+// xorshift-multiply chain over 64 bits needs quarter-rate 64-bit multiplies (extraction is VALU-bound).
+constexpr uint32_t FEISTEL_K[4] = {0x9E3779u, 0x85EBCAu, 0xC2B2AEu, 0x27D4EBu};
+MHM_HD uint32_t feistel_f(uint32_t v, uint32_t c, int n) {
+  return ((((v ^ (v >> 9)) & 0xffffffu) * c) >> 11) & ((1u << n) - 1);
+}
+
 MHM_HD uint64_t cmix(uint64_t x, int B) {
+#if MHMKC_FEISTEL
+  const int a = B >> 1, b = B - a;
+  uint32_t R = (uint32_t)x & ((1u << a) - 1), L = (uint32_t)(x >> a);
+  L ^= feistel_f(R, FEISTEL_K[0], b);
+  R ^= feistel_f(L, FEISTEL_K[1], a);
+  L ^= feistel_f(R, FEISTEL_K[2], b);
+  R ^= feistel_f(L, FEISTEL_K[3], a);
+  return ((uint64_t)L << a) | R;
+#else
   const uint64_t m = (1ull << B) - 1;
   const int s = (B + 1) >> 1;
   x ^= x >> s;
@@ -128,9 +149,19 @@ MHM_HD uint64_t cmix(uint64_t x, int B) {
   x = (x * CMIX_M2) & m;
   x ^= x >> s;
   return x;
+#endif
 }
 
 MHM_HD uint64_t cunmix(uint64_t y, int B) {
+#if MHMKC_FEISTEL
+  const int a = B >> 1, b = B - a;
+  uint32_t R = (uint32_t)y & ((1u << a) - 1), L = (uint32_t)(y >> a);
+  R ^= feistel_f(L, FEISTEL_K[3], a);
+  L ^= feistel_f(R, FEISTEL_K[2], b);
+  R ^= feistel_f(L, FEISTEL_K[1], a);
+  L ^= feistel_f(R, FEISTEL_K[0], b);
+  return ((uint64_t)L << a) | R;
+#else
   const uint64_t m = (1ull << B) - 1;
   const int s = (B + 1) >> 1;
   y ^= y >> s;
@@ -139,6 +170,7 @@ MHM_HD uint64_t cunmix(uint64_t y, int B) {
   y = (y * CMIX_I1) & m;
   y ^= y >> s;
   return y;
+#endif
 }
 
 // Partition hash of a compact key word (2k bits, left-aligned): the mixed key, left-aligned, so that the

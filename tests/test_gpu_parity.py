@@ -392,26 +392,24 @@ def _hot_key_last_bucket(k: int) -> str:
     rng = np.random.default_rng(k)
     nl = k // 32 + 1
     B = 2 * k
-    M = (1 << B) - 1
-    M1, M2 = 0xff51afd7ed558ccd, 0xc4ceb9fe1a85ec53
+    FK = (0x9E3779, 0x85EBCA, 0xC2B2AE, 0x27D4EB)  # kmer_ops.hpp cunmix (Feistel, MHMKC_FEISTEL)
 
-    def inv(a):
-        x = a
-        for _ in range(6):
-            x = (x * (2 - a * x)) & ((1 << 64) - 1)
-        return x
+    def f(v, c, n):
+        return ((((v ^ (v >> 9)) & 0xffffff) * c & 0xffffffff) >> 11) & ((1 << n) - 1)
 
-    I1, I2 = inv(M1), inv(M2)
-    s_ = (B + 1) >> 1
+    def cunmix(y):
+        a, bb = B >> 1, B - (B >> 1)
+        R, L = y & ((1 << a) - 1), y >> a
+        R ^= f(L, FK[3], a)
+        L ^= f(R, FK[2], bb)
+        R ^= f(L, FK[1], a)
+        L ^= f(R, FK[0], bb)
+        return (L << a) | R
+
     for _ in range(1 << 22):
         if k <= 21:  # cunmix of a y with the top bits set
             y = (((1 << 19) - 1) << (B - 19)) | int(rng.integers(0, 1 << (B - 19)))
-            y ^= y >> s_
-            y = (y * I2) & M
-            y ^= y >> s_
-            y = (y * I1) & M
-            y ^= y >> s_
-            key = np.array([y << (64 - B)], dtype=np.uint64)
+            key = np.array([cunmix(y) << (64 - B)], dtype=np.uint64)
         else:
             key = np.array([int(x) for x in rng.integers(0, 1 << 62, nl)], dtype=np.uint64)
             key[-1] &= np.uint64((~((1 << (64 - 2 * (k - 32 * (nl - 1)))) - 1)) & ((1 << 64) - 1))
