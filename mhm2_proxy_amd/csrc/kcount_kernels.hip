@@ -486,12 +486,16 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       if (!PACKED) sext[pos] = (uint8_t)((inf[j] >> 16) & 63u);
     }
   }
+  // A bin that overflows its capped segment flags the pass (the host redoes it with exact sizes) and writes
+  // nothing: its run offset becomes ~0, so the copy-out below tests one loaded word per record instead of
+  // recomputing the segment end (a 64-bit multiply per record)
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint32_t b = threadIdx.x + i * E_THREADS;
     if (b < nb) {
-      if (lim.cap && cnt[i] && off[i] + cnt[i] > lim.end(b)) atomicOr(err, 2u);
-      goff[b] = off[i];
+      const bool over = lim.cap && cnt[i] && off[i] + cnt[i] > lim.end(b);
+      if (over) atomicOr(err, 2u);
+      goff[b] = over ? ~0ull : off[i];
     }
   }
   __syncthreads();
@@ -500,8 +504,9 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
     const uint32_t pos = threadIdx.x + j * E_THREADS;
     if (pos < total) {
       const uint32_t d = sbin[pos];
-      const unsigned long long dst = goff[d] + (pos - lstart[d]);
-      if (lim.cap && dst >= lim.end(d)) continue;
+      const unsigned long long go = goff[d];
+      if (go == ~0ull) continue;
+      const unsigned long long dst = go + (pos - lstart[d]);
       uint64_t v[NL];
       if (C32) {
         v[0] = (uint64_t)stage32[pos] | (SF == SF_C40 ? (uint64_t)sext[pos] << 32 : 0ull);
@@ -915,6 +920,14 @@ constexpr int G_FULL = -8, G_BUSY = -9;
 template <int NL, typename K>
 __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_t *key, int g, const K (&v)[4]) {
   const K kl = (K)key[NL - 1];
+  if constexpr (NL == 1) {  // single-word keys: eight compares and selects, no branch (a key is never EMPTY)
+    int r = G_FULL;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;  // the first empty slot
+#pragma unroll
+    for (int i = 3; i >= 0; i--) r = v[i] == kl ? 4 * g + i : r;  // the key itself takes precedence
+    return r;
+  }
   int found = -1, empty = -1;
   bool busy = false;
 #pragma unroll
