@@ -153,7 +153,16 @@ __global__ __launch_bounds__(G_THREADS) void k_ctg_fold(PlaneSet keys, const uin
         R = r;
       }
     }
-    const uint64_t h = (NL == 1 && cmpB) ? cpart_hash(key[0], cmpB) : part_hash<NL>(key);  // as k_extract_scatter
+    uint64_t h;  // the partition hash of k_extract_scatter
+    if (NL == 1 && cmpB) {
+      h = cpart_hash(key[0], cmpB);
+    } else if (NL == 2 && cmpB) {  // mixed two-word records: L' of m2_mix, left-aligned
+      uint64_t L, R;
+      m2_mix(key, cmpB / 2, L, R);
+      h = L << (64 - cmpB / 2);
+    } else {
+      h = part_hash<NL>(key);
+    }
     const uint32_t coarse = (uint32_t)(h >> (64 - cb));
     if (coarse < own_lo || coarse >= own_hi) continue;  // another rank's hash range (it folds this key itself)
     const uint32_t fine = fb ? (uint32_t)((h >> (64 - cb - fb)) & ((1ull << fb) - 1)) : 0u;
@@ -259,7 +268,7 @@ hipError_t prepare(const CtgView &cv, int k, int qcut, int dmin, double dyn_mult
 
 size_t ctg_scratch_bytes(uint64_t n_windows, int nl) { return carve(nullptr, n_windows, nl, nullptr); }
 
-hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool compact, int qual_cutoff, int dmin_thres,
+hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool mixed, int qual_cutoff, int dmin_thres,
                        double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi, void *scratch,
                        size_t scratch_bytes,
                        uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,
@@ -269,7 +278,7 @@ hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool compact, int qual_
   if (cv.n_windows >= 0xffffffffull) return hipErrorInvalidValue;  // 32-bit window indices
   Scratch sc;
   if (carve(scratch, cv.n_windows, nl, &sc) > scratch_bytes) return hipErrorInvalidValue;
-  const int cmpB = compact ? 2 * k : 0;
+  const int cmpB = mixed ? 2 * k : 0;  // compact (NL = 1) or mixed two-word (NL = 2) records
   switch (nl) {
     case 1: return prepare<1>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);

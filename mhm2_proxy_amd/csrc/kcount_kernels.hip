@@ -317,12 +317,27 @@ __global__ void k_tile_first_read(ReadsView rv, uint32_t *out, uint32_t n_tiles,
 // ------------------------------------------------------------------------------------------------
 // extract: histogram
 
-// Partition hash of a window's key: MurmurHash3 h1 (part_hash), or the key bijection of compact records.
+// Partition hash of a window's key: MurmurHash3 h1 (part_hash), or the key bijection of mixed records
+// (compact: cmix; two words: L' of m2_mix), left-aligned so that the digits are its top bits.
 template <int NL, bool CMP>
 __device__ __forceinline__ uint64_t window_hash(const uint64_t *key, int k) {
-  if (CMP) return cpart_hash(key[0], 2 * k);
+  if (CMP && NL == 1) return cpart_hash(key[0], 2 * k);
+  if (CMP && NL == 2) {
+    uint64_t L, R;
+    m2_mix(key, k, L, R);
+    return L << (64 - k);
+  }
   return part_hash<NL>(key);
 }
+
+// Record layout traits: compact (one u32 word, NL = 1) and mixed two-word records (NL = 2, ext code in w[0],
+// kmer_ops.hpp m2_mix) are the two kinds of "mixed" records (CMP) whose bucket digits are implicit.
+template <int NL, bool CMP>
+struct RecKind {
+  static constexpr bool C32 = CMP && NL == 1;
+  static constexpr bool M2 = CMP && NL == 2;
+  static constexpr int XW = M2 ? 0 : NL - 1;  // the word holding the ext code of a packed record
+};
 
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
@@ -555,10 +570,23 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   const int hsh = p.hbits ? 64 - p.hbits : 0;
   const uint64_t hmask = p.hbits ? ~0ull : 0ull;
   const int csh = 64 - (2 * p.k - p.coarse_bits);  // compact: keep the low 2k - cb bits of the mixed key
+  const int m2_csh = p.k - p.coarse_bits;            // mixed two-word: L' >> m2_csh = coarse digit
+  const uint64_t m2_cmask = (1ull << m2_csh) - 1;
   uint64_t rk[W][NL];
   uint32_t inf[W];
   walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, p.k,
                    [&](int i, const uint64_t *key, uint32_t e, bool valid) {
+                     if constexpr (RecKind<NL, CMP>::M2) {  // (L' below the coarse digit) << 6 | ext, R'
+                       uint64_t L, R;
+                       m2_mix(key, p.k, L, R);
+                       rk[i][0] = ((L & m2_cmask) << EXT_BITS) | e;
+                       rk[i][1] = R;
+                       inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(L >> m2_csh) : 0u;
+#pragma unroll
+                       for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[i][w]));
+                       asm volatile("" : "+v"(inf[i]));
+                       return;
+                     }
                      const uint64_t h = window_hash<NL, CMP>(key, p.k);
 #pragma unroll
                      for (int w = 0; w < NL; w++) rk[i][w] = key[w];
@@ -577,7 +605,7 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
                    });
   const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
-  constexpr int SF = CMP ? SF_C40 : SF_WORDS;
+  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS;
   if (kEStaged)
     scatter_staged<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
                                       p.ovf);
@@ -593,7 +621,8 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
 template <int NL, bool PACKED, bool CMP>
 __device__ __forceinline__ uint32_t fine_digit(const uint64_t *rk, const PartitionParams &p) {
   const uint64_t fmask = (1ull << p.fine_bits) - 1;
-  if (CMP) return (uint32_t)((rk[0] >> (EXT_BITS + 2 * p.k - p.coarse_bits - p.fine_bits)) & fmask);
+  if (CMP && NL == 1) return (uint32_t)((rk[0] >> (EXT_BITS + 2 * p.k - p.coarse_bits - p.fine_bits)) & fmask);
+  if (CMP && NL == 2) return (uint32_t)((rk[0] >> (EXT_BITS + p.k - p.coarse_bits - p.fine_bits)) & fmask);
   if (PACKED && p.hbits >= p.fine_bits) {
     const uint64_t stored = (rk[NL - 1] >> EXT_BITS) & ((1ull << p.hbits) - 1);
     return (uint32_t)((stored >> (p.hbits - p.fine_bits)) & fmask);
@@ -646,7 +675,7 @@ __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch
   for (int j = 0; j < W; j++) {
     const uint32_t i = threadIdx.x + j * E_THREADS;
     const uint64_t idx = ch.start + (i < ch.count ? i : ch.count - 1);
-    if (CMP) {  // coarse compact record: low 32 bits + high byte
+    if (RecKind<NL, CMP>::C32) {  // coarse compact record: low 32 bits + high byte
       rk[j][0] = (uint64_t)gload((const uint32_t *)src.w[0] + idx);
       rx[j] = (uint32_t)gload(src.ext + idx);
       continue;
@@ -655,12 +684,12 @@ __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch
     for (int w = 0; w < NL; w++) rk[j][w] = gload(src.w[w] + idx);
     rx[j] = PACKED ? 0u : (uint32_t)gload(src.ext + idx);
   }
-  if (CMP) {
+  if (RecKind<NL, CMP>::C32) {
 #pragma unroll
     for (int j = 0; j < W; j++) rk[j][0] |= (uint64_t)rx[j] << 32;
   }
 #pragma unroll
-  for (int j = 0; j < W; j++) re[j] = PACKED ? (uint32_t)(rk[j][NL - 1] & 63u) : rx[j];
+  for (int j = 0; j < W; j++) re[j] = PACKED ? (uint32_t)(rk[j][RecKind<NL, CMP>::XW] & 63u) : rx[j];
 }
 
 template <int NL, bool PACKED, bool CMP>
@@ -702,8 +731,9 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
   uint64_t rk[W][NL];
   uint32_t re[W], inf[W];
   load_chunk<NL, PACKED, CMP, W>(src, ch, rk, re);
-  // compact: the fine record keeps the bits below the fine digit (+ the ext code), <= 32 bits
-  const uint64_t cmask = (1ull << (EXT_BITS + 2 * p.k - p.coarse_bits - p.fine_bits)) - 1;
+  // compact: the fine record keeps the bits below the fine digit (+ the ext code), <= 32 bits; mixed
+  // two-word: w[0] keeps L' below the fine digit (+ the ext code)
+  const uint64_t cmask = (1ull << (EXT_BITS + (NL == 1 ? 2 * p.k : p.k) - p.coarse_bits - p.fine_bits)) - 1;
 #pragma unroll
   for (int j = 0; j < W; j++) {
     inf[j] = (threadIdx.x + j * E_THREADS < ch.count)
@@ -718,7 +748,7 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
     lim = BinLimit{p.coarse_base[ch.coarse_local], fc, fc};
   }
   unsigned long long *cur = p.fine_cursor + (uint64_t)ch.coarse_local * nf;
-  constexpr int SF = CMP ? SF_C32 : SF_WORDS;
+  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS;
   if (kPStaged)
     scatter_staged<NL, PACKED, W, SF>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
   else
@@ -752,7 +782,7 @@ __global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigne
     ext_adds += (uint32_t)(((re[j] >> 3) & 7u) < 4u) + (uint32_t)((re[j] & 7u) < 4u);
     uint64_t h = 0x9E3779B97F4A7C15ull;
 #pragma unroll
-    for (int w = 0; w < NL; w++) h = fmix64(h ^ (w == NL - 1 ? rk[j][w] & ~low_mask : rk[j][w]));
+    for (int w = 0; w < NL; w++) h = fmix64(h ^ (w == RecKind<NL, CMP>::XW ? rk[j][w] & ~low_mask : rk[j][w]));
     const uint32_t rho = (uint32_t)__clzll(h | (uint64_t)(SKETCH_M - 1)) + 1;  // first 1 among the top bits
     atomicMax(&reg[h & (SKETCH_M - 1)], rho);
   }
@@ -838,8 +868,11 @@ __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, uns
 #define MHMKC_CRPT 4
 #endif
 template <int NL>
+#ifndef MHMKC_CRPT2
+#define MHMKC_CRPT2 2
+#endif
 constexpr int count_rpt() {
-  return NL == 1 ? MHMKC_CRPT : 2;
+  return NL == 1 ? MHMKC_CRPT : NL == 2 ? MHMKC_CRPT2 : 2;
 }
 
 // LDS slot hash of k_count. All keys of a fine bucket share their top MurmurHash3 bits, so the slot
@@ -917,6 +950,9 @@ __device__ __forceinline__ bool rest_equal(const CountLds<K> &t, int slot, const
 // Result of looking at one group for key: >= 0 the slot holding it, -1 - i an empty slot i (and the key is
 // not in the group), G_FULL no empty slot and no key, G_BUSY a multi-word key is being written.
 constexpr int G_FULL = -8, G_BUSY = -9;
+#ifndef MHMKC_EXAM2
+#define MHMKC_EXAM2 1
+#endif
 template <int NL, typename K>
 __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_t *key, int g, const K (&v)[4]) {
   const K kl = (K)key[NL - 1];
@@ -927,6 +963,18 @@ __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_
 #pragma unroll
     for (int i = 3; i >= 0; i--) r = v[i] == kl ? 4 * g + i : r;  // the key itself takes precedence
     return r;
+  }
+  if constexpr (NL == 2 && MHMKC_EXAM2) {  // the same on the last word, then one read of the first word
+    int r = G_FULL;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) r = v[i] == (K)KEY_BUSY ? G_BUSY : r;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) r = v[i] == kl ? 4 * g + i : r;
+    // a slot holding the last word: the key iff its first word matches too (a second slot of the group with
+    // the same last word is possible, so a mismatch falls back to the full examination below)
+    if (r < 0 || t.keys[r] == (K)key[0]) return r;
   }
   int found = -1, empty = -1;
   bool busy = false;
@@ -1142,12 +1190,18 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
     uint64_t tkey[NL];  // the key as the table holds it
 #pragma unroll
     for (int w = 0; w < NL; w++) tkey[w] = key[w];
-    if (CMP) {  // compact: the mixed key's bits below the bucket digits, above the ext code
+    if (RecKind<NL, CMP>::C32) {  // compact: the mixed key's bits below the bucket digits, above the ext code
       const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
       tkey[0] = (cmix(key[0] >> (64 - B), B) & ((1ull << rb) - 1)) << EXT_BITS;
+    } else if (RecKind<NL, CMP>::M2) {  // mixed two-word: L' below the bucket digits << 6, R'
+      uint64_t L, R;
+      m2_mix(key, p.k, L, R);
+      tkey[0] = (L & ((1ull << (p.k - p.coarse_bits - p.fine_bits)) - 1)) << EXT_BITS;
+      tkey[NL - 1] = R;
     }
-    int g = CMP ? cmp_group((uint32_t)tkey[0], 26 - (2 * p.k - p.coarse_bits - p.fine_bits), (uint32_t)ng)
-                : (int)__umulhi(slot_hash<NL>(tkey), (uint32_t)ng);
+    int g = RecKind<NL, CMP>::C32 ? cmp_group((uint32_t)tkey[0], 26 - (2 * p.k - p.coarse_bits - p.fine_bits), (uint32_t)ng)
+            : RecKind<NL, CMP>::M2 ? cmp_group((uint32_t)tkey[NL - 1], 16, (uint32_t)ng)
+                                   : (int)__umulhi(slot_hash<NL>(tkey), (uint32_t)ng);
     int slot = -1;
     for (int pr = 0; pr < C_PROBE; pr++) {  // find only: a key in the table is within its probe window
       K v[4];
@@ -1212,12 +1266,12 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
 // A deferred record goes back unchanged: key | raw low bits (ext code, stored hash bits).
 template <int NL, bool PACKED, bool CMP>
 __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, const uint64_t *key, uint32_t e) {
-  if (CMP) {
+  if (RecKind<NL, CMP>::C32) {
     ((uint32_t *)ps.w[0])[idx] = (uint32_t)(key[0] | e);
     return;
   }
 #pragma unroll
-  for (int w = 0; w < NL; w++) ps.w[w][idx] = (w == NL - 1 && PACKED) ? (key[w] | e) : key[w];
+  for (int w = 0; w < NL; w++) ps.w[w][idx] = (w == RecKind<NL, CMP>::XW && PACKED) ? (key[w] | e) : key[w];
   if (!PACKED) ps.ext[idx] = (uint8_t)e;
 }
 
@@ -1230,7 +1284,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // same word before any barrier.)
   if (p.err && (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2u)) return;
   extern __shared__ __align__(16) unsigned char smem[];
-  using K = typename std::conditional<CMP, uint32_t, uint64_t>::type;
+  using RK = RecKind<NL, CMP>;
+  using K = typename std::conditional<RK::C32, uint32_t, uint64_t>::type;
   CountLds<K> t;
   t.cap = p.cap;
   t.keys = (K *)smem;
@@ -1245,12 +1300,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
   unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
   // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
-  constexpr int MC = miss_cap(NL, CMP);
+  constexpr int MC = miss_cap(NL, RK::C32);
   // B_OVERLAP: phase B of round r overlaps phase A of round r + 1, so the miss list is double-buffered
   constexpr int MCL = B_OVERLAP ? (MC / 2) & ~63 : MC;
-  K *s_mkey = (K *)(smem + count_table_bytes(NL, CMP));
+  K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
-  constexpr int SPT = (count_cap(NL, CMP) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
+  constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -1265,7 +1320,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
   const int ng = t.cap >> 2;
   const K *last = t.keys + (NL - 1) * t.cap;
-  const int kshl = CMP ? 26 - (2 * p.k - p.coarse_bits - p.fine_bits) : 0;  // cmp_group
+  // cmp_group: compact keys from their top stored bits; mixed two-word keys from the low 16 bits of R' (the
+  // table's last word)
+  const int kshl = RK::C32 ? 26 - (2 * p.k - p.coarse_bits - p.fine_bits) : 16;
 
   // Persistent workgroups: workgroup w counts buckets w, w + G, w + 2G, ... (G = grid size). The first
   // round of the next bucket is loaded while the current one is finalized, so no bucket starts with an
@@ -1277,9 +1334,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // Compact records: a lane takes 4 consecutive records of the round with one 16-byte load (bucket bases are
   // multiples of 4 records: capped fine buckets are multiples of 16, the exact scan rounds them up), so one
   // address per 4 records; lanes past the end re-read the last aligned quad (inside the bucket's region).
-  static_assert(!CMP || R == 4, "compact rounds take one 16-byte load of 4 records per lane");
+  static_assert(!RK::C32 || R == 4, "compact rounds take one 16-byte load of 4 records per lane");
   auto prefetch = [&](const PlaneSet &src, uint32_t cnt, uint32_t first) {
-    if constexpr (CMP) {
+    if constexpr (RK::C32) {
       const uint32_t q = first + 4u * (uint32_t)tid, qmax = (cnt - 1) & ~3u;
       const u32x4 v = gload4((const uint32_t *)src.w[0] + (q < qmax ? q : qmax));
       nk[0][0] = v.x;
@@ -1294,7 +1351,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     for (int j = 0; j < R; j++) {
       const uint32_t i = first + (uint32_t)tid + (uint32_t)j * C_THREADS;
       const uint32_t idx = i < cnt ? i : cnt - 1;
-      if (CMP) {
+      if (RK::C32) {
         nk[j][0] = ((const uint32_t *)src.w[0])[idx];
       } else {
 #pragma unroll
@@ -1307,7 +1364,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     const uint64_t base = p.bucket_base[bb];
     cnt = (uint32_t)(p.bucket_end[bb] - base);  // < 2^32 records per bucket (host check)
     src = p.recs;
-    if (CMP) {
+    if (RK::C32) {
       src.w[0] = (uint64_t *)((uint32_t *)src.w[0] + base);
     } else {
 #pragma unroll
@@ -1377,12 +1434,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         uint32_t ce[R];
 #pragma unroll
         for (int j = 0; j < R; j++) {
-          const bool valid = (CMP ? r0 + 4u * (uint32_t)tid + (uint32_t)j : r0 + (uint32_t)tid + (uint32_t)j * C_THREADS) < n;
+          const bool valid = (RK::C32 ? r0 + 4u * (uint32_t)tid + (uint32_t)j : r0 + (uint32_t)tid + (uint32_t)j * C_THREADS) < n;
 #pragma unroll
           for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
           if (PACKED) {
-            ce[j] = valid ? (uint32_t)(ck[j][NL - 1] & low_mask) : NONE;
-            ck[j][NL - 1] &= ~low_mask;
+            ce[j] = valid ? (uint32_t)(ck[j][RK::XW] & low_mask) : NONE;
+            ck[j][RK::XW] &= ~low_mask;
           } else {
             ce[j] = valid ? nx[j] : NONE;
           }
@@ -1416,7 +1473,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           K v[C_BATCH][4];
 #pragma unroll
           for (int j = j0; j < j0 + C_BATCH; j++) {
-            g[j] = CMP ? cmp_group((uint32_t)ck[j][0], kshl, (uint32_t)ng)
+            g[j] = CMP ? cmp_group((uint32_t)ck[j][NL - 1], kshl, (uint32_t)ng)
                        : (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
             read_group(last, g[j], v[j - j0]);  // also for an invalid lane: harmless, keeps the batch uniform
           }
@@ -1488,7 +1545,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
           for (int w = 0; w < NL; w++) key[w] = mkey[w * MCL + q];
           const uint32_t e = me[q];
-          const int g = CMP ? cmp_group((uint32_t)key[0], kshl, (uint32_t)ng)
+          const int g = CMP ? cmp_group((uint32_t)key[NL - 1], kshl, (uint32_t)ng)
                             : (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
           K v[4];
           read_group(last, g, v);
@@ -1588,10 +1645,17 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         const int slot = fslot[j];
         const unsigned long long g = s_gbase + spos[j];
         uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
-        if (CMP) {  // key = cunmix(global fine bucket digits | stored bits)
+        if (RK::C32) {  // key = cunmix(global fine bucket digits | stored bits)
           const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
           const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
           ok[0] = cunmix(y, B) << (64 - B);
+        } else if (RK::M2) {  // key = m2_unmix(global fine bucket digits | stored L' bits, R')
+          const int rb = p.k - p.coarse_bits - p.fine_bits;
+          const uint64_t L = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          uint64_t kw[2];
+          m2_unmix(L, t.keys[t.cap + slot], p.k, kw);
+          ok[0] = kw[0];
+          ok[1] = kw[1];
         } else {
 #pragma unroll
           for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
@@ -1648,10 +1712,17 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       if ((surv_mask >> j) & 1u) {
         const int slot = tid + j * C_THREADS;
         uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
-        if (CMP) {  // key = cunmix(global fine bucket digits | stored bits)
+        if (RK::C32) {  // key = cunmix(global fine bucket digits | stored bits)
           const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
           const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
           ok[0] = cunmix(y, B) << (64 - B);
+        } else if (RK::M2) {  // key = m2_unmix(global fine bucket digits | stored L' bits, R')
+          const int rb = p.k - p.coarse_bits - p.fine_bits;
+          const uint64_t L = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          uint64_t kw[2];
+          m2_unmix(L, t.keys[t.cap + slot], p.k, kw);
+          ok[0] = kw[0];
+          ok[1] = kw[1];
         } else {
 #pragma unroll
           for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
@@ -1752,7 +1823,7 @@ static hipError_t do_extract_hist(const ExtractParams &p, hipStream_t s) {
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
   constexpr int T = kTile<NL>();
-  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_lds_bytes<NL>(), staged_area_bytes(NL, T, PK, CMP ? SF_C40 : SF_WORDS))
+  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_lds_bytes<NL>(), staged_area_bytes(NL, T, PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
                               : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
@@ -1772,7 +1843,7 @@ static hipError_t do_part_hist(const PartitionParams &p, hipStream_t s) {
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
   const uint32_t nf = 1u << p.fine_bits;
-  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kTile<NL>(), PK, CMP ? SF_C32 : SF_WORDS)
+  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kTile<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS)
                               : scatter_lds_bytes(nf);
   hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
@@ -1782,7 +1853,7 @@ static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
 
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_count(const CountParams &p, hipStream_t s) {
-  const size_t lds = count_lds_bytes(NL, CMP);
+  const size_t lds = count_lds_bytes(NL, RecKind<NL, CMP>::C32);
   hipError_t e = allow_lds(k_count<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
   const uint32_t grid = p.grid && p.grid < p.n_buckets ? p.grid : p.n_buckets;
@@ -1815,25 +1886,25 @@ hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigne
 
 hipError_t launch_extract_hist(const ExtractParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_tiles) return hipSuccess;
-  if (p.compact) return do_extract_hist<1, true, true>(p, s);
+  if (p.compact) return nl == 2 ? do_extract_hist<2, true, true>(p, s) : do_extract_hist<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_extract_hist, (p, s));
 }
 
 hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_tiles) return hipSuccess;
-  if (p.compact) return do_extract_scatter<1, true, true>(p, s);
+  if (p.compact) return nl == 2 ? do_extract_scatter<2, true, true>(p, s) : do_extract_scatter<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_extract_scatter, (p, s));
 }
 
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_chunks) return hipSuccess;
-  if (p.compact) return do_part_hist<1, true, true>(p, s);
+  if (p.compact) return nl == 2 ? do_part_hist<2, true, true>(p, s) : do_part_hist<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_part_hist, (p, s));
 }
 
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_chunks) return hipSuccess;
-  if (p.compact) return do_part_scatter<1, true, true>(p, s);
+  if (p.compact) return nl == 2 ? do_part_scatter<2, true, true>(p, s) : do_part_scatter<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_part_scatter, (p, s));
 }
 
@@ -1852,7 +1923,7 @@ static hipError_t do_sketch(const PartitionParams &p, uint32_t n, unsigned int *
 hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
                          hipStream_t s) {
   if (!n_chunks) return hipSuccess;
-  if (p.compact) return do_sketch<1, true, true>(p, n_chunks, hll, s);
+  if (p.compact) return nl == 2 ? do_sketch<2, true, true>(p, n_chunks, hll, s) : do_sketch<1, true, true>(p, n_chunks, hll, s);
   MHM_DISPATCH(nl, packed, do_sketch, (p, n_chunks, hll, s));
 }
 
@@ -1864,7 +1935,7 @@ hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, u
 
 hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_buckets) return hipSuccess;
-  if (p.compact) return do_count<1, true, true>(p, s);
+  if (p.compact) return nl == 2 ? do_count<2, true, true>(p, s) : do_count<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_count, (p, s));
 }
 

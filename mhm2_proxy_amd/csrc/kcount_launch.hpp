@@ -35,7 +35,8 @@ struct ExtractParams {
   int coarse_bits;                  // coarse digit = h1 >> (64 - coarse_bits)
   uint32_t n_bins;                  // 1 << coarse_bits
   int hbits;                        // hash bits stored in the record after the ext code (0: none)
-  int compact;                      // compact records (kmer_ops.hpp cmix): out = u32 plane w[0] + byte plane ext
+  int compact;                      // mixed records: compact (NL = 1, kmer_ops.hpp cmix): out = u32 plane w[0] +
+                                    // byte plane ext; NL = 2: m2_mix records, two u64 planes
   unsigned long long *hist;         // [n_bins] (E-hist)
   unsigned long long *cursor;       // [E_NSUB * n_bins] (E-scatter): cursor of segment (b, s) at s * n_bins + b
   uint64_t bin_cap;                 // capped mode: segment (b, s) owns [i*bin_cap, (i+1)*bin_cap), i = b*E_NSUB+s,
@@ -75,7 +76,8 @@ struct PartitionParams {
   int coarse_bits;
   int fine_bits;
   int hbits;                        // hash bits stored in the records (fine digit read from them if >= fine_bits)
-  int compact;                      // compact records: sources u32 + byte planes, out one u32 plane
+  int compact;                      // mixed records (see ExtractParams): compact sources u32 + byte planes, out
+                                    // one u32 plane; NL = 2: two u64 planes in and out
   unsigned long long *fine_hist;    // [n_coarse_local << fine_bits]
   unsigned long long *fine_cursor;  // [n_coarse_local << fine_bits]
   const unsigned long long *coarse_base;  // capped mode: first fine bucket of coarse bucket c starts here
@@ -89,7 +91,8 @@ struct CountParams {
   const unsigned long long *bucket_base;
   const unsigned long long *bucket_end;  // == the fine cursors after the scatter
   int hbits;                           // stored hash bits to strip from the last key word
-  int compact;                         // compact records (u32 plane w[0]); the key is rebuilt from the bucket
+  int compact;                         // mixed records (compact u32 plane w[0], or NL = 2 m2_mix words); the key
+                                       // is rebuilt from the bucket digits
   int coarse_bits, fine_bits;
   uint32_t bucket0;                    // global index of local fine bucket 0 (own_lo << fine_bits)
   uint32_t n_buckets;
@@ -136,7 +139,7 @@ size_t ctg_scratch_bytes(uint64_t n_windows, int nl);
 // order (insert_supermer_from_ctg) and sort the folded k-mers by local fine bucket. Outputs (n_out of them)
 // go to out_keys[NL] (SoA, each out_cap long), out_state, out_bucket.
 // Only k-mers whose coarse bucket is in [own_lo, own_hi) (this rank's hash range) are kept.
-hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool compact, int qual_cutoff, int dmin_thres,
+hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool mixed, int qual_cutoff, int dmin_thres,
                        double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi, void *scratch,
                        size_t scratch_bytes,
                        uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,

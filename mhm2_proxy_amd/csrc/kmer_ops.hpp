@@ -179,6 +179,42 @@ MHM_HD uint64_t cpart_hash(uint64_t w, int B) { return cmix(w >> (64 - B), B) <<
 
 MHM_HD bool compact_ok(int k, int nl) { return nl == 1 && k >= CMP_MIN_K && k <= CMP_MAX_K; }
 
+// ------------------------------------------------------------------------------------------------
+// Mixed two-word records (33 <= k <= 63, NL = 2). The 2k key bits are split into halves of
+// k bits, L (bases 0 .. k/2-ish, the top k bits) and R (the low k bits), and put through a 3-round Feistel
+// network, (L', R') = m2_mix(key). The coarse and fine digits are the top bits of L', so a record keeps
+//   w[0] = (L' below the digits) << 6 | ext code,   w[1] = R'
+// (16 B, no byte plane, no stored hash bits), and k_count rebuilds the key as m2_unmix(digits | w[0] >> 6, w[1]).
+// The round function is one 64-bit multiply folded onto itself (every output bit depends on every input
+// bit); MurmurHash3 of two words takes eight such multiplies, in extraction and again in the fine partition.
+constexpr uint64_t M2_K[3] = {0x9E3779B97F4A7C15ull, 0xC2B2AE3D27D4EB4Full, 0xD6E8FEB86659FD93ull};
+constexpr int M2_MIN_K = 33, M2_MAX_K = 63;
+MHM_HD uint64_t m2_f(uint64_t v, uint64_t c) {
+  const uint64_t p = (v ^ (v >> 31)) * c;
+  return p ^ (p >> 32);
+}
+MHM_HD bool mixed2_ok(int k, int nl) { return nl == 2 && k >= M2_MIN_K && k <= M2_MAX_K; }
+
+// key words (Kmer::longs layout, k bases) -> (L', R'), k bits each
+MHM_HD void m2_mix(const uint64_t *w, int k, uint64_t &L, uint64_t &R) {
+  const uint64_t m = (1ull << k) - 1;
+  L = w[0] >> (64 - k);
+  R = ((w[0] << (2 * k - 64)) | (w[1] >> (128 - 2 * k))) & m;  // x = L << k | R: x's low 64 bits, masked
+  L ^= m2_f(R, M2_K[0]) & m;
+  R ^= m2_f(L, M2_K[1]) & m;
+  L ^= m2_f(R, M2_K[2]) & m;
+}
+
+// (L', R') -> key words (the last word's unused low bits zero)
+MHM_HD void m2_unmix(uint64_t L, uint64_t R, int k, uint64_t *w) {
+  const uint64_t m = (1ull << k) - 1;
+  L ^= m2_f(R, M2_K[2]) & m;
+  R ^= m2_f(L, M2_K[1]) & m;
+  L ^= m2_f(R, M2_K[0]) & m;
+  w[0] = (L << (64 - k)) | (R >> (2 * k - 64));
+  w[1] = R << (128 - 2 * k);
+}
+
 // Reverse the order of the 32 two-bit groups of x.
 MHM_HD uint64_t rev2(uint64_t x) {
   x = __builtin_bswap64(x);
@@ -211,6 +247,7 @@ MHM_HD void revcomp(const uint64_t *w, uint64_t *rc, int k) {
 // Word-wise unsigned lexicographic compare == Kmer::operator< (src/kmer.cpp:265-272).
 template <int NL>
 MHM_HD bool kmer_less(const uint64_t *a, const uint64_t *b) {
+  if (NL == 2) return (a[0] < b[0]) | ((a[0] == b[0]) & (a[1] < b[1]));  // branch-free (walk_windows)
 #pragma unroll
   for (int i = 0; i < NL; i++) {
     if (a[i] != b[i]) return a[i] < b[i];

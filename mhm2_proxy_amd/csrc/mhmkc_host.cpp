@@ -139,6 +139,8 @@ struct mhmkc {
   int dmin = 2;  // the finish's depth threshold (mhmkc_set_dmin_thres)
   bool packed = true;
   bool compact = false;  // compact records (kmer_ops.hpp cmix): 5 B per coarse record, 4 B per fine record
+  bool mixed2 = false;   // mixed two-word records (kmer_ops.hpp m2_mix, 33 <= k <= 63): 16 B, no byte plane
+  bool mixed() const { return compact || mixed2; }  // the kernels' "compact" flag: bucket digits implicit
   int cb = 8, fb = 8, hbits = 0;
   uint32_t nb = 256, nf = 256;
   uint32_t own_lo = 0, own_hi = 256;  // owned coarse range [own_lo, own_hi)
@@ -332,7 +334,7 @@ int mhmkc::extract(Slab *sl, bool exact) {
   p.coarse_bits = cb;
   p.n_bins = nb;
   p.hbits = hbits;
-  p.compact = compact;
+  p.compact = mixed();
   p.hist = d_hist.as<unsigned long long>();
   unsigned long long *dcur = sl->meta.as<unsigned long long>();
   p.cursor = dcur;
@@ -783,7 +785,7 @@ int mhmkc::prepare_ctgs() {
   prof_begin(MHMKC_STAGE_OTHER);
   // the synchronous copies above keep the host vectors alive long enough: ctg_prepare waits for its
   // fold count before returning
-  e = mhm::ctg_prepare(cv, k, nl, compact, 1, dmin, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, own_hi,
+  e = mhm::ctg_prepare(cv, k, nl, mixed(), 1, dmin, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, own_hi,
                        d_ctg_scratch.p, sb, keys, d_ctg_state.as<uint32_t>(), d_ctg_bucket.as<uint32_t>(), &ctg_n,
                        d_err.as<unsigned int>(), stream);
   prof_end();
@@ -988,7 +990,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     sp.k = k;
     sp.coarse_bits = cb;
     sp.hbits = hbits;
-    sp.compact = compact;
+    sp.compact = mixed();
     std::vector<uint32_t> reg(mhm::SKETCH_M + 1);
     prof_begin(MHMKC_STAGE_OTHER);
     if ((e = grow(d_hll, 4 * mhm::SKETCH_M + 64)) != hipSuccess ||
@@ -1050,7 +1052,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   pp.coarse_bits = cb;
   pp.fine_bits = fb;
   pp.hbits = hbits;
-  pp.compact = compact;
+  pp.compact = mixed();
   pp.fine_hist = d_fine_hist.as<unsigned long long>();
   pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
   pp.err = d_err.as<unsigned int>();
@@ -1059,7 +1061,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.bucket_base = d_fine_base.as<unsigned long long>();
   cp.bucket_end = d_fine_cursor.as<unsigned long long>();
   cp.hbits = hbits;
-  cp.compact = compact;
+  cp.compact = mixed();
   cp.coarse_bits = cb;
   cp.fine_bits = fb;
   cp.bucket0 = own_lo << fb;
@@ -1280,6 +1282,12 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   const char *wide = getenv("MHMKC_WIDE_RECORDS");
   h->compact = mhm::compact_ok(k, nl) && 2 * k - h->cb <= 34 && !(wide && atoi(wide));
   if (h->compact) h->hbits = 0;
+  // mixed two-word records for 33 <= k <= 63 (the same switch keeps the plain key words)
+  h->mixed2 = mhm::mixed2_ok(k, nl) && !(wide && atoi(wide));
+  if (h->mixed2) {
+    h->packed = true;  // the ext code sits in w[0]
+    h->hbits = 0;
+  }
   h->nb = 1u << h->cb;
   h->own_lo = h->owner_lo(cfg->rank);
   h->own_hi = h->owner_lo(cfg->rank + 1);

@@ -11,6 +11,6 @@ cd /tmp
 for spec in "$@"; do
   n=${spec%%=*}; lib=${spec#*=}
   if [ -n "$lib" ]; then export MHMKC_LIB=$GRAFT_REPO_ROOT/$lib; else unset MHMKC_LIB; fi
-  timeout -s KILL 240 rocprofv3 --pmc $CNT --kernel-trace -d $OUT/$n -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-profile-events --h2d-steps 0 > $OUT.$n.log 2>&1 || { echo "pass $n failed"; tail -5 $OUT.$n.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc $CNT --kernel-trace -d $OUT/$n -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-profile-events --h2d-steps 0 ${BENCH_ARGS:-} > $OUT.$n.log 2>&1 || { echo "pass $n failed"; tail -5 $OUT.$n.log; exit 1; }
   echo "$n done"
 done
