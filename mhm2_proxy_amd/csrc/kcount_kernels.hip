@@ -911,6 +911,15 @@ struct CountLds {
 #define MHMKC_BOVERLAP 1
 #endif
 constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
+// Two-word keys take the whole miss space for one list (960 entries for 2048 records a round): with half of it
+// the first rounds of a bucket overflow the list into in-place inserts in phase A, and the waves that do them
+// hold the round barrier (k = 63: k_count 13.2 -> 12.6 ms)
+#ifndef MHMKC_BOV2
+#define MHMKC_BOV2 0
+#endif
+#ifndef MHMKC_BSPREAD
+#define MHMKC_BSPREAD 0
+#endif
 
 // Two-pass finalize (list the slots with count >= 2, then decide them densely); 0 = one pass over all slots.
 #ifndef MHMKC_FIN2
@@ -1302,7 +1311,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
   constexpr int MC = miss_cap(NL, RK::C32);
   // B_OVERLAP: phase B of round r overlaps phase A of round r + 1, so the miss list is double-buffered
-  constexpr int MCL = B_OVERLAP ? (MC / 2) & ~63 : MC;
+  constexpr bool BOV = B_OVERLAP && !(NL == 2 && MHMKC_BOV2 == 0);
+  constexpr int MCL = BOV ? (MC / 2) & ~63 : MC;
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
@@ -1462,8 +1472,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         }
 #endif
         unsigned int *nmiss = &s_nmiss[lr];
-        K *mkey = s_mkey + (B_OVERLAP ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
-        uint32_t *me = s_me + (B_OVERLAP ? (rnd & 1) * MCL : 0);
+        K *mkey = s_mkey + (BOV ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
+        uint32_t *me = s_me + (BOV ? (rnd & 1) * MCL : 0);
         // A. home-group lookups: the first groups of all R records are read in batches of C_BATCH (the
         //    reads of a batch in flight together), then found records are counted, missed ones listed.
         uint32_t old[R], defer = 0, okm = 0;
@@ -1517,7 +1527,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         STAMP(t_r2);
         STAMP_ADD(2, t_r2 - t_r1);
         // the next round's counter: its last readers (phase B two rounds back) are behind the previous barrier
-        if (B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
+        if (BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
         __syncthreads();
         STAMP(t_r3);
         STAMP_ADD(3, t_r3 - t_r2);
@@ -1539,8 +1549,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         const unsigned int M = min(*nmiss, (unsigned int)MCL);
 #endif
         if (tid == 0) s_missacc += M;
-        if (!B_OVERLAP && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
-        for (unsigned int q = tid; q < M; q += C_THREADS) {
+        if (!BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
+        // (MHMKC_BSPREAD: list entry q to lane q / 16 of wave q % 16, so every wave takes a share)
+        const unsigned int q0 = MHMKC_BSPREAD ? (unsigned int)(lane * (C_THREADS / 64) + wid) : (unsigned int)tid;
+        for (unsigned int q = q0; q < M; q += C_THREADS) {
           uint64_t key[NL];
 #pragma unroll
           for (int w = 0; w < NL; w++) key[w] = mkey[w * MCL + q];
@@ -1566,7 +1578,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         // other waves still work off this list: its misses go to the other list buffer and counter, and a
         // lookup that races an insert of phase B at worst misses and is resolved by its own phase B (slots
         // are only ever claimed, so the deferral rule of lds_insert holds across the two phases).
-        if (!B_OVERLAP) __syncthreads();
+        if (!BOV) __syncthreads();
 #if MHMKC_STAMP
         const uint64_t t_r4 = __builtin_amdgcn_s_memtime();
         STAMP_ADD(4, t_r4 - t_r3);

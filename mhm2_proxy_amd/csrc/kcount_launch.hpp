@@ -163,7 +163,14 @@ constexpr int E_NSUB = 8;
 #define MHMKC_CPAD 1
 #endif
 constexpr uint32_t CPAD = MHMKC_CPAD;  // cursor spacing in u64 words (segment i's cursor at i * CPAD)  // segments per coarse bucket: one per group of blocks sharing an XCD
-constexpr int C_THREADS = 1024;
+// k_count workgroups per CU (persistent): 1 = one 1024-thread workgroup with all 160 KB of LDS; 2 = two of
+// 512 threads with half the LDS each (one can count while the other waits at a barrier)
+#ifndef MHMKC_CSPLIT
+#define MHMKC_CSPLIT 1
+#endif
+constexpr int C_SPLIT = MHMKC_CSPLIT;
+constexpr int C_THREADS = 1024 / C_SPLIT;
+constexpr size_t C_LDS = 163840 / C_SPLIT;
 
 // Hash bits stored in a packed record next to the ext code (bits [6, 6 + hbits) of the last word).
 inline int stored_hash_bits(int k, int nl, bool packed) {
@@ -181,21 +188,24 @@ inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : 2048; }
 // 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
 // k_count LDS: table (keys, count, 4 extension words per slot) + 128 B of scalars + the miss list of a
 // round's phase B (key words + ext code per entry); together <= 160 KiB.
+#ifndef MHMKC_CAP2
+#define MHMKC_CAP2 4000
+#endif
 __host__ __device__ constexpr int count_key_bytes(bool cmp) { return cmp ? 4 : 8; }
 __host__ __device__ constexpr int count_cap(int nl, bool cmp = false) {
-  return cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? 4000 : nl == 3 ? 3264 : 2752;
+  return ((cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? MHMKC_CAP2 : nl == 3 ? 3264 : 2752) / C_SPLIT) & ~3;
 }
 __host__ __device__ constexpr size_t count_table_bytes(int nl, bool cmp = false) {
   return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 128;
 }
 __host__ __device__ constexpr int miss_cap(int nl, bool cmp = false) {
-  return (int)(((163840 - count_table_bytes(nl, cmp)) / (count_key_bytes(cmp) * nl + 4)) & ~(size_t)63);
+  return (int)(((C_LDS - count_table_bytes(nl, cmp)) / (count_key_bytes(cmp) * nl + 4)) & ~(size_t)63);
 }
 __host__ __device__ constexpr size_t count_lds_bytes(int nl, bool cmp = false) {
   return count_table_bytes(nl, cmp) + (size_t)miss_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4);
 }
-static_assert(count_lds_bytes(1) <= 163840 && count_lds_bytes(2) <= 163840 && count_lds_bytes(3) <= 163840 &&
-                  count_lds_bytes(4) <= 163840 && count_lds_bytes(1, true) <= 163840,
+static_assert(count_lds_bytes(1) <= C_LDS && count_lds_bytes(2) <= C_LDS && count_lds_bytes(3) <= C_LDS &&
+                  count_lds_bytes(4) <= C_LDS && count_lds_bytes(1, true) <= C_LDS,
               "k_count LDS budget");
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);

@@ -1066,7 +1066,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.fine_bits = fb;
   cp.bucket0 = own_lo << fb;
   cp.n_buckets = n_fine;
-  cp.grid = (uint32_t)std::max(0, n_cu);  // one persistent workgroup per CU (k_count needs ~160 KB of LDS)
+  cp.grid = (uint32_t)std::max(0, n_cu * mhm::C_SPLIT);  // persistent workgroups filling every CU's LDS
   cp.k = k;
   cp.cap = mhm::count_cap(nl, compact);
   if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
