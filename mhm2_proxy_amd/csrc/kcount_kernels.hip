@@ -545,6 +545,153 @@ constexpr bool kEStaged = MHMKC_ESTAGE != 0;
 constexpr bool kPStaged = MHMKC_PSTAGE != 0;
 
 // ------------------------------------------------------------------------------------------------
+// Mixed two-word extraction over the valid windows only (MHMKC_M2WALK). At k = 63 only 86 of a 150 bp read's
+// positions start a counted window, and the rolling walk above spends the same work on every position. Here
+// the valid windows of the tile (each read's interior windows [s + 1, e - k - 1], kcount_cpu.cpp:316-334) are
+// listed first, and window v of the list goes to thread v % 256, register slot v / 256: each window's
+// forward and reverse-complement words are funnel-loaded from the staged codes and from a reverse-complemented
+// copy of them, so no window depends on its predecessor, and waves whose slots are past the list skip them.
+// Measured at k = 63 on C2 reads: 10.2 ms against 9.6 ms for the rolling walk (the window's LDS reads are a
+// dependent chain the four waves per SIMD do not hide, where rolling keeps everything in registers), so it is
+// off by default; kept for A/B (MHMKC_M2WALK=1) and covered by the parity tests when enabled.
+#ifndef MHMKC_M2WALK
+#define MHMKC_M2WALK 0
+#endif
+constexpr bool kM2Walk = MHMKC_M2WALK != 0;
+#ifndef MHMKC_M2BATCH
+#define MHMKC_M2BATCH 2  // valid-window slots per branch-free block
+#endif
+
+// LDS after the staged tile: rc codes [NG] u64 | valid bits [T/32] u32 | their prefix [T/32 + 1] u32 | list [T] u16
+__host__ __device__ constexpr size_t m2walk_lds_bytes() {
+  return align16((size_t)kGroups<2>() * 8) + align16((size_t)(2 * (kTile<2>() / 32) + 1) * 4) + (size_t)kTile<2>() * 2;
+}
+
+// The 32 codes from position q of a staged code array, first in the top bits (branch-free funnel: q & 31 = 0
+// shifts the next word out entirely).
+__device__ __forceinline__ uint64_t funnel_codes(const uint64_t *a, int q) {
+  const int g = q >> 5, sh = (q & 31) * 2;
+  return (a[g] << sh) | ((a[g + 1] >> 1) >> (63 - sh));
+}
+
+template <int W>
+__device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t tile, const uint64_t *fwd,
+                                              const uint32_t *good, const uint32_t *start, unsigned char *scratch, uint64_t (&rk)[W][2],
+                                              uint32_t (&inf)[W]
+#ifdef MHMKC_ESTAMP
+                                              , uint64_t &es_list
+#endif
+) {
+  constexpr int T = kTile<2>(), NG = kGroups<2>(), NW = T / 32, P = NG * 32;
+  static_assert(NW == 64 && W * E_THREADS == T && (T / E_THREADS) <= 32 && 32 % (T / E_THREADS) == 0,
+                "one wave scans the valid bits; every position has a slot; a thread's positions in one word");
+  uint64_t *rcw = (uint64_t *)scratch;
+  uint32_t *vb = (uint32_t *)(scratch + align16((size_t)NG * 8));
+  uint32_t *vpre = vb + NW;
+  uint16_t *pos = (uint16_t *)(scratch + align16((size_t)NG * 8) + align16((size_t)(2 * NW + 1) * 4));
+  const int tid = threadIdx.x, k = p.k;
+  for (int g = tid; g < NG; g += E_THREADS) rcw[g] = rev2(~fwd[NG - 1 - g]);  // complement, reversed
+  if (tid < NW) {
+    // Valid-window bits of own positions 32w .. 32w + 31 (staged 32(w+1) + i), MSB first like the staged bit
+    // arrays: window i is valid iff no read start lies at staged positions [q, q + k] (the read-start bits of
+    // load_tile, which include the data end as a start) and it ends before the data does. The start bits
+    // from q on, as a 128-bit string X (position j at bit 127 - j of hi:lo), are dilated towards earlier
+    // positions: Y = OR of X << t for t = 0..k, by doubling to 32 terms, then Y32 | Y32 << (k + 1 - 32).
+    const int w = tid;
+    uint64_t hi = ((uint64_t)start[w + 1] << 32) | start[w + 2], lo = ((uint64_t)start[w + 3] << 32) | start[w + 4];
+#pragma unroll
+    for (int sft = 1; sft < 32; sft <<= 1) {
+      hi |= (hi << sft) | (lo >> (64 - sft));
+      lo |= lo << sft;
+    }
+    const int r = k + 1 - 32;  // in [2, 32]
+    hi |= (hi << r) | (lo >> (64 - r));
+    uint32_t valid = ~(uint32_t)(hi >> 32);
+    const int64_t lim = (int64_t)p.reads.n_bases - k - (int64_t)tile * T - 32 * w;  // window o needs o + k < n
+    valid &= lim >= 32 ? ~0u : lim <= 0 ? 0u : ~(~0u >> (int)lim);
+    vb[w] = valid;
+    const uint32_t c = __popc(valid);
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (tid >= d) x += y;
+    }
+    vpre[w] = x - c;
+    if (w == NW - 1) vpre[NW] = x;
+  }
+  __syncthreads();
+  {  // the list: every thread places its 8 positions (one word)
+    const int o0 = tid * (T / E_THREADS), w = o0 >> 5;
+    const uint32_t m = vb[w], base = vpre[w];
+#pragma unroll
+    for (int j = 0; j < T / E_THREADS; j++) {
+      const int i = (o0 + j) & 31;
+      if ((m >> (31 - i)) & 1u) pos[base + __popc(m & ~(~0u >> i))] = (uint16_t)(o0 + j);
+    }
+  }
+  __syncthreads();
+  const uint32_t nv = vpre[NW];
+#ifdef MHMKC_ESTAMP
+  es_list = __builtin_amdgcn_s_memtime();
+#endif
+  const uint64_t m1 = top_mask(k - 32);
+  const int m2_csh = k - p.coarse_bits;
+  const uint64_t m2_cmask = (1ull << m2_csh) - 1;
+  // every list position of the thread up front (v < T always; entries past nv are masked to the tile)
+  int q[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) q[i] = 32 + (int)(pos[tid + i * E_THREADS] & (T - 1));
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    rk[i][0] = 0;
+    rk[i][1] = 0;
+    inf[i] = 0;
+  }
+  // slots in pairs, each pair one branch-free block (the two windows' LDS reads in flight together); a wave
+  // whose pair starts past the list is done
+  constexpr int PB = MHMKC_M2BATCH;
+  static_assert(W % PB == 0, "slot batches");
+#pragma unroll
+  for (int i0 = 0; i0 < W; i0 += PB) {
+    if ((uint32_t)(tid & ~63) + (uint32_t)(i0 * E_THREADS) >= nv) break;
+#pragma unroll
+    for (int i = i0; i < i0 + PB; i++) {
+      const uint32_t v = (uint32_t)tid + (uint32_t)(i * E_THREADS);
+      const int qq = q[i];
+      uint64_t fw[2], rc[2];
+      fw[0] = funnel_codes(fwd, qq);
+      fw[1] = funnel_codes(fwd, qq + 32) & m1;
+      const int q0 = P - qq - k;  // the reverse complement starts here in rcw
+      rc[0] = funnel_codes(rcw, q0);
+      rc[1] = funnel_codes(rcw, q0 + 32) & m1;
+      const int ql = qq - 1, qr = qq + k;  // neighbours
+      const uint32_t cl = (uint32_t)(fwd[ql >> 5] >> (62 - 2 * (ql & 31))) & 3u;
+      const uint32_t cr = (uint32_t)(fwd[qr >> 5] >> (62 - 2 * (qr & 31))) & 3u;
+      const uint32_t gl = (good[ql >> 5] >> (31 - (ql & 31))) & 1u, gr = (good[qr >> 5] >> (31 - (qr & 31))) & 1u;
+      int l = gl ? (int)cl : EXT_NONE, r = gr ? (int)cr : EXT_NONE;
+      const bool use_rc = kmer_less<2>(rc, fw);
+      uint64_t key[2];
+      key[0] = use_rc ? rc[0] : fw[0];
+      key[1] = use_rc ? rc[1] : fw[1];
+      const int lr = (r == EXT_NONE) ? EXT_NONE : 3 - r, rr = (l == EXT_NONE) ? EXT_NONE : 3 - l;
+      if (use_rc) {
+        l = lr;
+        r = rr;
+      }
+      const uint32_t e = (uint32_t)((l << 3) | r);
+      uint64_t L, R;
+      m2_mix(key, k, L, R);
+      rk[i][0] = ((L & m2_cmask) << EXT_BITS) | e;
+      rk[i][1] = R;
+      inf[i] = v < nv ? (1u << 31) | (e << 16) | (uint32_t)(L >> m2_csh) : 0u;
+    }
+#pragma unroll
+    for (int i = i0; i < i0 + PB; i++) asm volatile("" : "+v"(rk[i][0]), "+v"(rk[i][1]), "+v"(inf[i]));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // extract: scatter into coarse buckets
 
 template <int NL, bool PACKED, bool CMP>
@@ -562,9 +709,16 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
     smem = carve_tile<NL>(smem0, fwd, good, start);
     area = nullptr;
   }
+#ifdef MHMKC_ESTAMP
+  const uint64_t es0 = __builtin_amdgcn_s_memtime();
+#endif
   scatter_clear((uint32_t *)smem, p.n_bins);
   const uint32_t tile = blockIdx.x;
   load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
+#ifdef MHMKC_ESTAMP
+  const uint64_t es1 = __builtin_amdgcn_s_memtime();
+  uint64_t es2 = es1;
+#endif
   const int sh = 64 - p.coarse_bits;
   // stored hash bits, branch-free (hbits == 0: none)
   const int hsh = p.hbits ? 64 - p.hbits : 0;
@@ -574,6 +728,13 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   const uint64_t m2_cmask = (1ull << m2_csh) - 1;
   uint64_t rk[W][NL];
   uint32_t inf[W];
+  if constexpr (RecKind<NL, CMP>::M2 && kM2Walk && kEStaged) {
+    m2_walk_valid<W>(p, tile, fwd, good, start, area + tile_lds_bytes<NL>(), rk, inf
+#ifdef MHMKC_ESTAMP
+                     , es2
+#endif
+    );
+  } else
   walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, p.k,
                    [&](int i, const uint64_t *key, uint32_t e, bool valid) {
                      if constexpr (RecKind<NL, CMP>::M2) {  // (L' below the coarse digit) << 6 | ext, R'
@@ -603,6 +764,9 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
                      for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[i][w]));
                      asm volatile("" : "+v"(inf[i]));
                    });
+#ifdef MHMKC_ESTAMP
+  const uint64_t es3 = __builtin_amdgcn_s_memtime();
+#endif
   const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
   constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS;
@@ -611,6 +775,16 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
                                       p.ovf);
   else
     scatter_regs<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
+#ifdef MHMKC_ESTAMP
+  const uint64_t es4 = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) {  // spread over 64 x 4 words (one address per phase would serialise)
+    unsigned long long *h = p.hist + 4 * ((blockIdx.x * 4 + (threadIdx.x >> 6)) & 63);
+    atomicAdd(&h[0], (unsigned long long)(es1 - es0));
+    atomicAdd(&h[1], (unsigned long long)(es2 - es1));
+    atomicAdd(&h[2], (unsigned long long)(es3 - es2));
+    atomicAdd(&h[3], (unsigned long long)(es4 - es3));
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1835,7 +2009,8 @@ static hipError_t do_extract_hist(const ExtractParams &p, hipStream_t s) {
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
   constexpr int T = kTile<NL>();
-  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_lds_bytes<NL>(), staged_area_bytes(NL, T, PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
+  const size_t tile_b = tile_lds_bytes<NL>() + (RecKind<NL, CMP>::M2 && kM2Walk ? m2walk_lds_bytes() : 0);
+  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_b, staged_area_bytes(NL, T, PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
                               : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;

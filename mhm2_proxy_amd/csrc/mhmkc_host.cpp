@@ -382,9 +382,23 @@ int mhmkc::extract(Slab *sl, bool exact) {
     return hip_fail(e, "cursor H2D");
   p.out = sl->planes;
   prof_begin(MHMKC_STAGE_ESCAT);
+#ifdef MHMKC_ESTAMP
+  (void)hipMemsetAsync(d_hist.p, 0, 2048, stream);
+#endif
   e = mhm::launch_extract_scatter(p, nl, packed, stream);
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "extract_scatter");
+#ifdef MHMKC_ESTAMP
+  {  // diagnostics build: extraction phase cycles summed over waves (k_extract_scatter stamps into hist[0..3])
+    unsigned long long hh[256], h[4] = {0, 0, 0, 0};
+    (void)hipMemcpyAsync(hh, d_hist.p, 2048, hipMemcpyDeviceToHost, stream);
+    (void)hipStreamSynchronize(stream);
+    for (int i = 0; i < 256; i++) h[i & 3] += hh[i];
+    const double t = (double)(h[0] + h[1] + h[2] + h[3]);
+    fprintf(stderr, "extract stamps: tile %.1f%% list %.1f%% walk %.1f%% scatter %.1f%%\n", 100 * h[0] / t,
+            100 * h[1] / t, 100 * h[2] / t, 100 * h[3] / t);
+  }
+#endif
   if ((e = hipMemcpyAsync(hc, dcur, (size_t)nseg * 8 + 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
     return hip_fail(e, "cursor D2H");
   sl->pending = true;

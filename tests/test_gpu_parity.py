@@ -301,10 +301,11 @@ def test_compact_overflow_at_min_fine_bits(k, monkeypatch):
     check_stats(st)
 
 
-@pytest.mark.parametrize("k", [21, 12])
+@pytest.mark.parametrize("k", [21, 12, 33, 47, 63])
 def test_compact_equals_wide_records(k, monkeypatch):
-    """The compact (4/5-byte, key rebuilt from the bucket) and 8-byte record layouts give the same table,
-    through the capped and the exact partition paths."""
+    """The mixed record layouts (compact 4/5-byte at k <= 21, two-word m2_mix at 33 <= k <= 63; the key rebuilt
+    from the bucket digits) and the plain key-word records give the same table, through the capped and the
+    exact partition paths."""
     b, o = synth_set(20000, 300000, 31)
     cmp_t, st_c = hip_table(b, o, k)
     monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
@@ -464,3 +465,36 @@ def test_c2_full_table_vs_cpu_restatement(k):
     del t
     assert (st["distinct"], st["purged"], st["n_out"]) == (rs["distinct"], rs["purged"], rs["n_out"])
     assert_tables_equal(got, ref, f"C2 k={k}: GPU vs CPU restatement")
+
+
+def long_ragged_set(k: int, seed: int = 61):
+    """Reads of every awkward length for the valid-window list of the two-word extraction: empty, < k + 2,
+    k + 2 (one window), k + 3, 150, and reads far longer than a 2048-base tile (a read spanning several
+    tiles, starting before the tile it is counted in), concatenated in a random order."""
+    rng = np.random.default_rng(seed)
+    g = m.synth_genome(400_000, seed)
+    lens = [0, 1, k, k + 1, k + 2, k + 3, 150, 151, 2047, 2048, 2049, 4000, 9000]
+    reads = []
+    for i in range(600):
+        L = lens[i % len(lens)] if i % 3 else int(rng.integers(0, 300))
+        a = int(rng.integers(0, g.size - L - 1))
+        q = np.where(rng.random(L) < 0.03, 5, 31).astype(np.uint8)
+        reads.append((g[a:a + L] & 7) | (q << 3))
+    rng.shuffle(reads)
+    offs = np.zeros(len(reads) + 1, dtype=np.uint64)
+    np.cumsum([r.size for r in reads], out=offs[1:])
+    return np.concatenate(reads).astype(np.uint8), offs
+
+
+@pytest.mark.parametrize("k", [33, 47, 63])
+def test_valid_window_walk_long_and_ragged_reads(k, monkeypatch):
+    """Two-word extraction over the listed valid windows == the oracle, for reads of length 0 .. 9000 (reads
+    crossing several extraction tiles), whole and as host chunks (slice views with a head offset)."""
+    b, o = long_ragged_set(k)
+    exp = oracle_table(b, o, k)
+    got, st = hip_table(b, o, k)
+    assert_tables_equal(got, exp, f"long/ragged reads, k={k}")
+    check_stats(st)
+    monkeypatch.setenv("MHMKC_CHUNK_BYTES", "5000")
+    got2, _ = hip_table(b, o, k)
+    assert_tables_equal(got2, exp, f"long/ragged reads in 5000-byte chunks, k={k}")
