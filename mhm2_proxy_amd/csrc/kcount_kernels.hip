@@ -1220,6 +1220,38 @@ __device__ int lds_insert(const CountLds<K> &t, const uint64_t *key, int g, int 
   return -2;
 }
 
+// Phase A claim of the home group's first empty slot for a key the group does not hold (MHMKC_CLAIMA): one CAS
+// instead of a trip through the miss list and phase B, for most new keys (a third of all records at k = 63).
+// Returns the slot, or the verdict unchanged when the CAS lost (the record then goes to the miss list).
+// Sound by lds_insert's argument: the home group had an empty slot, so the key is in no later group, and
+// of the lanes that saw this slot empty exactly one claims it; a single-word key that lost to its own key
+// is counted in the winner's slot, any other loser is resolved by phase B.
+#ifndef MHMKC_CLAIMA
+#define MHMKC_CLAIMA 1
+#endif
+constexpr bool kClaimA = MHMKC_CLAIMA != 0;
+template <int NL, typename K>
+__device__ __forceinline__ int claim_home(const CountLds<K> &t, const uint64_t *key, int g, int r) {
+  K *last = t.keys + (NL - 1) * t.cap;
+  const int sl = 4 * g + (-1 - r);
+  const K kl = (K)key[NL - 1];
+  if constexpr (NL == 1) {
+    K old;
+    if constexpr (sizeof(K) == 4)
+      old = atomicCAS((unsigned int *)&last[sl], 0xffffffffu, (unsigned int)kl);
+    else
+      old = atomicCAS((unsigned long long *)&last[sl], (unsigned long long)KEY_EMPTY, (unsigned long long)kl);
+    return (old == (K)KEY_EMPTY || old == kl) ? sl : r;
+  } else {
+    const K old = atomicCAS((unsigned long long *)&last[sl], (unsigned long long)KEY_EMPTY, (unsigned long long)KEY_BUSY);
+    if (old != (K)KEY_EMPTY) return r;
+#pragma unroll
+    for (int w = 0; w < NL - 1; w++) t.keys[w * t.cap + sl] = (K)key[w];
+    __hip_atomic_store(&last[sl], kl, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return sl;
+  }
+}
+
 // insert_supermer_from_read's per-k-mer update (src/kcount/kcount_cpu.cpp:343-352): count + 1,
 // left/right extension + 1 when they are A/C/G/T (ExtCounts::inc ignores the rest, :152-164).
 // Extension counters are 16-bit halves of u32 LDS words, added without a return value; the old count
@@ -1672,6 +1704,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             continue;
           }
           int r = slot[j];
+          if (kClaimA && r < 0 && r > G_FULL) slot[j] = r = claim_home<NL>(t, ck[j], g[j], r);  // -1 - i: slot i empty
           if (r < 0) {
             const unsigned int q = atomicAdd(nmiss, 1u);
             if (q < (unsigned int)MCL) {  // handed to phase B
