@@ -1230,6 +1230,12 @@ __device__ int lds_insert(const CountLds<K> &t, const uint64_t *key, int g, int 
 #define MHMKC_CLAIMA 1
 #endif
 constexpr bool kClaimA = MHMKC_CLAIMA != 0;
+// A full home group looks at the next group in phase A before listing the record: measured slower (k = 63
+// count 11.9 -> 12.5 ms, misses only 137M -> 130M: most misses are claim races, not full groups), so off.
+#ifndef MHMKC_PROBE2
+#define MHMKC_PROBE2 0
+#endif
+constexpr bool kProbe2 = MHMKC_PROBE2 != 0;
 template <int NL, typename K>
 __device__ __forceinline__ int claim_home(const CountLds<K> &t, const uint64_t *key, int g, int r) {
   K *last = t.keys + (NL - 1) * t.cap;
@@ -1704,7 +1710,32 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             continue;
           }
           int r = slot[j];
-          if (kClaimA && r < 0 && r > G_FULL) slot[j] = r = claim_home<NL>(t, ck[j], g[j], r);  // -1 - i: slot i empty
+          if (kClaimA && r < 0 && r > G_FULL) {  // -1 - i: slot i of the home group was empty
+            const int sl = 4 * g[j] + (-1 - r);
+            r = claim_home<NL>(t, ck[j], g[j], r);
+            if (NL > 1 && r < 0) {  // lost: the winner may have claimed it for this very key (a lane of this
+                                    // wave has published it by now; another wave's is left to phase B)
+              const K v = __hip_atomic_load(&last[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (v == (K)ck[j][NL - 1] && rest_equal<NL>(t, sl, ck[j])) r = sl;
+            }
+            slot[j] = r;
+          }
+          if (kProbe2 && r == G_FULL) {  // a full home group: look at the next one before listing the record
+            const int g2 = (g[j] + 1 == ng) ? 0 : g[j] + 1;
+            K v2[4];
+            read_group(last, g2, v2);
+            r = examine_group<NL>(t, ck[j], g2, v2);
+            if (kClaimA && r < 0 && r > G_FULL) {
+              const int sl = 4 * g2 + (-1 - r);
+              r = claim_home<NL>(t, ck[j], g2, r);
+              if (NL > 1 && r < 0) {
+                const K v = __hip_atomic_load(&last[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (v == (K)ck[j][NL - 1] && rest_equal<NL>(t, sl, ck[j])) r = sl;
+              }
+            }
+            if (r < 0) r = G_FULL;  // phase B probes again from the home group
+            slot[j] = r;
+          }
           if (r < 0) {
             const unsigned int q = atomicAdd(nmiss, 1u);
             if (q < (unsigned int)MCL) {  // handed to phase B
