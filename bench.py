@@ -62,6 +62,8 @@ def parse():
                     help="packed: PackedRead bytes in HBM (the headline); fastq: FASTQ text in HBM, parsed and "
                          "packed on the device inside every step (mhmkc_add_fastq_device)")
     ap.add_argument("--no-profile-events", action="store_true")
+    ap.add_argument("--kmermap-sample-rows", type=int, default=4_000_000,
+                    help="rows of the fetched table put into the C++ adapter's KmerMap to time it (0: skip)")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc passes (profiles/), if present")
     return ap.parse_args()
@@ -97,6 +99,41 @@ def lds_floor_seconds(st: dict, k: int) -> tuple:
                  nl / r["ds_read_b64"]))
     b = recs * (16 * g_reads + 4) + ext * 4 + miss * (16 * g_reads + 4 + 16 * nl)
     return t, b
+
+
+def kmermap_fill_ms(table, k: int, sample_rows: int):
+    """KmerMap materialisation on the host: the first sample_rows rows of the fetched table
+    go through the C++ adapter's fill loop (tools/bin/kmermap_fill, built by build(): KmerMap<MAX_K> is a
+    std::unordered_map, one thread, the emplace loop of KmerDHT::load_table / insert_into_local_hashtable),
+    timed in that process and extrapolated linearly to the whole table (a lower bound: a larger map misses
+    the caches more)."""
+    tool = ROOT / "tools" / "bin" / "kmermap_fill"
+    n = min(len(table), sample_rows)
+    if not sample_rows or not n or not tool.exists():
+        return None
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    d = tempfile.mkdtemp(prefix="mhmkc_fill_", dir="/dev/shm" if Path("/dev/shm").is_dir() else None)
+    try:
+        pre = str(Path(d) / "t")
+        np.ascontiguousarray(table.keys[:n]).tofile(pre + ".keys")
+        np.ascontiguousarray(table.counts[:n]).tofile(pre + ".counts")
+        np.ascontiguousarray(table.left[:n]).view(np.uint8).tofile(pre + ".left")
+        np.ascontiguousarray(table.right[:n]).view(np.uint8).tofile(pre + ".right")
+        r = subprocess.run([str(tool), str(k), str(n), pre], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return {"error": r.stderr.strip()[-200:]}
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        import shutil
+
+        shutil.rmtree(d, ignore_errors=True)
+    return {"sample_rows": n, "sample_ms": j["ms"], "rows": len(table),
+            "ms_extrapolated": round(j["ms"] * len(table) / n, 1),
+            "kind": "C++ adapter KmerMap<MAX_K> (std::unordered_map), 1 thread, tools/cpp/kmermap_fill.cpp"}
 
 
 def survey_model_bytes(st: dict, k: int, n_reads: int, read_len: int) -> float:
@@ -256,6 +293,8 @@ def main():
             pmc = json.loads(Path(args.pmc_json).read_text())
         except Exception:
             pmc = {}
+    # measured for this workload only (the config's own sizes)
+    pmc = {} if (args.reads_per_gpu or args.reads_total) else pmc.get("configs", {}).get(f"{args.config}/k{k}", {})
     if dom and launches.get(dom):
         ms_launch = stage_ms[dom] / launches[dom]
         alg = algorithmic_bytes(dom, st, k) / max(1, launches[dom] // steps)
@@ -286,6 +325,7 @@ def main():
     d2h_ms = (time.perf_counter() - t1) * 1e3
     d2h = {"ms": round(d2h_ms, 2), "rows": len(table), "bytes": int(len(table) * (8 * counter.n_longs + 4)),
            "GBps": round(len(table) * (8 * counter.n_longs + 4) / (d2h_ms * 1e-3) / 1e9, 2) if d2h_ms else None}
+    kmermap = kmermap_fill_ms(table, k, args.kmermap_sample_rows) if rank == 0 else None
     del table
 
     # the same step from reads in pinned host memory: chunked H2D on a copy stream, each chunk extracted as
@@ -349,6 +389,11 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "stages_ms_per_step": {s_: round(v, 3) for s_, v in per_step.items() if launches.get(s_)},
+            "achieved_measured_GBps_whole_step": round(
+                sum(pmc["per_launch_bytes"][s_] * launches[s_] / steps for s_ in launched) / (elapsed / steps) / 1e9, 1)
+            if pmc.get("per_launch_bytes") and all(s_ in pmc["per_launch_bytes"] for s_ in launched
+                                                   if s_ not in ("other", "tileidx")) else None,
+            "l2_hit": pmc.get("l2_hit"),
             "achieved_alg_GBps_whole_step": round(
                 sum(algorithmic_bytes(s_, st, k) * launches[s_] / steps for s_ in launched) / (elapsed / steps) / 1e9,
                 1) if st else None,
@@ -359,6 +404,8 @@ def main():
             } if st else None,
             "h2d_inclusive": h2d,
             "d2h_fetch": d2h,
+            "kmermap": kmermap,
+            "d2h_kmermap_ms": round(d2h["ms"] + kmermap["ms_extrapolated"], 1) if kmermap else None,
             "distinct_per_gpu": st["distinct"] if st else None,
             "n_out_per_gpu": st["n_out"] if st else None,
             "bytes_sent_rank0": st["bytes_sent"] if st else None,

@@ -3,6 +3,7 @@
   mhm2_proxy_amd/libmhmkc.so        hipcc --offload-arch=gfx950: HIP kernels + C ABI (include/mhmkc.h)
   mhm2_proxy_amd/libmhmkc_synth.so  gcc: deterministic synthetic read generator (include/mhmkc_synth.h)
   oracle/liboracle.so (+ _ref/)     make -C oracle: the CPU checker (test infrastructure only)
+  tools/bin/kmermap_fill            g++: KmerMap materialisation timing of the C++ adapter (bench.py)
 
 Incremental: a target is rebuilt only when one of its sources is newer.
 """
@@ -27,6 +28,8 @@ LIB_SOURCES = [CSRC / "kcount_kernels.hip", CSRC / "kcount_ctg.hip", CSRC / "kco
                CSRC / "mhmkc_host.cpp"]
 LIB_DEPS = LIB_SOURCES + [CSRC / "kcount_launch.hpp", CSRC / "kmer_ops.hpp", ROOT / "include" / "mhmkc.h"]
 SYNTH_DEPS = [CSRC / "synth.c", ROOT / "include" / "mhmkc_synth.h"]
+FILL = ROOT / "tools" / "bin" / "kmermap_fill"
+FILL_DEPS = [ROOT / "tools" / "cpp" / "kmermap_fill.cpp", ROOT / "include" / "mhmkc_kcount.hpp", ROOT / "include" / "mhmkc.h"]
 
 
 def _stale(target: Path, deps) -> bool:
@@ -73,10 +76,21 @@ def build_oracle(force: bool = False) -> Path:
     return ORACLE
 
 
+def build_fill(force: bool = False) -> Path:
+    if force or _stale(FILL, FILL_DEPS + [LIB]):
+        FILL.parent.mkdir(parents=True, exist_ok=True)
+        tmp = FILL.with_suffix(".tmp")
+        _run(["g++", "-O2", "-std=c++17", "-I", ROOT / "include", FILL_DEPS[0], "-L", PKG, "-lmhmkc", "-lz",
+              f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../../mhm2_proxy_amd", "-o", tmp])
+        tmp.replace(FILL)
+    return FILL
+
+
 def build_all(force: bool = False) -> None:
     build_lib(force)
     build_synth(force)
     build_oracle(force)
+    build_fill(force)
 
 
 if __name__ == "__main__":

@@ -4,7 +4,8 @@ profiles/pmc_traffic.json, which bench.py reports as roofline.traffic.
 traffic = (FETCH_SIZE * 2 + WRITE_SIZE) * 1024 bytes per launch: rocprofv3 reports both in KiB, and on
 gfx950 FETCH_SIZE counts half the bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section); the
 counts kernel's 8-byte loads match its algorithmic read volume under the same correction (within 0.2 %).
-  python tools/pmc_traffic.py <tag>
+  python tools/pmc_traffic.py <tag> <config key, e.g. C2/k21>
+Entries are kept per workload (bench.py reports one only for its own config and k).
 """
 import json
 import sys
@@ -12,14 +13,20 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 tag = sys.argv[1] if len(sys.argv) > 1 else "pmc"
+key = sys.argv[2] if len(sys.argv) > 2 else "C2/k21"
 summ = json.loads((ROOT / "gpurun_out" / f"{tag}_summary.json").read_text())
 stage_of = {"k_extract_scatter": "extract_scatter", "k_extract_hist": "extract_hist", "k_part_scatter": "part_scatter",
             "k_part_hist": "part_hist", "k_count": "count"}
-out = {}
+out, l2 = {}, {}
 for kern, c in summ.items():
     base = kern.split("<")[0]
     if base in stage_of and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         out[stage_of[base]] = int((c["FETCH_SIZE"] * 2 + c["WRITE_SIZE"]) * 1024)
-doc = {"per_launch_bytes": out, "source": f"gpurun_out/{tag}", "formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024"}
-(ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(doc, indent=1) + "\n")
+    if base in stage_of and "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        l2[stage_of[base]] = round(c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 3)
+path = ROOT / "profiles" / "pmc_traffic.json"
+doc = json.loads(path.read_text()) if path.exists() else {}
+doc = {"formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024", "configs": doc.get("configs", {})}
+doc["configs"][key] = {"per_launch_bytes": out, "l2_hit": l2, "source": f"profiles/{tag}_summary.json"}
+path.write_text(json.dumps(doc, indent=1) + "\n")
 print(json.dumps(doc, indent=1))
