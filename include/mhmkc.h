@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 5
+#define MHMKC_ABI_VERSION 6
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -113,6 +113,10 @@ typedef struct {
   uint64_t lds_misses;     /* count kernel: records not found in their home slot group (LDS slow path) */
   uint64_t lds_ext_adds;   /* count kernel: extension-counter increments (from the sampled first coarse bucket,
                               scaled to all records) */
+  uint64_t fq_pairs;       /* mhmkc_add_fastq_pairs: read pairs of the last call */
+  uint64_t fq_merged;      /* ... of which merged (merge_reads num_merged) */
+  uint64_t fq_ambiguous;   /* ... merge_reads' num_ambiguous increments */
+  uint64_t fq_overlap_bases; /* ... overlap bases of the merged pairs (merge_reads overlap_len) */
 } mhmkc_stats;
 
 enum {
@@ -169,8 +173,8 @@ int mhmkc_add_seqs(mhmkc_t h, const char *seqs, const uint64_t *seq_offsets, uin
  * Replaces FastqReader::get_next_fq_record (src/fastq.cpp:504-551: 4 lines per record, rtrim, the '@' and
  * '+' checks, get_fq_name :73-122, equal sequence and quality lengths) + the PackedRead constructor
  * (src/packed_reads.cpp:73-109: N and IUPAC codes -> 4, quality min(q - qual_offset, 31)) for reads that
- * reach kcount unchanged (single-end input, or pairs that merge_reads leaves unmerged: pair merging,
- * src/merge_reads.cpp:237-588, is not part of this library). Where the reference DIEs the call fails:
+ * reach kcount unchanged (single-end input; paired input goes through mhmkc_add_fastq_pairs, which merges
+ * the pairs first). Where the reference DIEs the call fails:
  * MHMKC_EINVAL for a malformed record (the message names the first bad record, 0-based),
  * MHMKC_EBADCHAR for a base outside A C G T N U R Y K M S W B D H V, MHMKC_EUNSUPPORTED for a line
  * longer than 2045 characters (the reference's fgets buffer, src/fastq.hpp:61, would split it).
@@ -181,7 +185,20 @@ int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes);
  * past n_bytes (the parser reads whole aligned dwords; the padding bytes are never interpreted). */
 int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes);
 
-/* The PackedReads of the last mhmkc_add_fastq[_device] call on the device: d_bytes[n_bases] in the
+/* Add read pairs given as interleaved FASTQ text (records 2p and 2p+1 are the mates /1 and /2 of pair p, the
+ * order FastqReader gives a pair of files, src/fastq.cpp:509-516): parsed on the device as mhmkc_add_fastq,
+ * then merged as merge_reads does (src/merge_reads.cpp:237-588: mate 2 reverse-complemented, offsets scanned
+ * with the mismatch, N and differential-quality rules, an unambiguous overlap merged base by base by quality),
+ * and the resulting PackedReads counted: for each pair the merged read and a dummy mate "N", or both mates
+ * unmerged (packed_reads_list of merge_reads). A last record without its mate is not added (the reference's
+ * loop stops there). Fails where the reference DIEs: the mhmkc_add_fastq errors, MHMKC_EINVAL for mates whose
+ * names differ or are not /1 and /2 ("Mismatched pairs"), for an overlap quality outside the Q2Perror table,
+ * MHMKC_EBADCHAR for an illegal base. Statistics: fq_pairs, fq_merged, fq_ambiguous, fq_overlap_bases. */
+int mhmkc_add_fastq_pairs(mhmkc_t h, const char *text, uint64_t n_bytes);
+/* Same, with device-resident text (only read during the call; 4 bytes of padding as for mhmkc_add_fastq_device). */
+int mhmkc_add_fastq_pairs_device(mhmkc_t h, const char *d_text, uint64_t n_bytes);
+
+/* The PackedReads of the last mhmkc_add_fastq[_pairs][_device] call on the device: d_bytes[n_bases] in the
  * PackedRead layout, d_offsets[n_reads + 1]. Valid until the next add_fastq, reset or destroy. Any
  * pointer may be NULL. */
 int mhmkc_fastq_packed(mhmkc_t h, const uint8_t **d_bytes, const uint64_t **d_offsets, uint64_t *n_reads,

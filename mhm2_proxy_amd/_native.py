@@ -39,7 +39,8 @@ ABI_SYMBOLS = [
     "mhmkc_config_init", "mhmkc_create", "mhmkc_destroy", "mhmkc_comm_id", "mhmkc_add_reads",
     "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_add_ctgs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_device_output",
     "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
-    "mhmkc_add_fastq", "mhmkc_add_fastq_device", "mhmkc_fastq_packed", "mhmkc_fastq_fetch",
+    "mhmkc_add_fastq", "mhmkc_add_fastq_device", "mhmkc_add_fastq_pairs", "mhmkc_add_fastq_pairs_device",
+    "mhmkc_fastq_packed", "mhmkc_fastq_fetch",
     "mhmkc_wait_stream", "mhmkc_set_dmin_thres", "mhmkc_set_transport", "mhmkc_minimizer_hashes",
 ]
 SYNTH_SYMBOLS = ["mhmkc_synth_config_init", "mhmkc_synth_genome", "mhmkc_synth_reads"]
@@ -95,6 +96,10 @@ class MhmkcStats(C.Structure):
         ("ms_h2d", C.c_double),
         ("lds_misses", C.c_uint64),
         ("lds_ext_adds", C.c_uint64),
+        ("fq_pairs", C.c_uint64),
+        ("fq_merged", C.c_uint64),
+        ("fq_ambiguous", C.c_uint64),
+        ("fq_overlap_bases", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -169,6 +174,8 @@ def lib() -> C.CDLL:
     L.mhmkc_add_ctgs.argtypes = [VP, C.c_char_p, VP, VP, U64]
     L.mhmkc_add_fastq.argtypes = [VP, C.c_char_p, U64]
     L.mhmkc_add_fastq_device.argtypes = [VP, VP, U64]
+    L.mhmkc_add_fastq_pairs.argtypes = [VP, C.c_char_p, U64]
+    L.mhmkc_add_fastq_pairs_device.argtypes = [VP, VP, U64]
     L.mhmkc_fastq_packed.argtypes = [VP, P(VP), P(VP), P(U64), P(U64)]
     L.mhmkc_fastq_fetch.argtypes = [VP, VP, VP]
     L.mhmkc_finish.argtypes = [VP, P(U64)]

@@ -328,6 +328,349 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pack(const char *text, const 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Read-pair merging (merge_reads, src/merge_reads.cpp:237-588) of an interleaved paired FASTQ text: records 2p
+// and 2p+1 are the mates of pair p (FastqReader interleaves a pair of files the same way, fastq.cpp:509-516).
+// k_fq_merge (one lane per pair) checks the pair's names, scans the offsets of the reverse-complemented mate 2
+// against mate 1 exactly as the reference does and records the verdict; k_fq_merge_pack (one 16-lane group
+// per output read) writes merge_reads' PackedReads: the merged read and a dummy "N" mate, or both mates.
+// The scan only ever changes qualities at N bases (an N's quality becomes the offset, :371-383), which the
+// output keeps; pairs with an N therefore scan copies of their quality lines in a scratch laid out like the
+// packed records (mate 1's qualities, mate 2's reversed), the others read the text in place.
+
+// Q2Perror (merge_reads.cpp:57-65), 81 entries
+__constant__ double Q2P_TAB[81] = {
+    1.0,       0.7943,    0.6309,    0.5012,    0.3981,    0.3162,    0.2512,    0.1995,    0.1585,    0.1259,     0.1,
+    0.07943,   0.06310,   0.05012,   0.03981,   0.03162,   0.02512,   0.01995,   0.01585,   0.01259,   0.01,       0.007943,
+    0.006310,  0.005012,  0.003981,  0.003162,  0.002512,  0.001995,  0.001585,  0.001259,  0.001,     0.0007943,  0.0006310,
+    0.0005012, 0.0003981, 0.0003162, 0.0002512, 0.0001995, 0.0001585, 0.0001259, 0.0001,    7.943e-05, 6.310e-05,  5.012e-05,
+    3.981e-05, 3.162e-05, 2.512e-05, 1.995e-05, 1.585e-05, 1.259e-05, 1e-05,     7.943e-06, 6.310e-06, 5.012e-06,  3.981e-06,
+    3.162e-06, 2.512e-06, 1.995e-06, 1.585e-06, 1.259e-06, 1e-06,     7.943e-07, 6.310e-07, 5.012e-07, 3.981e-07,  3.1622e-07,
+    2.512e-07, 1.995e-07, 1.585e-07, 1.259e-07, 1e-07,     7.943e-08, 6.310e-08, 5.012e-08, 3.981e-08, 3.1622e-08, 2.512e-08,
+    1.995e-08, 1.585e-08, 1.259e-08, 1e-08};
+
+// The lines of record r: id [b, te), sequence [sb, sb + L), quality [qb, qb + L); false when its lines are
+// not a valid record (k_fq_records reports that record)
+struct FqRec {
+  uint64_t idb, idte, sb, qb;
+  uint32_t L;
+};
+__device__ bool fq_rec(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t r, FqRec &o) {
+  uint64_t lw[5], lb[4], le[4], te[4];
+#pragma unroll
+  for (int i = 0; i < 5; i++) lw[i] = (4 * r + i) ? line_end[4 * r + i - 1] : 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    lb[i] = (4 * r + i) ? (lw[i] & FQ_LE_MASK) + 1 : 0;
+    le[i] = lw[i + 1] & FQ_LE_MASK;
+    te[i] = le[i] == n ? rtrim_end(text, lb[i], le[i]) : le[i] - ((lw[i + 1] >> FQ_LE_BITS) & 0xffffu);
+    if (le[i] - lb[i] > FQ_MAX_LINE) return false;
+  }
+  if (te[1] - lb[1] != te[3] - lb[3] || te[0] == lb[0]) return false;
+  o.idb = lb[0];
+  o.idte = te[0];
+  o.sb = lb[1];
+  o.qb = lb[3];
+  o.L = (uint32_t)(te[1] - lb[1]);
+  return true;
+}
+
+// get_fq_name + replace_spaces (fastq.cpp:73-122, :544): the normalized name of the trimmed id line [b, e) as
+// prefix [pb, pe) (the name without its last two characters) and the last character
+__device__ bool fq_norm(const char *s, uint64_t b, uint64_t e, uint64_t &pb, uint64_t &pe, char &last) {
+  const char *h = s + b + 1;
+  const uint64_t len = rtrim_end(s, b + 1, e) - (b + 1);
+  pb = b + 1;
+  if (len >= 3 && h[len - 2] != '/') {
+    if (h[len - 2] == 'R') {  // pair-R1 -> pair/1
+      pe = b + 1 + len - 3;
+      last = h[len - 1];
+      return true;
+    }
+    uint64_t tab = len, sp = len;
+    for (uint64_t i = 0; i < len && tab == len; i++) {
+      if (h[i] == '\t') tab = i;
+      if (h[i] == ' ' && sp == len) sp = i;
+    }
+    const uint64_t ep = tab < len ? tab : sp;
+    if (ep == len) {  // no comment: unchanged
+      pe = b + 1 + len - 2;
+      last = h[len - 1];
+      return true;
+    }
+    if (ep > 3 && h[ep - 2] == '/' && (h[ep - 1] == '1' || h[ep - 1] == '2')) {
+      pe = b + 1 + ep - 2;
+      last = h[ep - 1];
+      return true;
+    }
+    if (len < ep + 7 || h[ep + 2] != ':' || h[ep + 4] != ':' || h[ep + 6] != ':' || (h[ep + 1] != '1' && h[ep + 1] != '2'))
+      return false;
+    pe = b + 1 + ep;  // pair 1:N:... -> pair/1
+    last = h[ep + 1];
+    return true;
+  }
+  pe = b + 1 + (len >= 2 ? len - 2 : 0);
+  last = len ? h[len - 1] : 0;
+  return true;
+}
+
+// revcomp's complement (utils.cpp: IUPAC -> N), 0 for a character it DIEs on
+__device__ __forceinline__ char fq_comp(char c) {
+  switch (c) {
+    case 'A': return 'T';
+    case 'C': return 'G';
+    case 'G': return 'C';
+    case 'T': return 'A';
+  }
+  return base_code((unsigned char)c) == 4 ? 'N' : 0;
+}
+
+// per pair: (overlap + 1) of the merge (0: not merged) | has-N << 31
+constexpr uint32_t MP_HASN = 1u << 31;
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_merge(const char *text, uint64_t n,
+                                                          const unsigned long long *line_end, uint64_t n_pairs,
+                                                          const unsigned long long *rec_offs, int qual_offset,
+                                                          char *scratch, uint32_t *pair_info,
+                                                          unsigned long long *out_len, unsigned long long *err,
+                                                          unsigned long long *stats) {
+  const uint64_t p = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x;
+  uint64_t merged = 0, ambiguous = 0, ov_bases = 0;
+  if (p == n_pairs) out_len[2 * n_pairs] = 0;  // the scan's last element
+  if (p < n_pairs) {
+    pair_info[p] = 0;
+    out_len[2 * p] = 0;
+    out_len[2 * p + 1] = 0;
+    FqRec a, b;
+    uint64_t pb1, pe1, pb2, pe2;
+    char l1, l2;
+    if (fq_rec(text, n, line_end, 2 * p, a) && fq_rec(text, n, line_end, 2 * p + 1, b) &&
+        fq_norm(text, a.idb, a.idte, pb1, pe1, l1) && fq_norm(text, b.idb, b.idte, pb2, pe2, l2)) {
+      bool same = pe1 - pb1 == pe2 - pb2;
+      for (uint64_t i = 0; same && i < pe1 - pb1; i++) {
+        char x = text[pb1 + i], y = text[pb2 + i];
+        x = x == ' ' ? '_' : x;
+        y = y == ' ' ? '_' : y;
+        same = x == y;
+      }
+      if (!same) {
+        fq_fail(err, 2 * p + 1, FQ_E_PAIR_NAME);
+      } else if (l1 != '1' || l2 != '2') {
+        fq_fail(err, 2 * p + 1, FQ_E_PAIR_NUM);
+      } else {
+        const int L1 = (int)a.L, L2 = (int)b.L;
+        const char *s1 = text + a.sb, *tq1 = text + a.qb, *s2 = text + b.sb, *tq2 = text + b.qb;
+        bool hasN = false, bad2 = false;
+        for (int j = 0; j < L2; j++) {
+          const char c = fq_comp(s2[j]);
+          bad2 |= c == 0;
+          hasN |= c == 'N';
+        }
+        for (int x = 0; x < L1; x++) hasN |= s1[x] == 'N';
+        if (bad2) {
+          fq_fail(err, 2 * p + 1, FQ_E_CHAR2);
+        } else {
+          char *cq1 = scratch + rec_offs[2 * p], *crq2 = scratch + rec_offs[2 * p + 1];
+          if (hasN) {
+            for (int x = 0; x < L1; x++) cq1[x] = tq1[x];
+            for (int j = 0; j < L2; j++) crq2[j] = tq2[L2 - 1 - j];
+          }
+          auto Q1 = [&](int x) -> char { return hasN ? cq1[x] : tq1[x]; };
+          auto RQ2 = [&](int j) -> char { return hasN ? crq2[j] : tq2[L2 - 1 - j]; };
+          auto RC2 = [&](int j) -> char { return fq_comp(s2[L2 - 1 - j]); };
+          const int16_t MIN_OVERLAP = 12, EXTRA_TEST_OVERLAP = 2, MAX_MISMATCHES = 3, EXTRA_PER_1000 = 150;
+          const double MAX_PERROR = 0.025;
+          int abort_merge = 0;
+          bool qbad = false;
+          const int16_t len = (int16_t)(L2 < L1 ? L2 : L1);
+          const int16_t start_i = (len == (int16_t)L1) ? 0 : (int16_t)(L1 - len);
+          int16_t found_i = -1, best_i = -1;
+          for (int16_t i = 0; i < len - MIN_OVERLAP + EXTRA_TEST_OVERLAP && !qbad; i++) {
+            if (abort_merge) break;
+            const int16_t overlap = len - i;
+            const int16_t this_max = MAX_MISMATCHES + (EXTRA_PER_1000 * overlap / 1000);
+            const int16_t err_max = this_max * 4 / 3 + 1;
+            int16_t fast = 0;  // fast_count_mismatches (:183-230): the count, or more than err_max
+            for (int16_t j = 0; j < overlap && fast <= err_max; j++) fast += s1[start_i + i + j] != RC2(j);
+            if (fast > err_max) continue;
+            int16_t matches = 0, mismatches = 0, bothNs = 0, Ncount = 0, checked = 0;
+            double perror = 0.0;
+            for (int16_t j = 0; j < overlap; j++) {
+              checked++;
+              const int x = start_i + i + j;
+              const char ps = s1[x], rs = RC2(j);
+              if (ps == rs) {
+                matches++;
+                if (ps == 'N') {
+                  Ncount += 2;
+                  if (bothNs++) {
+                    abort_merge++;
+                    ambiguous++;
+                    break;
+                  }
+                }
+              } else {
+                mismatches++;
+                if (ps == 'N') {  // an N zeroes its own quality (hasN holds: the copies are in the scratch)
+                  mismatches++;
+                  Ncount++;
+                  cq1[x] = (char)qual_offset;
+                } else if (rs == 'N') {
+                  Ncount++;
+                  mismatches++;
+                  crq2[j] = (char)qual_offset;
+                }
+                const uint8_t qa = (uint8_t)(Q1(x) - qual_offset), qb = (uint8_t)(RQ2(j) - qual_offset);
+                if (qa >= 81 || qb >= 81) {  // the invalid-quality DIE of :409-413
+                  qbad = true;
+                  break;
+                }
+                if (ps == 'N')
+                  perror += Q2P_TAB[qb];
+                else if (rs == 'N')
+                  perror += Q2P_TAB[qa];
+                const uint8_t dq = qa > qb ? qa - qb : qb - qa;
+                perror += dq <= 2 ? 0.5 : Q2P_TAB[dq];
+              }
+              if (Ncount > 3) {
+                abort_merge++;
+                ambiguous++;
+                break;
+              }
+              if (mismatches > err_max) break;
+            }
+            if (qbad) break;
+            int16_t match_thres = overlap - this_max;
+            if (match_thres < MIN_OVERLAP) match_thres = MIN_OVERLAP;
+            if (matches >= match_thres && checked == overlap && mismatches <= this_max && perror / overlap <= MAX_PERROR) {
+              if (best_i < 0 && found_i < 0) {
+                best_i = i;
+              } else {
+                ambiguous++;
+                best_i = -1;
+                break;
+              }
+            } else if (checked == overlap && mismatches <= err_max && perror / overlap <= MAX_PERROR * 4 / 3) {
+              found_i = i;
+              if (best_i >= 0) {
+                ambiguous++;
+                best_i = -1;
+                break;
+              }
+            }
+          }
+          if (qbad) {
+            fq_fail(err, 2 * p + 1, FQ_E_QUAL);
+          } else {
+            uint32_t info = hasN ? MP_HASN : 0u;
+            if (best_i >= 0 && !abort_merge) {
+              const int ov = len - best_i;
+              info |= (uint32_t)ov + 1u;
+              out_len[2 * p] = (unsigned long long)(L1 + L2 - ov);
+              out_len[2 * p + 1] = 1;
+              merged = 1;
+              ov_bases = (uint64_t)ov;
+            } else {
+              out_len[2 * p] = (unsigned long long)L1;
+              out_len[2 * p + 1] = (unsigned long long)L2;
+            }
+            pair_info[p] = info;
+          }
+        }
+      }
+    }
+  }
+  merged = wave_sum64(merged);
+  ambiguous = wave_sum64(ambiguous);
+  ov_bases = wave_sum64(ov_bases);
+  if ((threadIdx.x & 63) == 0 && (merged | ambiguous)) {
+    atomicAdd(&stats[1], (unsigned long long)merged);
+    atomicAdd(&stats[2], (unsigned long long)ambiguous);
+    atomicAdd(&stats[3], (unsigned long long)ov_bases);
+  }
+}
+
+// PackedRead byte of base c with quality character q (packed_reads.cpp:87-105); false for a fatal character
+__device__ __forceinline__ uint8_t fq_byte(char c, char q, int qual_offset, bool &bad) {
+  const int code = base_code((unsigned char)c);
+  bad |= code < 0;
+  int v = (int)(signed char)q - qual_offset;
+  v = v > 31 ? 31 : v;
+  return (uint8_t)((code & 7) | (uint8_t)((unsigned char)v << 3));
+}
+
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_merge_pack(const char *text, uint64_t n,
+                                                               const unsigned long long *line_end, uint64_t n_pairs,
+                                                               const unsigned long long *rec_offs,
+                                                               const char *scratch, const uint32_t *pair_info,
+                                                               const unsigned long long *out_offs, int qual_offset,
+                                                               uint8_t *out, unsigned long long *err) {
+  const uint64_t o = (uint64_t)blockIdx.x * (FQ_THREADS / FQ_GROUP) + (threadIdx.x / FQ_GROUP);
+  const int gl = threadIdx.x % FQ_GROUP;
+  if (o >= 2 * n_pairs) return;
+  const uint64_t p = o >> 1;
+  const int mate = (int)(o & 1);
+  const uint64_t ob = out_offs[o];
+  const int Lo = (int)(out_offs[o + 1] - ob);
+  if (Lo == 0) return;
+  const uint32_t info = pair_info[p];
+  const int ov = (int)(info & ~MP_HASN) - 1;  // -1: not merged
+  const bool hasN = (info & MP_HASN) != 0;
+  uint8_t *dst = out + ob;
+  if (ov >= 0 && mate == 1) {  // the dummy mate "N" with quality qual_offset
+    if (gl == 0) dst[0] = 4;
+    return;
+  }
+  FqRec a, b;
+  if (!fq_rec(text, n, line_end, 2 * p, a) || !fq_rec(text, n, line_end, 2 * p + 1, b)) return;
+  const int L1 = (int)a.L, L2 = (int)b.L;
+  const char *s1 = text + a.sb, *tq1 = text + a.qb, *s2 = text + b.sb, *tq2 = text + b.qb;
+  const char *cq1 = scratch + rec_offs[2 * p], *crq2 = scratch + rec_offs[2 * p + 1];
+  bool bad = false;
+  if (mate == 1) {  // mate 2 as read
+    for (int x = gl; x < Lo; x += FQ_GROUP) dst[x] = fq_byte(s2[x], tq2[x], qual_offset, bad);
+    return;  // (its characters were checked by the revcomp of k_fq_merge)
+  }
+  const int st = L1 - (ov >= 0 ? ov : 0);  // the overlap is mate 1's last ov bases
+  const int max_match_qual = 41 + qual_offset;
+  for (int x = gl; x < Lo; x += FQ_GROUP) {
+    char c, q;
+    if (x < L1) {
+      c = s1[x];
+      q = hasN ? cq1[x] : tq1[x];
+      if (ov >= 0 && x >= st) {  // :449-469
+        const int j = x - st;
+        const char rc = fq_comp(s2[L2 - 1 - j]), rq = hasN ? crq2[j] : tq2[L2 - 1 - j];
+        if (c == rc) {
+          const uint16_t nq = (uint16_t)(q + rq - qual_offset);
+          q = (char)(nq > max_match_qual ? max_match_qual : nq);
+        } else {
+          uint8_t nq;
+          if (q < rq) {
+            nq = (uint8_t)(rq - q + qual_offset);
+            c = rc;
+          } else {
+            nq = (uint8_t)(q - rq + qual_offset);
+          }
+          q = (char)(nq > 2 + qual_offset ? nq : 2 + qual_offset);
+        }
+      }
+    } else {  // the rest of rc_seq2 (:472-473)
+      const int j = x - L1 + ov;
+      c = fq_comp(s2[L2 - 1 - j]);
+      q = hasN ? crq2[j] : tq2[L2 - 1 - j];
+    }
+    dst[x] = fq_byte(c, q, qual_offset, bad);
+  }
+  if (bad) fq_fail(err, 2 * p + 1, FQ_E_CHAR1);  // PackedRead of mate 1 (or the merged read) DIEs
+}
+
 }  // namespace
 
 size_t fq_scan_tmp_bytes(uint64_t n_items) {
@@ -359,6 +702,26 @@ hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long l
                              unsigned long long *len, unsigned long long *err, hipStream_t s) {
   const uint64_t nb = (n_rec + 1 + FQ_THREADS - 1) / FQ_THREADS;
   hipLaunchKernelGGL(k_fq_records, dim3((uint32_t)nb), dim3(FQ_THREADS), 0, s, text, n, line_end, n_rec, len, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_fq_merge(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
+                           const unsigned long long *rec_offs, int qual_offset, char *scratch, uint32_t *pair_info,
+                           unsigned long long *out_len, unsigned long long *err, unsigned long long *stats,
+                           hipStream_t s) {
+  k_fq_merge<<<dim3((unsigned)((n_pairs + 1 + FQ_THREADS - 1) / FQ_THREADS)), dim3(FQ_THREADS), 0, s>>>(
+      text, n, line_end, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_fq_merge_pack(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
+                                const unsigned long long *rec_offs, const char *scratch, const uint32_t *pair_info,
+                                const unsigned long long *out_offs, int qual_offset, uint8_t *out,
+                                unsigned long long *err, hipStream_t s) {
+  if (!n_pairs) return hipSuccess;
+  const uint64_t per = FQ_THREADS / FQ_GROUP;
+  k_fq_merge_pack<<<dim3((unsigned)((2 * n_pairs + per - 1) / per)), dim3(FQ_THREADS), 0, s>>>(
+      text, n, line_end, n_pairs, rec_offs, scratch, pair_info, out_offs, qual_offset, out, err);
   return hipGetLastError();
 }
 

@@ -238,6 +238,10 @@ constexpr int FQ_CHUNK = 4096;
 constexpr uint64_t FQ_MAX_LINE = 2045;
 // error kinds, in the order the reference checks them (src/fastq.cpp:525-547, packed_reads.cpp:104)
 enum { FQ_E_ID = 1, FQ_E_PLUS = 2, FQ_E_NAME = 3, FQ_E_LEN = 4, FQ_E_LONG = 5, FQ_E_CHAR = 6, FQ_E_TRUNC = 7 };
+// read-pair merging (merge_reads.cpp), reported at the pair's second record so that both records' own checks
+// come first, in the reference's order: names, pair numbers, mate 2's revcomp, an overlap quality, mate 1's
+// (or the merged read's) PackedRead
+enum { FQ_E_PAIR_NAME = 8, FQ_E_PAIR_NUM = 9, FQ_E_CHAR2 = 10, FQ_E_QUAL = 11, FQ_E_CHAR1 = 12 };
 size_t fq_scan_tmp_bytes(uint64_t n_items);
 hipError_t fq_scan(void *tmp, size_t tmp_bytes, const unsigned long long *in, unsigned long long *out,
                    uint64_t n_items, hipStream_t s);
@@ -253,6 +257,17 @@ hipError_t launch_fq_lines(const char *text, uint64_t n, const unsigned long lon
 // record << 4 | FQ_E_*)
 hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_rec,
                              unsigned long long *len, unsigned long long *err, hipStream_t s);
+// pair p = records 2p, 2p+1: verdict in pair_info, output read lengths (merged + 1, or L1, L2) in out_len
+// [2 n_pairs + 1]; stats[1..3] += merged pairs, ambiguous events, overlap bases. scratch: rec_offs[2 n_pairs]
+// bytes (quality copies of pairs with an N).
+hipError_t launch_fq_merge(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
+                           const unsigned long long *rec_offs, int qual_offset, char *scratch, uint32_t *pair_info,
+                           unsigned long long *out_len, unsigned long long *err, unsigned long long *stats,
+                           hipStream_t s);
+hipError_t launch_fq_merge_pack(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
+                                const unsigned long long *rec_offs, const char *scratch, const uint32_t *pair_info,
+                                const unsigned long long *out_offs, int qual_offset, uint8_t *out,
+                                unsigned long long *err, hipStream_t s);
 hipError_t launch_fq_pack(const char *text, const unsigned long long *line_end, uint64_t n_rec,
                           const unsigned long long *offs, int qual_offset, uint8_t *out, unsigned long long *err,
                           hipStream_t s);

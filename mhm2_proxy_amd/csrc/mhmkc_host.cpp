@@ -164,8 +164,9 @@ struct mhmkc {
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
   DevBuf d_fq_text, d_fq_chunk, d_fq_lines, d_fq_len, d_fq_tmp, d_fq_bytes, d_fq_offs, d_fq_err;
+  DevBuf d_fq_recoffs, d_fq_scratch, d_fq_pairinfo, d_fq_stats;  // pair merging
   uint64_t fq_reads = 0, fq_bases = 0;
-  int add_fastq(const char *d_text, uint64_t n);
+  int add_fastq(const char *d_text, uint64_t n, bool pairs = false);
   // contig pass (add_ctg_kmers): contigs in the PackedRead byte layout, kept on the host until finish
   std::vector<uint8_t> ctg_bytes;
   std::vector<uint64_t> ctg_offs{0}, ctg_win{0};  // byte offsets, counted-window prefix
@@ -1418,10 +1419,11 @@ int mhmkc_wait_stream(mhmkc_t h, void *stream) {
 }
 
 // FASTQ text on the device -> PackedReads in d_fq_bytes / d_fq_offs -> add_view (fastq.hip).
-int mhmkc::add_fastq(const char *d_text, uint64_t n) {
+int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
   int rc = begin_round();
   if (rc) return rc;
   fq_reads = fq_bases = 0;
+  if (pairs) st.fq_pairs = st.fq_merged = st.fq_ambiguous = st.fq_overlap_bases = 0;
   if (n == 0) return MHMKC_OK;
   if (n > mhm::FQ_LE_MASK) return fail(MHMKC_EINVAL, "FASTQ text larger than 2^40 bytes in one call");
   // the packed reads of an earlier add_fastq may still be read by a pending extraction: settle it first
@@ -1471,18 +1473,68 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n) {
   if ((e = hipMemcpyAsync(&n_bases, offs + R, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
       (e = hipStreamSynchronize(stream)) != hipSuccess)
     return hip_fail(e, "fastq records D2H");
-  if ((e = grow(d_fq_bytes, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess) return hip_fail(e, "fastq bytes");
-  prof_begin(MHMKC_STAGE_OTHER);
-  e = mhm::launch_fq_pack(d_text, lend, R, offs, cfg.qual_offset, d_fq_bytes.as<uint8_t>(), err_d, stream);
-  prof_end();
+  uint64_t R_out = R;  // reads added (pairs: two per pair)
+  if (!pairs) {
+    if ((e = grow(d_fq_bytes, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess) return hip_fail(e, "fastq bytes");
+    prof_begin(MHMKC_STAGE_OTHER);
+    e = mhm::launch_fq_pack(d_text, lend, R, offs, cfg.qual_offset, d_fq_bytes.as<uint8_t>(), err_d, stream);
+    prof_end();
+  } else {
+    // merge_reads: the record offsets lay out the quality scratch; the pair verdicts give the output lengths
+    const uint64_t P = R / 2;
+    R_out = 2 * P;
+    if ((e = grow(d_fq_recoffs, (R + 1) * 8)) != hipSuccess ||
+        (e = grow(d_fq_scratch, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess ||
+        (e = grow(d_fq_pairinfo, (P + 1) * 4)) != hipSuccess || (e = grow(d_fq_stats, 64)) != hipSuccess ||
+        (e = grow(d_fq_len, (2 * P + 1) * 8)) != hipSuccess)
+      return hip_fail(e, "fastq pairs");
+    const size_t tmp3 = mhm::fq_scan_tmp_bytes(2 * P + 1);
+    if (tmp3 > tmp_bytes) {
+      if ((e = grow(d_fq_tmp, tmp3)) != hipSuccess) return hip_fail(e, "fastq scan scratch");
+      tmp_bytes = tmp3;
+    }
+    unsigned long long *roffs = d_fq_recoffs.as<unsigned long long>(), *fst = d_fq_stats.as<unsigned long long>();
+    unsigned long long *len2 = d_fq_len.as<unsigned long long>();
+    prof_begin(MHMKC_STAGE_OTHER);
+    e = hipMemcpyAsync(roffs, offs, (R + 1) * 8, hipMemcpyDeviceToDevice, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(fst, 0, 32, stream);
+    if (e == hipSuccess)
+      e = mhm::launch_fq_merge(d_text, n, lend, P, roffs, cfg.qual_offset, d_fq_scratch.as<char>(),
+                               d_fq_pairinfo.as<uint32_t>(), len2, err_d, fst, stream);
+    if (e == hipSuccess) e = mhm::fq_scan(d_fq_tmp.p, tmp_bytes, len2, offs, 2 * P + 1, stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "fastq merge");
+    unsigned long long hs[4] = {0, 0, 0, 0};
+    if ((e = hipMemcpyAsync(&n_bases, offs + 2 * P, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(hs, fst, 32, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(stream)) != hipSuccess)
+      return hip_fail(e, "fastq merge D2H");
+    st.fq_pairs = P;
+    st.fq_merged = hs[1];
+    st.fq_ambiguous = hs[2];
+    st.fq_overlap_bases = hs[3];
+    if ((e = grow(d_fq_bytes, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess) return hip_fail(e, "fastq bytes");
+    prof_begin(MHMKC_STAGE_OTHER);
+    e = mhm::launch_fq_merge_pack(d_text, n, lend, P, roffs, d_fq_scratch.as<char>(), d_fq_pairinfo.as<uint32_t>(),
+                                  offs, cfg.qual_offset, d_fq_bytes.as<uint8_t>(), err_d, stream);
+    prof_end();
+  }
   unsigned long long first_err = ~0ull;
   if (e == hipSuccess) e = hipMemcpyAsync(&first_err, err_d, 8, hipMemcpyDeviceToHost, stream);
   if (e == hipSuccess) e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return hip_fail(e, "fastq pack");
   if (lines % 4) first_err = std::min<unsigned long long>(first_err, ((unsigned long long)R << 4) | mhm::FQ_E_TRUNC);
   if (first_err != ~0ull) {
-    const unsigned long long rec = first_err >> 4;
+    unsigned long long rec = first_err >> 4;
     switch ((int)(first_err & 15)) {
+      case mhm::FQ_E_PAIR_NAME:
+        return fail(MHMKC_EINVAL, "FASTQ records %llu and %llu: mismatched pair names", rec - 1, rec);
+      case mhm::FQ_E_PAIR_NUM:
+        return fail(MHMKC_EINVAL, "FASTQ records %llu and %llu: mismatched pair numbers (not /1, /2)", rec - 1, rec);
+      case mhm::FQ_E_CHAR2: return fail(MHMKC_EBADCHAR, "FASTQ record %llu: illegal base character", rec);
+      case mhm::FQ_E_QUAL:
+        return fail(MHMKC_EINVAL, "FASTQ records %llu and %llu: invalid quality score in the overlap", rec - 1, rec);
+      case mhm::FQ_E_CHAR1: return fail(MHMKC_EBADCHAR, "FASTQ record %llu: illegal base character", rec - 1);
       case mhm::FQ_E_ID: return fail(MHMKC_EINVAL, "invalid FASTQ record %llu: expected read name (@)", rec);
       case mhm::FQ_E_PLUS: return fail(MHMKC_EINVAL, "invalid FASTQ record %llu: expected '+'", rec);
       case mhm::FQ_E_NAME: return fail(MHMKC_EINVAL, "invalid FASTQ record %llu: incorrect name format", rec);
@@ -1495,14 +1547,14 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n) {
       default: return fail(MHMKC_EINVAL, "FASTQ text ends inside record %llu", rec);
     }
   }
-  fq_reads = R;
+  fq_reads = R_out;
   fq_bases = n_bases;
-  st.reads += R;
+  st.reads += R_out;
   st.bases += n_bases;
-  if (R == 0) return MHMKC_OK;
+  if (R_out == 0) return MHMKC_OK;
   qcut_pending = cfg.qual_cutoff;
   // the offsets were made here from checked records: the window count kernel re-checks them anyway
-  mhm::ReadsView rv{d_fq_bytes.as<uint8_t>(), d_fq_offs.as<uint64_t>(), R, n_bases, 0, 0, 0};
+  mhm::ReadsView rv{d_fq_bytes.as<uint8_t>(), d_fq_offs.as<uint64_t>(), R_out, n_bases, 0, 0, 0};
   return add_view(rv, 0, false);
 }
 
@@ -1518,7 +1570,13 @@ int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes) {
   return h->add_fastq(d_text, n_bytes);
 }
 
-int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes) {
+int mhmkc_add_fastq_pairs_device(mhmkc_t h, const char *d_text, uint64_t n_bytes) {
+  if (!h) return MHMKC_EINVAL;
+  if (n_bytes && !d_text) return h->fail(MHMKC_EINVAL, "null device buffer");
+  return h->add_fastq(d_text, n_bytes, true);
+}
+
+static int add_fastq_host(mhmkc_t h, const char *text, uint64_t n_bytes, bool pairs) {
   if (!h) return MHMKC_EINVAL;
   if (n_bytes && !text) return h->fail(MHMKC_EINVAL, "null host buffer");
   int rc = h->resolve_slabs();  // an earlier add_fastq's text may still be read
@@ -1527,9 +1585,15 @@ int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes) {
   if ((e = h->grow(h->d_fq_text, n_bytes + 16)) != hipSuccess) return h->hip_fail(e, "fastq staging");
   if (n_bytes && (e = hipMemcpyAsync(h->d_fq_text.p, text, n_bytes, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
     return h->hip_fail(e, "fastq H2D");
-  rc = h->add_fastq(h->d_fq_text.as<char>(), n_bytes);
+  rc = h->add_fastq(h->d_fq_text.as<char>(), n_bytes, pairs);
   if (rc == MHMKC_OK && (e = hipStreamSynchronize(h->stream)) != hipSuccess) return h->hip_fail(e, "add_fastq");
   return rc;
+}
+
+int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes) { return add_fastq_host(h, text, n_bytes, false); }
+
+int mhmkc_add_fastq_pairs(mhmkc_t h, const char *text, uint64_t n_bytes) {
+  return add_fastq_host(h, text, n_bytes, true);
 }
 
 int mhmkc_fastq_packed(mhmkc_t h, const uint8_t **d_bytes, const uint64_t **d_offsets, uint64_t *n_reads,

@@ -315,7 +315,15 @@ class KmerCounter:
         blob = text.encode("ascii") if isinstance(text, str) else bytes(text)
         self._check(N.lib().mhmkc_add_fastq(self._h, blob, len(blob)))
 
-    def add_fastq_tensor(self, text_t, n_bytes: int | None = None) -> None:
+    def add_fastq_pairs(self, text) -> None:
+        """Interleaved paired FASTQ text (mates /1, /2 back to back), parsed on the device, the pairs merged as
+        merge_reads does (src/merge_reads.cpp:237-588: merged read + dummy "N" mate, or both mates), then
+        counted. stats() reports fq_pairs / fq_merged / fq_ambiguous / fq_overlap_bases; fastq_packed() returns
+        merge_reads' PackedReads."""
+        blob = text.encode("ascii") if isinstance(text, str) else bytes(text)
+        self._check(N.lib().mhmkc_add_fastq_pairs(self._h, blob, len(blob)))
+
+    def add_fastq_tensor(self, text_t, n_bytes: int | None = None, pairs: bool = False) -> None:
         """FASTQ text already in HBM (a uint8 torch tensor on the counter's device). The parser reads whole
         aligned dwords, so the buffer must extend 4 bytes past the text: pass n_bytes <= numel - 4 to use the
         tensor as is; otherwise the text is copied into a padded buffer first."""
@@ -328,7 +336,8 @@ class KmerCounter:
             text_t = padded
         self._fq_text = text_t  # keep it alive while the call runs
         self._after_torch(text_t)
-        self._check(N.lib().mhmkc_add_fastq_device(self._h, text_t.data_ptr(), n))
+        fn = N.lib().mhmkc_add_fastq_pairs_device if pairs else N.lib().mhmkc_add_fastq_device
+        self._check(fn(self._h, text_t.data_ptr(), n))
 
     def fastq_packed(self) -> tuple[np.ndarray, np.ndarray]:
         """The PackedReads (bytes, offsets) of the last add_fastq call, copied to the host."""

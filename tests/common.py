@@ -199,3 +199,50 @@ def fastq_text(packed_bytes, offsets, *, seed: int = 0, crlf_every: int = 0, tra
     if not final_newline and t.endswith(b"\n"):
         t = t[:-2] if t.endswith(b"\r\n") else t[:-1]
     return t
+
+
+PAIR_NAME_STYLES = ("illumina18", "slash", "hudson", "tab", "slash_comment")
+
+
+def paired_fastq_text(n_pairs: int, seed: int = 0, *, genome_len: int = 200_000, read_len: int = 150,
+                      frag_mean: int = 240, frag_sd: int = 40, subst: float = 0.01, n_rate: float = 0.002,
+                      iupac: bool = True, low_q: float = 0.05, qual_offset: int = 33, uneven: bool = True) -> bytes:
+    """Interleaved paired FASTQ (mate 1 = a fragment's start, mate 2 = the reverse complement of its end), so
+    that most pairs overlap by 2L - F bases: substitutions at random qualities, N and IUPAC codes, low-quality
+    runs, unequal mate lengths, every name style get_fq_name accepts with /1 and /2 mates."""
+    rng = np.random.default_rng(seed)
+    g = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, size=genome_len)]
+    comp = np.zeros(256, dtype=np.uint8)
+    for a, b in (b"AT", b"CG", b"GC", b"TA"):
+        comp[a] = b
+    amb = np.frombuffer(b"NRYKMSWBDHV", dtype=np.uint8)
+    out = []
+    for i in range(n_pairs):
+        F = int(np.clip(rng.normal(frag_mean, frag_sd), 40, 2 * read_len + 60))
+        a = int(rng.integers(0, genome_len - F))
+        frag = g[a:a + F]
+        L1 = read_len if not uneven or i % 7 else int(rng.integers(20, read_len + 1))
+        L2 = read_len if not uneven or i % 11 else int(rng.integers(20, read_len + 1))
+        m1 = frag[:min(L1, F)].copy()
+        m2 = comp[frag[::-1][:min(L2, F)]].copy()
+        quals = []
+        for m in (m1, m2):
+            q = rng.integers(30, 41, size=m.size).astype(np.uint8)
+            tail = int(rng.integers(0, m.size // 3 + 1)) if rng.random() < 0.3 else 0
+            if tail:
+                q[m.size - tail:] = rng.integers(2, 20, size=tail)
+            sub = rng.random(m.size) < subst
+            m[sub] = g[rng.integers(0, 4, size=int(sub.sum()))]
+            q[sub] = rng.integers(2, 41, size=int(sub.sum()))
+            nn = rng.random(m.size) < n_rate
+            m[nn] = amb[rng.integers(0, len(amb) if iupac else 1, size=int(nn.sum()))]
+            lq = rng.random(m.size) < low_q
+            q[lq] = rng.integers(0, 12, size=int(lq.sum()))
+            quals.append((q + qual_offset).astype(np.uint8))
+        style = PAIR_NAME_STYLES[i % len(PAIR_NAME_STYLES)]
+        for mate, (m, q) in enumerate(((m1, quals[0]), (m2, quals[1])), start=1):
+            name = {"illumina18": f"@M0:{i}:FC:1:{i % 97}:{i % 13}:{i} {mate}:N:0:ACGT",
+                    "slash": f"@frag {i}/{mate}", "hudson": f"@pair{i}-R{mate}",
+                    "tab": f"@read{i}/{mate}\textra", "slash_comment": f"@read{i}/{mate} comment here"}[style]
+            out.append(name.encode() + b"\n" + m.tobytes() + b"\n+\n" + q.tobytes() + b"\n")
+    return b"".join(out)

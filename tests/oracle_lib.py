@@ -56,6 +56,8 @@ def oracle() -> C.CDLL:
         L.orc_count_records.restype = VP
         L.orc_fastq_pack.argtypes = [C.c_char_p, U64, I, VP, VP, VP]
         L.orc_fastq_pack.restype = C.c_int64
+        L.orc_merge_fastq.argtypes = [C.c_char_p, U64, I, VP, VP, VP, VP]
+        L.orc_merge_fastq.restype = C.c_int64
         L.orc_table_size.argtypes = [VP]
         L.orc_table_size.restype = U64
         L.orc_table_fetch.argtypes = [VP, VP, VP, VP, VP]
@@ -207,7 +209,8 @@ def target_rank(longs, k: int, rank_n: int) -> int:
     return int(oracle().orc_kmer_target_rank(a.ctypes.data, k, a.size, rank_n))
 
 
-FQ_KINDS = {1: "id", 2: "plus", 3: "name", 4: "len", 5: "long", 6: "char", 7: "trunc"}
+FQ_KINDS = {1: "id", 2: "plus", 3: "name", 4: "len", 5: "long", 6: "char", 7: "trunc", 8: "pair_name",
+            9: "pair_number", 10: "qual"}
 
 
 def fastq_pack(text: bytes, qual_offset: int = 33):
@@ -221,6 +224,23 @@ def fastq_pack(text: bytes, qual_offset: int = 33):
     if r < 0:
         raise FastqError(FQ_KINDS[-r], int(err[0]))
     return out[: int(offs[r])].copy(), offs[: r + 1].copy()
+
+
+def merge_fastq(text: bytes, qual_offset: int = 33):
+    """Interleaved paired FASTQ text -> merge_reads' PackedReads (merged read + "N" mate, or both mates) as
+    (bytes, offsets, stats {pairs, merged, ambiguous, overlap_bases}), or raises FastqError where the reference
+    DIEs (orc_merge_fastq: merge_reads.cpp:237-588 + PackedRead ctor)."""
+    n = len(text)
+    out = np.empty(max(n, 1), dtype=np.uint8)
+    offs = np.empty(n // 6 + 4, dtype=np.uint64)
+    stats = np.zeros(4, dtype=np.uint64)
+    err = np.zeros(1, dtype=np.uint64)
+    r = oracle().orc_merge_fastq(text, n, qual_offset, out.ctypes.data, offs.ctypes.data, stats.ctypes.data,
+                                 err.ctypes.data)
+    if r < 0:
+        raise FastqError(FQ_KINDS[-r], int(err[0]))
+    st = dict(zip(("pairs", "merged", "ambiguous", "overlap_bases"), (int(x) for x in stats)))
+    return out[: int(offs[r])].copy(), offs[: r + 1].copy(), st
 
 
 class FastqError(ValueError):
