@@ -428,168 +428,338 @@ __device__ __forceinline__ char fq_comp(char c) {
 // per pair: (overlap + 1) of the merge (0: not merged) | has-N << 31
 constexpr uint32_t MP_HASN = 1u << 31;
 
+// Where a pair's lines are (k_fq_pair_prep); L1 = ~0: the pair is not merged (a record or name error, which
+// is reported)
+struct PairDesc {
+  uint64_t s1, q1, s2, q2;
+  uint32_t L1, L2;
+};
+
+// One lane per pair: both records' lines and the name checks (:320-321). Many lanes in flight hide the chains
+// of dependent loads that name parsing is; the merge kernel then starts from one descriptor load.
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_prep(const char *text, uint64_t n,
+                                                              const unsigned long long *line_end, uint64_t n_pairs,
+                                                              PairDesc *desc, unsigned long long *err) {
+  const uint64_t p = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x;
+  if (p >= n_pairs) return;
+  PairDesc d{0, 0, 0, 0, ~0u, 0};
+  FqRec a, b;
+  uint64_t pb1, pe1, pb2, pe2;
+  char l1, l2;
+  if (fq_rec(text, n, line_end, 2 * p, a) && fq_rec(text, n, line_end, 2 * p + 1, b) &&
+      fq_norm(text, a.idb, a.idte, pb1, pe1, l1) && fq_norm(text, b.idb, b.idte, pb2, pe2, l2)) {
+    bool same = pe1 - pb1 == pe2 - pb2;
+    for (uint64_t i = 0; same && i < pe1 - pb1; i++) {
+      char x = text[pb1 + i], y = text[pb2 + i];
+      same = (x == ' ' ? '_' : x) == (y == ' ' ? '_' : y);
+    }
+    if (!same) {
+      fq_fail(err, 2 * p + 1, FQ_E_PAIR_NAME);
+    } else if (l1 != '1' || l2 != '2') {
+      fq_fail(err, 2 * p + 1, FQ_E_PAIR_NUM);
+    } else {
+      d = PairDesc{a.sb, a.qb, b.sb, b.qb, a.L, b.L};
+    }
+  }
+  desc[p] = d;
+}
+
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   return v;
 }
 
-__global__ __launch_bounds__(FQ_THREADS) void k_fq_merge(const char *text, uint64_t n,
-                                                          const unsigned long long *line_end, uint64_t n_pairs,
-                                                          const unsigned long long *rec_offs, int qual_offset,
-                                                          char *scratch, uint32_t *pair_info,
-                                                          unsigned long long *out_len, unsigned long long *err,
-                                                          unsigned long long *stats) {
-  const uint64_t p = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x;
+// One wave per pair (grid-stride). The pair is staged in the wave's LDS: mate 1's bases and qualities, mate
+// 2 reverse-complemented (RC) with its reversed qualities (RQ). Then
+//   1. fast filter (fast_count_mismatches, :183-230): lane t takes the offsets t, t + 64, ..., comparing four
+//      bytes at a time with an early exit; a ballot keeps the offsets with at most error_max_mismatch;
+//   2. the kept offsets, in increasing order, get the reference's base-by-base scan (:357-427), evaluated across
+//      the lanes: per position its match / mismatch / N increments, wave prefix sums of them find the position
+//      where the reference breaks (a second both-N, more than 3 N, too many mismatches, a bad quality), and the
+//      error-probability sum is added up position by position in the reference's order (double, two adds per
+//      N mismatch as there);
+//   3. the good / weak / ambiguous bookkeeping of :428-444 runs over those verdicts in order.
+// A scan's effect on qualities (an N's quality becomes the offset) does not change any later verdict: the
+// quality read at an N is always the one just set. It does change the output, so it is applied in LDS in scan
+// order and the qualities of pairs with an N go to the scratch for k_fq_merge_pack.
+constexpr int MG_WAVES = 4;
+constexpr int MG_MAXL = 2048;  // > FQ_MAX_LINE + 4 (unaligned 4-byte reads past a line stay inside)
+
+__device__ __forceinline__ uint32_t lds_u32(const char *p) {  // 4 bytes from any LDS byte address
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3u);
+  return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+}
+// 0xff in every byte of w equal to v, 0 elsewhere
+__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t w, uint32_t v) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) m |= (((w >> (8 * i)) & 0xffu) == v) ? 0xffu << (8 * i) : 0u;
+  return m;
+}
+// 4-bit codes of the four characters of w: A C G T N -> 0..4, anything else 15 (16 bits)
+__device__ __forceinline__ uint32_t nib4(uint32_t w) {
+  uint32_t out = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t c = (w >> (8 * i)) & 0xffu;
+    const uint32_t v = c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : c == 'N' ? 4u : 15u;
+    out |= v << (4 * i);
+  }
+  return out;
+}
+// fq_comp of every byte of w (A<->T, C<->G, N and IUPAC -> N, anything else 0)
+__device__ __forceinline__ uint32_t comp4(uint32_t w) {
+  constexpr uint32_t NI = (1u << ('N' - 'A')) | (1u << ('U' - 'A')) | (1u << ('R' - 'A')) | (1u << ('Y' - 'A')) |
+                          (1u << ('K' - 'A')) | (1u << ('M' - 'A')) | (1u << ('S' - 'A')) | (1u << ('W' - 'A')) |
+                          (1u << ('B' - 'A')) | (1u << ('D' - 'A')) | (1u << ('H' - 'A')) | (1u << ('V' - 'A'));
+  uint32_t out = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t c = (w >> (8 * i)) & 0xffu, k = c - 'A';
+    const uint32_t r = (c == 'A' || c == 'T') ? 149u - c : (c == 'C' || c == 'G') ? 138u - c
+                       : (k < 26u && ((NI >> k) & 1u)) ? (uint32_t)'N' : 0u;
+    out |= r << (8 * i);
+  }
+  return out;
+}
+__device__ __forceinline__ int nz_bytes(uint32_t x) {  // bytes of x that are not zero
+  x |= x >> 4;
+  x |= x >> 2;
+  x |= x >> 1;
+  return __popc(x & 0x01010101u);
+}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(v, d, 64);
+    if (lane >= d) v += y;
+  }
+  return v;
+}
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(64 * MG_WAVES, 4) void k_fq_merge(const char *text, const PairDesc *desc, uint64_t n_pairs,
+                                                             const unsigned long long *rec_offs, int qual_offset,
+                                                             char *scratch, uint32_t *pair_info,
+                                                             unsigned long long *out_len, unsigned long long *err,
+                                                             unsigned long long *stats) {
+  __shared__ __align__(16) char lds[MG_WAVES][4][MG_MAXL + 16];
+  // the bases again as 4-bit codes, 16 per word (A C G T N = 0..4, any other mate-1 character 15: it equals
+  // no mate-2 base), for the fast filter's 16-base compares
+  __shared__ __align__(16) uint64_t nib[MG_WAVES][2][MG_MAXL / 16 + 4];
+  // Q2Perror in LDS: a mismatch's table reads are divergent, and from constant memory each was a memory round
+  // trip on the scan's critical path
+  __shared__ double q2p[81];
+  for (int t = threadIdx.x; t < 81; t += blockDim.x) q2p[t] = Q2P_TAB[t];
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  char *S1 = lds[w][0], *RC = lds[w][1], *Q1 = lds[w][2], *RQ = lds[w][3];
+  uint64_t *S1n = nib[w][0], *RCn = nib[w][1];
+  const int16_t MIN_OVERLAP = 12, EXTRA_TEST_OVERLAP = 2, MAX_MISMATCHES = 3, EXTRA_PER_1000 = 150;
+  const double MAX_PERROR = 0.025;
   uint64_t merged = 0, ambiguous = 0, ov_bases = 0;
-  if (p == n_pairs) out_len[2 * n_pairs] = 0;  // the scan's last element
-  if (p < n_pairs) {
-    pair_info[p] = 0;
-    out_len[2 * p] = 0;
-    out_len[2 * p + 1] = 0;
-    FqRec a, b;
-    uint64_t pb1, pe1, pb2, pe2;
-    char l1, l2;
-    if (fq_rec(text, n, line_end, 2 * p, a) && fq_rec(text, n, line_end, 2 * p + 1, b) &&
-        fq_norm(text, a.idb, a.idte, pb1, pe1, l1) && fq_norm(text, b.idb, b.idte, pb2, pe2, l2)) {
-      bool same = pe1 - pb1 == pe2 - pb2;
-      for (uint64_t i = 0; same && i < pe1 - pb1; i++) {
-        char x = text[pb1 + i], y = text[pb2 + i];
-        x = x == ' ' ? '_' : x;
-        y = y == ' ' ? '_' : y;
-        same = x == y;
+  const uint64_t n_waves = (uint64_t)gridDim.x * MG_WAVES;
+  if (blockIdx.x == 0 && threadIdx.x == 0) out_len[2 * n_pairs] = 0;  // the scan's last element
+  for (uint64_t p = (uint64_t)blockIdx.x * MG_WAVES + w; p < n_pairs; p += n_waves) {
+    if (lane == 0) {
+      pair_info[p] = 0;
+      out_len[2 * p] = 0;
+      out_len[2 * p + 1] = 0;
+    }
+    const PairDesc d = desc[p];
+    if (d.L1 == ~0u) continue;  // (its error is reported)
+    const int L1 = (int)d.L1, L2 = (int)d.L2;
+    const char *s1 = text + d.s1, *tq1 = text + d.q1, *s2 = text + d.s2, *tq2 = text + d.q2;
+    // staging, four bytes per lane and step (one load round trip for reads up to 256 bases); a step may read
+    // up to three bytes before or after a line, which are text (the id line before it, the newline after it)
+    bool bad2 = false, hasN = false;
+    for (int x0 = 4 * lane; x0 < L1; x0 += 256) {
+      const uint32_t c = load4(s1, (uint32_t)x0), q = load4(tq1, (uint32_t)x0);
+      *(uint32_t *)(S1 + x0) = c;
+      *(uint32_t *)(Q1 + x0) = q;
+      ((uint16_t *)S1n)[x0 >> 2] = nib4(c);
+      const int nb = min(4, L1 - x0);
+      hasN |= (byte_eq_mask(c, 'N') & (0xffffffffu >> (32 - 8 * nb))) != 0;
+    }
+    for (int j0 = 4 * lane; j0 < L2; j0 += 256) {  // RC[j] = comp(s2[L2 - 1 - j]), RQ[j] = tq2[L2 - 1 - j]
+      const int a0 = L2 - 4 - j0;  // s2 bytes a0 .. a0 + 3 are RC[j0 + 3] .. RC[j0]
+      const uint32_t c = comp4(__builtin_bswap32(load4(s2 + a0, 0u))), q = __builtin_bswap32(load4(tq2 + a0, 0u));
+      *(uint32_t *)(RC + j0) = c;
+      *(uint32_t *)(RQ + j0) = q;
+      ((uint16_t *)RCn)[j0 >> 2] = nib4(c);
+      const int nb = min(4, L2 - j0);
+      const uint32_t valid = 0xffffffffu >> (32 - 8 * nb);
+      bad2 |= (byte_eq_mask(c, 0) & valid) != 0;
+      hasN |= (byte_eq_mask(c, 'N') & valid) != 0;
+    }
+    wave_sync_lds();
+    if (lane < 4) {  // the fast filter's 4-byte reads past the lines see fixed bytes
+      S1[L1 + lane] = 0;
+      RC[L2 + lane] = 1;
+    }
+    wave_sync_lds();
+    if (__ballot(bad2)) {
+      if (lane == 0) fq_fail(err, 2 * p + 1, FQ_E_CHAR2);
+      continue;
+    }
+    hasN = __ballot(hasN) != 0;
+    const int16_t len = (int16_t)(L2 < L1 ? L2 : L1);
+    const int16_t start_i = (len == (int16_t)L1) ? 0 : (int16_t)(L1 - len);
+    const int n_off = len - MIN_OVERLAP + EXTRA_TEST_OVERLAP;  // offsets i in [0, n_off)
+    int16_t found_i = -1, best_i = -1;
+    bool abort_merge = false, qbad = false, stop = false;
+    for (int r0 = 0; r0 < n_off && !stop; r0 += 64) {
+      // 1. fast filter of offsets r0 .. r0 + 63
+      const int i = r0 + lane;
+      bool pass = false;
+      if (i < n_off) {
+        const int ov = len - i;
+        const int emax = (MAX_MISMATCHES + (EXTRA_PER_1000 * ov / 1000)) * 4 / 3 + 1;
+        // 16 bases per step: mate 1 from base start_i + i on (a funnel of two code words) against mate 2's
+        const int b0 = 4 * (start_i + i), k0 = b0 >> 6, sh = b0 & 63;
+        int mm = 0;
+        for (int j = 0; j < ov && mm <= emax; j += 16) {
+          const int k = k0 + (j >> 4);
+          const uint64_t a = (S1n[k] >> sh) | ((S1n[k + 1] << 1) << (63 - sh));
+          uint64_t x = a ^ RCn[j >> 4];
+          x = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111111111111111ull;
+          const int left = ov - j;  // bases of this step inside the overlap
+          if (left < 16) x &= (1ull << (4 * left)) - 1;
+          mm += __popcll(x);
+        }
+        pass = mm <= emax;
       }
-      if (!same) {
-        fq_fail(err, 2 * p + 1, FQ_E_PAIR_NAME);
-      } else if (l1 != '1' || l2 != '2') {
-        fq_fail(err, 2 * p + 1, FQ_E_PAIR_NUM);
-      } else {
-        const int L1 = (int)a.L, L2 = (int)b.L;
-        const char *s1 = text + a.sb, *tq1 = text + a.qb, *s2 = text + b.sb, *tq2 = text + b.qb;
-        bool hasN = false, bad2 = false;
-        for (int j = 0; j < L2; j++) {
-          const char c = fq_comp(s2[j]);
-          bad2 |= c == 0;
-          hasN |= c == 'N';
-        }
-        for (int x = 0; x < L1; x++) hasN |= s1[x] == 'N';
-        if (bad2) {
-          fq_fail(err, 2 * p + 1, FQ_E_CHAR2);
-        } else {
-          char *cq1 = scratch + rec_offs[2 * p], *crq2 = scratch + rec_offs[2 * p + 1];
-          if (hasN) {
-            for (int x = 0; x < L1; x++) cq1[x] = tq1[x];
-            for (int j = 0; j < L2; j++) crq2[j] = tq2[L2 - 1 - j];
+      uint64_t kept = __ballot(pass);
+      // 2. + 3. the kept offsets in order
+      while (kept && !stop) {
+        const int io = r0 + __ffsll((long long)kept) - 1;
+        kept &= kept - 1;
+        const int16_t overlap = len - (int16_t)io;
+        const int16_t this_max = MAX_MISMATCHES + (EXTRA_PER_1000 * overlap / 1000);
+        const int16_t err_max = this_max * 4 / 3 + 1;
+        const int base = start_i + io;
+        uint32_t cM = 0, cN = 0, cB = 0, matches = 0;
+        int jb = -1, ev = 0;  // break position; 1 too many mismatches, 2 abort (N rules), 3 bad quality
+        double perror = 0.0;
+        for (int c0 = 0; c0 < overlap && jb < 0; c0 += 64) {
+          const int j = c0 + lane;
+          const bool in = j < overlap;
+          const char ps = in ? S1[base + j] : 'A', rs = in ? RC[j] : 'A';
+          const bool eq = in && ps == rs, both = eq && ps == 'N', mis = in && ps != rs;
+          const bool nmis = mis && (ps == 'N' || rs == 'N');
+          const uint8_t qa = ps == 'N' ? 0 : (uint8_t)(Q1[base + j] - qual_offset);
+          const uint8_t qb = rs == 'N' ? 0 : (uint8_t)(RQ[j] - qual_offset);
+          const bool bq = mis && (qa >= 81 || qb >= 81);
+          const uint32_t M = cM + wave_incl_scan(mis ? 1u + (uint32_t)nmis : 0u, lane);
+          const uint32_t NC = cN + wave_incl_scan(both ? 2u : (uint32_t)nmis, lane);
+          const uint32_t B = cB + wave_incl_scan(both ? 1u : 0u, lane);
+          // the reference's checks at j, in its order: a second both-N (in the match branch), a bad quality (in
+          // the mismatch branch), then more than 3 N, then too many mismatches
+          const int e = !in ? 0 : (both && B >= 2) ? 2 : bq ? 3 : NC > 3 ? 2 : (int)M > err_max ? 1 : 0;
+          const uint64_t evm = __ballot(e != 0);
+          const int f = evm ? __ffsll((long long)evm) - 1 : 64;
+          const uint64_t upto = f < 64 ? (f == 63 ? ~0ull : ((2ull << f) - 1)) : ~0ull;  // lanes <= f
+          matches += (uint32_t)__popcll(__ballot(eq) & upto);
+          // the error-probability sum, mismatch by mismatch in order
+          double t1 = 0.0, t2 = 0.0;
+          if (mis && !bq) {
+            t1 = ps == 'N' ? q2p[qb] : rs == 'N' ? q2p[qa] : 0.0;
+            const uint8_t dq = qa > qb ? qa - qb : qb - qa;
+            t2 = dq <= 2 ? 0.5 : q2p[dq];
           }
-          auto Q1 = [&](int x) -> char { return hasN ? cq1[x] : tq1[x]; };
-          auto RQ2 = [&](int j) -> char { return hasN ? crq2[j] : tq2[L2 - 1 - j]; };
-          auto RC2 = [&](int j) -> char { return fq_comp(s2[L2 - 1 - j]); };
-          const int16_t MIN_OVERLAP = 12, EXTRA_TEST_OVERLAP = 2, MAX_MISMATCHES = 3, EXTRA_PER_1000 = 150;
-          const double MAX_PERROR = 0.025;
-          int abort_merge = 0;
-          bool qbad = false;
-          const int16_t len = (int16_t)(L2 < L1 ? L2 : L1);
-          const int16_t start_i = (len == (int16_t)L1) ? 0 : (int16_t)(L1 - len);
-          int16_t found_i = -1, best_i = -1;
-          for (int16_t i = 0; i < len - MIN_OVERLAP + EXTRA_TEST_OVERLAP && !qbad; i++) {
-            if (abort_merge) break;
-            const int16_t overlap = len - i;
-            const int16_t this_max = MAX_MISMATCHES + (EXTRA_PER_1000 * overlap / 1000);
-            const int16_t err_max = this_max * 4 / 3 + 1;
-            int16_t fast = 0;  // fast_count_mismatches (:183-230): the count, or more than err_max
-            for (int16_t j = 0; j < overlap && fast <= err_max; j++) fast += s1[start_i + i + j] != RC2(j);
-            if (fast > err_max) continue;
-            int16_t matches = 0, mismatches = 0, bothNs = 0, Ncount = 0, checked = 0;
-            double perror = 0.0;
-            for (int16_t j = 0; j < overlap; j++) {
-              checked++;
-              const int x = start_i + i + j;
-              const char ps = s1[x], rs = RC2(j);
-              if (ps == rs) {
-                matches++;
-                if (ps == 'N') {
-                  Ncount += 2;
-                  if (bothNs++) {
-                    abort_merge++;
-                    ambiguous++;
-                    break;
-                  }
-                }
-              } else {
-                mismatches++;
-                if (ps == 'N') {  // an N zeroes its own quality (hasN holds: the copies are in the scratch)
-                  mismatches++;
-                  Ncount++;
-                  cq1[x] = (char)qual_offset;
-                } else if (rs == 'N') {
-                  Ncount++;
-                  mismatches++;
-                  crq2[j] = (char)qual_offset;
-                }
-                const uint8_t qa = (uint8_t)(Q1(x) - qual_offset), qb = (uint8_t)(RQ2(j) - qual_offset);
-                if (qa >= 81 || qb >= 81) {  // the invalid-quality DIE of :409-413
-                  qbad = true;
-                  break;
-                }
-                if (ps == 'N')
-                  perror += Q2P_TAB[qb];
-                else if (rs == 'N')
-                  perror += Q2P_TAB[qa];
-                const uint8_t dq = qa > qb ? qa - qb : qb - qa;
-                perror += dq <= 2 ? 0.5 : Q2P_TAB[dq];
-              }
-              if (Ncount > 3) {
-                abort_merge++;
-                ambiguous++;
-                break;
-              }
-              if (mismatches > err_max) break;
-            }
-            if (qbad) break;
-            int16_t match_thres = overlap - this_max;
-            if (match_thres < MIN_OVERLAP) match_thres = MIN_OVERLAP;
-            if (matches >= match_thres && checked == overlap && mismatches <= this_max && perror / overlap <= MAX_PERROR) {
-              if (best_i < 0 && found_i < 0) {
-                best_i = i;
-              } else {
-                ambiguous++;
-                best_i = -1;
-                break;
-              }
-            } else if (checked == overlap && mismatches <= err_max && perror / overlap <= MAX_PERROR * 4 / 3) {
-              found_i = i;
-              if (best_i >= 0) {
-                ambiguous++;
-                best_i = -1;
-                break;
-              }
-            }
+          uint64_t mm = __ballot(mis && !bq) & upto;
+          const uint64_t nm = __ballot(nmis);
+          while (mm) {
+            const int l = __ffsll((long long)mm) - 1;
+            mm &= mm - 1;
+            if ((nm >> l) & 1ull) perror += __shfl(t1, l, 64);
+            perror += __shfl(t2, l, 64);
           }
-          if (qbad) {
-            fq_fail(err, 2 * p + 1, FQ_E_QUAL);
+          // the scan's quality effects (an N's quality := the offset), in LDS for the output
+          if (nmis && j <= c0 + f) {
+            if (ps == 'N')
+              Q1[base + j] = (char)qual_offset;
+            else
+              RQ[j] = (char)qual_offset;
+          }
+          if (f < 64) {
+            jb = c0 + f;
+            ev = __shfl(e, f, 64);
+            cM = __shfl(M, f, 64);
           } else {
-            uint32_t info = hasN ? MP_HASN : 0u;
-            if (best_i >= 0 && !abort_merge) {
-              const int ov = len - best_i;
-              info |= (uint32_t)ov + 1u;
-              out_len[2 * p] = (unsigned long long)(L1 + L2 - ov);
-              out_len[2 * p + 1] = 1;
-              merged = 1;
-              ov_bases = (uint64_t)ov;
-            } else {
-              out_len[2 * p] = (unsigned long long)L1;
-              out_len[2 * p + 1] = (unsigned long long)L2;
-            }
-            pair_info[p] = info;
+            cM = __shfl(M, 63, 64);
+            cN = __shfl(NC, 63, 64);
+            cB = __shfl(B, 63, 64);
           }
         }
+        wave_sync_lds();
+        if (ev == 3) {
+          qbad = true;
+          stop = true;
+          break;
+        }
+        const int16_t checked = jb >= 0 ? (int16_t)(jb + 1) : overlap;
+        const int16_t mismatches = (int16_t)cM;
+        if (ev == 2) {
+          abort_merge = true;
+          ambiguous++;
+        }
+        int16_t match_thres = overlap - this_max;
+        if (match_thres < MIN_OVERLAP) match_thres = MIN_OVERLAP;
+        if ((int16_t)matches >= match_thres && checked == overlap && mismatches <= this_max &&
+            perror / overlap <= MAX_PERROR) {
+          if (best_i < 0 && found_i < 0) {
+            best_i = (int16_t)io;
+          } else {
+            ambiguous++;
+            best_i = -1;
+            stop = true;
+          }
+        } else if (checked == overlap && mismatches <= err_max && perror / overlap <= MAX_PERROR * 4 / 3) {
+          found_i = (int16_t)io;
+          if (best_i >= 0) {
+            ambiguous++;
+            best_i = -1;
+            stop = true;
+          }
+        }
+        if (abort_merge) stop = true;  // the next offset's "if (abort_merge) break"
       }
     }
+    if (qbad) {
+      if (lane == 0) fq_fail(err, 2 * p + 1, FQ_E_QUAL);
+      continue;
+    }
+    uint32_t info = hasN ? MP_HASN : 0u;
+    if (best_i >= 0 && !abort_merge) {
+      const int ov = len - best_i;
+      info |= (uint32_t)ov + 1u;
+      if (lane == 0) {
+        out_len[2 * p] = (unsigned long long)(L1 + L2 - ov);
+        out_len[2 * p + 1] = 1;
+      }
+      merged++;
+      ov_bases += (uint64_t)ov;
+    } else if (lane == 0) {
+      out_len[2 * p] = (unsigned long long)L1;
+      out_len[2 * p + 1] = (unsigned long long)L2;
+    }
+    if (lane == 0) pair_info[p] = info;
+    if (hasN) {  // the qualities as the scan left them, for k_fq_merge_pack
+      char *cq1 = scratch + rec_offs[2 * p], *crq2 = scratch + rec_offs[2 * p + 1];
+      for (int x = lane; x < L1; x += 64) cq1[x] = Q1[x];
+      for (int j = lane; j < L2; j += 64) crq2[j] = RQ[j];
+    }
+    wave_sync_lds();  // the next pair overwrites the wave's LDS
   }
-  merged = wave_sum64(merged);
-  ambiguous = wave_sum64(ambiguous);
-  ov_bases = wave_sum64(ov_bases);
-  if ((threadIdx.x & 63) == 0 && (merged | ambiguous)) {
+  if (lane == 0 && (merged | ambiguous)) {
     atomicAdd(&stats[1], (unsigned long long)merged);
     atomicAdd(&stats[2], (unsigned long long)ambiguous);
     atomicAdd(&stats[3], (unsigned long long)ov_bases);
@@ -605,70 +775,89 @@ __device__ __forceinline__ uint8_t fq_byte(char c, char q, int qual_offset, bool
   return (uint8_t)((code & 7) | (uint8_t)((unsigned char)v << 3));
 }
 
-__global__ __launch_bounds__(FQ_THREADS) void k_fq_merge_pack(const char *text, uint64_t n,
-                                                               const unsigned long long *line_end, uint64_t n_pairs,
-                                                               const unsigned long long *rec_offs,
-                                                               const char *scratch, const uint32_t *pair_info,
-                                                               const unsigned long long *out_offs, int qual_offset,
-                                                               uint8_t *out, unsigned long long *err) {
-  const uint64_t o = (uint64_t)blockIdx.x * (FQ_THREADS / FQ_GROUP) + (threadIdx.x / FQ_GROUP);
-  const int gl = threadIdx.x % FQ_GROUP;
-  if (o >= 2 * n_pairs) return;
-  const uint64_t p = o >> 1;
-  const int mate = (int)(o & 1);
-  const uint64_t ob = out_offs[o];
-  const int Lo = (int)(out_offs[o + 1] - ob);
-  if (Lo == 0) return;
-  const uint32_t info = pair_info[p];
-  const int ov = (int)(info & ~MP_HASN) - 1;  // -1: not merged
-  const bool hasN = (info & MP_HASN) != 0;
-  uint8_t *dst = out + ob;
-  if (ov >= 0 && mate == 1) {  // the dummy mate "N" with quality qual_offset
-    if (gl == 0) dst[0] = 4;
-    return;
-  }
-  FqRec a, b;
-  if (!fq_rec(text, n, line_end, 2 * p, a) || !fq_rec(text, n, line_end, 2 * p + 1, b)) return;
-  const int L1 = (int)a.L, L2 = (int)b.L;
-  const char *s1 = text + a.sb, *tq1 = text + a.qb, *s2 = text + b.sb, *tq2 = text + b.qb;
-  const char *cq1 = scratch + rec_offs[2 * p], *crq2 = scratch + rec_offs[2 * p + 1];
-  bool bad = false;
-  if (mate == 1) {  // mate 2 as read
-    for (int x = gl; x < Lo; x += FQ_GROUP) dst[x] = fq_byte(s2[x], tq2[x], qual_offset, bad);
-    return;  // (its characters were checked by the revcomp of k_fq_merge)
-  }
-  const int st = L1 - (ov >= 0 ? ov : 0);  // the overlap is mate 1's last ov bases
+// One wave per pair (grid-stride), four output bytes per lane and step: the pair's output reads from its
+// descriptor in one round of loads. Merged read (x < L1 - ov: mate 1; the overlap: the higher-quality base,
+// :449-469; then the rest of mate 2 reverse-complemented, :472-473) + the dummy "N", or both mates as read.
+__global__ __launch_bounds__(64 * MG_WAVES) void k_fq_merge_pack(const char *text, const PairDesc *desc, uint64_t n_pairs,
+                                                                  const unsigned long long *rec_offs,
+                                                                  const char *scratch, const uint32_t *pair_info,
+                                                                  const unsigned long long *out_offs, int qual_offset,
+                                                                  uint8_t *out, unsigned long long *err) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int max_match_qual = 41 + qual_offset;
-  for (int x = gl; x < Lo; x += FQ_GROUP) {
-    char c, q;
-    if (x < L1) {
-      c = s1[x];
-      q = hasN ? cq1[x] : tq1[x];
-      if (ov >= 0 && x >= st) {  // :449-469
-        const int j = x - st;
-        const char rc = fq_comp(s2[L2 - 1 - j]), rq = hasN ? crq2[j] : tq2[L2 - 1 - j];
-        if (c == rc) {
-          const uint16_t nq = (uint16_t)(q + rq - qual_offset);
-          q = (char)(nq > max_match_qual ? max_match_qual : nq);
-        } else {
-          uint8_t nq;
-          if (q < rq) {
-            nq = (uint8_t)(rq - q + qual_offset);
-            c = rc;
-          } else {
-            nq = (uint8_t)(q - rq + qual_offset);
-          }
-          q = (char)(nq > 2 + qual_offset ? nq : 2 + qual_offset);
-        }
+  for (uint64_t p = (uint64_t)blockIdx.x * MG_WAVES + w; p < n_pairs; p += (uint64_t)gridDim.x * MG_WAVES) {
+    const PairDesc d = desc[p];
+    if (d.L1 == ~0u) continue;
+    const uint32_t info = pair_info[p];
+    const int ov = (int)(info & ~MP_HASN) - 1;  // -1: not merged
+    const bool hasN = (info & MP_HASN) != 0;
+    const int L1 = (int)d.L1, L2 = (int)d.L2;
+    const char *s1 = text + d.s1, *tq1 = text + d.q1, *s2 = text + d.s2, *tq2 = text + d.q2;
+    const char *cq1 = scratch + rec_offs[2 * p], *crq2 = scratch + rec_offs[2 * p + 1];
+    uint8_t *dst0 = out + out_offs[2 * p], *dst1 = out + out_offs[2 * p + 1];
+    const int Lo0 = ov >= 0 ? L1 + L2 - ov : L1, st = ov >= 0 ? L1 - ov : L1;
+    bool bad = false;
+    for (int x0 = 4 * lane; x0 < Lo0; x0 += 256) {
+      const uint32_t cs = x0 < L1 ? load4(s1 + x0, 0u) : 0u;
+      const uint32_t cq = x0 < L1 ? load4((hasN ? cq1 : tq1) + x0, 0u) : 0u;
+      uint32_t rc = 0, rq = 0;
+      const int jj = x0 - st;  // RC index of output byte x0
+      if (ov >= 0 && jj > -4) {
+        rc = comp4(__builtin_bswap32(load4(s2 + (L2 - 4 - jj), 0u)));
+        // (the scratch copy is in RC order; before its start, shift instead of reading before the buffer)
+        rq = hasN ? (jj >= 0 ? load4(crq2 + jj, 0u) : load4(crq2, 0u) << (8 * -jj))
+                  : __builtin_bswap32(load4(tq2 + (L2 - 4 - jj), 0u));
       }
-    } else {  // the rest of rc_seq2 (:472-473)
-      const int j = x - L1 + ov;
-      c = fq_comp(s2[L2 - 1 - j]);
-      q = hasN ? crq2[j] : tq2[L2 - 1 - j];
+      uint32_t ob = 0;
+      const int nb = min(4, Lo0 - x0);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int x = x0 + i;
+        char c = (char)(cs >> (8 * i)), q = (char)(cq >> (8 * i));
+        const char r = (char)(rc >> (8 * i)), rqq = (char)(rq >> (8 * i));
+        if (ov >= 0 && x >= st) {
+          if (x < L1) {  // :449-469
+            if (c == r) {
+              const uint16_t nq = (uint16_t)(q + rqq - qual_offset);
+              q = (char)(nq > max_match_qual ? max_match_qual : nq);
+            } else {
+              uint8_t nq;
+              if (q < rqq) {
+                nq = (uint8_t)(rqq - q + qual_offset);
+                c = r;
+              } else {
+                nq = (uint8_t)(q - rqq + qual_offset);
+              }
+              q = (char)(nq > 2 + qual_offset ? nq : 2 + qual_offset);
+            }
+          } else {
+            c = r;
+            q = rqq;
+          }
+        }
+        bool bb = false;
+        const uint8_t v = fq_byte(c, q, qual_offset, bb);
+        bad |= bb && i < nb;
+        ob |= (uint32_t)v << (8 * i);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (i < nb) dst0[x0 + i] = (uint8_t)(ob >> (8 * i));
     }
-    dst[x] = fq_byte(c, q, qual_offset, bad);
+    if (ov >= 0) {
+      if (lane == 0) dst1[0] = 4;  // the dummy mate "N" with quality qual_offset
+    } else {
+      for (int x0 = 4 * lane; x0 < L2; x0 += 256) {  // mate 2 as read (its bases passed the revcomp check)
+        const uint32_t cs = load4(s2 + x0, 0u), cq = load4(tq2 + x0, 0u);
+        const int nb = min(4, L2 - x0);
+        bool bb = false;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (i < nb) dst1[x0 + i] = fq_byte((char)(cs >> (8 * i)), (char)(cq >> (8 * i)), qual_offset, bb);
+      }
+    }
+    if (__ballot(bad) && lane == 0) fq_fail(err, 2 * p + 1, FQ_E_CHAR1);  // mate 1's (or the merged) PackedRead
   }
-  if (bad) fq_fail(err, 2 * p + 1, FQ_E_CHAR1);  // PackedRead of mate 1 (or the merged read) DIEs
 }
 
 }  // namespace
@@ -705,23 +894,34 @@ hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long l
   return hipGetLastError();
 }
 
+size_t fq_pair_desc_bytes(uint64_t n_pairs) { return (size_t)n_pairs * sizeof(PairDesc) + 64; }
+
 hipError_t launch_fq_merge(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
-                           const unsigned long long *rec_offs, int qual_offset, char *scratch, uint32_t *pair_info,
-                           unsigned long long *out_len, unsigned long long *err, unsigned long long *stats,
-                           hipStream_t s) {
-  k_fq_merge<<<dim3((unsigned)((n_pairs + 1 + FQ_THREADS - 1) / FQ_THREADS)), dim3(FQ_THREADS), 0, s>>>(
-      text, n, line_end, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats);
+                           const unsigned long long *rec_offs, int qual_offset, char *scratch, void *desc_buf,
+                           uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
+                           unsigned long long *stats, hipStream_t s) {
+  PairDesc *desc = (PairDesc *)desc_buf;
+  if (n_pairs) {
+    k_fq_pair_prep<<<dim3((unsigned)((n_pairs + FQ_THREADS - 1) / FQ_THREADS)), dim3(FQ_THREADS), 0, s>>>(
+        text, n, line_end, n_pairs, desc, err);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  // grid-stride over the pairs, one wave each; enough waves to fill the chip several times over
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n_pairs + MG_WAVES - 1) / MG_WAVES, 16384));
+  k_fq_merge<<<dim3((unsigned)blocks), dim3(64 * MG_WAVES), 0, s>>>(text, desc, n_pairs, rec_offs, qual_offset,
+                                                                      scratch, pair_info, out_len, err, stats);
   return hipGetLastError();
 }
 
-hipError_t launch_fq_merge_pack(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
+hipError_t launch_fq_merge_pack(const char *text, const void *desc_buf, uint64_t n_pairs,
                                 const unsigned long long *rec_offs, const char *scratch, const uint32_t *pair_info,
                                 const unsigned long long *out_offs, int qual_offset, uint8_t *out,
                                 unsigned long long *err, hipStream_t s) {
   if (!n_pairs) return hipSuccess;
-  const uint64_t per = FQ_THREADS / FQ_GROUP;
-  k_fq_merge_pack<<<dim3((unsigned)((2 * n_pairs + per - 1) / per)), dim3(FQ_THREADS), 0, s>>>(
-      text, n, line_end, n_pairs, rec_offs, scratch, pair_info, out_offs, qual_offset, out, err);
+  const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n_pairs + MG_WAVES - 1) / MG_WAVES, 16384));
+  k_fq_merge_pack<<<dim3((unsigned)blocks), dim3(64 * MG_WAVES), 0, s>>>(
+      text, (const PairDesc *)desc_buf, n_pairs, rec_offs, scratch, pair_info, out_offs, qual_offset, out, err);
   return hipGetLastError();
 }
 

@@ -260,11 +260,13 @@ hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long l
 // pair p = records 2p, 2p+1: verdict in pair_info, output read lengths (merged + 1, or L1, L2) in out_len
 // [2 n_pairs + 1]; stats[1..3] += merged pairs, ambiguous events, overlap bases. scratch: rec_offs[2 n_pairs]
 // bytes (quality copies of pairs with an N).
+// bytes of the per-pair line descriptors (desc_buf) of launch_fq_merge / launch_fq_merge_pack
+size_t fq_pair_desc_bytes(uint64_t n_pairs);
 hipError_t launch_fq_merge(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
-                           const unsigned long long *rec_offs, int qual_offset, char *scratch, uint32_t *pair_info,
-                           unsigned long long *out_len, unsigned long long *err, unsigned long long *stats,
-                           hipStream_t s);
-hipError_t launch_fq_merge_pack(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
+                           const unsigned long long *rec_offs, int qual_offset, char *scratch, void *desc_buf,
+                           uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
+                           unsigned long long *stats, hipStream_t s);
+hipError_t launch_fq_merge_pack(const char *text, const void *desc_buf, uint64_t n_pairs,
                                 const unsigned long long *rec_offs, const char *scratch, const uint32_t *pair_info,
                                 const unsigned long long *out_offs, int qual_offset, uint8_t *out,
                                 unsigned long long *err, hipStream_t s);

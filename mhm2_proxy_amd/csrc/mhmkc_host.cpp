@@ -164,7 +164,7 @@ struct mhmkc {
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
   DevBuf d_fq_text, d_fq_chunk, d_fq_lines, d_fq_len, d_fq_tmp, d_fq_bytes, d_fq_offs, d_fq_err;
-  DevBuf d_fq_recoffs, d_fq_scratch, d_fq_pairinfo, d_fq_stats;  // pair merging
+  DevBuf d_fq_recoffs, d_fq_scratch, d_fq_pairinfo, d_fq_stats, d_fq_desc;  // pair merging
   uint64_t fq_reads = 0, fq_bases = 0;
   int add_fastq(const char *d_text, uint64_t n, bool pairs = false);
   // contig pass (add_ctg_kmers): contigs in the PackedRead byte layout, kept on the host until finish
@@ -1486,6 +1486,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
     if ((e = grow(d_fq_recoffs, (R + 1) * 8)) != hipSuccess ||
         (e = grow(d_fq_scratch, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess ||
         (e = grow(d_fq_pairinfo, (P + 1) * 4)) != hipSuccess || (e = grow(d_fq_stats, 64)) != hipSuccess ||
+        (e = grow(d_fq_desc, mhm::fq_pair_desc_bytes(P))) != hipSuccess ||
         (e = grow(d_fq_len, (2 * P + 1) * 8)) != hipSuccess)
       return hip_fail(e, "fastq pairs");
     const size_t tmp3 = mhm::fq_scan_tmp_bytes(2 * P + 1);
@@ -1499,7 +1500,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
     e = hipMemcpyAsync(roffs, offs, (R + 1) * 8, hipMemcpyDeviceToDevice, stream);
     if (e == hipSuccess) e = hipMemsetAsync(fst, 0, 32, stream);
     if (e == hipSuccess)
-      e = mhm::launch_fq_merge(d_text, n, lend, P, roffs, cfg.qual_offset, d_fq_scratch.as<char>(),
+      e = mhm::launch_fq_merge(d_text, n, lend, P, roffs, cfg.qual_offset, d_fq_scratch.as<char>(), d_fq_desc.p,
                                d_fq_pairinfo.as<uint32_t>(), len2, err_d, fst, stream);
     if (e == hipSuccess) e = mhm::fq_scan(d_fq_tmp.p, tmp_bytes, len2, offs, 2 * P + 1, stream);
     prof_end();
@@ -1515,7 +1516,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
     st.fq_overlap_bases = hs[3];
     if ((e = grow(d_fq_bytes, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess) return hip_fail(e, "fastq bytes");
     prof_begin(MHMKC_STAGE_OTHER);
-    e = mhm::launch_fq_merge_pack(d_text, n, lend, P, roffs, d_fq_scratch.as<char>(), d_fq_pairinfo.as<uint32_t>(),
+    e = mhm::launch_fq_merge_pack(d_text, d_fq_desc.p, P, roffs, d_fq_scratch.as<char>(), d_fq_pairinfo.as<uint32_t>(),
                                   offs, cfg.qual_offset, d_fq_bytes.as<uint8_t>(), err_d, stream);
     prof_end();
   }
