@@ -545,7 +545,7 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(64 * MG_WAVES, 4) void k_fq_merge(const char *text, const PairDesc *desc, uint64_t n_pairs,
+__global__ __launch_bounds__(64 * MG_WAVES, 3) void k_fq_merge(const char *text, const PairDesc *desc, uint64_t n_pairs,
                                                              const unsigned long long *rec_offs, int qual_offset,
                                                              char *scratch, uint32_t *pair_info,
                                                              unsigned long long *out_len, unsigned long long *err,

@@ -1085,11 +1085,12 @@ struct CountLds {
 #define MHMKC_BOVERLAP 1
 #endif
 constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
-// Two-word keys take the whole miss space for one list (960 entries for 2048 records a round): with half of it
-// the first rounds of a bucket overflow the list into in-place inserts in phase A, and the waves that do them
-// hold the round barrier (k = 63: k_count 13.2 -> 12.6 ms)
+// MHMKC_BOV2=0: two-word keys take the whole miss space for one list (960 entries for 2048 records a round).
+// Before phase-A claims the double-buffered half (480) overflowed in the first rounds of a bucket into
+// in-place inserts that held the round barrier (k = 63: 13.2 -> 12.6 ms with one list); with claims a round
+// lists ~330 records and the overlapped double buffer is faster again (11.90 -> 11.64 ms).
 #ifndef MHMKC_BOV2
-#define MHMKC_BOV2 0
+#define MHMKC_BOV2 1
 #endif
 #ifndef MHMKC_BSPREAD
 #define MHMKC_BSPREAD 0

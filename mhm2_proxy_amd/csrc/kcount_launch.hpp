@@ -169,7 +169,10 @@ constexpr uint32_t CPAD = MHMKC_CPAD;  // cursor spacing in u64 words (segment i
 #define MHMKC_CSPLIT 1
 #endif
 constexpr int C_SPLIT = MHMKC_CSPLIT;
-constexpr int C_THREADS = 1024 / C_SPLIT;
+#ifndef MHMKC_CTHREADS
+#define MHMKC_CTHREADS (1024 / MHMKC_CSPLIT)
+#endif
+constexpr int C_THREADS = MHMKC_CTHREADS;
 constexpr size_t C_LDS = 163840 / C_SPLIT;
 
 // Hash bits stored in a packed record next to the ext code (bits [6, 6 + hbits) of the last word).
