@@ -295,6 +295,139 @@ __device__ __forceinline__ void walk_windows(const uint64_t *fwd, const uint32_t
   }
 }
 
+// The per-thread span of walk_windows, for the mixed-record walks below: the bits of the W windows' neighbours
+// and read starts, the last read start before the span and the data bounds (see walk_windows).
+template <int NL>
+struct WalkSpan {
+  int lp0, last, end, beg;
+  uint64_t incoming;                 // the base entering at window i: bits 63 - 2i, 62 - 2i
+  uint32_t gl_bits, gr_bits, st_bits, cl;
+  __device__ __forceinline__ WalkSpan(const uint64_t *fwd, const uint32_t *good, const uint32_t *start, uint32_t tile,
+                                      uint64_t n_bases, uint32_t head, int k) {
+    constexpr int T = kTile<NL>(), W = T / E_THREADS;
+    lp0 = 32 + W * (int)threadIdx.x;
+    incoming = codes64(fwd, lp0 + k);
+    gl_bits = bits32(good, lp0 - 1);
+    gr_bits = bits32(good, lp0 + k);
+    st_bits = bits32(start, lp0 + k);
+    last = lp0 - 1;
+    const int q0 = lp0, q1 = lp0 + k - 1;
+    for (int g = q1 >> 5; g >= (q0 >> 5); g--) {
+      uint32_t m = start[g];
+      const int lo = max(q0, g * 32), hi = min(q1, g * 32 + 31);
+      m &= (~0u >> (lo - g * 32)) & (~0u << (31 - (hi - g * 32)));
+      if (m) {
+        last = g * 32 + 31 - (__ffs(m) - 1);
+        break;
+      }
+    }
+    const int64_t end64 = (int64_t)n_bases - ((int64_t)tile * T - 32);
+    end = end64 > (int64_t)(1 << 30) ? (1 << 30) : (int)end64;
+    beg = tile == 0 ? (int)head + 32 : -(1 << 30);
+    cl = (uint32_t)(codes64(fwd, lp0 - 1) >> 62);
+  }
+  static __device__ __forceinline__ uint64_t codes64(const uint64_t *fwd, int q) {  // 32 codes from q, first on top
+    const int g = q >> 5, sh = (q & 31) * 2;
+    uint64_t v = fwd[g];
+    if (sh) v = (v << sh) | (fwd[g + 1] >> (64 - sh));
+    return v;
+  }
+  static __device__ __forceinline__ uint32_t bits32(const uint32_t *a, int q) {  // 32 bits from q, first in bit 31
+    const int g = q >> 5, sh = q & 31;
+    uint32_t v = a[g];
+    if (sh) v = (v << sh) | (a[g + 1] >> (32 - sh));
+    return v;
+  }
+  // window i: the entering base (its right neighbour), the ext code in both orientations, validity
+  __device__ __forceinline__ bool step(int i, int k, uint32_t &cr, uint32_t &e_f, uint32_t &e_r) {
+    const int lp = lp0 + i;
+    cr = (uint32_t)(incoming >> (62 - 2 * i)) & 3u;
+    const bool gl = (gl_bits >> (31 - i)) & 1u, gr = (gr_bits >> (31 - i)) & 1u;
+    if ((st_bits >> (31 - i)) & 1u) last = lp + k;
+    const uint32_t l = gl ? cl : (uint32_t)EXT_NONE, r = gr ? cr : (uint32_t)EXT_NONE;
+    const uint32_t lr = gr ? cr ^ 3u : (uint32_t)EXT_NONE, rr = gl ? cl ^ 3u : (uint32_t)EXT_NONE;
+    e_f = (l << 3) | r;   // forward: (left << 3) | right
+    e_r = (lr << 3) | rr;  // reverse complement: complemented and swapped
+    return (last < lp) && (lp + k < end) && (lp > beg);
+  }
+};
+
+// Compact-record walk (10 <= k <= 21, §3.7): the windows of walk_windows with the key kept right-aligned in its
+// B = 2k bits, the form cmix takes, so no Kmer-layout word is built or shifted into the mix; the record is
+// (y below the coarse digit) << 6 | ext with y = cmix(canonical key), the bin the coarse digit (y's top cb bits).
+// Extraction is VALU-issue bound (§4): this walk issues ~40 % fewer VALU instructions per window.
+template <int W>
+__device__ __forceinline__ void walk_c32(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
+                                         uint32_t tile, uint64_t n_bases, uint32_t head, int k, int cb,
+                                         uint64_t (&rk)[W][1], uint32_t (&inf)[W]) {
+  WalkSpan<1> sp(fwd, good, start, tile, n_bases, head, k);
+  const int B = 2 * k, a = B >> 1, b = B - a, rb = B - cb;
+  const uint64_t mB = (1ull << B) - 1, rmask = (1ull << rb) - 1;
+  uint64_t fw = WalkSpan<1>::codes64(fwd, sp.lp0) >> (64 - B);
+  uint64_t rc = rev2(~fw) >> (64 - B);
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    uint32_t cr, e_f, e_r;
+    const bool valid = sp.step(i, k, cr, e_f, e_r);
+    const bool use_rc = rc < fw;
+    const uint64_t x = use_rc ? rc : fw;
+    const uint32_t e = use_rc ? e_r : e_f;
+    uint32_t R = (uint32_t)x & ((1u << a) - 1), L = (uint32_t)(x >> a);
+    cmix_lr(L, R, a, b);
+    const uint64_t y = ((uint64_t)L << a) | R;
+    rk[i][0] = ((y & rmask) << EXT_BITS) | e;
+    inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(y >> rb) : 0u;
+    asm volatile("" : "+v"(rk[i][0]), "+v"(inf[i]));
+    // roll: base lp leaves (the next window's left neighbour), cr enters
+    sp.cl = (uint32_t)(fw >> (B - 2));
+    fw = ((fw << 2) | cr) & mB;
+    rc = (rc >> 2) | ((uint64_t)(cr ^ 3u) << (B - 2));
+  }
+}
+
+// Mixed two-word walk (33 <= k <= 63, §3.7b): the 2k-bit key kept as its two k-bit halves (L = the top k bits,
+// R = the low k bits), the form m2_mix_lr takes, rolled and compared as halves; record w[0] = (L' below the coarse
+// digit) << 6 | ext, w[1] = R', bin = the coarse digit (L''s top cb bits).
+template <int W>
+__device__ __forceinline__ void walk_m2(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
+                                        uint32_t tile, uint64_t n_bases, uint32_t head, int k, int cb,
+                                        uint64_t (&rk)[W][2], uint32_t (&inf)[W]) {
+  WalkSpan<2> sp(fwd, good, start, tile, n_bases, head, k);
+  const uint64_t mk = (1ull << k) - 1;
+  const int csh = k - cb;
+  const uint64_t cmask = (1ull << csh) - 1;
+  uint64_t fL, fR, rL, rR;
+  {
+    uint64_t w[2], rw[2];
+    w[0] = WalkSpan<2>::codes64(fwd, sp.lp0);
+    w[1] = WalkSpan<2>::codes64(fwd, sp.lp0 + 32) & top_mask(k - 32);
+    revcomp<2>(w, rw, k);
+    fL = w[0] >> (64 - k);
+    fR = ((w[0] << (2 * k - 64)) | (w[1] >> (128 - 2 * k))) & mk;
+    rL = rw[0] >> (64 - k);
+    rR = ((rw[0] << (2 * k - 64)) | (rw[1] >> (128 - 2 * k))) & mk;
+  }
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    uint32_t cr, e_f, e_r;
+    const bool valid = sp.step(i, k, cr, e_f, e_r);
+    const bool use_rc = (rL < fL) | ((rL == fL) & (rR < fR));
+    uint64_t L = use_rc ? rL : fL, R = use_rc ? rR : fR;
+    const uint32_t e = use_rc ? e_r : e_f;
+    m2_mix_lr(L, R, k);
+    rk[i][0] = ((L & cmask) << EXT_BITS) | e;
+    rk[i][1] = R;
+    inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(L >> csh) : 0u;
+    asm volatile("" : "+v"(rk[i][0]), "+v"(rk[i][1]), "+v"(inf[i]));
+    // roll the halves: the 2k-bit forward key shifts left by one base, the reverse complement right
+    sp.cl = (uint32_t)(fL >> (k - 2));
+    fL = ((fL << 2) | (fR >> (k - 2))) & mk;
+    fR = ((fR << 2) | cr) & mk;
+    rR = (rR >> 2) | ((rL & 3u) << (k - 2));
+    rL = (rL >> 2) | ((uint64_t)(cr ^ 3u) << (k - 2));
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // tile index
 
@@ -558,6 +691,11 @@ constexpr bool kPStaged = MHMKC_PSTAGE != 0;
 #define MHMKC_M2WALK 0
 #endif
 constexpr bool kM2Walk = MHMKC_M2WALK != 0;
+// Mixed-record walks (walk_c32, walk_m2: the key as the mix takes it); 0 = the generic walk_windows + window_hash.
+#ifndef MHMKC_MIXWALK
+#define MHMKC_MIXWALK 1
+#endif
+constexpr bool kMixedWalk = MHMKC_MIXWALK != 0;
 #ifndef MHMKC_M2BATCH
 #define MHMKC_M2BATCH 2  // valid-window slots per branch-free block
 #endif
@@ -697,6 +835,7 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) {
   constexpr int T = kTile<NL>(), W = T / E_THREADS;
+  const int kk = p.k;
   extern __shared__ __align__(16) unsigned char smem0[];
   uint64_t *fwd;
   uint32_t *good, *start;
@@ -723,23 +862,27 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   // stored hash bits, branch-free (hbits == 0: none)
   const int hsh = p.hbits ? 64 - p.hbits : 0;
   const uint64_t hmask = p.hbits ? ~0ull : 0ull;
-  const int csh = 64 - (2 * p.k - p.coarse_bits);  // compact: keep the low 2k - cb bits of the mixed key
-  const int m2_csh = p.k - p.coarse_bits;            // mixed two-word: L' >> m2_csh = coarse digit
+  const int csh = 64 - (2 * kk - p.coarse_bits);  // compact: keep the low 2k - cb bits of the mixed key
+  const int m2_csh = kk - p.coarse_bits;            // mixed two-word: L' >> m2_csh = coarse digit
   const uint64_t m2_cmask = (1ull << m2_csh) - 1;
   uint64_t rk[W][NL];
   uint32_t inf[W];
-  if constexpr (RecKind<NL, CMP>::M2 && kM2Walk && kEStaged) {
+  if constexpr (RecKind<NL, CMP>::C32 && kMixedWalk) {
+    walk_c32<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, rk, inf);
+  } else if constexpr (RecKind<NL, CMP>::M2 && kMixedWalk && !kM2Walk) {
+    walk_m2<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, rk, inf);
+  } else if constexpr (RecKind<NL, CMP>::M2 && kM2Walk && kEStaged) {
     m2_walk_valid<W>(p, tile, fwd, good, start, area + tile_lds_bytes<NL>(), rk, inf
 #ifdef MHMKC_ESTAMP
                      , es2
 #endif
     );
   } else
-  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, p.k,
+  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk,
                    [&](int i, const uint64_t *key, uint32_t e, bool valid) {
                      if constexpr (RecKind<NL, CMP>::M2) {  // (L' below the coarse digit) << 6 | ext, R'
                        uint64_t L, R;
-                       m2_mix(key, p.k, L, R);
+                       m2_mix(key, kk, L, R);
                        rk[i][0] = ((L & m2_cmask) << EXT_BITS) | e;
                        rk[i][1] = R;
                        inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(L >> m2_csh) : 0u;
@@ -748,7 +891,7 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
                        asm volatile("" : "+v"(inf[i]));
                        return;
                      }
-                     const uint64_t h = window_hash<NL, CMP>(key, p.k);
+                     const uint64_t h = window_hash<NL, CMP>(key, kk);
 #pragma unroll
                      for (int w = 0; w < NL; w++) rk[i][w] = key[w];
                      if (CMP) {
@@ -1509,7 +1652,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   using RK = RecKind<NL, CMP>;
   using K = typename std::conditional<RK::C32, uint32_t, uint64_t>::type;
   CountLds<K> t;
-  t.cap = p.cap;
+  t.cap = p.cap & 0xffff;  // (< 2^16: the compiler then multiplies plane indices by it with v_mul_u32_u24)
   t.keys = (K *)smem;
   t.cnt = (uint32_t *)(t.keys + NL * t.cap);
   t.ext = t.cnt + t.cap;

@@ -122,23 +122,48 @@ constexpr uint64_t CMIX_I1 = inv_odd(CMIX_M1), CMIX_I2 = inv_odd(CMIX_M2);
 #ifndef MHMKC_FEISTEL
 #define MHMKC_FEISTEL 1
 #endif
-// MHMKC_FEISTEL (default): a 4-round Feistel network on the two halves of the B key bits (a = B/2 low bits,
-// b = B - a <= 21 high bits; a Feistel round is invertible whatever its round function). The round function
-// takes bits [11, 11 + n) of the low 32 bits of a 24 x 24-bit product: one full-rate v_mul_u32_u24, where the
-// xorshift-multiply chain over 64 bits needs quarter-rate 64-bit multiplies (extraction is VALU-bound).
+// MHMKC_FEISTEL (default): a Feistel network on the two halves of the B key bits (a = B/2 low bits, b = B - a <= 21
+// high bits; a Feistel round is invertible whatever its round function). The round function takes bits [11, 11 + n)
+// of the low 32 bits of a 24 x 24-bit product: one full-rate v_mul_u32_u24, where the xorshift-multiply chain over
+// 64 bits needs quarter-rate 64-bit multiplies (extraction is VALU-bound). Three rounds (CMIX_ROUNDS): the bucket
+// digits are the top bits of the third round's L (L ^ f(R) ^ f(R ^ f(L ^ f(R)))), k_count's home group the bits
+// below them and the top of the second round's R; a fourth round only re-mixed R.
+#ifndef MHMKC_CMIX_ROUNDS
+#define MHMKC_CMIX_ROUNDS 3
+#endif
 constexpr uint32_t FEISTEL_K[4] = {0x9E3779u, 0x85EBCAu, 0xC2B2AEu, 0x27D4EBu};
-MHM_HD uint32_t feistel_f(uint32_t v, uint32_t c, int n) {
-  return ((((v ^ (v >> 9)) & 0xffffffu) * c) >> 11) & ((1u << n) - 1);
+// 24 x 24-bit product, low 32 bits (v_mul_u32_u24, full rate; a plain masked product can come out as the
+// quarter-rate v_mul_lo_u32 when the compiler loses track of the mask)
+MHM_HD uint32_t mul24(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;  // (inline asm: hipcc turns __umul24 of a non-constant-bounded operand into v_mul_lo_u32)
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
+  return r;
+#else
+  return (a & 0xffffffu) * (b & 0xffffffu);
+#endif
+}
+MHM_HD uint32_t feistel_f(uint32_t v, uint32_t c, int n) { return (mul24(v ^ (v >> 9), c) >> 11) & ((1u << n) - 1); }
+
+// The Feistel rounds on the halves (L: b bits, R: a bits) and their inverse.
+MHM_HD void cmix_lr(uint32_t &L, uint32_t &R, int a, int b) {
+  L ^= feistel_f(R, FEISTEL_K[0], b);
+  R ^= feistel_f(L, FEISTEL_K[1], a);
+  L ^= feistel_f(R, FEISTEL_K[2], b);
+  if (MHMKC_CMIX_ROUNDS > 3) R ^= feistel_f(L, FEISTEL_K[3], a);
+}
+MHM_HD void cunmix_lr(uint32_t &L, uint32_t &R, int a, int b) {
+  if (MHMKC_CMIX_ROUNDS > 3) R ^= feistel_f(L, FEISTEL_K[3], a);
+  L ^= feistel_f(R, FEISTEL_K[2], b);
+  R ^= feistel_f(L, FEISTEL_K[1], a);
+  L ^= feistel_f(R, FEISTEL_K[0], b);
 }
 
 MHM_HD uint64_t cmix(uint64_t x, int B) {
 #if MHMKC_FEISTEL
   const int a = B >> 1, b = B - a;
   uint32_t R = (uint32_t)x & ((1u << a) - 1), L = (uint32_t)(x >> a);
-  L ^= feistel_f(R, FEISTEL_K[0], b);
-  R ^= feistel_f(L, FEISTEL_K[1], a);
-  L ^= feistel_f(R, FEISTEL_K[2], b);
-  R ^= feistel_f(L, FEISTEL_K[3], a);
+  cmix_lr(L, R, a, b);
   return ((uint64_t)L << a) | R;
 #else
   const uint64_t m = (1ull << B) - 1;
@@ -156,10 +181,7 @@ MHM_HD uint64_t cunmix(uint64_t y, int B) {
 #if MHMKC_FEISTEL
   const int a = B >> 1, b = B - a;
   uint32_t R = (uint32_t)y & ((1u << a) - 1), L = (uint32_t)(y >> a);
-  R ^= feistel_f(L, FEISTEL_K[3], a);
-  L ^= feistel_f(R, FEISTEL_K[2], b);
-  R ^= feistel_f(L, FEISTEL_K[1], a);
-  L ^= feistel_f(R, FEISTEL_K[0], b);
+  cunmix_lr(L, R, a, b);
   return ((uint64_t)L << a) | R;
 #else
   const uint64_t m = (1ull << B) - 1;
@@ -195,22 +217,68 @@ MHM_HD uint64_t m2_f(uint64_t v, uint64_t c) {
 }
 MHM_HD bool mixed2_ok(int k, int nl) { return nl == 2 && k >= M2_MIN_K && k <= M2_MAX_K; }
 
+// MHMKC_M2FAST (default): the round functions hash their k-bit input to 32 bits with full-rate 24-bit multiplies
+// and xor them into the 32 bits that are used downstream: the top 32 bits of L (the bucket digits are the top
+// bits of L'), the low 32 bits of R (k_count's home group is the low 16 bits of R'). A Feistel round is a
+// bijection whatever its round function and wherever it xors, so the other bits may pass unmixed. Each 64-bit
+// multiply of m2_f is four quarter-rate VALU ops, and extraction at k = 63 is VALU-bound. Two rounds: the digits
+// are top(L) ^ h(R), R (the last ~k/2 bases) being all but unique per k-mer, and the home group is
+// low(R) ^ h(L'); a third round only re-mixed L.
+#ifndef MHMKC_M2FAST
+#define MHMKC_M2FAST 1
+#endif
+#ifndef MHMKC_M2_ROUNDS
+#define MHMKC_M2_ROUNDS 2
+#endif
+constexpr uint32_t M2_C[6] = {0x9E3779u, 0x85EBCBu, 0xC2B2AFu, 0x27D4EBu, 0x165667u, 0x3A2659u};
+MHM_HD uint32_t m2_h(uint64_t v, uint32_t c1, uint32_t c2) {  // <= 63-bit v -> 32 bits
+  const uint32_t hi = (uint32_t)(v >> 32);
+  uint32_t u = (uint32_t)v ^ ((hi << 7) | (hi >> 25));
+  u ^= u >> 16;
+  u = mul24(u, c1);
+  u ^= u >> 15;
+  u = mul24(u, c2);
+  u ^= u >> 16;
+  return u;
+}
+
+// The rounds on the halves: (L, R) -> (L', R'), k bits each, and back.
+MHM_HD void m2_mix_lr(uint64_t &L, uint64_t &R, int k) {
+#if MHMKC_M2FAST
+  L ^= (uint64_t)m2_h(R, M2_C[0], M2_C[1]) << (k - 32);
+  R ^= (uint64_t)m2_h(L, M2_C[2], M2_C[3]);
+  if (MHMKC_M2_ROUNDS > 2) L ^= (uint64_t)m2_h(R, M2_C[4], M2_C[5]) << (k - 32);
+#else
+  const uint64_t m = (1ull << k) - 1;
+  L ^= m2_f(R, M2_K[0]) & m;
+  R ^= m2_f(L, M2_K[1]) & m;
+  L ^= m2_f(R, M2_K[2]) & m;
+#endif
+}
+MHM_HD void m2_unmix_lr(uint64_t &L, uint64_t &R, int k) {
+#if MHMKC_M2FAST
+  if (MHMKC_M2_ROUNDS > 2) L ^= (uint64_t)m2_h(R, M2_C[4], M2_C[5]) << (k - 32);
+  R ^= (uint64_t)m2_h(L, M2_C[2], M2_C[3]);
+  L ^= (uint64_t)m2_h(R, M2_C[0], M2_C[1]) << (k - 32);
+#else
+  const uint64_t m = (1ull << k) - 1;
+  L ^= m2_f(R, M2_K[2]) & m;
+  R ^= m2_f(L, M2_K[1]) & m;
+  L ^= m2_f(R, M2_K[0]) & m;
+#endif
+}
+
 // key words (Kmer::longs layout, k bases) -> (L', R'), k bits each
 MHM_HD void m2_mix(const uint64_t *w, int k, uint64_t &L, uint64_t &R) {
   const uint64_t m = (1ull << k) - 1;
   L = w[0] >> (64 - k);
   R = ((w[0] << (2 * k - 64)) | (w[1] >> (128 - 2 * k))) & m;  // x = L << k | R: x's low 64 bits, masked
-  L ^= m2_f(R, M2_K[0]) & m;
-  R ^= m2_f(L, M2_K[1]) & m;
-  L ^= m2_f(R, M2_K[2]) & m;
+  m2_mix_lr(L, R, k);
 }
 
 // (L', R') -> key words (the last word's unused low bits zero)
 MHM_HD void m2_unmix(uint64_t L, uint64_t R, int k, uint64_t *w) {
-  const uint64_t m = (1ull << k) - 1;
-  L ^= m2_f(R, M2_K[2]) & m;
-  R ^= m2_f(L, M2_K[1]) & m;
-  L ^= m2_f(R, M2_K[0]) & m;
+  m2_unmix_lr(L, R, k);
   w[0] = (L << (64 - k)) | (R >> (2 * k - 64));
   w[1] = R << (128 - 2 * k);
 }

@@ -389,7 +389,7 @@ def test_analyze_kmers_dmin_thres(k):
 
 def _hot_key_last_bucket(k: int) -> str:
     """A canonical k-mer whose partition hash has the top 19 bits set: the last fine bucket of the last coarse
-    bucket for any fine-bit count <= 11 (compact cmix at k <= 21, MurmurHash3 above)."""
+    bucket for any fine-bit count <= 11 (compact cmix at k <= 21, m2_mix at 33..63, MurmurHash3 otherwise)."""
     rng = np.random.default_rng(k)
     nl = k // 32 + 1
     B = 2 * k
@@ -398,17 +398,38 @@ def _hot_key_last_bucket(k: int) -> str:
     def f(v, c, n):
         return ((((v ^ (v >> 9)) & 0xffffff) * c & 0xffffffff) >> 11) & ((1 << n) - 1)
 
-    def cunmix(y):
+    def cunmix(y):  # three rounds (MHMKC_CMIX_ROUNDS)
         a, bb = B >> 1, B - (B >> 1)
         R, L = y & ((1 << a) - 1), y >> a
-        R ^= f(L, FK[3], a)
         L ^= f(R, FK[2], bb)
         R ^= f(L, FK[1], a)
         L ^= f(R, FK[0], bb)
         return (L << a) | R
 
+    M2C = (0x9E3779, 0x85EBCB, 0xC2B2AF, 0x27D4EB, 0x165667, 0x3A2659)  # kmer_ops.hpp m2_h (MHMKC_M2FAST)
+    M32 = 0xffffffff
+
+    def m2_h(v, c1, c2):
+        hi = (v >> 32) & M32
+        u = (v & M32) ^ (((hi << 7) | (hi >> 25)) & M32)
+        u ^= u >> 16
+        u = ((u & 0xffffff) * c1) & M32
+        u ^= u >> 15
+        u = ((u & 0xffffff) * c2) & M32
+        return u ^ (u >> 16)
+
+    def m2_unmix(L, R):  # (L', R') -> key words; two rounds (MHMKC_M2_ROUNDS)
+        R ^= m2_h(L, M2C[2], M2C[3])
+        L ^= m2_h(R, M2C[0], M2C[1]) << (k - 32)
+        x = (L << k) | R  # 2k bits, left-aligned in 128
+        x <<= 128 - 2 * k
+        return np.array([x >> 64, x & ((1 << 64) - 1)], dtype=np.uint64)
+
     for _ in range(1 << 22):
-        if k <= 21:  # cunmix of a y with the top bits set
+        if 33 <= k <= 63:  # m2_unmix of an L' with the top bits set (the mixed two-word records' digits)
+            L = (((1 << 19) - 1) << (k - 19)) | int(rng.integers(0, 1 << (k - 19)))
+            key = m2_unmix(L, int(rng.integers(0, 1 << 62)) & ((1 << k) - 1))
+        elif k <= 21:  # cunmix of a y with the top bits set
             y = (((1 << 19) - 1) << (B - 19)) | int(rng.integers(0, 1 << (B - 19)))
             key = np.array([cunmix(y) << (64 - B)], dtype=np.uint64)
         else:
@@ -422,7 +443,7 @@ def _hot_key_last_bucket(k: int) -> str:
     raise AssertionError("no key found")
 
 
-@pytest.mark.parametrize("k", [21, 33])
+@pytest.mark.parametrize("k", [21, 33, 63, 77])
 def test_capped_overflow_in_last_bucket(k):
     """a hot k-mer in the LAST fine bucket of the LAST coarse bucket overflows its capped
     fine bucket. k_count must not run over the bucket (it returns at once when k_part_scatter flagged the

@@ -79,3 +79,26 @@ def test_table_lines_dump_format(tmp_path):
     with gzip.open(p, "wt") as f:
         f.write("\n".join(t.lines()) + "\n")
     assert gzip.open(p, "rt").read() == "ACGTA 7 A F\n"
+
+
+def test_mixed_record_bijection_and_flatness(tmp_path):
+    """kmer_ops.hpp cmix / m2_mix and their inverses (mixed records): round trips at every k
+    in 10..21 and 33..63,
+    and flat bucket digits and home groups over the consecutive (correlated) canonical windows of one sequence."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+
+    if not shutil.which("g++"):
+        pytest.skip("g++ missing")
+    src = Path(__file__).parent / "cpp" / "mix_check.cpp"
+    exe = tmp_path / "mix_check"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wno-unknown-pragmas", str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, check=True).stdout
+    assert "roundtrip ok" in out
+    rows = [ln.split() for ln in out.splitlines() if ln.startswith("k ")]
+    assert len(rows) == 6
+    for r in rows:
+        coarse, fine, group = float(r[3]), float(r[5]), float(r[7])
+        # 256 coarse bins of ~7800 windows, up to 2^17 fine bins of ~15 (Poisson max), 1000 groups of 2000
+        assert coarse < 1.08 and group < 1.12 and fine < 3.0, r
