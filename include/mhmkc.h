@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 6
+#define MHMKC_ABI_VERSION 7
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -117,6 +117,7 @@ typedef struct {
   uint64_t fq_merged;      /* ... of which merged (merge_reads num_merged) */
   uint64_t fq_ambiguous;   /* ... merge_reads' num_ambiguous increments */
   uint64_t fq_overlap_bases; /* ... overlap bases of the merged pairs (merge_reads overlap_len) */
+  uint64_t table_slots;    /* count kernel: LDS table slots used per fine bucket (fitted to the sketch estimate) */
 } mhmkc_stats;
 
 enum {

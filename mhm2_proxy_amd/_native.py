@@ -100,6 +100,7 @@ class MhmkcStats(C.Structure):
         ("fq_merged", C.c_uint64),
         ("fq_ambiguous", C.c_uint64),
         ("fq_overlap_bases", C.c_uint64),
+        ("table_slots", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -1238,6 +1238,9 @@ constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
 #ifndef MHMKC_BSPREAD
 #define MHMKC_BSPREAD 0
 #endif
+#ifndef MHMKC_WAVEQ
+#define MHMKC_WAVEQ 1
+#endif
 
 // Two-pass finalize (list the slots with count >= 2, then decide them densely); 0 = one pass over all slots.
 #ifndef MHMKC_FIN2
@@ -1669,6 +1672,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // B_OVERLAP: phase B of round r overlaps phase A of round r + 1, so the miss list is double-buffered
   constexpr bool BOV = B_OVERLAP && !(NL == 2 && MHMKC_BOV2 == 0);
   constexpr int MCL = BOV ? (MC / 2) & ~63 : MC;
+  // MHMKC_WAVEQ: a miss queue per wave (MW entries of the miss space) instead of one shared list, worked off by
+  // its own wave after the round barrier once it holds WQ_THR entries, and emptied after the last round
+  constexpr bool WQ = MHMKC_WAVEQ != 0;
+  constexpr int MW = MC / (C_THREADS / 64);
+  constexpr int WQ_THR = MW / 2 < 64 ? MW / 2 : 64;
+  const uint32_t wq_base = (uint32_t)(threadIdx.x >> 6) * (uint32_t)MW;
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
@@ -1680,7 +1689,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   constexpr int R = count_rpt<NL>();
   constexpr uint32_t NONE = 0xffffffffu;
   constexpr uint32_t RND = (uint32_t)R * C_THREADS;
-  constexpr uint32_t HOT = 0xC000u - 2u * RND;  // see ext_clamp
+  // see ext_clamp: between two barriers a round's records and at most the miss space's queued records are added
+  constexpr uint32_t HOT = 0xC000u - 2u * (RND + (MHMKC_WAVEQ ? (uint32_t)miss_cap(NL, RecKind<NL, CMP>::C32) : 0u));
   static_assert(HOT > 0x8000u, "round too large for the extension-counter clamp");
   constexpr int C_BATCH = MHMKC_CBATCH < R ? MHMKC_CBATCH : R;
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
@@ -1794,6 +1804,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     auto rounds = [&](auto cold_tag) {
       constexpr bool COLD = decltype(cold_tag)::value;
       int rnd = 0, lr = 0;           // lr = rnd % 3: the round's miss counter
+      uint32_t wq_n = 0;             // WQ: entries in this wave's miss queue (wave-uniform)
       for (uint32_t r0 = 0; r0 < n; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
         STAMP(t_r0);
         uint64_t ck[R][NL];
@@ -1832,7 +1843,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         uint32_t *me = s_me + (BOV ? (rnd & 1) * MCL : 0);
         // A. home-group lookups: the first groups of all R records are read in batches of C_BATCH (the
         //    reads of a batch in flight together), then found records are counted, missed ones listed.
-        uint32_t old[R], defer = 0, okm = 0;
+        uint32_t old[R], defer = 0, okm = 0, missm = 0;
         int slot[R], g[R];
 #pragma unroll
         for (int j0 = 0; j0 < R; j0 += C_BATCH) {
@@ -1881,6 +1892,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             slot[j] = r;
           }
           if (r < 0) {
+            if constexpr (WQ) {  // listed below, in wave-uniform code
+              missm |= 1u << j;
+              slot[j] = r;
+              continue;
+            }
             const unsigned int q = atomicAdd(nmiss, 1u);
             if (q < (unsigned int)MCL) {  // handed to phase B
 #pragma unroll
@@ -1903,13 +1919,46 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #endif
           okm |= 1u << j;
         }
+        if constexpr (WQ) {
+          // this wave's misses join its own queue (ballot + prefix: no LDS atomic); a queue without room for
+          // them inserts in place, as a full shared list did
+#pragma unroll
+          for (int j = 0; j < R; j++) {
+            const bool mj = (missm >> j) & 1u;
+            const uint64_t bal = __ballot(mj);
+            const uint32_t tot = (uint32_t)__popcll(bal);
+            if (wq_n + tot <= (uint32_t)MW) {
+              if (mj) {
+                const uint32_t q = wq_base + wq_n +
+                                   __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+#pragma unroll
+                for (int w = 0; w < NL; w++) s_mkey[w * MC + q] = (K)ck[j][w];
+                s_me[q] = ce[j];
+                slot[j] = -3;
+              }
+              wq_n += tot;
+            } else if (mj) {
+              const int r = lds_insert<NL>(t, ck[j], g[j], slot[j]);
+              if (r == -1) defer |= 1u << j;
+              if (r == -2) s_err = 1;
+              slot[j] = r;
+              if (r >= 0) {
+                if (COLD)
+                  lds_add_nr(t, r, ce[j], &s_wave[wid]);
+                else
+                  old[j] = lds_add(t, r, ce[j]);
+                okm |= 1u << j;
+              }
+            }
+          }
+        }
 #pragma unroll
         for (int j = 0; j < R; j++)
           if (!COLD && ((okm >> j) & 1u) && old[j] >= HOT) lds_clamp(t, slot[j], ce[j]);
         STAMP(t_r2);
         STAMP_ADD(2, t_r2 - t_r1);
         // the next round's counter: its last readers (phase B two rounds back) are behind the previous barrier
-        if (BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
+        if (!WQ && BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
         __syncthreads();
         STAMP(t_r3);
         STAMP_ADD(3, t_r3 - t_r2);
@@ -1923,6 +1972,46 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
               store_record<NL, PACKED, CMP>(ps, pos, ck[j], ce[j]);
             }
           }
+        }
+        if constexpr (WQ) {
+          // B. this wave's queue, 64 entries at a time once it holds WQ_THR (all of it after the sweep's last
+          // round): whole-wave batches, and every wave takes its own share of the slow path, so no wave holds
+          // the next barrier with the misses of all the others
+          const bool last_round = r0 + RND >= n;
+          while (wq_n >= (uint32_t)WQ_THR || (last_round && wq_n > 0)) {
+            const uint32_t take = wq_n < 64u ? wq_n : 64u;
+            const uint32_t qb = wq_n - take;
+            if ((uint32_t)lane < take) {
+              const uint32_t q = wq_base + qb + (uint32_t)lane;
+              uint64_t key[NL];
+#pragma unroll
+              for (int w = 0; w < NL; w++) key[w] = s_mkey[w * MC + q];
+              const uint32_t e = s_me[q];
+              const int g = CMP ? cmp_group((uint32_t)key[NL - 1], kshl, (uint32_t)ng)
+                                : (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
+              K v[4];
+              read_group(last, g, v);
+              const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
+              if (r >= 0) {
+                if (COLD)
+                  lds_add_nr(t, r, e, &s_wave[wid]);
+                else if (lds_add(t, r, e) >= HOT)
+                  lds_clamp(t, r, e);
+              } else if (r == -1) {
+                const unsigned int pos = atomicAdd(&s_ovf, 1u);
+                store_record<NL, PACKED, CMP>(ps, pos, key, e);
+              } else {
+                s_err = 1;
+              }
+            }
+            if (lane == 0) atomicAdd(&s_missacc, (unsigned long long)take);
+            wq_n = qb;
+          }
+#if MHMKC_STAMP
+          const uint64_t t_r4w = __builtin_amdgcn_s_memtime();
+          STAMP_ADD(4, t_r4w - t_r3);
+#endif
+          continue;
         }
         // B. the miss list, densely
 #if MHMKC_EXP_NOB

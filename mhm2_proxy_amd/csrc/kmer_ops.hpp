@@ -133,7 +133,8 @@ constexpr uint64_t CMIX_I1 = inv_odd(CMIX_M1), CMIX_I2 = inv_odd(CMIX_M2);
 #endif
 constexpr uint32_t FEISTEL_K[4] = {0x9E3779u, 0x85EBCAu, 0xC2B2AEu, 0x27D4EBu};
 // 24 x 24-bit product, low 32 bits (v_mul_u32_u24, full rate; a plain masked product can come out as the
-// quarter-rate v_mul_lo_u32 when the compiler loses track of the mask)
+// quarter-rate v_mul_lo_u32 when the compiler loses track of the mask). b must be wave-uniform (an SGPR operand:
+// every caller passes a constant).
 MHM_HD uint32_t mul24(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t r;  // (inline asm: hipcc turns __umul24 of a non-constant-bounded operand into v_mul_lo_u32)

@@ -295,6 +295,13 @@ struct mhmkc {
 
 // Fine partition target: distinct keys per fine bucket <= FINE_LOAD x LDS table slots.
 constexpr double FINE_LOAD = 0.7;
+// Load of the LDS table k_count uses per bucket, after the fine partition is fixed (0 = the whole table, the
+// default: a table fitted to 0.6-0.8 of the estimate was measured slower, 6.28 -> 7.14-10.2 ms at C2, because
+// the home-group hit rate falls with the load faster than the per-slot clear and finalize work does).
+static const double CAP_LOAD = [] {
+  const char *env = getenv("MHMKC_CAP_LOAD");
+  return env ? atof(env) : 0.0;
+}();
 
 // HyperLogLog estimate (Flajolet et al. 2007) with the linear-counting correction for small counts.
 static double hll_estimate(const std::vector<uint32_t> &reg) {
@@ -995,6 +1002,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   // of distinct keys to records grows with k and the error rate, so the record count alone misjudges it)
   const uint32_t cap_slots = (uint32_t)mhm::count_cap(nl, compact);
   fb = 4;
+  double est_fine = 0;  // estimated distinct keys per fine bucket (0: no estimate)
   if (n_c0) {
     mhm::PartitionParams sp{};
     sp.runs = d_runs;
@@ -1022,6 +1030,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     const double est = hll_estimate(reg);
     st.distinct_estimate = (uint64_t)(est * no);
     while (fb < 11 && est / (double)(1u << fb) > FINE_LOAD * cap_slots) fb++;
+    est_fine = est;
   } else {  // no records in the first coarse bucket: ~4 records per slot
     const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
     while (fb < 11 && (avg_coarse >> fb) > (uint64_t)cap_slots * 4) fb++;
@@ -1029,6 +1038,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
   fb = std::max(fb, min_fine_bits());
   nf = 1u << fb;
+  est_fine /= nf;
   const uint32_t n_fine = no * nf;
   st.fine_buckets = n_fine;
   if ((rc = prepare_ctgs())) return rc;
@@ -1084,6 +1094,15 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   cp.grid = (uint32_t)std::max(0, n_cu * mhm::C_SPLIT);  // persistent workgroups filling every CU's LDS
   cp.k = k;
   cp.cap = mhm::count_cap(nl, compact);
+  // The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
+  // LDS table (C2: 0.44). The table k_count clears and finalizes per bucket is cut to CAP_LOAD of the estimate
+  // (multiples of 64 slots): both passes cost per slot, not per key.
+  if (est_fine > 0 && CAP_LOAD > 0) {
+    const double want = est_fine / CAP_LOAD;
+    const uint32_t fit = (uint32_t)std::min<double>(cp.cap, std::max(1024.0, std::ceil(want / 64.0) * 64.0));
+    cp.cap = std::min(cp.cap, (int)fit);
+  }
+  st.table_slots = (uint64_t)cp.cap;
   if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
   cp.dmin_thres = dmin;
   cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
