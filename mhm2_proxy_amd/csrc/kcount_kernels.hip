@@ -22,12 +22,9 @@
 
 namespace mhm {
 
-#ifndef MHMKC_TILE1
-#define MHMKC_TILE1 4096
-#endif
 template <int NL>
 constexpr int kTile() {
-  return NL == 1 ? MHMKC_TILE1 : 2048;
+  return NL == 1 ? MHMKC_TILE1 : MHMKC_TILE2;
 }
 template <int NL>
 constexpr int kGroups() {
@@ -566,12 +563,14 @@ __device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const 
   }
 }
 
+constexpr size_t WSUM_BYTES = ((E_THREADS / 64 + 1) * 4 + 15) & ~(size_t)15;  // block_excl_scan's wave sums
+
 // Staged variant: the records are first written to LDS in bin order, then copied out so that consecutive
 // lanes store consecutive addresses of one bin (runs of ~T/nb records instead of one line per lane).
 // LDS: counters [lcnt | goff | lstart | wsum] then the stage area [NL][T] u64 | sbin[T] u16 | sext[T] u8,
 // which may alias the tile (the first barrier below is after every thread's walk).
 __host__ __device__ constexpr size_t staged_cnt_bytes(uint32_t nb) {
-  return scatter_lds_bytes(nb) + (((size_t)nb * 4 + 15) & ~(size_t)15) + 32;
+  return scatter_lds_bytes(nb) + (((size_t)nb * 4 + 15) & ~(size_t)15) + WSUM_BYTES;
 }
 // Compact records are staged at their stored width: u32 (+ the high byte for SF_C40).
 __host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packed, int sf = SF_WORDS) {
@@ -589,7 +588,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   uint32_t *lcnt = (uint32_t *)smem;
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
   uint32_t *lstart = (uint32_t *)(smem + scatter_lds_bytes(nb));
-  uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - 32);
+  uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - WSUM_BYTES);
   constexpr bool C32 = SF != SF_WORDS;  // compact: low 32 bits in stage32, the high byte (SF_C40) in sext
   uint64_t *stage = (uint64_t *)area;
   uint32_t *stage32 = (uint32_t *)area;
@@ -1246,6 +1245,10 @@ constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
 #ifndef MHMKC_FIN2
 #define MHMKC_FIN2 1
 #endif
+// Finalize pass 1 on quads of slots from the counters alone (no key-plane read).
+#ifndef MHMKC_FINQ
+#define MHMKC_FINQ 1
+#endif
 
 // Groups a key may probe before its record is deferred to the next sweep of its bucket.
 #ifndef MHMKC_CPROBE
@@ -1253,6 +1256,10 @@ constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
 #endif
 constexpr int C_PROBE = MHMKC_CPROBE;
 // First-group reads a lane keeps in flight in k_count.
+// (two-word keys: one at a time, measured 11.39 -> 11.24 ms at k = 63; their group read is two ds_read_b128)
+#ifndef MHMKC_CBATCH2
+#define MHMKC_CBATCH2 1
+#endif
 #ifndef MHMKC_CBATCH
 #define MHMKC_CBATCH 2
 #endif
@@ -1692,7 +1699,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // see ext_clamp: between two barriers a round's records and at most the miss space's queued records are added
   constexpr uint32_t HOT = 0xC000u - 2u * (RND + (MHMKC_WAVEQ ? (uint32_t)miss_cap(NL, RecKind<NL, CMP>::C32) : 0u));
   static_assert(HOT > 0x8000u, "round too large for the extension-counter clamp");
-  constexpr int C_BATCH = MHMKC_CBATCH < R ? MHMKC_CBATCH : R;
+  constexpr int CB0 = NL == 2 ? MHMKC_CBATCH2 : MHMKC_CBATCH;
+  constexpr int C_BATCH = CB0 < R ? CB0 : R;
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
   const int ng = t.cap >> 2;
   const K *last = t.keys + (NL - 1) * t.cap;
@@ -2081,6 +2089,34 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     unsigned int *s_fin = (unsigned int *)(s_u64 + 3);  // [0] listed slots, [1] survivors (zeroed between buckets)
     uint32_t occ = 0;
     unsigned long long sum = 0;
+#if MHMKC_FINQ
+    // pass 1 over quads of slots: an occupied slot has count >= 1 (every claim is followed by its add; a contig
+    // entry's depth is >= 1) and a free one count 0, so the counters alone decide, read four slots at a time
+    // (one ds_read_b128 per counter plane, consecutive lanes on consecutive quads: no bank conflicts)
+    constexpr int QPT = (count_cap(NL, RK::C32) / 4 + C_THREADS - 1) / C_THREADS;
+#pragma unroll
+    for (int j = 0; j < QPT; j++) {
+      const int qd = tid + j * C_THREADS;
+      if (4 * qd < t.cap) {
+        const uint4 c4 = *(const uint4 *)(t.cnt + 4 * qd);
+        uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+        if (kCold2 && cold) {  // slot_count's cold encoding, four at a time
+          const uint4 a4 = *(const uint4 *)(t.ext + 4 * qd), b4 = *(const uint4 *)(t.ext + t.cap + 4 * qd);
+          const uint32_t a[4] = {a4.x, a4.y, a4.z, a4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            c[i] = (c[i] >> 31) ? c[i] & 0x7fffffffu
+                                : c[i] + (a[i] & 0xffffu) + (a[i] >> 16) + (bb[i] & 0xffffu) + (bb[i] >> 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          occ += c[i] != 0u;
+          sum += c[i];
+          if (c[i] >= 2) flist[atomicAdd(&s_fin[0], 1u)] = (uint16_t)(4 * qd + i);
+        }
+      }
+    }
+#else
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
       const int slot = tid + j * C_THREADS;
@@ -2091,6 +2127,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         if (c32 >= 2) flist[atomicAdd(&s_fin[0], 1u)] = (uint16_t)slot;
       }
     }
+#endif
     __syncthreads();
     const uint32_t n_list = s_fin[0];
     uint32_t surv_mask = 0, spos[SPT];

@@ -157,7 +157,11 @@ enum {
 };
 constexpr int STAT_ALLOC = 16;  // stats[8..13]: k_count phase stamps in MHMKC_STAMP builds
 
-constexpr int E_THREADS = 256;
+// threads of the extract / partition workgroups (each thread takes tile / E_THREADS windows or records)
+#ifndef MHMKC_ETHREADS
+#define MHMKC_ETHREADS 256
+#endif
+constexpr int E_THREADS = MHMKC_ETHREADS;
 constexpr int E_NSUB = 8;
 #ifndef MHMKC_CPAD
 #define MHMKC_CPAD 1
@@ -186,7 +190,10 @@ inline int stored_hash_bits(int k, int nl, bool packed) {
 #ifndef MHMKC_TILE1
 #define MHMKC_TILE1 4096
 #endif
-inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : 2048; }
+#ifndef MHMKC_TILE2
+#define MHMKC_TILE2 2048
+#endif
+inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : MHMKC_TILE2; }
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS); compact records keep
 // 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
 // k_count LDS: table (keys, count, 4 extension words per slot) + 128 B of scalars + the miss list of a
