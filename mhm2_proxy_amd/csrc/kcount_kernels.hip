@@ -23,8 +23,16 @@
 namespace mhm {
 
 template <int NL>
-constexpr int kTile() {
+constexpr int kTile() {  // bases per extract tile
   return NL == 1 ? MHMKC_TILE1 : MHMKC_TILE2;
+}
+template <int NL>
+constexpr int kEThreads() {  // threads per extract workgroup
+  return NL == 1 ? MHMKC_ETHREADS1 : MHMKC_ETHREADS2;
+}
+template <int NL>
+constexpr int kPTile() {  // records per partition chunk (E_THREADS threads)
+  return NL == 1 ? MHMKC_PTILE1 : MHMKC_PTILE2;
 }
 template <int NL>
 constexpr int kGroups() {
@@ -216,7 +224,7 @@ __device__ __forceinline__ int next_start(const uint32_t *start, int q) {
 template <int NL, typename Emit>
 __device__ __forceinline__ void walk_windows(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
                                              uint32_t tile, uint64_t n_bases, uint32_t head, int k, Emit &&emit) {
-  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+  constexpr int T = kTile<NL>(), W = T / kEThreads<NL>();
   static_assert(W <= 32, "one 32-bit mask per thread span");
   const int klast = k - 32 * (NL - 1);
   const uint64_t tmask = top_mask(klast);
@@ -301,7 +309,7 @@ struct WalkSpan {
   uint32_t gl_bits, gr_bits, st_bits, cl;
   __device__ __forceinline__ WalkSpan(const uint64_t *fwd, const uint32_t *good, const uint32_t *start, uint32_t tile,
                                       uint64_t n_bases, uint32_t head, int k) {
-    constexpr int T = kTile<NL>(), W = T / E_THREADS;
+    constexpr int T = kTile<NL>(), W = T / kEThreads<NL>();
     lp0 = 32 + W * (int)threadIdx.x;
     incoming = codes64(fwd, lp0 + k);
     gl_bits = bits32(good, lp0 - 1);
@@ -470,14 +478,14 @@ struct RecKind {
 };
 
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
-  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+__global__ __launch_bounds__(kEThreads<NL>()) void k_extract_hist(ExtractParams p) {
+  constexpr int ET = kEThreads<NL>(), T = kTile<NL>(), W = T / ET;
   extern __shared__ __align__(16) unsigned char smem[];
   uint64_t *fwd;
   uint32_t *good, *start;
   unsigned char *rest = carve_tile<NL>(smem, fwd, good, start);
   uint32_t *hist = (uint32_t *)rest;
-  for (uint32_t b = threadIdx.x; b < p.n_bins; b += E_THREADS) hist[b] = 0;
+  for (uint32_t b = threadIdx.x; b < p.n_bins; b += ET) hist[b] = 0;
   const uint32_t tile = blockIdx.x;
   load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
   const int sh = 64 - p.coarse_bits;
@@ -485,7 +493,7 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_hist(ExtractParams p) {
     if (valid) atomicAdd(&hist[(uint32_t)(window_hash<NL, CMP>(key, p.k) >> sh)], 1u);
   });
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < p.n_bins; b += E_THREADS) {
+  for (uint32_t b = threadIdx.x; b < p.n_bins; b += ET) {
     const uint32_t c = hist[b];
     if (c) atomicAdd(&p.hist[b], (unsigned long long)c);
   }
@@ -528,14 +536,15 @@ struct BinLimit {
 __host__ __device__ constexpr size_t scatter_cnt_bytes(uint32_t nb) { return ((size_t)nb * 4 + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t nb) { return scatter_cnt_bytes(nb) + (size_t)nb * 8; }
 
+template <int NT = E_THREADS>
 __device__ __forceinline__ void scatter_clear(uint32_t *lcnt, uint32_t nb) {
-  for (uint32_t b = threadIdx.x; b < nb; b += E_THREADS) lcnt[b] = 0;
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) lcnt[b] = 0;
 }
 
 // Bin b's cursor is cursor[b * cstride]. In a capped layout a bin that would overflow sets err bit 1
 // and its excess records are not written (the host then redoes the pass with exact bin sizes).
 // Called after lcnt has been cleared and a barrier.
-template <int NL, bool PACKED, int W, int SF>
+template <int NL, bool PACKED, int W, int SF, int NT = E_THREADS>
 __device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
                                              unsigned char *smem, unsigned long long *cursor, uint32_t cstride,
                                              const PlaneSet &out, const BinLimit lim, unsigned int *err) {
@@ -545,7 +554,7 @@ __device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const 
 #pragma unroll
   for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += E_THREADS) {
+  for (uint32_t b = threadIdx.x; b < nb; b += NT) {
     const uint32_t c = lcnt[b];
     const unsigned long long off = c ? atomicAdd(&cursor[(uint64_t)b * cstride], (unsigned long long)c) : 0ull;
     if (lim.cap && c && off + c > lim.end(b)) atomicOr(err, 2u);
@@ -563,7 +572,7 @@ __device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const 
   }
 }
 
-constexpr size_t WSUM_BYTES = ((E_THREADS / 64 + 1) * 4 + 15) & ~(size_t)15;  // block_excl_scan's wave sums
+constexpr size_t WSUM_BYTES = ((1024 / 64 + 1) * 4 + 15) & ~(size_t)15;  // block_excl_scan's wave sums (<= 1024 threads)
 
 // Staged variant: the records are first written to LDS in bin order, then copied out so that consecutive
 // lanes store consecutive addresses of one bin (runs of ~T/nb records instead of one line per lane).
@@ -579,12 +588,12 @@ __host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packe
                         : (size_t)nl * T * 8 + (size_t)T * 2 + (packed ? 0 : (size_t)T);
 }
 
-template <int NL, bool PACKED, int W, int SF>
+template <int NL, bool PACKED, int W, int SF, int NT = E_THREADS>
 __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
                                                unsigned char *smem, unsigned char *area,
                                                unsigned long long *cursor, uint32_t cstride, const PlaneSet &out,
                                                const BinLimit lim, unsigned int *err) {
-  constexpr int T = W * E_THREADS;
+  constexpr int T = W * NT;
   uint32_t *lcnt = (uint32_t *)smem;
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
   uint32_t *lstart = (uint32_t *)(smem + scatter_lds_bytes(nb));
@@ -600,12 +609,12 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   __syncthreads();
   // Reserve each bin's run in the global layout. The returned offsets stay in registers while the bins are
   // scanned and the records staged, so the atomics' round trip overlaps that LDS work (a bin count up to
-  // SCATTER_MAX_BINS = 8 * E_THREADS).
+  // SCATTER_MAX_BINS = 8 * NT).
   unsigned long long off[8];
   uint32_t cnt[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint32_t b = threadIdx.x + i * E_THREADS;
+    const uint32_t b = threadIdx.x + i * NT;
     off[i] = 0;
     cnt[i] = 0;
     if (b < nb) {
@@ -616,7 +625,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
     }
   }
   __syncthreads();
-  const uint32_t total = block_excl_scan<E_THREADS>(lstart, (int)nb, wsum);
+  const uint32_t total = block_excl_scan<NT>(lstart, (int)nb, wsum);
 #pragma unroll
   for (int j = 0; j < W; j++) {
     if (inf[j] >> 31) {
@@ -638,7 +647,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   // recomputing the segment end (a 64-bit multiply per record)
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint32_t b = threadIdx.x + i * E_THREADS;
+    const uint32_t b = threadIdx.x + i * NT;
     if (b < nb) {
       const bool over = lim.cap && cnt[i] && off[i] + cnt[i] > lim.end(b);
       if (over) atomicOr(err, 2u);
@@ -648,7 +657,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < W; j++) {
-    const uint32_t pos = threadIdx.x + j * E_THREADS;
+    const uint32_t pos = threadIdx.x + j * NT;
     if (pos < total) {
       const uint32_t d = sbin[pos];
       const unsigned long long go = goff[d];
@@ -720,14 +729,14 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
 #endif
 ) {
   constexpr int T = kTile<2>(), NG = kGroups<2>(), NW = T / 32, P = NG * 32;
-  static_assert(NW == 64 && W * E_THREADS == T && (T / E_THREADS) <= 32 && 32 % (T / E_THREADS) == 0,
+  static_assert(NW == 64 && W * kEThreads<2>() == T && (T / kEThreads<2>()) <= 32 && 32 % (T / kEThreads<2>()) == 0,
                 "one wave scans the valid bits; every position has a slot; a thread's positions in one word");
   uint64_t *rcw = (uint64_t *)scratch;
   uint32_t *vb = (uint32_t *)(scratch + align16((size_t)NG * 8));
   uint32_t *vpre = vb + NW;
   uint16_t *pos = (uint16_t *)(scratch + align16((size_t)NG * 8) + align16((size_t)(2 * NW + 1) * 4));
   const int tid = threadIdx.x, k = p.k;
-  for (int g = tid; g < NG; g += E_THREADS) rcw[g] = rev2(~fwd[NG - 1 - g]);  // complement, reversed
+  for (int g = tid; g < NG; g += kEThreads<2>()) rcw[g] = rev2(~fwd[NG - 1 - g]);  // complement, reversed
   if (tid < NW) {
     // Valid-window bits of own positions 32w .. 32w + 31 (staged 32(w+1) + i), MSB first like the staged bit
     // arrays: window i is valid iff no read start lies at staged positions [q, q + k] (the read-start bits of
@@ -759,10 +768,10 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
   }
   __syncthreads();
   {  // the list: every thread places its 8 positions (one word)
-    const int o0 = tid * (T / E_THREADS), w = o0 >> 5;
+    const int o0 = tid * (T / kEThreads<2>()), w = o0 >> 5;
     const uint32_t m = vb[w], base = vpre[w];
 #pragma unroll
-    for (int j = 0; j < T / E_THREADS; j++) {
+    for (int j = 0; j < T / kEThreads<2>(); j++) {
       const int i = (o0 + j) & 31;
       if ((m >> (31 - i)) & 1u) pos[base + __popc(m & ~(~0u >> i))] = (uint16_t)(o0 + j);
     }
@@ -778,7 +787,7 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
   // every list position of the thread up front (v < T always; entries past nv are masked to the tile)
   int q[W];
 #pragma unroll
-  for (int i = 0; i < W; i++) q[i] = 32 + (int)(pos[tid + i * E_THREADS] & (T - 1));
+  for (int i = 0; i < W; i++) q[i] = 32 + (int)(pos[tid + i * kEThreads<2>()] & (T - 1));
 #pragma unroll
   for (int i = 0; i < W; i++) {
     rk[i][0] = 0;
@@ -791,10 +800,10 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
   static_assert(W % PB == 0, "slot batches");
 #pragma unroll
   for (int i0 = 0; i0 < W; i0 += PB) {
-    if ((uint32_t)(tid & ~63) + (uint32_t)(i0 * E_THREADS) >= nv) break;
+    if ((uint32_t)(tid & ~63) + (uint32_t)(i0 * kEThreads<2>()) >= nv) break;
 #pragma unroll
     for (int i = i0; i < i0 + PB; i++) {
-      const uint32_t v = (uint32_t)tid + (uint32_t)(i * E_THREADS);
+      const uint32_t v = (uint32_t)tid + (uint32_t)(i * kEThreads<2>());
       const int qq = q[i];
       uint64_t fw[2], rc[2];
       fw[0] = funnel_codes(fwd, qq);
@@ -832,8 +841,8 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
 // extract: scatter into coarse buckets
 
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) {
-  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+__global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractParams p) {
+  constexpr int ET = kEThreads<NL>(), T = kTile<NL>(), W = T / ET;
   const int kk = p.k;
   extern __shared__ __align__(16) unsigned char smem0[];
   uint64_t *fwd;
@@ -850,7 +859,7 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
 #ifdef MHMKC_ESTAMP
   const uint64_t es0 = __builtin_amdgcn_s_memtime();
 #endif
-  scatter_clear((uint32_t *)smem, p.n_bins);
+  scatter_clear<ET>((uint32_t *)smem, p.n_bins);
   const uint32_t tile = blockIdx.x;
   load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
 #ifdef MHMKC_ESTAMP
@@ -913,10 +922,10 @@ __global__ __launch_bounds__(E_THREADS) void k_extract_scatter(ExtractParams p) 
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
   constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS;
   if (kEStaged)
-    scatter_staged<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
+    scatter_staged<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
                                       p.ovf);
   else
-    scatter_regs<NL, PACKED, W, SF>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
+    scatter_regs<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
 #ifdef MHMKC_ESTAMP
   const uint64_t es4 = __builtin_amdgcn_s_memtime();
   if ((threadIdx.x & 63) == 0) {  // spread over 64 x 4 words (one address per phase would serialise)
@@ -1010,7 +1019,7 @@ __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch
 
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
-  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+  constexpr int T = kPTile<NL>(), W = T / E_THREADS;
   extern __shared__ __align__(16) uint32_t hist[];  // the only LDS object
   const uint32_t nf = 1u << p.fine_bits;
   for (uint32_t b = threadIdx.x; b < nf; b += E_THREADS) hist[b] = 0;
@@ -1036,7 +1045,7 @@ __global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
 
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
-  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+  constexpr int T = kPTile<NL>(), W = T / E_THREADS;
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t nf = 1u << p.fine_bits;
   scatter_clear((uint32_t *)smem, nf);
@@ -1079,7 +1088,7 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
 // a sample of the whole).
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigned int *hll) {
-  constexpr int T = kTile<NL>(), W = T / E_THREADS;
+  constexpr int T = kPTile<NL>(), W = T / E_THREADS;
   __shared__ unsigned int reg[SKETCH_M];
   __shared__ unsigned int s_ext;
   if (threadIdx.x == 0) s_ext = 0;
@@ -2336,7 +2345,7 @@ static hipError_t do_extract_hist(const ExtractParams &p, hipStream_t s) {
   const size_t lds = tile_lds_bytes<NL>() + (size_t)p.n_bins * 4;
   hipError_t e = allow_lds(k_extract_hist<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_extract_hist<NL, PK, CMP><<<dim3(p.n_tiles), dim3(E_THREADS), lds, s>>>(p);
+  k_extract_hist<NL, PK, CMP><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p);
   return hipGetLastError();
 }
 
@@ -2348,7 +2357,7 @@ static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
                               : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_extract_scatter<NL, PK, CMP><<<dim3(p.n_tiles), dim3(E_THREADS), lds, s>>>(p);
+  k_extract_scatter<NL, PK, CMP><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p);
   return hipGetLastError();
 }
 
@@ -2364,7 +2373,7 @@ static hipError_t do_part_hist(const PartitionParams &p, hipStream_t s) {
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
   const uint32_t nf = 1u << p.fine_bits;
-  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kTile<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS)
+  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kPTile<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS)
                               : scatter_lds_bytes(nf);
   hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;

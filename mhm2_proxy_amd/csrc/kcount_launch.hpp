@@ -194,6 +194,21 @@ inline int stored_hash_bits(int k, int nl, bool packed) {
 #define MHMKC_TILE2 2048
 #endif
 inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : MHMKC_TILE2; }
+// threads of an extract workgroup (tile_bases / threads windows each)
+#ifndef MHMKC_ETHREADS1
+#define MHMKC_ETHREADS1 E_THREADS
+#endif
+#ifndef MHMKC_ETHREADS2
+#define MHMKC_ETHREADS2 E_THREADS
+#endif
+// records per partition chunk (one E_THREADS workgroup)
+#ifndef MHMKC_PTILE1
+#define MHMKC_PTILE1 4096
+#endif
+#ifndef MHMKC_PTILE2
+#define MHMKC_PTILE2 2048
+#endif
+inline int chunk_records(int nl) { return nl == 1 ? MHMKC_PTILE1 : MHMKC_PTILE2; }
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS); compact records keep
 // 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
 // k_count LDS: table (keys, count, 4 extension words per slot) + 128 B of scalars + the miss list of a

@@ -952,7 +952,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       return fail(MHMKC_EUNSUPPORTED, "more than 2^32 records in one hash bucket (split the input into batches of ranks)");
 
   // run table: one entry per non-empty (source, segment) span; the device expands it into chunks
-  const int T = mhm::tile_bases(nl);
+  const int T = mhm::chunk_records(nl);  // records per partition chunk
   std::vector<mhm::SRun> runs;
   std::vector<mhm::PlaneSet> ps;
   uint64_t n_chunks = 0, n_c0 = 0;  // n_c0: chunks of the first owned coarse bucket (they come first)
