@@ -24,7 +24,7 @@ namespace mhm {
 
 template <int NL>
 constexpr int kTile() {  // bases per extract tile
-  return NL == 1 ? MHMKC_TILE1 : MHMKC_TILE2;
+  return NL == 1 ? MHMKC_TILE1 : NL == 2 ? MHMKC_TILE2 : MHMKC_TILE3;
 }
 template <int NL>
 constexpr int kEThreads() {  // threads per extract workgroup
@@ -698,7 +698,7 @@ constexpr bool kPStaged = MHMKC_PSTAGE != 0;
 #ifndef MHMKC_M2WALK
 #define MHMKC_M2WALK 0
 #endif
-constexpr bool kM2Walk = MHMKC_M2WALK != 0;
+constexpr bool kM2Walk = MHMKC_M2WALK != 0 && MHMKC_TILE2 == 2048;  // (its valid-bit scan is one wave over 64 words)
 // Mixed-record walks (walk_c32, walk_m2: the key as the mix takes it); 0 = the generic walk_windows + window_hash.
 #ifndef MHMKC_MIXWALK
 #define MHMKC_MIXWALK 1

@@ -190,10 +190,16 @@ inline int stored_hash_bits(int k, int nl, bool packed) {
 #ifndef MHMKC_TILE1
 #define MHMKC_TILE1 4096
 #endif
+// two-word keys: 4096-base tiles of 16 windows per thread (78 KB of LDS, two workgroups per CU) measured faster
+// than 2048 (k = 63 extract 9.29 -> 8.52 ms, k = 33 10.10 -> 9.68 ms; 512 threads x 4096: 8.84 ms, 512 x 8192:
+// 11.2 ms); three and four words keep 2048 (their records would not fit the registers at 16 per thread)
 #ifndef MHMKC_TILE2
-#define MHMKC_TILE2 2048
+#define MHMKC_TILE2 4096
 #endif
-inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : MHMKC_TILE2; }
+#ifndef MHMKC_TILE3
+#define MHMKC_TILE3 2048
+#endif
+inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : nl == 2 ? MHMKC_TILE2 : MHMKC_TILE3; }
 // threads of an extract workgroup (tile_bases / threads windows each)
 #ifndef MHMKC_ETHREADS1
 #define MHMKC_ETHREADS1 E_THREADS
