@@ -118,6 +118,7 @@ typedef struct {
   uint64_t fq_ambiguous;   /* ... merge_reads' num_ambiguous increments */
   uint64_t fq_overlap_bases; /* ... overlap bases of the merged pairs (merge_reads overlap_len) */
   uint64_t table_slots;    /* count kernel: LDS table slots used per fine bucket (fitted to the sketch estimate) */
+  uint64_t fq_file_blocks; /* mhmkc_add_fastq[_pairs]_file: blocks of the last call */
 } mhmkc_stats;
 
 enum {
@@ -198,6 +199,15 @@ int mhmkc_add_fastq_device(mhmkc_t h, const char *d_text, uint64_t n_bytes);
 int mhmkc_add_fastq_pairs(mhmkc_t h, const char *text, uint64_t n_bytes);
 /* Same, with device-resident text (only read during the call; 4 bytes of padding as for mhmkc_add_fastq_device). */
 int mhmkc_add_fastq_pairs_device(mhmkc_t h, const char *d_text, uint64_t n_bytes);
+
+/* FASTQ file ingest with the file I/O overlapped: the file at `path` is read in blocks of
+ * MHMKC_FQ_BLOCK bytes (environment; default 256 MB) into pinned memory, each block copied to the device and parsed
+ * (as mhmkc_add_fastq / mhmkc_add_fastq_pairs) as soon as it is read, its cut last record (pair) carried into the
+ * next block; a block's extraction runs on the device while the next block is read. Errors as for the text entry
+ * points (record indices in messages count from the start of the failing block); MHMKC_EINVAL if the file cannot
+ * be opened or read. mhmkc_fastq_packed / mhmkc_fastq_fetch then hold the last block's PackedReads only. */
+int mhmkc_add_fastq_file(mhmkc_t h, const char *path);
+int mhmkc_add_fastq_pairs_file(mhmkc_t h, const char *path);
 
 /* The PackedReads of the last mhmkc_add_fastq[_pairs][_device] call on the device: d_bytes[n_bases] in the
  * PackedRead layout, d_offsets[n_reads + 1]. Valid until the next add_fastq, reset or destroy. Any

@@ -297,6 +297,11 @@ class HashTableInserter {
   void add_fastq(const std::string &text) {
     check(mhmkc_add_fastq(h_, text.data(), text.size()), h_, "mhmkc_add_fastq");
   }
+  // a FASTQ file read in blocks, each parsed and counted on the device while the next is read
+  void add_fastq_file(const std::string &path, bool pairs = false) {
+    check(pairs ? mhmkc_add_fastq_pairs_file(h_, path.c_str()) : mhmkc_add_fastq_file(h_, path.c_str()), h_,
+          "mhmkc_add_fastq_file");
+  }
   // the PackedReads of the last add_fastq, copied back (for a host that keeps them, as main.cpp does)
   void fastq_packed_reads(PackedReads &pr) const {
     uint64_t n_reads = 0, n_bases = 0;
@@ -368,6 +373,7 @@ class KmerDHT {
   void init_ctg_kmers(int max_elems) { ht_inserter.init_ctg_kmers(max_elems); }  // kmer_dht.cpp:169-172
   void add_packed_reads(const PackedReads &pr) { ht_inserter.add_packed_reads(pr); }
   void add_fastq(const std::string &text) { ht_inserter.add_fastq(text); }
+  void add_fastq_file(const std::string &path, bool pairs = false) { ht_inserter.add_fastq_file(path, pairs); }
   void flush_updates() { ht_inserter.flush_inserts(); }
   void finish_updates() { ht_inserter.insert_into_local_hashtable(local_kmers); }
   // fill the local KmerMap from a finished table in mhmkc_fetch's layout (n_longs = N_LONGS words per key)

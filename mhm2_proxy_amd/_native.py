@@ -40,6 +40,7 @@ ABI_SYMBOLS = [
     "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_add_ctgs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_device_output",
     "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
     "mhmkc_add_fastq", "mhmkc_add_fastq_device", "mhmkc_add_fastq_pairs", "mhmkc_add_fastq_pairs_device",
+    "mhmkc_add_fastq_file", "mhmkc_add_fastq_pairs_file",
     "mhmkc_fastq_packed", "mhmkc_fastq_fetch",
     "mhmkc_wait_stream", "mhmkc_set_dmin_thres", "mhmkc_set_transport", "mhmkc_minimizer_hashes",
 ]
@@ -101,6 +102,7 @@ class MhmkcStats(C.Structure):
         ("fq_ambiguous", C.c_uint64),
         ("fq_overlap_bases", C.c_uint64),
         ("table_slots", C.c_uint64),
+        ("fq_file_blocks", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -177,6 +179,8 @@ def lib() -> C.CDLL:
     L.mhmkc_add_fastq_device.argtypes = [VP, VP, U64]
     L.mhmkc_add_fastq_pairs.argtypes = [VP, C.c_char_p, U64]
     L.mhmkc_add_fastq_pairs_device.argtypes = [VP, VP, U64]
+    L.mhmkc_add_fastq_file.argtypes = [VP, C.c_char_p]
+    L.mhmkc_add_fastq_pairs_file.argtypes = [VP, C.c_char_p]
     L.mhmkc_fastq_packed.argtypes = [VP, P(VP), P(VP), P(U64), P(U64)]
     L.mhmkc_fastq_fetch.argtypes = [VP, VP, VP]
     L.mhmkc_finish.argtypes = [VP, P(U64)]

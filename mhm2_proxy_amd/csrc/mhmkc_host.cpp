@@ -20,6 +20,11 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <thread>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "../../include/mhmkc.h"
 #include "kcount_launch.hpp"
@@ -166,7 +171,10 @@ struct mhmkc {
   DevBuf d_fq_text, d_fq_chunk, d_fq_lines, d_fq_len, d_fq_tmp, d_fq_bytes, d_fq_offs, d_fq_err;
   DevBuf d_fq_recoffs, d_fq_scratch, d_fq_pairinfo, d_fq_stats, d_fq_desc;  // pair merging
   uint64_t fq_reads = 0, fq_bases = 0;
-  int add_fastq(const char *d_text, uint64_t n, bool pairs = false);
+  // consumed != nullptr: a block of a longer text (mhmkc_add_fastq_file) whose last record may be cut; only the
+  // complete records (pairs) are parsed and *consumed is the length of their text
+  int add_fastq(const char *d_text, uint64_t n, bool pairs = false, uint64_t *consumed = nullptr);
+  PinBuf fq_file_buf;  // mhmkc_add_fastq_file: two blocks (one read while the other is copied; pinned)
   // contig pass (add_ctg_kmers): contigs in the PackedRead byte layout, kept on the host until finish
   std::vector<uint8_t> ctg_bytes;
   std::vector<uint64_t> ctg_offs{0}, ctg_win{0};  // byte offsets, counted-window prefix
@@ -1399,6 +1407,7 @@ void mhmkc_destroy(mhmkc_t h) {
   for (DevBuf *b : cbufs) b->release();
   h->x_send.release();
   h->x_recv.release();
+  h->fq_file_buf.release();
   for (auto &p : h->prof) {
     h->ev_pool.push_back(p.a);
     h->ev_pool.push_back(p.b);
@@ -1438,9 +1447,10 @@ int mhmkc_wait_stream(mhmkc_t h, void *stream) {
 }
 
 // FASTQ text on the device -> PackedReads in d_fq_bytes / d_fq_offs -> add_view (fastq.hip).
-int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
+int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs, uint64_t *consumed) {
   int rc = begin_round();
   if (rc) return rc;
+  if (consumed) *consumed = 0;
   fq_reads = fq_bases = 0;
   if (pairs) st.fq_pairs = st.fq_merged = st.fq_ambiguous = st.fq_overlap_bases = 0;
   if (n == 0) return MHMKC_OK;
@@ -1465,10 +1475,12 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
       (e = hipMemcpyAsync(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
       (e = hipStreamSynchronize(stream)) != hipSuccess)
     return hip_fail(e, "fastq newline count D2H");
-  // fgets returns a last line without its newline
-  const uint64_t lines = newlines + (last != '\n' ? 1 : 0);
+  // fgets returns a last line without its newline; a block's last line without one continues in the next block
+  const uint64_t all_lines = newlines + (last != '\n' ? 1 : 0);
+  const uint64_t lines = consumed ? (pairs ? newlines / 8 * 8 : newlines / 4 * 4) : all_lines;
   const uint64_t R = lines / 4;
-  if ((e = grow(d_fq_lines, std::max<uint64_t>(lines, 1) * 8)) != hipSuccess) return hip_fail(e, "fastq lines");
+  if (consumed && R == 0) return MHMKC_OK;  // no complete record (pair) yet: the caller reads more
+  if ((e = grow(d_fq_lines, std::max<uint64_t>(all_lines, 1) * 8)) != hipSuccess) return hip_fail(e, "fastq lines");
   if ((e = grow(d_fq_len, (R + 1) * 8)) != hipSuccess || (e = grow(d_fq_offs, (R + 1) * 8)) != hipSuccess ||
       (e = grow(d_fq_err, 8)) != hipSuccess)
     return hip_fail(e, "fastq records");
@@ -1482,7 +1494,8 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
   const unsigned long long n_end = n;
   prof_begin(MHMKC_STAGE_OTHER);
   e = mhm::launch_fq_lines(d_text, n, cbase, lend, stream);
-  if (e == hipSuccess && last != '\n') e = hipMemcpyAsync(lend + lines - 1, &n_end, 8, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess && !consumed && last != '\n')
+    e = hipMemcpyAsync(lend + lines - 1, &n_end, 8, hipMemcpyHostToDevice, stream);
   if (e == hipSuccess) e = hipMemsetAsync(err_d, 0xff, 8, stream);
   if (e == hipSuccess) e = mhm::launch_fq_records(d_text, n, lend, R, len, err_d, stream);
   if (e == hipSuccess) e = mhm::fq_scan(d_fq_tmp.p, tmp_bytes, len, offs, R + 1, stream);
@@ -1567,6 +1580,11 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs) {
       default: return fail(MHMKC_EINVAL, "FASTQ text ends inside record %llu", rec);
     }
   }
+  if (consumed) {  // the text of the complete records: up to the newline of their last line
+    unsigned long long le = 0;
+    if ((e = hipMemcpy(&le, lend + lines - 1, 8, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "fastq block end");
+    *consumed = std::min<uint64_t>(n, (uint64_t)(le & mhm::FQ_LE_MASK) + 1);
+  }
   fq_reads = R_out;
   fq_bases = n_bases;
   st.reads += R_out;
@@ -1611,6 +1629,109 @@ static int add_fastq_host(mhmkc_t h, const char *text, uint64_t n_bytes, bool pa
 }
 
 int mhmkc_add_fastq(mhmkc_t h, const char *text, uint64_t n_bytes) { return add_fastq_host(h, text, n_bytes, false); }
+
+// A FASTQ file (interleaved pairs with `pairs`) read in blocks of MHMKC_FQ_BLOCK bytes (default 256 MB) into two
+// pinned buffers: while block i is copied to the device and parsed, block i + 1 is read by a reader thread (with
+// MHMKC_FQ_THREADS parallel preads, default 8), and the extraction of block i runs on the device while block i + 1
+// is parsed: file I/O overlapped with the count kernels (the reference reads its share of the
+// file with FastqReader, src/fastq.cpp:504-551, and counts after the whole read). Each block's last, possibly cut,
+// record (pair) is carried to the front of the next block (a reserve of FQ_CARRY bytes before its data).
+constexpr uint64_t FQ_CARRY = 1ull << 20;
+static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
+  if (!h) return MHMKC_EINVAL;
+  if (!path) return h->fail(MHMKC_EINVAL, "null path");
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return h->fail(MHMKC_EINVAL, "cannot open FASTQ file %s", path);
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    return h->fail(MHMKC_EINVAL, "cannot stat FASTQ file %s", path);
+  }
+  const uint64_t size = (uint64_t)sb.st_size;
+  uint64_t block = 256ull << 20;
+  if (const char *env = getenv("MHMKC_FQ_BLOCK")) block = std::max<uint64_t>(64, strtoull(env, nullptr, 10));
+  int nthr = 8;
+  if (const char *env = getenv("MHMKC_FQ_THREADS")) nthr = std::max(1, std::min(64, atoi(env)));
+  const uint64_t slot = FQ_CARRY + block + 64;  // one buffer: carry reserve | block data | padding
+  hipError_t e;
+  if ((e = h->fq_file_buf.ensure(2 * slot)) != hipSuccess) {
+    close(fd);
+    return h->hip_fail(e, "fastq file blocks");
+  }
+  char *buf[2] = {h->fq_file_buf.as<char>(), h->fq_file_buf.as<char>() + slot};
+  // block i's data: file bytes [i * block, min(size, (i + 1) * block)), read in parallel pieces
+  auto read_block = [&](uint64_t i, char *dst) -> bool {
+    const uint64_t off = i * block, len = std::min(block, size - off);
+    const uint64_t piece = (len + nthr - 1) / nthr;
+    std::vector<std::thread> th;
+    std::vector<char> ok(nthr, 1);
+    for (int t = 0; t < nthr; t++) {
+      const uint64_t a = std::min(len, t * piece), b = std::min(len, a + piece);
+      if (a == b) continue;
+      th.emplace_back([&, t, a, b] {
+        for (uint64_t p = a; p < b;) {
+          const ssize_t r = pread(fd, dst + p, (size_t)(b - p), (off_t)(off + p));
+          if (r <= 0) {
+            ok[t] = 0;
+            return;
+          }
+          p += (uint64_t)r;
+        }
+      });
+    }
+    for (auto &x : th) x.join();
+    for (char v : ok)
+      if (!v) return false;
+    return true;
+  };
+  const uint64_t n_blocks = (size + block - 1) / block;
+  int rc = MHMKC_OK;
+  uint64_t carry = 0, blocks = 0;
+  uint64_t acc[4] = {0, 0, 0, 0};  // pair statistics summed over the blocks
+  if (n_blocks && !read_block(0, buf[0] + FQ_CARRY)) rc = h->fail(MHMKC_EINVAL, "read error in FASTQ file %s", path);
+  for (uint64_t i = 0; rc == MHMKC_OK && i < n_blocks; i++) {
+    char *cur = buf[i & 1], *nxt = buf[(i + 1) & 1];
+    const uint64_t len = std::min(block, size - i * block);
+    char *text = cur + FQ_CARRY - carry;
+    const uint64_t n = carry + len;
+    const bool last = i + 1 == n_blocks;
+    bool read_ok = true;
+    std::thread reader;
+    if (!last) reader = std::thread([&, i] { read_ok = read_block(i + 1, nxt + FQ_CARRY); });
+    uint64_t used = 0;
+    if ((rc = h->resolve_slabs()) == MHMKC_OK) {  // the previous block's text may still be read by its extraction
+      if ((e = h->grow(h->d_fq_text, n + 16)) != hipSuccess ||
+          (e = hipMemcpyAsync(h->d_fq_text.p, text, n, hipMemcpyHostToDevice, h->stream)) != hipSuccess)
+        rc = h->hip_fail(e, "fastq block H2D");
+      else
+        rc = h->add_fastq(h->d_fq_text.as<char>(), n, pairs, last ? nullptr : &used);
+    }
+    if (reader.joinable()) reader.join();
+    if (rc) break;
+    if (!read_ok) {
+      rc = h->fail(MHMKC_EINVAL, "read error in FASTQ file %s", path);
+      break;
+    }
+    blocks++;
+    if (pairs) {
+      acc[0] += h->st.fq_pairs, acc[1] += h->st.fq_merged, acc[2] += h->st.fq_ambiguous, acc[3] += h->st.fq_overlap_bases;
+    }
+    if (last) break;
+    carry = n - used;  // the cut record (pair), or the whole block if it held no complete one
+    if (carry > FQ_CARRY) {
+      rc = h->fail(MHMKC_EUNSUPPORTED, "FASTQ record longer than %llu bytes", (unsigned long long)FQ_CARRY);
+      break;
+    }
+    memcpy(nxt + FQ_CARRY - carry, text + used, carry);
+  }
+  close(fd);
+  if (pairs) h->st.fq_pairs = acc[0], h->st.fq_merged = acc[1], h->st.fq_ambiguous = acc[2], h->st.fq_overlap_bases = acc[3];
+  h->st.fq_file_blocks = blocks;
+  return rc;
+}
+
+int mhmkc_add_fastq_file(mhmkc_t h, const char *path) { return add_fastq_file(h, path, false); }
+int mhmkc_add_fastq_pairs_file(mhmkc_t h, const char *path) { return add_fastq_file(h, path, true); }
 
 int mhmkc_add_fastq_pairs(mhmkc_t h, const char *text, uint64_t n_bytes) {
   return add_fastq_host(h, text, n_bytes, true);

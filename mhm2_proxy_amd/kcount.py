@@ -323,6 +323,13 @@ class KmerCounter:
         blob = text.encode("ascii") if isinstance(text, str) else bytes(text)
         self._check(N.lib().mhmkc_add_fastq_pairs(self._h, blob, len(blob)))
 
+    def add_fastq_file(self, path, pairs: bool = False) -> None:
+        """A FASTQ file (interleaved pairs with pairs=True) read in blocks into pinned memory, each block parsed
+        and counted on the device while the next is read (mhmkc_add_fastq_file: the file I/O overlapped with the
+        kernels). Block size: MHMKC_FQ_BLOCK bytes (default 256 MB). fastq_packed() then holds the last block."""
+        fn = N.lib().mhmkc_add_fastq_pairs_file if pairs else N.lib().mhmkc_add_fastq_file
+        self._check(fn(self._h, os.fsencode(str(path))))
+
     def add_fastq_tensor(self, text_t, n_bytes: int | None = None, pairs: bool = False) -> None:
         """FASTQ text already in HBM (a uint8 torch tensor on the counter's device). The parser reads whole
         aligned dwords, so the buffer must extend 4 bytes past the text: pass n_bytes <= numel - 4 to use the
