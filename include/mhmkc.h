@@ -205,7 +205,8 @@ int mhmkc_add_fastq_pairs_device(mhmkc_t h, const char *d_text, uint64_t n_bytes
  * (as mhmkc_add_fastq / mhmkc_add_fastq_pairs) as soon as it is read, its cut last record (pair) carried into the
  * next block; a block's extraction runs on the device while the next block is read. Errors as for the text entry
  * points (record indices in messages count from the start of the failing block); MHMKC_EINVAL if the file cannot
- * be opened or read. mhmkc_fastq_packed / mhmkc_fastq_fetch then hold the last block's PackedReads only. */
+ * be opened or read. mhmkc_fastq_packed / mhmkc_fastq_fetch then hold the PackedReads of the whole file (every
+ * block's, appended on the device: the later k rounds count them with mhmkc_add_reads_device). */
 int mhmkc_add_fastq_file(mhmkc_t h, const char *path);
 int mhmkc_add_fastq_pairs_file(mhmkc_t h, const char *path);
 

@@ -17,6 +17,8 @@
 // kcount_launch.hpp FQ_E_*), which is where the reference DIEs.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <rocprim/device/device_scan.hpp>
 
 #include "kcount_launch.hpp"
@@ -932,6 +934,20 @@ hipError_t launch_fq_pack(const char *text, const unsigned long long *line_end, 
   if (nb)
     hipLaunchKernelGGL(k_fq_pack, dim3((uint32_t)nb), dim3(FQ_THREADS), 0, s, text, line_end, n_rec, offs,
                        qual_offset, out, err);
+  return hipGetLastError();
+}
+
+// dst[i] = src[i] + delta (the offsets of one block's PackedReads appended to a file's; mhmkc_add_fastq_file)
+__global__ __launch_bounds__(256) void k_offs_rebase(unsigned long long *dst, const unsigned long long *src, uint64_t n,
+                                                     unsigned long long delta) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) dst[i] = src[i] + delta;
+}
+
+hipError_t launch_offs_rebase(unsigned long long *dst, const unsigned long long *src, uint64_t n, unsigned long long delta,
+                              hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>(4096, (n + 255) / 256);
+  k_offs_rebase<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(dst, src, n, delta);
   return hipGetLastError();
 }
 

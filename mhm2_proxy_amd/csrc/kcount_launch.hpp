@@ -278,6 +278,8 @@ hipError_t fq_scan(void *tmp, size_t tmp_bytes, const unsigned long long *in, un
                    uint64_t n_items, hipStream_t s);
 // newlines per FQ_CHUNK chunk -> chunk[ceil(n / FQ_CHUNK)]
 hipError_t launch_fq_count(const char *text, uint64_t n, unsigned long long *chunk, hipStream_t s);
+hipError_t launch_offs_rebase(unsigned long long *dst, const unsigned long long *src, uint64_t n, unsigned long long delta,
+                              hipStream_t s);
 // every newline, in order, from the scanned chunk counts, as one word per line: position (bits 0-39),
 // trailing whitespace count of the line it ends (bits 40-55), first character of the next line (56-63)
 constexpr int FQ_LE_BITS = 40;

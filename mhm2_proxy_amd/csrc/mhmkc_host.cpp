@@ -169,6 +169,7 @@ struct mhmkc {
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
   DevBuf d_fq_text, d_fq_chunk, d_fq_lines, d_fq_len, d_fq_tmp, d_fq_bytes, d_fq_offs, d_fq_err;
+  DevBuf d_fqa_bytes, d_fqa_offs;  // mhmkc_add_fastq_file: the PackedReads of all blocks (swapped in at the end)
   DevBuf d_fq_recoffs, d_fq_scratch, d_fq_pairinfo, d_fq_stats, d_fq_desc;  // pair merging
   uint64_t fq_reads = 0, fq_bases = 0;
   // consumed != nullptr: a block of a longer text (mhmkc_add_fastq_file) whose last record may be cut; only the
@@ -204,6 +205,7 @@ struct mhmkc {
     return code;
   }
   int hip_fail(hipError_t e, const char *what) {
+    (void)hipGetLastError();  // reported here: not again by the next launch's hipGetLastError check
     return fail(MHMKC_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
   }
 
@@ -1398,6 +1400,7 @@ void mhmkc_destroy(mhmkc_t h) {
                     &h->d_out_keys, &h->d_out_counts, &h->d_out_left,   &h->d_out_right,  &h->d_out_cursor,
                     &h->d_recv,     &h->d_xg,         &h->d_hll,        &h->d_dest,       &h->d_ohist,
                     &h->d_out2_keys, &h->d_out2_counts, &h->d_out2_left, &h->d_out2_right, &h->d_mh,
+                    &h->d_fqa_bytes, &h->d_fqa_offs,
                     &h->d_fq_text,  &h->d_fq_chunk,   &h->d_fq_lines,   &h->d_fq_len,     &h->d_fq_tmp,
                     &h->d_fq_bytes, &h->d_fq_offs,    &h->d_fq_err};
   for (DevBuf *b : bufs) b->release();
@@ -1685,6 +1688,23 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
     return true;
   };
   const uint64_t n_blocks = (size + block - 1) / block;
+  // the PackedReads of every block, appended on the device (the later k rounds count them again, as the
+  // reference keeps packed_reads_list, src/main.cpp); a buffer that grows keeps its content
+  uint64_t a_reads = 0, a_bases = 0;
+  auto keep_grow = [&](DevBuf &b, size_t used, size_t need) -> hipError_t {
+    if (need <= b.cap && b.p) return hipSuccess;
+    hipError_t ge = hipStreamSynchronize(h->stream);
+    if (ge != hipSuccess) return ge;
+    DevBuf nb;
+    if ((ge = nb.ensure(std::max(need, 2 * b.cap))) != hipSuccess) return ge;
+    if (used && b.p && (ge = hipMemcpy(nb.p, b.p, std::min(used, b.cap), hipMemcpyDeviceToDevice)) != hipSuccess) {
+      nb.release();
+      return ge;
+    }
+    b.release();
+    b = nb;
+    return hipSuccess;
+  };
   int rc = MHMKC_OK;
   uint64_t carry = 0, blocks = 0;
   uint64_t acc[4] = {0, 0, 0, 0};  // pair statistics summed over the blocks
@@ -1713,6 +1733,21 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
       break;
     }
     blocks++;
+    if (h->fq_reads) {
+      const uint64_t r = h->fq_reads, nb = h->fq_bases;
+      if ((e = keep_grow(h->d_fqa_bytes, a_bases, a_bases + nb + 64)) != hipSuccess ||
+          (e = keep_grow(h->d_fqa_offs, (a_reads + 1) * 8, (a_reads + r + 1) * 8)) != hipSuccess ||
+          (a_reads == 0 && (e = hipMemsetAsync(h->d_fqa_offs.p, 0, 8, h->stream)) != hipSuccess) ||
+          (nb && (e = hipMemcpyAsync(h->d_fqa_bytes.as<char>() + a_bases, h->d_fq_bytes.p, nb, hipMemcpyDeviceToDevice,
+                                     h->stream)) != hipSuccess) ||
+          (e = mhm::launch_offs_rebase(h->d_fqa_offs.as<unsigned long long>() + a_reads + 1,
+                                       h->d_fq_offs.as<unsigned long long>() + 1, r, a_bases, h->stream)) != hipSuccess) {
+        rc = h->hip_fail(e, "fastq file packed reads");
+        break;
+      }
+      a_reads += r;
+      a_bases += nb;
+    }
     if (pairs) {
       acc[0] += h->st.fq_pairs, acc[1] += h->st.fq_merged, acc[2] += h->st.fq_ambiguous, acc[3] += h->st.fq_overlap_bases;
     }
@@ -1725,6 +1760,15 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
     memcpy(nxt + FQ_CARRY - carry, text + used, carry);
   }
   close(fd);
+  if (rc == MHMKC_OK) {  // mhmkc_fastq_packed / mhmkc_fastq_fetch now see every block's PackedReads
+    if (a_reads == 0 && ((e = keep_grow(h->d_fqa_offs, 0, 8)) != hipSuccess ||
+                         (e = hipMemsetAsync(h->d_fqa_offs.p, 0, 8, h->stream)) != hipSuccess))
+      rc = h->hip_fail(e, "fastq file packed reads");
+    std::swap(h->d_fq_bytes, h->d_fqa_bytes);  // (the last block's extraction may still read the old buffer:
+    std::swap(h->d_fq_offs, h->d_fqa_offs);    //  both stay allocated)
+    h->fq_reads = a_reads;
+    h->fq_bases = a_bases;
+  }
   if (pairs) h->st.fq_pairs = acc[0], h->st.fq_merged = acc[1], h->st.fq_ambiguous = acc[2], h->st.fq_overlap_bases = acc[3];
   h->st.fq_file_blocks = blocks;
   return rc;

@@ -326,7 +326,8 @@ class KmerCounter:
     def add_fastq_file(self, path, pairs: bool = False) -> None:
         """A FASTQ file (interleaved pairs with pairs=True) read in blocks into pinned memory, each block parsed
         and counted on the device while the next is read (mhmkc_add_fastq_file: the file I/O overlapped with the
-        kernels). Block size: MHMKC_FQ_BLOCK bytes (default 256 MB). fastq_packed() then holds the last block."""
+        kernels). Block size: MHMKC_FQ_BLOCK bytes (default 256 MB). fastq_packed() then holds the PackedReads of
+        the whole file (for the later k rounds, as the reference keeps packed_reads_list)."""
         fn = N.lib().mhmkc_add_fastq_pairs_file if pairs else N.lib().mhmkc_add_fastq_file
         self._check(fn(self._h, os.fsencode(str(path))))
 

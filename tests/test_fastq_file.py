@@ -42,8 +42,10 @@ def test_gpu_fastq_file_equals_oracle(tmp_path, monkeypatch, k, block, variant):
     with m.KmerCounter(k, device=0) as cnt:
         cnt.add_fastq_file(path)
         st = cnt.stats()
+        gb, go = cnt.fastq_packed()  # every block's PackedReads, appended
         cnt.finish()
         got = cnt.fetch().sorted()
+    assert (go == po).all() and (gb == pb).all()
     assert st["reads"] == len(po) - 1 and st["bases"] == int(po[-1])
     assert st["fq_file_blocks"] >= (len(t) // block if block < len(t) else 1)
     _assert_table(got, pb, po, k)
@@ -78,10 +80,12 @@ def test_gpu_fastq_pairs_file_equals_oracle(tmp_path, monkeypatch, block):
     with m.KmerCounter(21, device=0) as cnt:
         cnt.add_fastq_file(path, pairs=True)
         st = cnt.stats()
+        gb, go = cnt.fastq_packed()
         cnt.finish()
         got = cnt.fetch().sorted()
     for key in ("pairs", "merged", "ambiguous", "overlap_bases"):
         assert st["fq_" + key] == pst[key], key
+    assert len(go) == len(po) and (go == po).all() and (gb == pb).all()
     _assert_table(got, pb, po, 21)
 
 
