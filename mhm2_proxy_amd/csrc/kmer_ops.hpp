@@ -317,11 +317,15 @@ MHM_HD void revcomp(const uint64_t *w, uint64_t *rc, int k) {
 template <int NL>
 MHM_HD bool kmer_less(const uint64_t *a, const uint64_t *b) {
   if (NL == 2) return (a[0] < b[0]) | ((a[0] == b[0]) & (a[1] < b[1]));  // branch-free (walk_windows)
+  // branch-free for any NL: an early return per word made the unrolled extraction walk of three- and four-word
+  // keys one divergent branch per word and window
+  bool lt = false, decided = false;
 #pragma unroll
   for (int i = 0; i < NL; i++) {
-    if (a[i] != b[i]) return a[i] < b[i];
+    lt = decided ? lt : (a[i] < b[i]);
+    decided |= a[i] != b[i];
   }
-  return false;
+  return lt;
 }
 
 // Packed-record mode: the 6-bit ext code fits into the zero low bits of the last key word.
