@@ -511,7 +511,8 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_hist(ExtractParams 
 // Global store formats of a scatter: the record words (+ the ext byte plane when not packed), or a
 // compact record (kmer_ops.hpp cmix) split into a u32 plane w[0] + a byte plane ext (coarse buckets,
 // <= 40 bits) or a u32 plane alone (fine buckets, <= 32 bits).
-enum { SF_WORDS = 0, SF_C40 = 1, SF_C32 = 2 };
+// SF_AOS2: two-word records as one 16-byte record (the fine records of mixed two-word keys, MHMKC_M2AOS)
+enum { SF_WORDS = 0, SF_C40 = 1, SF_C32 = 2, SF_AOS2 = 3 };
 
 template <int NL, bool PACKED, int SF>
 __device__ __forceinline__ void store_out(const PlaneSet &out, uint64_t dst, const uint64_t *v, uint32_t ext) {
@@ -520,6 +521,8 @@ __device__ __forceinline__ void store_out(const PlaneSet &out, uint64_t dst, con
     out.ext[dst] = (uint8_t)(v[0] >> 32);
   } else if (SF == SF_C32) {
     ((uint32_t *)out.w[0])[dst] = (uint32_t)v[0];
+  } else if (SF == SF_AOS2) {
+    ((ulonglong2 *)out.w[0])[dst] = make_ulonglong2(v[0], v[1]);
   } else {
 #pragma unroll
     for (int w = 0; w < NL; w++) out.w[w][dst] = v[w];
@@ -598,7 +601,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
   uint32_t *lstart = (uint32_t *)(smem + scatter_lds_bytes(nb));
   uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - WSUM_BYTES);
-  constexpr bool C32 = SF != SF_WORDS;  // compact: low 32 bits in stage32, the high byte (SF_C40) in sext
+  constexpr bool C32 = SF == SF_C40 || SF == SF_C32;  // compact: low 32 bits in stage32, the high byte (SF_C40) in sext
   uint64_t *stage = (uint64_t *)area;
   uint32_t *stage32 = (uint32_t *)area;
   uint16_t *sbin = C32 ? (uint16_t *)(stage32 + T) : (uint16_t *)(stage + NL * T);
@@ -684,6 +687,13 @@ constexpr bool kEStaged = MHMKC_ESTAGE != 0;
 #define MHMKC_PSTAGE 1
 #endif
 constexpr bool kPStaged = MHMKC_PSTAGE != 0;
+// Fine records of mixed two-word keys as 16-byte records instead of two u64 planes: a fine bucket's run of a
+// partition chunk is one contiguous span (64 B runs became 2 x 32 B ones in the planes), k_count loads a record
+// with one 16-byte load.
+#ifndef MHMKC_M2AOS
+#define MHMKC_M2AOS 1
+#endif
+constexpr bool kM2Aos = MHMKC_M2AOS != 0;
 
 // ------------------------------------------------------------------------------------------------
 // Mixed two-word extraction over the valid windows only (MHMKC_M2WALK). At k = 63 only 86 of a 150 bp read's
@@ -1073,7 +1083,7 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
     lim = BinLimit{p.coarse_base[ch.coarse_local], fc, fc};
   }
   unsigned long long *cur = p.fine_cursor + (uint64_t)ch.coarse_local * nf;
-  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS;
+  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C32 : (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
   if (kPStaged)
     scatter_staged<NL, PACKED, W, SF>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
   else
@@ -1654,6 +1664,10 @@ __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, c
     ((uint32_t *)ps.w[0])[idx] = (uint32_t)(key[0] | e);
     return;
   }
+  if (RecKind<NL, CMP>::M2 && kM2Aos) {
+    ((ulonglong2 *)ps.w[0])[idx] = make_ulonglong2(key[0] | e, key[NL - 1]);
+    return;
+  }
 #pragma unroll
   for (int w = 0; w < NL; w++) ps.w[w][idx] = (w == RecKind<NL, CMP>::XW && PACKED) ? (key[w] | e) : key[w];
   if (!PACKED) ps.ext[idx] = (uint8_t)e;
@@ -1746,6 +1760,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       const uint32_t idx = i < cnt ? i : cnt - 1;
       if (RK::C32) {
         nk[j][0] = ((const uint32_t *)src.w[0])[idx];
+      } else if (RK::M2 && kM2Aos) {  // one 16-byte record
+        const u32x4 v = gload4((const uint32_t *)src.w[0] + 4 * (uint64_t)idx);
+        nk[j][0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        nk[j][NL - 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
       } else {
 #pragma unroll
         for (int w = 0; w < NL; w++) nk[j][w] = src.w[w][idx];
@@ -1759,6 +1777,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     src = p.recs;
     if (RK::C32) {
       src.w[0] = (uint64_t *)((uint32_t *)src.w[0] + base);
+    } else if (RK::M2 && kM2Aos) {
+      src.w[0] += 2 * base;
     } else {
 #pragma unroll
       for (int w = 0; w < NL; w++) src.w[w] += base;
