@@ -687,12 +687,9 @@ constexpr bool kEStaged = MHMKC_ESTAGE != 0;
 #define MHMKC_PSTAGE 1
 #endif
 constexpr bool kPStaged = MHMKC_PSTAGE != 0;
-// Fine records of mixed two-word keys as 16-byte records instead of two u64 planes: a fine bucket's run of a
-// partition chunk is one contiguous span (64 B runs became 2 x 32 B ones in the planes), k_count loads a record
-// with one 16-byte load.
-#ifndef MHMKC_M2AOS
-#define MHMKC_M2AOS 1
-#endif
+// Records of mixed two-word keys as 16-byte records instead of two u64 planes (kcount_launch.hpp MHMKC_M2AOS): a
+// bucket's run of a tile or chunk is one contiguous span (64 B runs became 2 x 32 B ones in the planes), and a
+// record is one 16-byte load.
 constexpr bool kM2Aos = MHMKC_M2AOS != 0;
 
 // ------------------------------------------------------------------------------------------------
@@ -930,7 +927,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
 #endif
   const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
-  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS;
+  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
   if (kEStaged)
     scatter_staged<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
                                       p.ovf);
@@ -1013,6 +1010,13 @@ __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch
     if (RecKind<NL, CMP>::C32) {  // coarse compact record: low 32 bits + high byte
       rk[j][0] = (uint64_t)gload((const uint32_t *)src.w[0] + idx);
       rx[j] = (uint32_t)gload(src.ext + idx);
+      continue;
+    }
+    if (RecKind<NL, CMP>::M2 && kM2Aos) {  // one 16-byte record
+      const u32x4 v = gload4((const uint32_t *)src.w[0] + 4 * idx);
+      rk[j][0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      rk[j][NL - 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      rx[j] = 0u;
       continue;
     }
 #pragma unroll

@@ -215,6 +215,11 @@ inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : nl == 2 ? MHMKC_T
 #define MHMKC_PTILE2 2048
 #endif
 inline int chunk_records(int nl) { return nl == 1 ? MHMKC_PTILE1 : MHMKC_PTILE2; }
+// Mixed two-word records (33 <= k <= 63) as one 16-byte record in the first of their two planes' space, in the
+// coarse slabs and the fine buckets (0: two u64 planes)
+#ifndef MHMKC_M2AOS
+#define MHMKC_M2AOS 1
+#endif
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS); compact records keep
 // 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
 // k_count LDS: table (keys, count, 4 extension words per slot) + 128 B of scalars + the miss list of a

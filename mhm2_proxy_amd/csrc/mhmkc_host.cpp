@@ -684,8 +684,9 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
   mhm::PlaneSet rps{};
   if ((rc = set_planes(d_recv, recv_total, rps))) return rc;
   // 4. transfers, per peer in slab and plane order on both sides
-  const int np = compact ? 1 : nl;
-  const size_t wb = compact ? 4 : 8;  // bytes of a word-plane entry
+  const bool aos = mixed2 && MHMKC_M2AOS;  // one 16-byte record per entry in the first plane's place
+  const int np = (compact || aos) ? 1 : nl;
+  const size_t wb = compact ? 4 : aos ? 16 : 8;  // bytes of a word-plane entry
   std::vector<Xfer> snd, rcv;
   for (int p = 0; p < g; p++) {
     if (p == me) continue;
