@@ -511,8 +511,13 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_hist(ExtractParams 
 // Global store formats of a scatter: the record words (+ the ext byte plane when not packed), or a
 // compact record (kmer_ops.hpp cmix) split into a u32 plane w[0] + a byte plane ext (coarse buckets,
 // <= 40 bits) or a u32 plane alone (fine buckets, <= 32 bits).
-// SF_AOS2: two-word records as one 16-byte record (the fine records of mixed two-word keys, MHMKC_M2AOS)
+// SF_AOS2: two-word records as one 16-byte record (the records of mixed two-word keys, MHMKC_M2AOS)
 enum { SF_WORDS = 0, SF_C40 = 1, SF_C32 = 2, SF_AOS2 = 3 };
+// ... staged in LDS as 16-byte records too (one ds_write_b128 / ds_read_b128 instead of two 8-byte ones)
+#ifndef MHMKC_AOSSTAGE
+#define MHMKC_AOSSTAGE 1
+#endif
+constexpr bool kAosStage = MHMKC_AOSSTAGE != 0;
 
 template <int NL, bool PACKED, int SF>
 __device__ __forceinline__ void store_out(const PlaneSet &out, uint64_t dst, const uint64_t *v, uint32_t ext) {
@@ -637,6 +642,8 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       if (C32) {
         stage32[pos] = (uint32_t)rk[j][0];
         if (SF == SF_C40) sext[pos] = (uint8_t)(rk[j][0] >> 32);
+      } else if (SF == SF_AOS2 && kAosStage) {  // one 16-byte LDS write per record
+        ((ulonglong2 *)stage)[pos] = make_ulonglong2(rk[j][0], rk[j][NL - 1]);
       } else {
 #pragma unroll
         for (int w = 0; w < NL; w++) stage[w * T + pos] = rk[j][w];
@@ -669,6 +676,10 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       uint64_t v[NL];
       if (C32) {
         v[0] = (uint64_t)stage32[pos] | (SF == SF_C40 ? (uint64_t)sext[pos] << 32 : 0ull);
+      } else if (SF == SF_AOS2 && kAosStage) {
+        const ulonglong2 q = ((const ulonglong2 *)stage)[pos];
+        v[0] = q.x;
+        v[NL - 1] = q.y;
       } else {
 #pragma unroll
         for (int w = 0; w < NL; w++) v[w] = stage[w * T + pos];
