@@ -1274,6 +1274,11 @@ constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
 #ifndef MHMKC_WAVEQ
 #define MHMKC_WAVEQ 1
 #endif
+// Per-wave deferral positions and no round barrier in cold sweeps (needs MHMKC_WAVEQ; 0 = dense deferral at the
+// front of the bucket behind a barrier every round)
+#ifndef MHMKC_WDEF
+#define MHMKC_WDEF 1
+#endif
 
 // Two-pass finalize (list the slots with count >= 2, then decide them densely); 0 = one pass over all slots.
 #ifndef MHMKC_FIN2
@@ -1704,7 +1709,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   t.keys = (K *)smem;
   t.cnt = (uint32_t *)(t.keys + NL * t.cap);
   t.ext = t.cnt + t.cap;
-  // scalars live after the table in the same dynamic region (count_lds_bytes adds 128 bytes)
+  // scalars live after the table in the same dynamic region (count_lds_bytes adds 192 bytes)
   unsigned long long *s_u64 = (unsigned long long *)(t.ext + 4 * t.cap);
   unsigned long long &s_gbase = s_u64[0];
   unsigned long long *s_red = s_u64 + 1;  // [3]
@@ -1712,6 +1717,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned int &s_ovf = *(unsigned int *)(s_u64 + 5);
   unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
   unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
+  unsigned int *s_wdef = (unsigned int *)(s_u64 + 16);  // [16] per-wave deferred records of the sweep (WQ)
   // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
   constexpr int MC = miss_cap(NL, RK::C32);
   // B_OVERLAP: phase B of round r overlaps phase A of round r + 1, so the miss list is double-buffered
@@ -1720,6 +1726,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // MHMKC_WAVEQ: a miss queue per wave (MW entries of the miss space) instead of one shared list, worked off by
   // its own wave after the round barrier once it holds WQ_THR entries, and emptied after the last round
   constexpr bool WQ = MHMKC_WAVEQ != 0;
+  constexpr bool WDEF = WQ && MHMKC_WDEF != 0;
   constexpr int MW = MC / (C_THREADS / 64);
   constexpr int WQ_THR = MW / 2 < 64 ? MW / 2 : 64;
   const uint32_t wq_base = (uint32_t)(threadIdx.x >> 6) * (uint32_t)MW;
@@ -1757,10 +1764,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // multiples of 4 records: capped fine buckets are multiples of 16, the exact scan rounds them up), so one
   // address per 4 records; lanes past the end re-read the last aligned quad (inside the bucket's region).
   static_assert(!RK::C32 || R == 4, "compact rounds take one 16-byte load of 4 records per lane");
-  auto prefetch = [&](const PlaneSet &src, uint32_t cnt, uint32_t first) {
+  // nwv: NONE for a dense sweep of cnt records, else this wave's records of a re-sweep (wave-owned positions,
+  // see defer_pos; lanes past them read the bucket's first record or quad)
+  auto prefetch = [&](const PlaneSet &src, uint32_t cnt, uint32_t first, uint32_t nwv) {
+    const uint32_t dbase = first / RND * (uint32_t)(64 * R);
     if constexpr (RK::C32) {
       const uint32_t q = first + 4u * (uint32_t)tid, qmax = (cnt - 1) & ~3u;
-      const u32x4 v = gload4((const uint32_t *)src.w[0] + (q < qmax ? q : qmax));
+      const uint32_t qq = nwv == NONE ? (q < qmax ? q : qmax) : (dbase + 4u * (uint32_t)lane < nwv ? q : 0u);
+      const u32x4 v = gload4((const uint32_t *)src.w[0] + qq);
       nk[0][0] = v.x;
       nk[1][0] = v.y;
       nk[2][0] = v.z;
@@ -1772,7 +1783,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
     for (int j = 0; j < R; j++) {
       const uint32_t i = first + (uint32_t)tid + (uint32_t)j * C_THREADS;
-      const uint32_t idx = i < cnt ? i : cnt - 1;
+      const uint32_t idx = nwv == NONE ? (i < cnt ? i : cnt - 1) : (dbase + (uint32_t)(64 * j + lane) < nwv ? i : 0u);
       if (RK::C32) {
         nk[j][0] = ((const uint32_t *)src.w[0])[idx];
       } else if (RK::M2 && kM2Aos) {  // one 16-byte record
@@ -1801,6 +1812,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     if (!PACKED) src.ext += base;
   };
 
+  // Position of a record deferred to the next sweep. With per-wave queues a wave defers only records it loaded
+  // itself, so its d-th deferral goes to its own d-th record position of the sweep (wave-owned positions in round
+  // order: lanes 64 apart for one record per lane, 4 consecutive records per lane for compact quads), which it
+  // has already consumed: no other wave reads it, and the waves need no barrier between rounds. The next sweep
+  // reads the first s_wdef[w] positions of every wave w. (Shared list: the dense front of the bucket, behind
+  // the round barrier.)
+  auto defer_pos = [&]() -> uint32_t {
+    const uint32_t q = atomicAdd(&s_ovf, 1u);
+    if (!WDEF) return q;
+    const uint32_t d = atomicAdd(&s_wdef[wid], 1u), rr = d / (uint32_t)(64 * R), rem = d % (uint32_t)(64 * R);
+    return rr * RND + (RK::C32 ? (uint32_t)wid * 256u + rem : rem / 64u * C_THREADS + (uint32_t)wid * 64u + rem % 64u);
+  };
   unsigned long long my_occ = 0, my_purged = 0, my_sum = 0, my_out = 0, my_sweeps = 0, my_maxb = 0;
   unsigned long long &s_missacc = s_u64[4];  // phase-B records of this workgroup (the LDS op mix, stats)
 #if MHMKC_STAMP
@@ -1814,10 +1837,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   PlaneSet ps;
   uint32_t n;
   bucket(b, ps, n);
-  if (n) prefetch(ps, n, 0);
+  if (n) prefetch(ps, n, 0, NONE);
   while (true) {  // buckets
   my_maxb = my_maxb > n ? my_maxb : n;
   bool first_sweep = true;
+  // records of this wave in a re-sweep (NONE: the first sweep, dense over [0, n)) and the sweep's round bound
+  uint32_t nw = NONE, lim = n;
   uint32_t nb_next = 0;
   PlaneSet ps_next;
   const uint32_t b_next = b + gridDim.x;
@@ -1838,6 +1863,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       s_ovf = 0;
       s_err = 0;
     }
+    if (tid < C_THREADS / 64) s_wdef[tid] = 0;
     __syncthreads();
     STAMP(t_sw1);
     STAMP_ADD(0, t_sw1 - t_sw0);
@@ -1849,7 +1875,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     //   B. after a barrier the miss list is worked off densely, one record per lane (probing, CAS insert,
     //      counting), so the ~20 % of records that need the slow path no longer hold every wave of the
     //      workgroup in a divergent loop.
-    if (!first_sweep && n) prefetch(ps, n, 0);  // a re-sweep reads the deferred records
+    if (!first_sweep && n) prefetch(ps, n, 0, nw);  // a re-sweep reads the deferred records
     first_sweep = false;
     // a sweep of fewer than 0xC000 records cannot bring a counter to the clamp level: its rounds count
     // with non-returning adds and carry no clamp check (COLD instantiation of the round loop)
@@ -1857,13 +1883,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       constexpr bool COLD = decltype(cold_tag)::value;
       int rnd = 0, lr = 0;           // lr = rnd % 3: the round's miss counter
       uint32_t wq_n = 0;             // WQ: entries in this wave's miss queue (wave-uniform)
-      for (uint32_t r0 = 0; r0 < n; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
+      for (uint32_t r0 = 0; r0 < lim; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
         STAMP(t_r0);
         uint64_t ck[R][NL];
         uint32_t ce[R];
 #pragma unroll
         for (int j = 0; j < R; j++) {
-          const bool valid = (RK::C32 ? r0 + 4u * (uint32_t)tid + (uint32_t)j : r0 + (uint32_t)tid + (uint32_t)j * C_THREADS) < n;
+          const bool valid =
+              nw == NONE ? (RK::C32 ? r0 + 4u * (uint32_t)tid + (uint32_t)j : r0 + (uint32_t)tid + (uint32_t)j * C_THREADS) < n
+                         : (uint32_t)rnd * (uint32_t)(64 * R) + (uint32_t)(RK::C32 ? 4 * lane + j : 64 * j + lane) < nw;
 #pragma unroll
           for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
           if (PACKED) {
@@ -1879,7 +1907,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #endif
         STAMP(t_r1);
         STAMP_ADD(1, t_r1 - t_r0);
-        if (r0 + RND < n) prefetch(ps, n, r0 + RND);
+        if (r0 + RND < lim) prefetch(ps, n, r0 + RND, nw);
 #if MHMKC_EXP_LOADONLY
         {
           uint32_t acc = 0;
@@ -2011,17 +2039,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         STAMP_ADD(2, t_r2 - t_r1);
         // the next round's counter: its last readers (phase B two rounds back) are behind the previous barrier
         if (!WQ && BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
-        __syncthreads();
+        // The round barrier. A cold sweep with per-wave queues needs none: no clamp bound to keep (§3.4), every wave
+        // works off its own queue, and deferred records go to positions their own wave has consumed (defer_pos),
+        // so the waves drift apart freely until the sweep's barrier (k = 63 count 10.9 -> 9.2 ms).
+        if (!(COLD && WDEF)) __syncthreads();
         STAMP(t_r3);
         STAMP_ADD(3, t_r3 - t_r2);
-        // deferred records go back to the front of the bucket, to positions every lane has consumed
-        // (< r0 + RND), for the next sweep
+        // deferred records go back into the bucket for the next sweep, to positions already consumed (defer_pos)
         if (defer) {
 #pragma unroll
           for (int j = 0; j < R; j++) {
             if ((defer >> j) & 1u) {
-              const unsigned int pos = atomicAdd(&s_ovf, 1u);
-              store_record<NL, PACKED, CMP>(ps, pos, ck[j], ce[j]);
+              store_record<NL, PACKED, CMP>(ps, defer_pos(), ck[j], ce[j]);
             }
           }
         }
@@ -2050,8 +2079,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
                 else if (lds_add(t, r, e) >= HOT)
                   lds_clamp(t, r, e);
               } else if (r == -1) {
-                const unsigned int pos = atomicAdd(&s_ovf, 1u);
-                store_record<NL, PACKED, CMP>(ps, pos, key, e);
+                store_record<NL, PACKED, CMP>(ps, defer_pos(), key, e);
               } else {
                 s_err = 1;
               }
@@ -2091,8 +2119,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             else if (lds_add(t, r, e) >= HOT)
               lds_clamp(t, r, e);
           } else if (r == -1) {
-            const unsigned int pos = atomicAdd(&s_ovf, 1u);
-            store_record<NL, PACKED, CMP>(ps, pos, key, e);
+            store_record<NL, PACKED, CMP>(ps, defer_pos(), key, e);
           } else {
             s_err = 1;
           }
@@ -2121,7 +2148,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
     if (last_sweep && b_next < p.n_buckets) {
       bucket(b_next, ps_next, nb_next);
-      if (nb_next) prefetch(ps_next, nb_next, 0);
+      if (nb_next) prefetch(ps_next, nb_next, 0, NONE);
     }
 
 #if MHMKC_FIN2
@@ -2309,6 +2336,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     if (s_err && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
     if (last_sweep) break;
     n = s_ovf;
+    lim = n;
+    if (WDEF) {  // each wave re-reads its own deferred records; the rounds cover the largest share
+      nw = s_wdef[wid];
+      uint32_t mx = 0;
+#pragma unroll
+      for (int w = 0; w < C_THREADS / 64; w++) mx = mx > s_wdef[w] ? mx : s_wdef[w];
+      lim = (mx + (uint32_t)(64 * R) - 1) / (uint32_t)(64 * R) * RND;
+    }
     my_sweeps++;
     // overflow records were written by this workgroup: make them visible to its own loads
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");

@@ -222,7 +222,7 @@ inline int chunk_records(int nl) { return nl == 1 ? MHMKC_PTILE1 : MHMKC_PTILE2;
 #endif
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS); compact records keep
 // 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
-// k_count LDS: table (keys, count, 4 extension words per slot) + 128 B of scalars + the miss list of a
+// k_count LDS: table (keys, count, 4 extension words per slot) + 192 B of scalars + the miss list of a
 // round's phase B (key words + ext code per entry); together <= 160 KiB.
 #ifndef MHMKC_CAP2
 #define MHMKC_CAP2 4000
@@ -232,7 +232,7 @@ __host__ __device__ constexpr int count_cap(int nl, bool cmp = false) {
   return ((cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? MHMKC_CAP2 : nl == 3 ? 3264 : 2752) / C_SPLIT) & ~3;
 }
 __host__ __device__ constexpr size_t count_table_bytes(int nl, bool cmp = false) {
-  return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 128;
+  return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 192;
 }
 __host__ __device__ constexpr int miss_cap(int nl, bool cmp = false) {
   return (int)(((C_LDS - count_table_bytes(nl, cmp)) / (count_key_bytes(cmp) * nl + 4)) & ~(size_t)63);

@@ -97,7 +97,7 @@ def test_batches_equal_single(k):
     assert_tables_equal(many, one, "5 batches vs 1")
 
 
-@pytest.mark.parametrize("k,wide", [(21, True), (15, False), (17, False), (63, False)])
+@pytest.mark.parametrize("k,wide", [(21, True), (15, False), (17, False), (63, False), (77, False)])
 def test_forced_overflow_sweeps(k, wide, monkeypatch):
     """Tiny LDS tables force the multi-sweep path (a closed table overflows whole keys to the next sweep).
     Compact records (k <= 21) need >= 2k - 34 fine bits, so k = 15, 17 cover them with one fine bucket."""
