@@ -1728,7 +1728,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   constexpr bool WQ = MHMKC_WAVEQ != 0;
   constexpr bool WDEF = WQ && MHMKC_WDEF != 0;
   constexpr int MW = MC / (C_THREADS / 64);
+#ifdef MHMKC_WQ_DIV  // (A/B: work the queue off at MW / MHMKC_WQ_DIV entries)
+  constexpr int WQ_THR = MW / MHMKC_WQ_DIV < 64 ? MW / MHMKC_WQ_DIV : 64;
+#else
   constexpr int WQ_THR = MW / 2 < 64 ? MW / 2 : 64;
+#endif
   const uint32_t wq_base = (uint32_t)(threadIdx.x >> 6) * (uint32_t)MW;
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
