@@ -2,7 +2,10 @@
 """Benchmark of the MI355X-native kcount stage (BASELINE.json metric: k-mers/s, whole node, k=21, 150 bp).
 
   python bench.py --gpus N --steps K --warmup W
-  (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... bench.py)
+  (N > 1: either under python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...,
+   or plain: bench.py then starts the N ranks itself as child processes, before it touches the GPU)
+  python bench.py --gpus N --transport host ...   N ranks exchanging through the host-staged transport
+   (mhmkc_set_transport over gloo); ranks share the visible GPUs round-robin, so N ranks can be rehearsed on one GPU
 
 A step = one full counting round of this rank's resident read shard: extract -> coarse partition ->
 RCCL all-to-all (N > 1) -> fine partition -> LDS hash-table count -> finalize + compacted output table,
@@ -68,6 +71,10 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--kmermap-sample-rows", type=int, default=4_000_000,
                     help="rows of the fetched table put into the C++ adapter's KmerMap to time it (0: skip)")
+    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+                    help="exchange between ranks (N > 1): rccl = one rank per GPU, RCCL grouped send/recv over xGMI; "
+                         "host = mhmkc_set_transport over a gloo process group (pinned D2H, gloo, H2D), ranks share "
+                         "the visible GPUs round-robin (a rehearsal of the multi-rank path on one GPU)")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc passes (profiles/), if present")
     return ap.parse_args()
@@ -230,8 +237,44 @@ def cpu_baseline(b, o, k, n_reads, threads):
                       f"{dt:.1f} s"}
 
 
+def launch_ranks(n: int) -> int:
+    """--gpus N > 1 without torch.distributed.run: start the N ranks as child processes of this one (this process
+    never touches the GPU: no exec from a GPU process), with the env torchrun would give them (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT). The first rank to fail ends the others; the exit code
+    is the first non-zero one."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MHMKC_BENCH_CHILD="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rc, live = 0, list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                print(f"bench.py: rank {procs.index(p)} exited with {r}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus))
     import numpy as np
     import torch
 
@@ -239,16 +282,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-        world = args.gpus if world == 1 else world
-    torch.cuda.set_device(local)
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    host_xp = world > 1 and args.transport == "host"
+    n_dev = torch.cuda.device_count()
+    if n_dev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    if not host_xp and local >= n_dev:
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local} (one rank per GPU, RCCL), but {n_dev} visible; "
+                         "use --transport host to run several ranks on one GPU")
+    local_dev = local % n_dev if host_xp else local
+    torch.cuda.set_device(local_dev)
     dist = None
+    cdev = torch.device("cpu") if host_xp else torch.device("cuda", local_dev)  # where the timing reductions run
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if host_xp:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_dev))
+    local = local_dev
 
     import mhm2_proxy_amd as m
 
@@ -301,11 +355,12 @@ def main():
     torch.cuda.synchronize()
 
     cid = None
-    if world > 1:
+    if world > 1 and not host_xp:
         obj = [m.comm_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         cid = obj[0]
-    counter = m.KmerCounter(k, device=local, rank=rank, n_ranks=world, comm_id=cid)
+    counter = m.KmerCounter(k, device=local, rank=rank, n_ranks=world, comm_id=cid,
+                            transport=m.TorchDistTransport() if host_xp else None)
     counter.set_profiling(not args.no_profile_events)
 
     def step():
@@ -342,10 +397,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([occ_total], dtype=torch.float64, device=dev)
+        c = torch.tensor([occ_total], dtype=torch.float64, device=cdev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         occ_total = int(c.item())
 
@@ -414,7 +469,7 @@ def main():
             torch.cuda.synchronize()
             dt = time.perf_counter() - t1
             if dist:
-                tt_ = torch.tensor([dt], dtype=torch.float64, device=dev)
+                tt_ = torch.tensor([dt], dtype=torch.float64, device=cdev)
                 dist.all_reduce(tt_, op=dist.ReduceOp.MAX)
                 dt = float(tt_.item())
             if i:  # the first is a warm-up (pinned staging, chunk events)
@@ -452,7 +507,9 @@ def main():
             "config": {"workload": (f"{args.config}: {total} x {L}bp synthetic reads ({R} on rank 0), k={k}, genome "
                                     f"{G} bp, seed {seed}"),
                        "k": k, "reads_total": total, "reads_per_gpu": R, "read_len": L, "genome_len": G,
-                       "occurrences_per_step": occ_total // steps, "parallelism": f"hash-range x{world}"},
+                       "occurrences_per_step": occ_total // steps, "parallelism": f"hash-range x{world}",
+                       "transport": args.transport if world > 1 else None,
+                       "physical_gpus": min(world, n_dev) if host_xp else world},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "stages_ms_per_step": {s_: round(v, 3) for s_, v in per_step.items() if launches.get(s_)},
@@ -477,6 +534,15 @@ def main():
             "distinct_per_gpu": st["distinct"] if st else None,
             "n_out_per_gpu": st["n_out"] if st else None,
             "bytes_sent_rank0": st["bytes_sent"] if st else None,
+            "exchange": ({"transport": ("host-staged (mhmkc_set_transport over gloo: pinned D2H, gloo all-to-all-v, "
+                                        f"H2D), {world} ranks on {min(world, n_dev)} physical GPU(s)")
+                          if host_xp else "RCCL grouped ncclSend/ncclRecv over xGMI, one rank per GPU",
+                          "ms_per_step_rank0": round(per_step.get("exchange", 0.0), 3),
+                          "bytes_sent_per_step_rank0": st["bytes_sent"], "bytes_recv_per_step_rank0": st["bytes_recv"],
+                          "bytes_sent_per_occurrence": round(st["bytes_sent"] / max(1, st["occurrences"]), 3),
+                          "GBps_rank0": round(st["bytes_sent"] / (per_step["exchange"] * 1e-3) / 1e9, 2)
+                          if per_step.get("exchange") else None}
+                         if world > 1 and st else None),
             "synth_seconds": round(gen_s, 2),
         }
         if args.input == "fastq-file":

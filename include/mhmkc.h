@@ -204,8 +204,10 @@ int mhmkc_add_fastq_pairs_device(mhmkc_t h, const char *d_text, uint64_t n_bytes
  * MHMKC_FQ_BLOCK bytes (environment; default 256 MB) into pinned memory, each block copied to the device and parsed
  * (as mhmkc_add_fastq / mhmkc_add_fastq_pairs) as soon as it is read, its cut last record (pair) carried into the
  * next block; a block's extraction runs on the device while the next block is read. Errors as for the text entry
- * points (record indices in messages count from the start of the failing block); MHMKC_EINVAL if the file cannot
- * be opened or read. mhmkc_fastq_packed / mhmkc_fastq_fetch then hold the PackedReads of the whole file (every
+ * points (record indices in messages count from the start of the failing block; the message names the block and
+ * the file byte its text starts at); MHMKC_EINVAL if the file cannot be opened or read. A failure after the first
+ * block leaves the earlier blocks' reads in the round: mhmkc_finish then fails with MHMKC_ESTATE until
+ * mhmkc_reset. mhmkc_fastq_packed / mhmkc_fastq_fetch then hold the PackedReads of the whole file (every
  * block's, appended on the device: the later k rounds count them with mhmkc_add_reads_device). */
 int mhmkc_add_fastq_file(mhmkc_t h, const char *path);
 int mhmkc_add_fastq_pairs_file(mhmkc_t h, const char *path);

@@ -2061,8 +2061,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         if constexpr (WQ) {
           // B. this wave's queue, 64 entries at a time once it holds WQ_THR (all of it after the sweep's last
           // round): whole-wave batches, and every wave takes its own share of the slow path, so no wave holds
-          // the next barrier with the misses of all the others
-          const bool last_round = r0 + RND >= n;
+          // the next barrier with the misses of all the others. The sweep's rounds run while r0 < lim (lim = n
+          // in a first sweep; in a re-sweep lim >= n covers the largest wave share of deferred records), so the
+          // queue is drained in the round the loop ends with.
+          const bool last_round = r0 + RND >= lim;
           while (wq_n >= (uint32_t)WQ_THR || (last_round && wq_n > 0)) {
             const uint32_t take = wq_n < 64u ? wq_n : 64u;
             const uint32_t qb = wq_n - take;

@@ -188,6 +188,7 @@ struct mhmkc {
   std::string err;
   bool finished = false;
   bool began = false;
+  bool partial = false;  // a failed mhmkc_add_fastq_file left part of a file in the round (finish refuses it)
   uint64_t n_out = 0;
   mhmkc_stats st{};
   bool profiling = false;
@@ -931,6 +932,7 @@ int mhmkc::handoff() {
 // Fine buckets are capped at 1.25x their expected size (+256): a single scatter pass, no histogram. If a
 // bucket overflows, the count kernel returns at once and the pass is redone with part_hist + scan.
 int mhmkc::finish(uint64_t *n_out_ret) {
+  if (partial) return fail(MHMKC_ESTATE, "a failed mhmkc_add_fastq_file left part of the file in this round; call mhmkc_reset");
   int rc = begin_round();
   if (rc) return rc;
   if ((rc = resolve_slabs())) return rc;
@@ -1728,7 +1730,13 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
         rc = h->add_fastq(h->d_fq_text.as<char>(), n, pairs, last ? nullptr : &used);
     }
     if (reader.joinable()) reader.join();
-    if (rc) break;
+    if (rc) {  // locate the bad record: the parser numbers records from the start of this block's text
+      char where[160];
+      snprintf(where, sizeof where, " (FASTQ file block %llu, whose text starts at file byte %llu)",
+               (unsigned long long)i, (unsigned long long)(i * block - carry));
+      h->err += where;
+      break;
+    }
     if (!read_ok) {
       rc = h->fail(MHMKC_EINVAL, "read error in FASTQ file %s", path);
       break;
@@ -1761,6 +1769,9 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
     memcpy(nxt + FQ_CARRY - carry, text + used, carry);
   }
   close(fd);
+  // earlier blocks may already be in the round (counted reads, extractions enqueued): the handle refuses to
+  // finish a round that holds part of a file until mhmkc_reset
+  if (rc && blocks) h->partial = true;
   if (rc == MHMKC_OK) {  // mhmkc_fastq_packed / mhmkc_fastq_fetch now see every block's PackedReads
     if (a_reads == 0 && ((e = keep_grow(h->d_fqa_offs, 0, 8)) != hipSuccess ||
                          (e = hipMemsetAsync(h->d_fqa_offs.p, 0, 8, h->stream)) != hipSuccess))
@@ -1964,6 +1975,7 @@ int mhmkc_reset(mhmkc_t h) {
   h->fq_reads = h->fq_bases = 0;
   h->finished = false;
   h->began = false;
+  h->partial = false;
   h->n_out = 0;
   memset(&h->st, 0, sizeof h->st);
   if ((e = hipMemsetAsync(h->d_err.p, 0, 16, h->stream)) != hipSuccess) return h->hip_fail(e, "reset");

@@ -105,7 +105,18 @@ def test_gpu_fastq_file_errors(tmp_path, monkeypatch):
         with pytest.raises(m.MhmkcError) as e:
             cnt.add_fastq_file(_write(tmp_path, "bad.fq", b"\n".join(bad) + b"\n"))
         assert str(e.value).startswith("MHMKC_EBADCHAR"), str(e.value)
-    trunc = b"\n".join(lines[:-2]) + b"\n"  # the last record lacks its '+' and quality lines
+        # the message locates the failing block in the file, and the round that holds the earlier
+        # blocks refuses to finish until reset
+        assert re.search(r"FASTQ file block [1-9]\d*, whose text starts at file byte [1-9]\d*", str(e.value)), str(e.value)
+        with pytest.raises(m.MhmkcError) as e2:
+            cnt.finish()
+        assert str(e2.value).startswith("MHMKC_ESTATE"), str(e2.value)
+        cnt.reset()
+        cnt.add_fastq_file(_write(tmp_path, "good.fq", b"\n".join(lines) + b"\n"))
+        cnt.finish()
+        from common import assert_tables_equal, oracle_table
+        assert_tables_equal(cnt.fetch(), oracle_table(b, o, 21), "after reset")
+    trunc =b"\n".join(lines[:-2]) + b"\n"  # the last record lacks its '+' and quality lines
     with m.KmerCounter(21, device=0) as cnt:
         with pytest.raises(m.MhmkcError) as e:
             cnt.add_fastq_file(_write(tmp_path, "trunc.fq", trunc))

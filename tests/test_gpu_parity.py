@@ -113,6 +113,24 @@ def test_forced_overflow_sweeps(k, wide, monkeypatch):
     check_stats(st)
 
 
+@pytest.mark.parametrize("k,wide", [(15, False), (21, True), (63, False)])
+def test_forced_overflow_hot_sweep(k, wide, monkeypatch):
+    """A hot first sweep (>= 0xC000 records: the checked round loop with its round barrier and clamp) that
+    overflows a 64-slot table: the poly-A k-mer's bucket also holds ~100-200 distinct keys of the random reads,
+    so keys are deferred with the per-wave defer positions, then counted by a re-sweep with its own round bound
+    (no earlier test overflowed a non-cold sweep)."""
+    b, o = hot_set()
+    exp = oracle_table(b, o, k)
+    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
+    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    if wide:
+        monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
+    got, st = hip_table(b, o, k)
+    assert st["max_bucket"] >= 0xC000, st["max_bucket"]
+    assert st["overflow_sweeps"] > 0
+    assert_tables_equal(got, exp, f"hot sweep overflow k={k}")
+
+
 def test_add_seqs_matches_packed():
     b, o = synth_set(500, 5000, 21)
     pr = m.PackedReads.from_arrays(b, o)
@@ -383,7 +401,9 @@ def test_analyze_kmers_dmin_thres(k):
     m.analyze_kmers(k, 0, 33, [m.PackedReads.from_arrays(b, o)], 3, [], dht)
     exp = oracle_table(b, o, k, dmin_thres=3)
     assert_tables_equal(dht.table, exp, "analyze_kmers dmin 3")
-    assert len(exp) != len(oracle_table(b, o, k, dmin_thres=2)) or True
+    # the input must make dmin 3 matter, or the check above could not tell set_dmin_thres from a no-op
+    with pytest.raises(AssertionError):
+        assert_tables_equal(dht.table, oracle_table(b, o, k, dmin_thres=2), "dmin 3 vs 2")
     dht.counter.close()
 
 

@@ -57,16 +57,22 @@ def test_ranks_equal_single_rank(k, world, seed, tmp_path):
     check_parts(parts, k, oracle_table(b, o, k), f"union of {world} ranks, k={k}")
 
 
-@pytest.mark.parametrize("k,world,seed", [(21, 3, 721), (63, 2, 763)])
+@pytest.mark.parametrize("k,world,seed", [(21, 3, 721), (33, 2, 733), (55, 3, 755), (63, 2, 763), (63, 3, 764),
+                                          (77, 2, 777), (99, 3, 799)])
 def test_minimizer_owner_handoff(k, world, seed, tmp_path):
-    """MHMKC_OWNER_MINIMIZER: after finish every k-mer is on its get_kmer_target_rank, as dbjg expects."""
+    """MHMKC_OWNER_MINIMIZER: after finish every k-mer is on its get_kmer_target_rank, as dbjg expects (every
+    row checked against the oracle's target rank; m = 15/23/27 and one to four key words)."""
     parts = run_ranks(k, world, tmp_path, seed=seed, minimizer=True)
     b, o = synth_set(1200, 9000, seed)
     check_parts(parts, k, oracle_table(b, o, k), f"minimizer owners, k={k}")
     nl = k // 32 + 1
+    L = O.oracle()
+    mlen = L.orc_minimizer_len(k)
     for r, p in enumerate(parts):
-        for key in p["keys"][:400]:
-            assert O.target_rank(key[:nl], k, world) == r
+        keys = np.ascontiguousarray(p["keys"][:, :nl], dtype=np.uint64)
+        owner = np.fromiter((L.orc_kmer_target_rank(keys[i].ctypes.data, k, nl, world) for i in range(len(keys))),
+                            dtype=np.int64, count=len(keys))
+        assert (owner == r).all(), f"rank {r}: {(owner != r).sum()} rows not on their target rank (m={mlen})"
     assert sum(int(p["handoff_sent"]) for p in parts) == sum(int(p["handoff_recv"]) for p in parts) > 0
 
 
