@@ -69,8 +69,8 @@ def parse():
                          "in blocks into pinned memory, each block parsed and counted while the next is read "
                          "(mhmkc_add_fastq_file): the step includes the file read and the H2D")
     ap.add_argument("--no-profile-events", action="store_true")
-    ap.add_argument("--kmermap-sample-rows", type=int, default=4_000_000,
-                    help="rows of the fetched table put into the C++ adapter's KmerMap to time it (0: skip)")
+    ap.add_argument("--kmermap-sample-rows", type=int, default=-1,
+                    help="rows of the fetched table put into the C++ adapter's KmerMap to time it (-1: all, 0: skip)")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                     help="exchange between ranks (N > 1): rccl = one rank per GPU, RCCL grouped send/recv over xGMI; "
                          "host = mhmkc_set_transport over a gloo process group (pinned D2H, gloo, H2D), ranks share "
@@ -112,14 +112,15 @@ def lds_floor_seconds(st: dict, k: int) -> tuple:
     return t, b
 
 
-def kmermap_fill_ms(table, k: int, sample_rows: int):
-    """KmerMap materialisation on the host: the first sample_rows rows of the fetched table
-    go through the C++ adapter's fill loop (tools/bin/kmermap_fill, built by build(): KmerMap<MAX_K> is a
-    std::unordered_map, one thread, the emplace loop of KmerDHT::load_table / insert_into_local_hashtable),
-    timed in that process and extrapolated linearly to the whole table (a lower bound: a larger map misses
-    the caches more)."""
+def kmermap_fill_ms(table, k: int, sample_rows: int, ordered: bool):
+    """KmerMap materialisation on the host: the first sample_rows rows of the fetched table go
+    into the C++ adapter's KmerMap<MAX_K> (include/mhmkc_kcount.hpp: open addressing with one-byte tags, the
+    reference's bytell_hash_map family, src/utils.hpp:57-64) through KmerDHT::load_table's fill loop
+    (tools/bin/kmermap_fill, built by build(); one thread, as insert_into_local_hashtable runs per rank), timed in
+    that process; ordered: the rows came from mhmkc_fetch_ordered (the map's slot order). The whole table by
+    default; a sample is extrapolated linearly (a lower bound: a larger map misses the caches more)."""
     tool = ROOT / "tools" / "bin" / "kmermap_fill"
-    n = min(len(table), sample_rows)
+    n = min(len(table), sample_rows) if sample_rows >= 0 else len(table)
     if not sample_rows or not n or not tool.exists():
         return None
     import subprocess
@@ -134,9 +135,9 @@ def kmermap_fill_ms(table, k: int, sample_rows: int):
         np.ascontiguousarray(table.counts[:n]).tofile(pre + ".counts")
         np.ascontiguousarray(table.left[:n]).view(np.uint8).tofile(pre + ".left")
         np.ascontiguousarray(table.right[:n]).view(np.uint8).tofile(pre + ".right")
-        r = subprocess.run([str(tool), str(k), str(n), pre], capture_output=True, text=True, timeout=300)
+        r = subprocess.run([str(tool), str(k), str(n), pre], capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
-            return {"error": r.stderr.strip()[-200:]}
+            return {"error": (r.stdout + r.stderr).strip()[-300:]}
         j = json.loads(r.stdout.strip().splitlines()[-1])
     finally:
         import shutil
@@ -144,7 +145,10 @@ def kmermap_fill_ms(table, k: int, sample_rows: int):
         shutil.rmtree(d, ignore_errors=True)
     return {"sample_rows": n, "sample_ms": j["ms"], "rows": len(table),
             "ms_extrapolated": round(j["ms"] * len(table) / n, 1),
-            "kind": "C++ adapter KmerMap<MAX_K> (std::unordered_map), 1 thread, tools/cpp/kmermap_fill.cpp"}
+            "ms_per_row_emplace_loop": round(j["ms_emplace_loop"] / n * 1e6, 2),
+            "order": "mhmkc_fetch_ordered (KmerMap slot order)" if ordered else "mhmkc_fetch (unordered)",
+            "kind": "C++ adapter KmerMap<MAX_K> (open addressing, 1-byte tags, huge pages), KmerDHT::load_table's "
+                    "prefetched fill, 1 thread, tools/cpp/kmermap_fill.cpp"}
 
 
 def survey_model_bytes(st: dict, k: int, n_reads: int, read_len: int) -> float:
@@ -447,7 +451,12 @@ def main():
     d2h_ms = (time.perf_counter() - t1) * 1e3
     d2h = {"ms": round(d2h_ms, 2), "rows": len(table), "bytes": int(len(table) * (8 * counter.n_longs + 4)),
            "GBps": round(len(table) * (8 * counter.n_longs + 4) / (d2h_ms * 1e-3) / 1e9, 2) if d2h_ms else None}
-    kmermap = kmermap_fill_ms(table, k, args.kmermap_sample_rows) if rank == 0 else None
+    del table
+    # the same table in the KmerMap's slot order (device sort), then the adapter's fill
+    t1 = time.perf_counter()
+    table = counter.fetch(ordered=True)
+    d2h["ordered_ms"] = round((time.perf_counter() - t1) * 1e3, 2)
+    kmermap = kmermap_fill_ms(table, k, args.kmermap_sample_rows, True) if rank == 0 else None
     del table
 
     # the same step from reads in pinned host memory: chunked H2D on a copy stream, each chunk extracted as
@@ -530,7 +539,8 @@ def main():
             "h2d_inclusive": h2d,
             "d2h_fetch": d2h,
             "kmermap": kmermap,
-            "d2h_kmermap_ms": round(d2h["ms"] + kmermap["ms_extrapolated"], 1) if kmermap else None,
+            "d2h_kmermap_ms": round(d2h["ordered_ms"] + kmermap["ms_extrapolated"], 1)
+            if kmermap and "ms_extrapolated" in kmermap else None,
             "distinct_per_gpu": st["distinct"] if st else None,
             "n_out_per_gpu": st["n_out"] if st else None,
             "bytes_sent_rank0": st["bytes_sent"] if st else None,

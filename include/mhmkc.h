@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 7
+#define MHMKC_ABI_VERSION 8
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -248,6 +248,26 @@ int mhmkc_finish(mhmkc_t h, uint64_t *n_out);
  * counts[n_out], left[n_out], right[n_out] ('A','C','G','T','F' or 'X'). Order is unspecified, as the
  * reference's KmerMap iteration order is. Replaces the KmerMap fill (kcount_cpu.cpp:503-522). */
 int mhmkc_fetch(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right);
+
+/* The hash the C++ adapter's KmerMap (include/mhmkc_kcount.hpp) places a key with: a multiply-xorshift mix of its
+ * n_longs words; the map's home slot for a key is the top log2(capacity) bits. */
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+static inline uint64_t mhmkc_map_hash(const uint64_t *w, int n_longs) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int i = 0; i < n_longs; i++) {
+    h = (h ^ w[i]) * 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 31;
+  }
+  h *= 0x94D049BB133111EBull;
+  return h ^ (h >> 29);
+}
+
+/* mhmkc_fetch with the rows ordered by the top 32 bits of mhmkc_map_hash (a radix sort on the device): filling a
+ * KmerMap in that order walks its slot array once from front to back instead of touching a random slot per row
+ * (insert_into_local_hashtable's loop, src/kcount/kcount_cpu.cpp:503-522). At most 2^32-1 rows. */
+int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right);
 
 /* Device pointers of the finished table (valid until the next reset/destroy). */
 int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,

@@ -4,8 +4,8 @@
 // against the same names:
 //   Kmer<MAX_K>                      src/kmer.hpp:61-160   (longs layout, set_k/get_k, hash, revcomp, ...)
 //   KmerCounts                       src/kcount/kmer_dht.hpp:62-68
-//   KmerMap<MAX_K>                   src/kcount/kmer_dht.hpp:92-93 (std::unordered_map here; bytell is vendored
-//                                    in the reference, the container type does not affect the contents)
+//   KmerMap<MAX_K>                   src/kcount/kmer_dht.hpp:92-93 (an open-addressing map, as the reference's
+//                                    bytell_hash_map; the container type does not affect the contents)
 //   PackedReads                      src/packed_reads.hpp:120-167 (contiguous bytes + offsets)
 //   HashTableInserter<MAX_K>         src/kcount/kmer_dht.hpp:95-116
 //   SeqBlockInserter<MAX_K>          src/kcount/kcount.hpp:57-69
@@ -16,6 +16,7 @@
 // gzip through zlib: link with -lz.
 #pragma once
 
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <zlib.h>
 
@@ -25,9 +26,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <memory>
 #include <string>
 #include <algorithm>
+#include <type_traits>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "mhmkc.h"
@@ -172,8 +176,211 @@ struct KmerCounts {
   char left = 0, right = 0;
 };
 
+// KmerMap<MAX_K>: an open-addressing map in the spirit of the reference's ska::bytell_hash_map (USE_BYTELL,
+// src/utils.hpp:57-64; KmerMap = HASH_TABLE<Kmer<MAX_K>, KmerCounts>, src/kcount/kmer_dht.hpp:92-93): one flat slot
+// array, linear probing over a power-of-two capacity, a one-byte tag per slot (0 empty, 0x80 | 7 hash bits) so
+// that a probe compares keys only on a tag match, load <= 7/8. It offers what the reference's callers use
+// (find / end, begin..end iteration, insert / emplace / operator[], size, reserve, clear, swap; no erase: kcount
+// and dbjg never erase) plus fill(): the bulk insert of a fetched table with the slots of the next rows
+// prefetched, so that filling a table larger than the caches is not one DRAM round trip per row
+// (insert_into_local_hashtable's loop, src/kcount/kcount_cpu.cpp:503-522; a node-allocating std::unordered_map
+// took 136 ns per row at C2).
 template <int MAX_K>
-using KmerMap = std::unordered_map<Kmer<MAX_K>, KmerCounts, KmerHash<MAX_K>>;
+class KmerMap {
+ public:
+  using key_type = Kmer<MAX_K>;
+  using mapped_type = KmerCounts;
+  using value_type = std::pair<key_type, mapped_type>;  // first is not const: slots move when the map grows
+
+  template <bool CONST>
+  class iter {
+    using M = typename std::conditional<CONST, const KmerMap, KmerMap>::type;
+    using V = typename std::conditional<CONST, const value_type, value_type>::type;
+    M *m_ = nullptr;
+    size_t i_ = 0;
+    void skip() {
+      while (i_ < m_->cap_ && !m_->tag_[i_]) i_++;
+    }
+    friend class KmerMap;
+
+   public:
+    iter() = default;
+    iter(M *m, size_t i, bool do_skip) : m_(m), i_(i) {
+      if (do_skip) skip();
+    }
+    operator iter<true>() const { return iter<true>(m_, i_, false); }
+    V &operator*() const { return m_->slot_[i_]; }
+    V *operator->() const { return &m_->slot_[i_]; }
+    iter &operator++() {
+      i_++;
+      skip();
+      return *this;
+    }
+    iter operator++(int) {
+      iter t = *this;
+      ++*this;
+      return t;
+    }
+    bool operator==(const iter &o) const { return i_ == o.i_; }
+    bool operator!=(const iter &o) const { return i_ != o.i_; }
+  };
+  using iterator = iter<false>;
+  using const_iterator = iter<true>;
+
+  KmerMap() = default;
+  size_t size() const { return size_; }
+  bool empty() const { return size_ == 0; }
+  size_t bucket_count() const { return cap_; }
+  iterator begin() { return iterator(this, 0, true); }
+  iterator end() { return iterator(this, cap_, false); }
+  const_iterator begin() const { return const_iterator(this, 0, true); }
+  const_iterator end() const { return const_iterator(this, cap_, false); }
+  void clear() {
+    if (cap_) std::memset(tag_.get(), 0, cap_);
+    size_ = 0;
+  }
+  void swap(KmerMap &o) {
+    std::swap(tag_, o.tag_);
+    std::swap(slot_, o.slot_);
+    std::swap(cap_, o.cap_);
+    std::swap(size_, o.size_);
+    std::swap(shift_, o.shift_);
+  }
+  void reserve(size_t n) {
+    size_t c = 16;
+    while (c - c / 8 < n) c <<= 1;
+    if (c > cap_) rehash(c);
+  }
+
+  iterator find(const key_type &k) {
+    if (!cap_) return end();
+    const size_t i = locate(k, hash_of(k));
+    return iterator(this, tag_[i] ? i : cap_, false);
+  }
+  const_iterator find(const key_type &k) const {
+    const size_t i = cap_ ? const_cast<KmerMap *>(this)->locate(k, hash_of(k)) : 0;
+    return const_iterator(this, cap_ && tag_[i] ? i : cap_, false);
+  }
+  size_t count(const key_type &k) const { return find(k) != end(); }
+  std::pair<iterator, bool> emplace(const key_type &k, const mapped_type &v) { return put(k, v, hash_of(k)); }
+  std::pair<iterator, bool> insert(const value_type &kv) { return put(kv.first, kv.second, hash_of(kv.first)); }
+  mapped_type &operator[](const key_type &k) { return put(k, mapped_type(), hash_of(k)).first->second; }
+
+  // Bulk insert of n finished rows in mhmkc_fetch's layout (keys: N_LONGS words per row). Rows whose key is
+  // already present keep the present entry (as insert does).
+  void fill(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n) {
+    reserve(size_ + n);
+    // three stages per row: A (row i + kAhead2) hashes the key and prefetches its home tags; B (row i + kAhead1) scans the
+    // tags, now cached, for the slot the insert will take (the end of the probe run: at load 3/4 it is several cache
+    // lines past the home slot) and prefetches that slot; C (row i) inserts
+    constexpr int kAhead2 = 48, kAhead1 = 16, kRing = 64;
+    uint64_t h[kRing];
+    const int nl = key_type::N_LONGS;
+    auto stage_a = [&](uint64_t j) {
+      h[j % kRing] = hash_words(keys + j * nl);
+      __builtin_prefetch(&tag_[home(h[j % kRing])], 1, 1);
+    };
+    auto stage_b = [&](uint64_t j) {
+      const uint64_t hj = h[j % kRing];
+      const uint8_t t = tag_of(hj);
+      size_t i = home(hj);
+      for (int q = 0; q < 64 && tag_[i] && tag_[i] != t; q++) i = (i + 1) & (cap_ - 1);
+      __builtin_prefetch(&slot_[i], 1, 1);
+    };
+    for (uint64_t j = 0; j < n && j < (uint64_t)kAhead2; j++) stage_a(j);
+    for (uint64_t j = 0; j < n && j < (uint64_t)kAhead1; j++) stage_b(j);
+    for (uint64_t i = 0; i < n; i++) {
+      if (i + kAhead2 < n) stage_a(i + kAhead2);
+      if (i + kAhead1 < n) stage_b(i + kAhead1);
+      KmerCounts kc;
+      kc.count = counts[i];
+      kc.left = left[i];
+      kc.right = right[i];
+      put(key_type(keys + i * nl), kc, h[i % kRing]);
+    }
+  }
+
+ private:
+  // tags and slots live in 2 MB-aligned anonymous memory advised for transparent huge pages: a table larger than the
+  // caches is touched at random, and with 4 KB pages every probe would also miss the TLB
+  struct Free {
+    size_t bytes = 0;
+    void operator()(void *p) const {
+      if (p) munmap(p, bytes);
+    }
+  };
+  template <typename T>
+  using Buf = std::unique_ptr<T[], Free>;
+  template <typename T>
+  static Buf<T> alloc(size_t n) {
+    const size_t bytes = ((n * sizeof(T)) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) die("KmerMap: out of memory");
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+    return Buf<T>((T *)p, Free{bytes});  // zero-filled by the kernel; value_type is trivially copyable
+  }
+  Buf<uint8_t> tag_;
+  Buf<value_type> slot_;
+  size_t cap_ = 0, size_ = 0;
+  int shift_ = 64;  // 64 - log2(cap_): the home slot is the top bits of the hash
+  // the key words' multiply-xorshift mix (mhmkc_map_hash: the device orders mhmkc_fetch_ordered's rows by its top
+  // bits, the home slot here, so that a fill in that order streams through the slot array)
+  static uint64_t hash_words(const uint64_t *w) { return mhmkc_map_hash(w, key_type::N_LONGS); }
+  static uint64_t hash_of(const key_type &k) { return hash_words(k.get_longs()); }
+  static uint8_t tag_of(uint64_t h) { return (uint8_t)(0x80u | (h & 0x7fu)); }
+  size_t home(uint64_t h) const { return (size_t)(h >> shift_); }
+  // the slot holding k, or the empty slot ending its probe sequence (cap_ > 0, load < 1). Eight tags per step
+  // (SWAR zero-byte tests on a 64-bit load: the first empty tag and the tag matches), one at a time at the wrap.
+  size_t locate(const key_type &k, uint64_t h) {
+    const uint8_t t = tag_of(h);
+    constexpr uint64_t L1 = 0x0101010101010101ull, H8 = 0x8080808080808080ull;
+    size_t i = home(h);
+    while (true) {
+      if (i + 8 <= cap_) {
+        uint64_t x;
+        std::memcpy(&x, &tag_[i], 8);
+        const uint64_t y = x ^ (L1 * t);
+        const uint64_t zero = (x - L1) & ~x & H8;  // bytes that are empty (exact below the first one)
+        uint64_t match = (y - L1) & ~y & H8;       // bytes equal to t (exact below the first one)
+        const int first_empty = zero ? __builtin_ctzll(zero) >> 3 : 8;
+        while (match) {
+          const int b = __builtin_ctzll(match) >> 3;
+          if (b >= first_empty) break;
+          if (tag_[i + b] == t && slot_[i + b].first == k) return i + b;
+          match &= match - 1;
+        }
+        if (first_empty < 8) return i + first_empty;
+        i = (i + 8) & (cap_ - 1);
+      } else {
+        if (!tag_[i]) return i;
+        if (tag_[i] == t && slot_[i].first == k) return i;
+        i = (i + 1) & (cap_ - 1);
+      }
+    }
+  }
+  std::pair<iterator, bool> put(const key_type &k, const mapped_type &v, uint64_t h) {
+    if (size_ + 1 > cap_ - cap_ / 8) rehash(cap_ ? 2 * cap_ : 16);
+    const size_t i = locate(k, h);
+    if (tag_[i]) return {iterator(this, i, false), false};
+    tag_[i] = tag_of(h);
+    slot_[i].first = k;
+    slot_[i].second = v;
+    size_++;
+    return {iterator(this, i, false), true};
+  }
+  void rehash(size_t c) {
+    Buf<uint8_t> ot = alloc<uint8_t>(c);
+    Buf<value_type> os = alloc<value_type>(c);
+    ot.swap(tag_);
+    os.swap(slot_);
+    const size_t oc = cap_;
+    cap_ = c;
+    shift_ = 64 - __builtin_ctzll((unsigned long long)c);
+    size_ = 0;
+    for (size_t i = 0; i < oc; i++)
+      if (ot[i]) put(os[i].first, os[i].second, hash_of(os[i].first));
+  }
+};
 
 // ---------------------------------------------------------------------------------------------
 // PackedReads (byte layout of src/packed_reads.cpp:73-109)
@@ -334,15 +541,9 @@ class HashTableInserter {
     std::vector<uint64_t> keys(n * Kmer<MAX_K>::N_LONGS);
     std::vector<uint16_t> counts(n);
     std::vector<char> left(n), right(n);
-    check(mhmkc_fetch(h_, keys.data(), counts.data(), left.data(), right.data()), h_, "mhmkc_fetch");
-    local_kmers.reserve(local_kmers.size() + n);
-    for (uint64_t i = 0; i < n; i++) {
-      KmerCounts kc;
-      kc.count = counts[i];
-      kc.left = left[i];
-      kc.right = right[i];
-      local_kmers.emplace(Kmer<MAX_K>(&keys[i * Kmer<MAX_K>::N_LONGS]), kc);
-    }
+    // rows in the map's slot order (a device sort), so that the fill streams through the slot array
+    check(mhmkc_fetch_ordered(h_, keys.data(), counts.data(), left.data(), right.data()), h_, "mhmkc_fetch_ordered");
+    local_kmers.fill(keys.data(), counts.data(), left.data(), right.data(), n);
   }
   mhmkc_stats stats() const {
     mhmkc_stats s;
@@ -378,14 +579,7 @@ class KmerDHT {
   void finish_updates() { ht_inserter.insert_into_local_hashtable(local_kmers); }
   // fill the local KmerMap from a finished table in mhmkc_fetch's layout (n_longs = N_LONGS words per key)
   void load_table(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n) {
-    local_kmers.reserve(local_kmers.size() + n);
-    for (uint64_t i = 0; i < n; i++) {
-      KmerCounts kc;
-      kc.count = counts[i];
-      kc.left = left[i];
-      kc.right = right[i];
-      local_kmers.emplace(Kmer<MAX_K>(&keys[i * Kmer<MAX_K>::N_LONGS]), kc);
-    }
+    local_kmers.fill(keys, counts, left, right, n);
   }
   KmerCounts *get_local_kmer_counts(const Kmer<MAX_K> &kmer) {
     auto it = local_kmers.find(kmer);

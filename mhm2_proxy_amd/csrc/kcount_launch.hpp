@@ -322,6 +322,10 @@ struct OutRows {
 // KmerDHT minimizer length for k (src/kcount/kmer_dht.cpp:114-116)
 inline int minimizer_len_for(int k) { return k * 2 / 3 + 1 < 15 ? 15 : (k * 2 / 3 + 1 > 27 ? 27 : k * 2 / 3 + 1); }
 // minimizer_hash_fast of n keys (nlo words each, the first k/32+1 used)
+// mhmkc_fetch_ordered: the output rows in the order of the top 32 bits of mhmkc_map_hash (kcount_owner.hip)
+size_t map_order_scratch_bytes(uint64_t n);
+hipError_t launch_map_order(const OutRows &in, uint64_t n, int nlo, void *scratch, size_t scratch_bytes, const OutRows &out,
+                            hipStream_t s);
 hipError_t launch_minimizer_hash(const uint64_t *keys, uint64_t n, int nlo, int k, int m, uint64_t *out, hipStream_t s);
 // dest[i] = owner rank of row i; hist[r] += rows owned by rank r (zero hist first)
 hipError_t launch_owner_hist(const uint64_t *keys, uint64_t n, int nlo, int k, int m, int n_ranks, uint8_t *dest,

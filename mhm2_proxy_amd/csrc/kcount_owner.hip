@@ -6,8 +6,11 @@
 // that owner when the handle asks for it (mhmkc_config.output_owner). These kernels compute the owner of
 // each output row and group the rows by owner for the exchange.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+
+#include "../../include/mhmkc.h"
 
 #include "kcount_launch.hpp"
 #include "kmer_ops.hpp"
@@ -107,7 +110,50 @@ __global__ __launch_bounds__(O_THREADS) void k_owner_scatter(OutRows in, uint64_
   }
 }
 
+// mhmkc_fetch_ordered: the top 32 bits of the KmerMap hash of every output row (mhmkc_map_hash, include/mhmkc.h) as
+// the sort key, the row index as the value
+__global__ __launch_bounds__(O_THREADS) void k_map_hash(const uint64_t *keys, uint64_t n, int nlo, uint32_t *hkey,
+                                                        uint32_t *idx) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    hkey[i] = (uint32_t)(mhmkc_map_hash(keys + i * (uint64_t)nlo, nlo) >> 32);
+    idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(O_THREADS) void k_gather_rows(OutRows in, const uint32_t *idx, uint64_t n, int nlo, OutRows out) {
+  for (uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = idx[o];
+    for (int w = 0; w < nlo; w++) out.keys[o * nlo + w] = in.keys[i * nlo + w];
+    out.counts[o] = in.counts[i];
+    out.left[o] = in.left[i];
+    out.right[o] = in.right[i];
+  }
+}
+
 }  // namespace
+
+size_t map_order_scratch_bytes(uint64_t n) {
+  size_t t = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, t, (const uint32_t *)nullptr, (uint32_t *)nullptr, (const uint32_t *)nullptr,
+                                  (uint32_t *)nullptr, (size_t)n);
+  return 4 * ((n + 63) / 64 * 64) * 4 + t + 256;
+}
+
+hipError_t launch_map_order(const OutRows &in, uint64_t n, int nlo, void *scratch, size_t scratch_bytes, const OutRows &out,
+                            hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (n >= 0xffffffffull || scratch_bytes < map_order_scratch_bytes(n)) return hipErrorInvalidValue;
+  const size_t a = (n + 63) / 64 * 64;
+  uint32_t *hk = (uint32_t *)scratch, *hk2 = hk + a, *ix = hk2 + a, *ix2 = ix + a;
+  void *tmp = ix2 + a;
+  size_t tb = scratch_bytes - 4 * a * 4;
+  k_map_hash<<<grid_for(n), O_THREADS, 0, s>>>(in.keys, n, nlo, hk, ix);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if ((e = rocprim::radix_sort_pairs(tmp, tb, hk, hk2, ix, ix2, (size_t)n, 0, 32, s)) != hipSuccess) return e;
+  k_gather_rows<<<grid_for(n), O_THREADS, 0, s>>>(in, ix2, n, nlo, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_minimizer_hash(const uint64_t *keys, uint64_t n, int nlo, int k, int m, uint64_t *out, hipStream_t s) {
   if (!n) return hipSuccess;

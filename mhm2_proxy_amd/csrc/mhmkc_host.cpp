@@ -165,6 +165,7 @@ struct mhmkc {
   DevBuf d_hist, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
   DevBuf d_hll, d_dest, d_ohist, d_out2_keys, d_out2_counts, d_out2_left, d_out2_right, d_mh;
+  DevBuf d_ord;  // mhmkc_fetch_ordered: sort keys, row indices, radix-sort scratch
   PinBuf x_send, x_recv;  // host-staged exchange
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
@@ -1402,7 +1403,7 @@ void mhmkc_destroy(mhmkc_t h) {
                     &h->d_fine_base, &h->d_fine_cursor, &h->d_chunks,    &h->d_srcs,       &h->d_r2,
                     &h->d_out_keys, &h->d_out_counts, &h->d_out_left,   &h->d_out_right,  &h->d_out_cursor,
                     &h->d_recv,     &h->d_xg,         &h->d_hll,        &h->d_dest,       &h->d_ohist,
-                    &h->d_out2_keys, &h->d_out2_counts, &h->d_out2_left, &h->d_out2_right, &h->d_mh,
+                    &h->d_out2_keys, &h->d_out2_counts, &h->d_out2_left, &h->d_out2_right, &h->d_mh, &h->d_ord,
                     &h->d_fqa_bytes, &h->d_fqa_offs,
                     &h->d_fq_text,  &h->d_fq_chunk,   &h->d_fq_lines,   &h->d_fq_len,     &h->d_fq_tmp,
                     &h->d_fq_bytes, &h->d_fq_offs,    &h->d_fq_err};
@@ -1940,6 +1941,34 @@ int mhmkc_fetch(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *r
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) return h->hip_fail(e, "fetch");
   return MHMKC_OK;
+}
+
+int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right) {
+  if (!h) return MHMKC_EINVAL;
+  if (!h->finished) return h->fail(MHMKC_ESTATE, "fetch before finish");
+  const uint64_t n = h->n_out;
+  if (!n) return MHMKC_OK;
+  if (n >= 0xffffffffull) return h->fail(MHMKC_EUNSUPPORTED, "mhmkc_fetch_ordered: at most 2^32-1 rows");
+  const int nlo = h->nlo;
+  const size_t sb = mhm::map_order_scratch_bytes(n);
+  hipError_t e;
+  // the second output set holds the ordered rows (it is only used inside finish, by the owner hand-off)
+  if ((e = h->grow(h->d_ord, sb)) != hipSuccess || (e = h->grow(h->d_out2_keys, n * 8 * nlo + 64)) != hipSuccess ||
+      (e = h->grow(h->d_out2_counts, n * 2 + 64)) != hipSuccess || (e = h->grow(h->d_out2_left, n + 64)) != hipSuccess ||
+      (e = h->grow(h->d_out2_right, n + 64)) != hipSuccess)
+    return h->hip_fail(e, "fetch_ordered buffers");
+  mhm::OutRows in{h->d_out_keys.as<uint64_t>(), h->d_out_counts.as<uint16_t>(), h->d_out_left.as<char>(),
+                  h->d_out_right.as<char>()};
+  mhm::OutRows out{h->d_out2_keys.as<uint64_t>(), h->d_out2_counts.as<uint16_t>(), h->d_out2_left.as<char>(),
+                   h->d_out2_right.as<char>()};
+  if ((e = mhm::launch_map_order(in, n, nlo, h->d_ord.p, h->d_ord.cap, out, h->stream)) != hipSuccess)
+    return h->hip_fail(e, "fetch_ordered sort");
+  if (keys) e = hipMemcpyAsync(keys, out.keys, n * 8 * nlo, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && counts) e = hipMemcpyAsync(counts, out.counts, n * 2, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && left) e = hipMemcpyAsync(left, out.left, n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && right) e = hipMemcpyAsync(right, out.right, n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fetch_ordered");
 }
 
 int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,

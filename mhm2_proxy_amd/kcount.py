@@ -413,7 +413,9 @@ class KmerCounter:
         self.n_out = int(n.value)
         return self.n_out
 
-    def fetch(self) -> KmerTable:
+    def fetch(self, ordered: bool = False) -> KmerTable:
+        """The finished table on the host (mhmkc_fetch). ordered=True: rows in the order of the top 32 bits of
+        map_hash(key) (mhmkc_fetch_ordered, a device sort), the slot order of the C++ adapter's KmerMap."""
         if self.n_out is None:
             raise RuntimeError("fetch before finish")
         n = self.n_out
@@ -421,8 +423,8 @@ class KmerCounter:
         counts = np.empty(n, dtype=np.uint16)
         left = np.empty(n, dtype=np.uint8)
         right = np.empty(n, dtype=np.uint8)
-        self._check(N.lib().mhmkc_fetch(self._h, keys.ctypes.data, counts.ctypes.data, left.ctypes.data,
-                                        right.ctypes.data))
+        fn = N.lib().mhmkc_fetch_ordered if ordered else N.lib().mhmkc_fetch
+        self._check(fn(self._h, keys.ctypes.data, counts.ctypes.data, left.ctypes.data, right.ctypes.data))
         return KmerTable(self.k, keys, counts, left, right)
 
     def device_output(self) -> dict:
@@ -506,6 +508,17 @@ def comm_id() -> bytes:
 
 # ------------------------------------------------------------------------------------------------
 # KmerDHT / analyze_kmers mirror
+
+
+def map_hash(longs) -> int:
+    """mhmkc_map_hash (include/mhmkc.h): the C++ adapter's KmerMap hash of a key's words."""
+    M = (1 << 64) - 1
+    h = 0x9E3779B97F4A7C15
+    for w in longs:
+        h = ((h ^ int(w)) * 0xBF58476D1CE4E5B9) & M
+        h ^= h >> 31
+    h = (h * 0x94D049BB133111EB) & M
+    return h ^ (h >> 29)
 
 
 def _quick_hash(v: int) -> int:

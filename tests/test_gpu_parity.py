@@ -539,3 +539,18 @@ def test_valid_window_walk_long_and_ragged_reads(k, monkeypatch):
     monkeypatch.setenv("MHMKC_CHUNK_BYTES", "5000")
     got2, _ = hip_table(b, o, k)
     assert_tables_equal(got2, exp, f"long/ragged reads in 5000-byte chunks, k={k}")
+
+
+@pytest.mark.parametrize("k,nl", [(21, 0), (63, 0), (21, 2), (99, 0)])
+def test_fetch_ordered(k, nl):
+    """mhmkc_fetch_ordered: the same rows as mhmkc_fetch, ordered by the top 32 bits of mhmkc_map_hash (the slot
+    order of the C++ adapter's KmerMap)."""
+    b, o = synth_set(2000, 10000, 90 + k)
+    with m.KmerCounter(k, n_longs=nl) as c:
+        c.add_packed_reads(b, o)
+        c.finish()
+        plain = c.fetch()
+        ordered = c.fetch(ordered=True)
+    assert_tables_equal(ordered, plain, "ordered fetch")
+    top = np.array([m.kcount.map_hash(row) >> 32 for row in ordered.keys.tolist()], dtype=np.uint64)
+    assert len(top) > 1000 and (np.diff(top.astype(np.int64)) >= 0).all()
