@@ -75,6 +75,10 @@ def parse():
                     help="exchange between ranks (N > 1): rccl = one rank per GPU, RCCL grouped send/recv over xGMI; "
                          "host = mhmkc_set_transport over a gloo process group (pinned D2H, gloo, H2D), ranks share "
                          "the visible GPUs round-robin (a rehearsal of the multi-rank path on one GPU)")
+    ap.add_argument("--owner", choices=("hash", "minimizer"), default="hash",
+                    help="N > 1: where a finished k-mer lives: hash = the counting hash range (record exchange); "
+                         "minimizer = the reference's get_kmer_target_rank (k >= 33: supermer exchange, DESIGN.md "
+                         "§3.5b; k <= 31: record exchange + hand-off)")
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="per-kernel HBM bytes per launch from rocprofv3 --pmc passes (profiles/), if present")
     return ap.parse_args()
@@ -364,7 +368,8 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         cid = obj[0]
     counter = m.KmerCounter(k, device=local, rank=rank, n_ranks=world, comm_id=cid,
-                            transport=m.TorchDistTransport() if host_xp else None)
+                            transport=m.TorchDistTransport() if host_xp else None,
+                            output_owner=m.MHMKC_OWNER_MINIMIZER if args.owner == "minimizer" else m.MHMKC_OWNER_HASH)
     counter.set_profiling(not args.no_profile_events)
 
     def step():
@@ -550,6 +555,10 @@ def main():
                           "ms_per_step_rank0": round(per_step.get("exchange", 0.0), 3),
                           "bytes_sent_per_step_rank0": st["bytes_sent"], "bytes_recv_per_step_rank0": st["bytes_recv"],
                           "bytes_sent_per_occurrence": round(st["bytes_sent"] / max(1, st["occurrences"]), 3),
+                          "owner": args.owner,
+                          "wire": ("supermers (2-bit codes + extension bits in 32-base words + a descriptor)"
+                                   if st["smer_count"] else "records"),
+                          "handoff_rows_sent_rank0": st["handoff_sent"],
                           "GBps_rank0": round(st["bytes_sent"] / (per_step["exchange"] * 1e-3) / 1e9, 2)
                           if per_step.get("exchange") else None}
                          if world > 1 and st else None),

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 8
+#define MHMKC_ABI_VERSION 9
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -119,6 +119,8 @@ typedef struct {
   uint64_t fq_overlap_bases; /* ... overlap bases of the merged pairs (merge_reads overlap_len) */
   uint64_t table_slots;    /* count kernel: LDS table slots used per fine bucket (fitted to the sketch estimate) */
   uint64_t fq_file_blocks; /* mhmkc_add_fastq[_pairs]_file: blocks of the last call */
+  uint64_t smer_count;     /* supermer exchange: supermers this rank built (all destinations, itself included) */
+  uint64_t smer_words;     /* ... their 32-base words (each a u64 of 2-bit codes + a u32 of extension bits) */
 } mhmkc_stats;
 
 enum {

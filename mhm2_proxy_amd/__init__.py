@@ -10,6 +10,7 @@ from .kcount import (  # noqa: F401
     KmerDHT,
     KmerTable,
     PackedReads,
+    SharedGpuCounter,
     TorchDistTransport,
     analyze_kmers,
     comm_id,
@@ -27,4 +28,5 @@ __all__ = [
     "KmerCounter", "KmerCounts", "KmerDHT", "KmerTable", "PackedReads", "analyze_kmers", "comm_id",
     "get_kmer_target_rank", "kmer_from_string", "kmer_to_string", "keys_to_strings", "n_longs_for",
     "synth_genome", "synth_reads", "MhmkcError", "TorchDistTransport", "MHMKC_OWNER_HASH", "MHMKC_OWNER_MINIMIZER",
+    "SharedGpuCounter",
 ]

@@ -104,6 +104,8 @@ class MhmkcStats(C.Structure):
         ("fq_overlap_bases", C.c_uint64),
         ("table_slots", C.c_uint64),
         ("fq_file_blocks", C.c_uint64),
+        ("smer_count", C.c_uint64),
+        ("smer_words", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -113,7 +113,8 @@ __device__ __forceinline__ uint32_t single_choice(uint32_t code, uint32_t count,
 template <int NL>
 __global__ __launch_bounds__(G_THREADS) void k_ctg_fold(PlaneSet keys, const uint32_t *aux, const uint32_t *perm,
                                                          uint64_t n, int dmin, double dyn_mult, int cb, int fb,
-                                                         uint32_t own_lo, uint32_t own_hi, int cmpB, PlaneSet fkeys, uint32_t *fstate,
+                                                         uint32_t own_lo, uint32_t own_hi, int cmpB, int k, CtgOwner ow,
+                                                         PlaneSet fkeys, uint32_t *fstate,
                                                          uint32_t *fbucket, uint32_t *fidx,
                                                          unsigned long long *counter) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -165,6 +166,8 @@ __global__ __launch_bounds__(G_THREADS) void k_ctg_fold(PlaneSet keys, const uin
     }
     const uint32_t coarse = (uint32_t)(h >> (64 - cb));
     if (coarse < own_lo || coarse >= own_hi) continue;  // another rank's hash range (it folds this key itself)
+    // supermer exchange: this rank holds the k-mers of its get_kmer_target_rank (kmer_dht.cpp:193-196)
+    if (ow.n_ranks && (int)(quick_hash(minimizer_fast(key, k, ow.m)) % (uint64_t)ow.n_ranks) != ow.rank) continue;
     const uint32_t fine = fb ? (uint32_t)((h >> (64 - cb - fb)) & ((1ull << fb) - 1)) : 0u;
     const unsigned long long o = atomicAdd(counter, 1ull);
 #pragma unroll
@@ -223,8 +226,8 @@ size_t carve(void *base, uint64_t n, int nl, Scratch *sc) {
 
 template <int NL>
 hipError_t prepare(const CtgView &cv, int k, int qcut, int dmin, double dyn_mult, int cb, int fb, uint32_t own_lo,
-                   uint32_t own_hi, int cmpB, const Scratch &sc, uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket,
-                   uint64_t *n_out, unsigned int *err, hipStream_t s) {
+                   uint32_t own_hi, int cmpB, const CtgOwner &ow, const Scratch &sc, uint64_t *const out_keys[4],
+                   uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out, unsigned int *err, hipStream_t s) {
   const uint64_t n = cv.n_windows;
   hipError_t e;
   k_ctg_extract<NL><<<grid_for(n), G_THREADS, 0, s>>>(cv, k, qcut, sc.keys, sc.aux, err);
@@ -244,7 +247,7 @@ hipError_t prepare(const CtgView &cv, int k, int qcut, int dmin, double dyn_mult
   }
   if ((e = hipMemsetAsync(sc.counter, 0, 8, s)) != hipSuccess) return e;
   k_ctg_fold<NL><<<grid_for(n), G_THREADS, 0, s>>>(sc.keys, sc.aux, perm, n, dmin, dyn_mult, cb, fb, own_lo, own_hi, cmpB,
-                                                   sc.fkeys,
+                                                   k, ow, sc.fkeys,
                                                    sc.fstate, sc.fbucket, sc.fidx, sc.counter);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   unsigned long long f = 0;
@@ -269,8 +272,8 @@ hipError_t prepare(const CtgView &cv, int k, int qcut, int dmin, double dyn_mult
 size_t ctg_scratch_bytes(uint64_t n_windows, int nl) { return carve(nullptr, n_windows, nl, nullptr); }
 
 hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool mixed, int qual_cutoff, int dmin_thres,
-                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi, void *scratch,
-                       size_t scratch_bytes,
+                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi,
+                       const CtgOwner &ow, void *scratch, size_t scratch_bytes,
                        uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,
                        unsigned int *err, hipStream_t s) {
   *n_out = 0;
@@ -280,13 +283,13 @@ hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool mixed, int qual_cu
   if (carve(scratch, cv.n_windows, nl, &sc) > scratch_bytes) return hipErrorInvalidValue;
   const int cmpB = mixed ? 2 * k : 0;  // compact (NL = 1) or mixed two-word (NL = 2) records
   switch (nl) {
-    case 1: return prepare<1>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
+    case 1: return prepare<1>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, ow, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
-    case 2: return prepare<2>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
+    case 2: return prepare<2>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, ow, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
-    case 3: return prepare<3>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
+    case 3: return prepare<3>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, ow, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
-    case 4: return prepare<4>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, sc, out_keys,
+    case 4: return prepare<4>(cv, k, qual_cutoff, dmin_thres, dyn_mult, coarse_bits, fine_bits, own_lo, own_hi, cmpB, ow, sc, out_keys,
                               out_state, out_bucket, n_out, err, s);
   }
   return hipErrorInvalidValue;

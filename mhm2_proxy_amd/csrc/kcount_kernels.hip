@@ -957,6 +957,374 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
 }
 
 // ------------------------------------------------------------------------------------------------
+// Supermer exchange (MHMKC_OWNER_MINIMIZER with several ranks and keys of two or more words).
+// The reference ships a read's k-mers to their owners as supermers: runs of consecutive windows with the same
+// get_kmer_target_rank, each run sent as its bases plus one flanking base on either side
+// (SeqBlockInserter::process_seq, src/kcount/kcount_cpu.cpp:73-103 -> add_supermer, kmer_dht.cpp:222-224). Here:
+//   k_smer_owner  per extraction tile: the canonical m-mer of every position (rolled along a strip per thread),
+//                 the window minimizer as a sliding maximum over k - m + 1 of them (van Herk / Gil-Werman: block
+//                 prefix and suffix maxima in LDS), owner = quick_hash(minimizer) % n_ranks for every counted
+//                 window (one byte per position to global memory), and per destination the supermers and words
+//                 the tile will send (runs are cut at tile edges);
+//   k_smer_pack   the same runs again from the owner bytes; each supermer's L = n + k + 1 bases go to its
+//                 destination's exact span (cursors from the counts) as whole 32-base words: 2-bit codes (u64,
+//                 N -> G, MSB first like the staged tile) + "extension countable" bits (u32), and one u64
+//                 descriptor (word offset << 16 | n windows);
+//   k_smer_extract on the owner: every window of the received supermers, tile by tile over the window index
+//                 (a thread's windows are consecutive, so its supermer is found once and then advanced), the key
+//                 read straight from the code words, the record and its coarse bin as k_extract_scatter makes
+//                 them, and the same staged scatter (or a bin histogram for the exact layout).
+// A window's supermer holds both of its neighbours, so its record equals the one the read gives (interior windows
+// of the pseudo-read, kcount_cpu.cpp:316-334).
+
+template <int NL>
+__host__ __device__ constexpr int smer_pmax() {  // m-mer positions of a tile: T + k - m + 1 <= T + 32 NL
+  return kTile<NL>() + 32 * NL;
+}
+__host__ __device__ constexpr int smer_words(int n, int k) { return (n + k + 1 + 31) / 32; }
+
+// The supermer starting at tile window i: its window count, 0 when no supermer starts there (not a counted window,
+// or the previous window has the same owner). Runs are cut at the tile's last window.
+template <int T>
+__device__ __forceinline__ int smer_run(const uint8_t *own, int i) {
+  const uint8_t d = own[i];
+  if (d == 0xFF || (i > 0 && own[i - 1] == d)) return 0;
+  int n = 1;
+  while (i + n < T && own[i + n] == d) n++;
+  return n;
+}
+
+template <int NL>
+__host__ __device__ constexpr size_t smer_owner_lds(int n_ranks) {
+  return tile_lds_bytes<NL>() + 2 * (size_t)smer_pmax<NL>() * 8 + (size_t)kTile<NL>() + (size_t)n_ranks * 8;
+}
+
+template <int NL>
+__global__ __launch_bounds__(kEThreads<NL>()) void k_smer_owner(SmerParams p) {
+  constexpr int ET = kEThreads<NL>(), T = kTile<NL>(), W = T / ET, PMX = smer_pmax<NL>();
+  static_assert(T % 16 == 0 && (T + 32 * NL) / ET + 1 <= 32, "one funnel word of incoming bases per strip");
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint64_t *fwd;
+  uint32_t *good, *start;
+  unsigned char *rest = carve_tile<NL>(smem, fwd, good, start);
+  uint64_t *sm = (uint64_t *)rest, *pmx = sm + PMX;
+  uint8_t *own = (uint8_t *)(pmx + PMX);
+  uint32_t *dcnt = (uint32_t *)(own + T);  // [2 G]: words, supermers per destination
+  const int G = p.n_ranks, k = p.k, m = p.m, w = k - m + 1;
+  for (int i = threadIdx.x; i < 2 * G; i += ET) dcnt[i] = 0;
+  const uint32_t tile = blockIdx.x;
+  load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
+  // 1. canonical m-mer (right-aligned 2m bits, min of forward and reverse complement) of positions 32 + i
+  const int pm = T + k - m + 1;
+  {
+    const int S = (pm + ET - 1) / ET, i0 = (int)threadIdx.x * S, i1 = min(i0 + S, pm);
+    if (i0 < i1) {
+      const uint64_t mm = (1ull << (2 * m)) - 1;
+      const uint64_t x = WalkSpan<NL>::codes64(fwd, 32 + i0);
+      uint64_t f = x >> (64 - 2 * m), r = rev2(~x) & mm;
+      const uint64_t inc = WalkSpan<NL>::codes64(fwd, 32 + i0 + m);  // the base entering after position i0 + t
+      for (int i = i0; i < i1; i++) {
+        sm[i] = f < r ? f : r;
+        const uint32_t c = (uint32_t)(inc >> (62 - 2 * (i - i0))) & 3u;
+        f = ((f << 2) | c) & mm;
+        r = (r >> 2) | ((uint64_t)(3u - c) << (2 * m - 2));
+      }
+    }
+  }
+  __syncthreads();
+  // 2. blocks of w positions: prefix maxima into pmx, suffix maxima in place; the minimizer of the window at
+  //    32 + i (its m-mers i .. i + w - 1) is max(sm[i], pmx[i + w - 1])
+  for (int b = threadIdx.x; b * w < pm; b += ET) {
+    const int lo = b * w, hi = min(lo + w, pm);
+    uint64_t v = 0;
+    for (int i = lo; i < hi; i++) {
+      v = sm[i] > v ? sm[i] : v;
+      pmx[i] = v;
+    }
+    v = 0;
+    for (int i = hi - 1; i >= lo; i--) {
+      v = sm[i] > v ? sm[i] : v;
+      sm[i] = v;
+    }
+  }
+  __syncthreads();
+  // 3. the owner of every counted window, get_kmer_target_rank = minimizer_hash_fast % rank_n
+  //    (kmer_dht.cpp:193-196; quick_hash of the minimizer left-aligned, src/kmer.cpp:454-463)
+  {
+    WalkSpan<NL> sp(fwd, good, start, tile, p.reads.n_bases, p.reads.head, k);
+    uint64_t last_min = ~0ull;
+    uint32_t last_own = 0;
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+      uint32_t cr, ef, er;
+      const bool valid = sp.step(j, k, cr, ef, er);
+      const int i = (int)threadIdx.x * W + j;
+      const uint64_t a = sm[i], b2 = pmx[i + w - 1];
+      const uint64_t mn = a > b2 ? a : b2;
+      if (valid && mn != last_min) {
+        last_min = mn;
+        last_own = (uint32_t)(quick_hash(mn << (64 - 2 * m)) % (uint64_t)G);
+      }
+      own[i] = valid ? (uint8_t)last_own : (uint8_t)0xFF;
+    }
+  }
+  __syncthreads();
+  // 4. the supermers of the tile and what they will send, per destination
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const int i = (int)threadIdx.x * W + j;
+    const int n = smer_run<T>(own, i);
+    if (n) {
+      const uint32_t d = own[i];
+      atomicAdd(&dcnt[2 * d], (uint32_t)smer_words(n, k));
+      atomicAdd(&dcnt[2 * d + 1], 1u);
+    }
+  }
+  uint32_t *gown = (uint32_t *)(p.owners + (uint64_t)tile * T);
+  for (int i = threadIdx.x; i < T / 4; i += ET) gown[i] = ((const uint32_t *)own)[i];
+  __syncthreads();
+  for (int d = threadIdx.x; d < G; d += ET) {
+    if (dcnt[2 * d + 1]) {
+      atomicAdd(&p.hist[2 * d], (unsigned long long)dcnt[2 * d]);
+      atomicAdd(&p.hist[2 * d + 1], (unsigned long long)dcnt[2 * d + 1]);
+    }
+  }
+}
+
+template <int NL>
+__host__ __device__ constexpr size_t smer_pack_lds(int n_ranks) {
+  return tile_lds_bytes<NL>() + (size_t)kTile<NL>() + (size_t)n_ranks * 8 + (size_t)n_ranks * 16;
+}
+
+template <int NL>
+__global__ __launch_bounds__(kEThreads<NL>()) void k_smer_pack(SmerParams p) {
+  constexpr int ET = kEThreads<NL>(), T = kTile<NL>(), W = T / ET, NG = kGroups<NL>();
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint64_t *fwd;
+  uint32_t *good, *start;
+  unsigned char *rest = carve_tile<NL>(smem, fwd, good, start);
+  uint8_t *own = rest;
+  uint32_t *dcnt = (uint32_t *)(own + T);                                       // [2 G]
+  unsigned long long *goff = (unsigned long long *)(dcnt + 2 * p.n_ranks);  // [2 G] (8-byte aligned: dcnt is 16)
+  const int G = p.n_ranks, k = p.k;
+  for (int i = threadIdx.x; i < 2 * G; i += ET) dcnt[i] = 0;
+  const uint32_t tile = blockIdx.x;
+  load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
+  const uint32_t *gown = (const uint32_t *)(p.owners + (uint64_t)tile * T);
+  for (int i = threadIdx.x; i < T / 4; i += ET) ((uint32_t *)own)[i] = gown[i];
+  __syncthreads();
+  uint32_t wr[W], sr[W];
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const int i = (int)threadIdx.x * W + j;
+    const int n = smer_run<T>(own, i);
+    wr[j] = sr[j] = 0;
+    if (n) {
+      const uint32_t d = own[i];
+      wr[j] = atomicAdd(&dcnt[2 * d], (uint32_t)smer_words(n, k));
+      sr[j] = atomicAdd(&dcnt[2 * d + 1], 1u);
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < G; d += ET) {
+    const uint32_t nw = dcnt[2 * d], ns = dcnt[2 * d + 1];
+    goff[2 * d] = ns ? atomicAdd(&p.cursor[2 * d], (unsigned long long)nw) : 0ull;
+    goff[2 * d + 1] = ns ? atomicAdd(&p.cursor[2 * d + 1], (unsigned long long)ns) : 0ull;
+  }
+  __syncthreads();
+  // the staged words past the tile read as zero (they only fill masked bits of a supermer's last word)
+  auto code_at = [&](int g) { return g < NG ? fwd[g] : 0ull; };
+  auto good_at = [&](int g) { return g < NG ? good[g] : 0u; };
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const int i = (int)threadIdx.x * W + j;
+    const int n = smer_run<T>(own, i);
+    if (!n) continue;
+    const uint32_t d = own[i];
+    const unsigned long long wo = goff[2 * d] + wr[j], so = goff[2 * d + 1] + sr[j];
+    if (so >= p.n_smer || wo + smer_words(n, k) > p.n_words) {  // (counts of the two passes disagree: a bug)
+      atomicOr(p.err, 8u);
+      continue;
+    }
+    p.desc[so] = ((uint64_t)wo << 16) | (uint64_t)n;
+    const int L = n + k + 1, q0 = 32 + i - 1;  // bases: the left flank, the n windows' bases, the right flank
+    for (int g = 0; g < smer_words(n, k); g++) {
+      const int q = q0 + 32 * g, gi = q >> 5, sh = q & 31;
+      uint64_t cw = code_at(gi);
+      uint32_t gw = good_at(gi);
+      if (sh) {
+        cw = (cw << (2 * sh)) | (code_at(gi + 1) >> (64 - 2 * sh));
+        gw = (gw << sh) | (good_at(gi + 1) >> (32 - sh));
+      }
+      const int rem = L - 32 * g;
+      if (rem < 32) {
+        cw &= top_mask(rem);
+        gw &= ~(~0u >> rem);
+      }
+      p.codes[wo + g] = cw;
+      p.good[wo + g] = gw;
+    }
+  }
+}
+
+// The record of one window and its coarse bin, as k_extract_scatter's emit makes them (mixed two-word records,
+// or the key words + packed ext code / stored hash bits).
+template <int NL, bool PACKED, bool CMP>
+__device__ __forceinline__ void window_record(const uint64_t *key, uint32_t e, bool valid, const ExtractParams &p,
+                                              uint64_t (&rk)[NL], uint32_t &inf) {
+  const int kk = p.k;
+  if constexpr (RecKind<NL, CMP>::M2) {
+    const int m2_csh = kk - p.coarse_bits;
+    uint64_t L, R;
+    m2_mix(key, kk, L, R);
+    rk[0] = ((L & ((1ull << m2_csh) - 1)) << EXT_BITS) | e;
+    rk[1] = R;
+    inf = valid ? (1u << 31) | (e << 16) | (uint32_t)(L >> m2_csh) : 0u;
+    return;
+  }
+  const uint64_t h = window_hash<NL, CMP>(key, kk);
+#pragma unroll
+  for (int w = 0; w < NL; w++) rk[w] = key[w];
+  if (PACKED) {
+    const int hsh = p.hbits ? 64 - p.hbits : 0;
+    const uint64_t hmask = p.hbits ? ~0ull : 0ull;
+    rk[NL - 1] |= e;
+    rk[NL - 1] |= (((h << p.coarse_bits) >> hsh) & hmask) << EXT_BITS;
+  }
+  inf = valid ? (1u << 31) | (e << 16) | (uint32_t)(h >> (64 - p.coarse_bits)) : 0u;
+}
+
+// 32 codes from base q of a supermer code stream, first on top
+__device__ __forceinline__ uint64_t smer_codes64(const uint64_t *c, uint64_t q) {
+  const uint64_t g = q >> 5;
+  const int sh = (int)(q & 31) * 2;
+  return (gload(c + g) << sh) | ((gload(c + g + 1) >> 1) >> (63 - sh));
+}
+
+template <int NL, bool PACKED, bool CMP, bool HIST>
+__global__ __launch_bounds__(kEThreads<NL>()) void k_smer_extract(ExtractParams p, SmerSource src) {
+  constexpr int ET = kEThreads<NL>(), T = kTile<NL>(), W = T / ET;  // T windows per tile, W per thread
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int k = p.k;
+  const uint32_t tile = blockIdx.x;
+  if (HIST)
+    for (uint32_t b = threadIdx.x; b < p.n_bins; b += ET) ((uint32_t *)smem)[b] = 0;
+  else
+    scatter_clear<ET>((uint32_t *)smem, p.n_bins);
+  const uint64_t J0 = (uint64_t)tile * T + (uint64_t)threadIdx.x * W;
+  // the supermer holding window J0: the last s with wpre[s] <= J0, among the tile's supermers
+  uint64_t s = src.tile_first[tile];
+  {
+    uint64_t hi = src.tile_first[tile + 1] + 1;
+    if (hi > src.n_smer) hi = src.n_smer;
+    while (hi - s > 1) {
+      const uint64_t mid = (s + hi) >> 1;
+      if (gload(src.wpre + mid) <= J0)
+        s = mid;
+      else
+        hi = mid;
+    }
+  }
+  uint64_t ws = gload(src.wpre + s), we = gload(src.wpre + s + 1), dsc = gload(src.desc + s);
+  const uint64_t tmask = top_mask(k - 32 * (NL - 1));
+  uint64_t rk[W][NL];
+  uint32_t inf[W];
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const uint64_t J = J0 + (uint64_t)j;
+    const bool valid = J < src.n_windows;
+    if (valid)
+      while (J >= we) {
+        s++;
+        ws = we;
+        we = gload(src.wpre + s + 1);
+        dsc = gload(src.desc + s);
+      }
+    // base of the window in the stream: its supermer's first word, the left flank, the window's offset
+    uint64_t P = valid ? 32 * (dsc >> 16) + 1 + (J - ws) : 32;
+    if ((P >> 5) + NL + 2 > src.n_words) {  // a descriptor past the stream (a bug): flag it, read nothing there
+      if (valid) atomicOr(p.err, 8u);
+      P = 32;
+    }
+    uint64_t fw[NL], rc[NL];
+#pragma unroll
+    for (int w = 0; w < NL; w++) fw[w] = smer_codes64(src.codes, P + 32 * (uint64_t)w);
+    fw[NL - 1] &= tmask;
+    const uint64_t ql = P - 1, qr = P + (uint64_t)k;
+    const uint32_t cl = (uint32_t)(gload(src.codes + (ql >> 5)) >> (62 - 2 * (ql & 31))) & 3u;
+    const uint32_t cr = (uint32_t)(gload(src.codes + (qr >> 5)) >> (62 - 2 * (qr & 31))) & 3u;
+    const uint32_t gl = (gload(src.good + (ql >> 5)) >> (31 - (ql & 31))) & 1u;
+    const uint32_t gr = (gload(src.good + (qr >> 5)) >> (31 - (qr & 31))) & 1u;
+    revcomp<NL>(fw, rc, k);
+    const bool use_rc = kmer_less<NL>(rc, fw);
+    uint64_t key[NL];
+#pragma unroll
+    for (int w = 0; w < NL; w++) key[w] = use_rc ? rc[w] : fw[w];
+    uint32_t l = gl ? cl : (uint32_t)EXT_NONE, r = gr ? cr : (uint32_t)EXT_NONE;
+    if (use_rc) {
+      const uint32_t nl_ = gr ? 3u - cr : (uint32_t)EXT_NONE, nr_ = gl ? 3u - cl : (uint32_t)EXT_NONE;
+      l = nl_;
+      r = nr_;
+    }
+    window_record<NL, PACKED, CMP>(key, (l << 3) | r, valid, p, rk[j], inf[j]);
+#pragma unroll
+    for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[j][w]));
+    asm volatile("" : "+v"(inf[j]));
+  }
+  if constexpr (HIST) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < W; j++)
+      if (inf[j] >> 31) atomicAdd(&((uint32_t *)smem)[inf[j] & 0xffffu], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < p.n_bins; b += ET) {
+      const uint32_t c = ((uint32_t *)smem)[b];
+      if (c) atomicAdd(&p.hist[b], (unsigned long long)c);
+    }
+  } else {
+    __syncthreads();
+    const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
+    const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
+    constexpr int SF = (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
+    scatter_staged<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, smem + staged_cnt_bytes(p.n_bins),
+                                          p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
+  }
+}
+
+// Descriptors of one received span: word offsets moved by delta (mod 2^64: the span's place in the concatenated
+// stream minus its place in the sender's planes), window counts for the scan.
+__global__ __launch_bounds__(256) void k_smer_rebase(uint64_t *desc, uint64_t n, uint64_t delta,
+                                                     unsigned long long *nwin) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t d = desc[i] + (delta << 16);
+    desc[i] = d;
+    nwin[i] = d & 0xffffu;
+  }
+}
+
+// Per window tile t (T windows): the supermer holding its first window (the last s with wpre[s] <= t T);
+// tile_first[n_tiles] = n_smer - 1.
+__global__ __launch_bounds__(256) void k_smer_tiles(const uint64_t *wpre, uint64_t n_smer, uint64_t *tile_first,
+                                                    uint32_t n_tiles, int T) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > n_tiles) return;
+  if (t == n_tiles) {
+    tile_first[t] = n_smer - 1;
+    return;
+  }
+  const uint64_t J = (uint64_t)t * (uint64_t)T;
+  uint64_t lo = 0, hi = n_smer;  // wpre[0] = 0 <= J
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (wpre[mid] <= J)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  tile_first[t] = lo;
+}
+
+// ------------------------------------------------------------------------------------------------
 // partition coarse -> fine
 
 // Fine digit of a record: from the hash bits stored next to the ext code when there are enough of them,
@@ -1911,7 +2279,16 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #endif
         STAMP(t_r1);
         STAMP_ADD(1, t_r1 - t_r0);
-        if (r0 + RND < lim) prefetch(ps, n, r0 + RND, nw);
+        // (unconditional: in the last round it re-reads this round's records, never used. A load under a branch
+        // left its registers to a phi whose copies made hipcc wait for the load right there, vmcnt(0), so the next
+        // round's records were fetched with the whole HBM latency exposed every round)
+#ifndef MHMKC_PF_UNCOND
+#define MHMKC_PF_UNCOND 1
+#endif
+        if (MHMKC_PF_UNCOND)
+          prefetch(ps, n, r0 + RND < lim ? r0 + RND : r0, nw);
+        else if (r0 + RND < lim)
+          prefetch(ps, n, r0 + RND, nw);
 #if MHMKC_EXP_LOADONLY
         {
           uint32_t acc = 0;
@@ -2152,7 +2529,16 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
     if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
-    if (last_sweep && b_next < p.n_buckets) {
+    if (MHMKC_PF_UNCOND) {
+      // the next bucket's first round, loaded while this one is finalized; unconditional (as the round prefetch:
+      // a load under a branch was waited for at once): without a next bucket, or before a re-sweep (which loads
+      // its own first round), it re-reads this bucket's first records, never used (cnt >= 1 keeps the read at
+      // or next to the bucket's base, inside the records' allocation)
+      const bool nxt = last_sweep && b_next < p.n_buckets;
+      if (nxt) bucket(b_next, ps_next, nb_next);
+      const bool use_next = nxt && nb_next;
+      prefetch(use_next ? ps_next : ps, use_next ? nb_next : (n ? n : 1u), 0, NONE);
+    } else if (last_sweep && b_next < p.n_buckets) {
       bucket(b_next, ps_next, nb_next);
       if (nb_next) prefetch(ps_next, nb_next, 0, NONE);
     }
@@ -2543,6 +2929,93 @@ hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s
   if (!p.n_buckets) return hipSuccess;
   if (p.compact) return nl == 2 ? do_count<2, true, true>(p, s) : do_count<1, true, true>(p, s);
   MHM_DISPATCH(nl, packed, do_count, (p, s));
+}
+
+// ------------------------------------------------------------------------------------------------
+// supermer exchange launchers (NL >= 2)
+
+template <int NL>
+static hipError_t do_smer_owner(const SmerParams &p, hipStream_t s) {
+  const size_t lds = smer_owner_lds<NL>(p.n_ranks);
+  hipError_t e = allow_lds(k_smer_owner<NL>, lds);
+  if (e != hipSuccess) return e;
+  k_smer_owner<NL><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p);
+  return hipGetLastError();
+}
+
+template <int NL>
+static hipError_t do_smer_pack(const SmerParams &p, hipStream_t s) {
+  const size_t lds = smer_pack_lds<NL>(p.n_ranks);
+  hipError_t e = allow_lds(k_smer_pack<NL>, lds);
+  if (e != hipSuccess) return e;
+  k_smer_pack<NL><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p);
+  return hipGetLastError();
+}
+
+hipError_t launch_smer_owner(const SmerParams &p, int nl, hipStream_t s) {
+  if (!p.n_tiles) return hipSuccess;
+  if (p.n_ranks < 2 || p.n_ranks > 255 || p.m < 1 || p.m > 28 || p.m > p.k) return hipErrorInvalidValue;
+  switch (nl) {
+    case 2: return do_smer_owner<2>(p, s);
+    case 3: return do_smer_owner<3>(p, s);
+    case 4: return do_smer_owner<4>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_smer_pack(const SmerParams &p, int nl, hipStream_t s) {
+  if (!p.n_tiles) return hipSuccess;
+  if (p.n_ranks < 2 || p.n_ranks > 255) return hipErrorInvalidValue;
+  switch (nl) {
+    case 2: return do_smer_pack<2>(p, s);
+    case 3: return do_smer_pack<3>(p, s);
+    case 4: return do_smer_pack<4>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int NL, bool PK, bool CMP, bool HIST>
+static hipError_t do_smer_extract(const ExtractParams &p, const SmerSource &src, hipStream_t s) {
+  constexpr int T = kTile<NL>();
+  constexpr int SF = (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
+  const size_t lds = HIST ? (size_t)p.n_bins * 4 : staged_cnt_bytes(p.n_bins) + staged_area_bytes(NL, T, PK, SF);
+  hipError_t e = allow_lds(k_smer_extract<NL, PK, CMP, HIST>, lds);
+  if (e != hipSuccess) return e;
+  k_smer_extract<NL, PK, CMP, HIST><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p, src);
+  return hipGetLastError();
+}
+
+template <bool HIST>
+static hipError_t smer_extract_nl(const ExtractParams &p, const SmerSource &src, int nl, bool packed, hipStream_t s) {
+  if (p.compact) return nl == 2 ? do_smer_extract<2, true, true, HIST>(p, src, s) : hipErrorInvalidValue;
+  switch (nl * 2 + (packed ? 1 : 0)) {
+    case 4: return do_smer_extract<2, false, false, HIST>(p, src, s);
+    case 5: return do_smer_extract<2, true, false, HIST>(p, src, s);
+    case 6: return do_smer_extract<3, false, false, HIST>(p, src, s);
+    case 7: return do_smer_extract<3, true, false, HIST>(p, src, s);
+    case 8: return do_smer_extract<4, false, false, HIST>(p, src, s);
+    case 9: return do_smer_extract<4, true, false, HIST>(p, src, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_smer_extract(const ExtractParams &p, const SmerSource &src, int nl, bool packed, bool hist,
+                               hipStream_t s) {
+  if (!p.n_tiles) return hipSuccess;
+  return hist ? smer_extract_nl<true>(p, src, nl, packed, s) : smer_extract_nl<false>(p, src, nl, packed, s);
+}
+
+hipError_t launch_smer_rebase(uint64_t *desc, uint64_t n, uint64_t delta, unsigned long long *nwin, hipStream_t s) {
+  if (!n) return hipSuccess;
+  k_smer_rebase<<<dim3((unsigned)std::min<uint64_t>(4096, (n + 255) / 256)), dim3(256), 0, s>>>(desc, n, delta, nwin);
+  return hipGetLastError();
+}
+
+hipError_t launch_smer_tiles(const uint64_t *wpre, uint64_t n_smer, uint64_t *tile_first, uint32_t n_tiles, int tile,
+                             hipStream_t s) {
+  if (!n_smer) return hipSuccess;
+  k_smer_tiles<<<dim3((n_tiles + 1 + 255) / 256), dim3(256), 0, s>>>(wpre, n_smer, tile_first, n_tiles, tile);
+  return hipGetLastError();
 }
 
 }  // namespace mhm

@@ -46,6 +46,44 @@ struct ExtractParams {
   unsigned int *ovf;                // bit 1: a capped bin of this slab overflowed (per slab)
 };
 
+// Supermer exchange (kcount_kernels.hip). Sender side, per read slab: owners and per-destination
+// counts (k_smer_owner), then the supermers packed into exact per-destination spans (k_smer_pack).
+struct SmerParams {
+  ReadsView reads;
+  const uint32_t *tile_first_read;
+  uint32_t n_tiles;
+  int k, m, n_ranks, qual_cutoff;
+  uint8_t *owners;              // [n_tiles * tile]: owner of the window at each tile position, 0xFF: not counted
+  unsigned long long *hist;     // [2 n_ranks]: words, supermers per destination (k_smer_owner adds)
+  unsigned long long *cursor;   // [2 n_ranks]: word cursor, supermer cursor per destination (k_smer_pack)
+  uint64_t *codes;              // supermer bases, 2-bit codes, 32 per word (MSB first)
+  uint32_t *good;               // their "extension countable" bits, 32 per word
+  uint64_t *desc;               // per supermer: first word << 16 | windows
+  uint64_t n_words, n_smer;     // the planes' sizes (k_smer_pack writes nothing past them: err bit 3)
+  unsigned int *err;
+};
+// Receiver side: the received supermers of every peer back to back (descriptors rebased), their window prefix
+// wpre[n_smer + 1], and per tile of window indices the supermer holding its first window.
+struct SmerSource {
+  const uint64_t *codes;
+  const uint32_t *good;
+  const uint64_t *desc;
+  const uint64_t *wpre;
+  const uint64_t *tile_first;   // [n_tiles + 1]
+  uint64_t n_smer, n_windows;
+  uint64_t n_words;             // code / good words (a window reaching past them is not read: err bit 3)
+};
+hipError_t launch_smer_owner(const SmerParams &p, int nl, hipStream_t s);
+hipError_t launch_smer_pack(const SmerParams &p, int nl, hipStream_t s);
+// records of the received supermers into a coarse slab (p.out / p.cursor as launch_extract_scatter), or (hist) the
+// exact bin histogram into p.hist
+hipError_t launch_smer_extract(const ExtractParams &p, const SmerSource &src, int nl, bool packed, bool hist,
+                               hipStream_t s);
+// descriptors of a received span: word offsets += delta (mod 2^64), nwin[i] = windows of supermer i
+hipError_t launch_smer_rebase(uint64_t *desc, uint64_t n, uint64_t delta, unsigned long long *nwin, hipStream_t s);
+hipError_t launch_smer_tiles(const uint64_t *wpre, uint64_t n_smer, uint64_t *tile_first, uint32_t n_tiles, int tile,
+                             hipStream_t s);
+
 // One chunk of S work: <= tile records of one (source, coarse bucket) segment.
 struct SChunk {
   uint64_t start;        // first record index in the source planes
@@ -133,6 +171,12 @@ struct CtgView {
   uint64_t n_windows;
 };
 
+// Owner filter of the contig pass with the supermer exchange: keep the k-mers whose get_kmer_target_rank
+// (quick_hash(minimizer_fast(m)) % n_ranks) is `rank`; n_ranks = 0: no filter.
+struct CtgOwner {
+  int n_ranks, rank, m;
+};
+
 // Contig pass (kcount_ctg.hip). Scratch sizes come from ctg_scratch_bytes.
 size_t ctg_scratch_bytes(uint64_t n_windows, int nl);
 // Extract, sort by key (stable: contig order kept within a key), fold every key's contig occurrences in
@@ -140,8 +184,8 @@ size_t ctg_scratch_bytes(uint64_t n_windows, int nl);
 // go to out_keys[NL] (SoA, each out_cap long), out_state, out_bucket.
 // Only k-mers whose coarse bucket is in [own_lo, own_hi) (this rank's hash range) are kept.
 hipError_t ctg_prepare(const CtgView &cv, int k, int nl, bool mixed, int qual_cutoff, int dmin_thres,
-                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi, void *scratch,
-                       size_t scratch_bytes,
+                       double dyn_mult, int coarse_bits, int fine_bits, uint32_t own_lo, uint32_t own_hi,
+                       const CtgOwner &ow, void *scratch, size_t scratch_bytes,
                        uint64_t *const out_keys[4], uint32_t *out_state, uint32_t *out_bucket, uint64_t *n_out,
                        unsigned int *err, hipStream_t s);
 
@@ -321,11 +365,11 @@ struct OutRows {
 };
 // KmerDHT minimizer length for k (src/kcount/kmer_dht.cpp:114-116)
 inline int minimizer_len_for(int k) { return k * 2 / 3 + 1 < 15 ? 15 : (k * 2 / 3 + 1 > 27 ? 27 : k * 2 / 3 + 1); }
-// minimizer_hash_fast of n keys (nlo words each, the first k/32+1 used)
 // mhmkc_fetch_ordered: the output rows in the order of the top 32 bits of mhmkc_map_hash (kcount_owner.hip)
 size_t map_order_scratch_bytes(uint64_t n);
 hipError_t launch_map_order(const OutRows &in, uint64_t n, int nlo, void *scratch, size_t scratch_bytes, const OutRows &out,
                             hipStream_t s);
+// minimizer_hash_fast of n keys (nlo words each, the first k/32+1 used)
 hipError_t launch_minimizer_hash(const uint64_t *keys, uint64_t n, int nlo, int k, int m, uint64_t *out, hipStream_t s);
 // dest[i] = owner rank of row i; hist[r] += rows owned by rank r (zero hist first)
 hipError_t launch_owner_hist(const uint64_t *keys, uint64_t n, int nlo, int k, int m, int n_ranks, uint8_t *dest,

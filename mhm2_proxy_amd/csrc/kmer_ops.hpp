@@ -328,6 +328,42 @@ MHM_HD bool kmer_less(const uint64_t *a, const uint64_t *b) {
   return lt;
 }
 
+// quick_hash (src/hash_funcs.c:332-342)
+MHM_HD uint64_t quick_hash(uint64_t v) {
+  v = v * 3935559000370003845ull + 2691343689449507681ull;
+  v ^= v >> 21;
+  v ^= v << 37;
+  v ^= v >> 4;
+  v *= 4768777513237032717ull;
+  v ^= v << 20;
+  v ^= v >> 41;
+  v ^= v << 5;
+  return v;
+}
+
+// Kmer::get_minimizer_fast(m, least_complement = true) (src/kmer.cpp:344-393, 395-403): the greatest, over
+// the m-mer positions i in [0, k-m], of min(forward m-mer i, its reverse complement), each left-aligned in a
+// word with the low bits zero (ZERO_MASK[m], :81-87). The reference reads the reverse-complement candidate
+// of position i as the m-mer at k-m-i of revcomp(kmer), which is the reverse complement of forward m-mer
+// i; here both are rolled base by base (forward shifts a base in at the bottom, the reverse complement
+// shifts the complemented base in at the top), m <= 28.
+MHM_HD uint64_t minimizer_fast(const uint64_t *w, int k, int m) {
+  const uint64_t mm = (1ull << (2 * m)) - 1;
+  const int up = 64 - 2 * m;
+  uint64_t f = 0, r = 0, best = 0;
+  for (int j = 0; j < k; j++) {
+    const uint64_t b = (w[j >> 5] >> (62 - 2 * (j & 31))) & 3u;
+    f = ((f << 2) | b) & mm;
+    r = (r >> 2) | ((3u - b) << (2 * m - 2));
+    if (j >= m - 1) {
+      const uint64_t fl = f << up, rl = r << up;
+      const uint64_t least = fl < rl ? fl : rl;
+      best = least > best ? least : best;
+    }
+  }
+  return best;
+}
+
 // Packed-record mode: the 6-bit ext code fits into the zero low bits of the last key word.
 MHM_HD bool ext_packs(int k, int nl) { return 2 * (k - 32 * (nl - 1)) + EXT_BITS <= 64; }
 

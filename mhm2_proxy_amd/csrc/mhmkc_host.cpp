@@ -107,6 +107,12 @@ struct Slab {
   bool pending = false;  // final cursors not read yet
   std::vector<uint64_t> counts;  // [nb * NSUB]
   std::vector<uint64_t> bases;   // [nb * NSUB + 1] segment starts, bases[nb * NSUB] = end of the slab
+  // supermer exchange: a read slab's supermers per destination (words and supermers, their exact spans), or
+  // (recv) the records of the supermers this rank received
+  bool recv = false;
+  uint64_t *codes = nullptr, *desc = nullptr;
+  uint32_t *good = nullptr;
+  std::vector<uint64_t> sw, ss, swb, ssb;  // [G] words, supermers per destination and their first word / supermer
 };
 
 // Device copy of one host batch (mhmkc_add_reads); it lives until finish (a slab may be re-extracted).
@@ -166,6 +172,13 @@ struct mhmkc {
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
   DevBuf d_hll, d_dest, d_ohist, d_out2_keys, d_out2_counts, d_out2_left, d_out2_right, d_mh;
   DevBuf d_ord;  // mhmkc_fetch_ordered: sort keys, row indices, radix-sort scratch
+  // supermer exchange (smer): owner bytes of a slab's tiles; the received supermers (codes, good bits, descriptors),
+  // their window counts / prefix, per-tile first supermer, scan scratch
+  bool smer = false;
+  DevBuf d_owners, d_rcodes, d_rgood, d_rdesc, d_rnwin, d_rwpre, d_rtiles, d_rtmp;
+  mhm::SmerSource rsrc{};
+  int smer_build(Slab *sl);
+  int smer_exchange(std::vector<Source> &srcs);
   PinBuf x_send, x_recv;  // host-staged exchange
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
@@ -262,7 +275,9 @@ struct mhmkc {
 
   Slab *new_slab() {
     if (n_slabs == slabs.size()) slabs.push_back(new Slab());
-    return slabs[n_slabs++];
+    Slab *sl = slabs[n_slabs++];
+    sl->recv = false;
+    return sl;
   }
   Arena *new_arena() {
     if (n_arenas == arenas.size()) arenas.push_back(new Arena());
@@ -360,10 +375,12 @@ int mhmkc::extract(Slab *sl, bool exact) {
   p.cursor = dcur;
   p.err = d_err.as<unsigned int>();
   p.ovf = (unsigned int *)(dcur + nseg);
-  prof_begin(MHMKC_STAGE_TILEIDX);
-  e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
-  prof_end();
-  if (e != hipSuccess) return hip_fail(e, "tile index");
+  if (!sl->recv) {  // (the received supermers' tile index is made once by smer_exchange)
+    prof_begin(MHMKC_STAGE_TILEIDX);
+    e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "tile index");
+  }
   if (exact) {
     std::vector<uint64_t> hist(nb);
     prof_begin(MHMKC_STAGE_OTHER);
@@ -371,7 +388,7 @@ int mhmkc::extract(Slab *sl, bool exact) {
     prof_end();
     if (e != hipSuccess) return hip_fail(e, "memset");
     prof_begin(MHMKC_STAGE_EHIST);
-    e = mhm::launch_extract_hist(p, nl, packed, stream);
+    e = sl->recv ? mhm::launch_smer_extract(p, rsrc, nl, packed, true, stream) : mhm::launch_extract_hist(p, nl, packed, stream);
     prof_end();
     if (e != hipSuccess) return hip_fail(e, "extract_hist");
     if ((e = hipMemcpyAsync(hist.data(), d_hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
@@ -405,7 +422,7 @@ int mhmkc::extract(Slab *sl, bool exact) {
 #ifdef MHMKC_ESTAMP
   (void)hipMemsetAsync(d_hist.p, 0, 2048, stream);
 #endif
-  e = mhm::launch_extract_scatter(p, nl, packed, stream);
+  e = sl->recv ? mhm::launch_smer_extract(p, rsrc, nl, packed, false, stream) : mhm::launch_extract_scatter(p, nl, packed, stream);
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "extract_scatter");
 #ifdef MHMKC_ESTAMP
@@ -457,6 +474,7 @@ int mhmkc::add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known) {
   sl->n = 0;
   st.occurrences += wins;
   st.slabs++;
+  if (smer) return smer_build(sl);
   return extract(sl, getenv("MHMKC_DEBUG_EXACT") != nullptr);  // tests force the exact layout
 }
 
@@ -733,6 +751,199 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// supermer exchange: MHMKC_OWNER_MINIMIZER with several ranks and keys of two or more words.
+// A read slab becomes supermers per destination rank (get_kmer_target_rank, kmer_dht.cpp:193-196) instead of
+// records; finish ships them (the reference's add_supermer -> ThreeTierAggrStore, kmer_dht.cpp:222-224) and every
+// rank extracts the records of the supermers it received, over the whole hash range.
+
+int mhmkc::smer_build(Slab *sl) {
+  const int T = mhm::tile_bases(nl), g = G();
+  hipError_t e;
+  if ((e = grow(d_tiles, (size_t)sl->tiles * 4 + 64)) != hipSuccess) return hip_fail(e, "tile index");
+  if ((e = grow(d_owners, (size_t)sl->tiles * T + 64)) != hipSuccess) return hip_fail(e, "supermer owners");
+  if ((e = sl->meta.ensure((size_t)g * 32 + 64)) != hipSuccess) return hip_fail(e, "supermer counters");
+  if ((e = sl->pin.ensure((size_t)g * 32 + 64)) != hipSuccess) return hip_fail(e, "supermer counters (host)");
+  unsigned long long *hist = sl->meta.as<unsigned long long>(), *cur = hist + 2 * g;
+  mhm::SmerParams sp{};
+  sp.reads = sl->rv;
+  sp.tile_first_read = d_tiles.as<uint32_t>();
+  sp.n_tiles = sl->tiles;
+  sp.k = k;
+  sp.m = mlen;
+  sp.n_ranks = g;
+  sp.qual_cutoff = sl->qcut;
+  sp.owners = d_owners.as<uint8_t>();
+  sp.hist = hist;
+  sp.cursor = cur;
+  sp.err = d_err.as<unsigned int>();
+  prof_begin(MHMKC_STAGE_TILEIDX);
+  e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
+  prof_end();
+  if (e == hipSuccess) e = hipMemsetAsync(hist, 0, (size_t)g * 16, stream);
+  if (e != hipSuccess) return hip_fail(e, "supermer owners");
+  prof_begin(MHMKC_STAGE_EHIST);
+  e = mhm::launch_smer_owner(sp, nl, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "smer_owner");
+  uint64_t *hc = sl->pin.as<uint64_t>();
+  if ((e = hipMemcpyAsync(hc, hist, (size_t)g * 16, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess)
+    return hip_fail(e, "supermer counts");
+  sl->sw.assign(g, 0), sl->ss.assign(g, 0), sl->swb.assign(g + 1, 0), sl->ssb.assign(g + 1, 0);
+  for (int d = 0; d < g; d++) {
+    sl->sw[d] = hc[2 * d];
+    sl->ss[d] = hc[2 * d + 1];
+    sl->swb[d + 1] = sl->swb[d] + sl->sw[d];
+    sl->ssb[d + 1] = sl->ssb[d] + sl->ss[d];
+  }
+  const uint64_t W = sl->swb[g], S = sl->ssb[g];
+  const size_t cb_ = align_up(W * 8 + 16, 256), gb_ = align_up(W * 4 + 16, 256);
+  if ((e = grow(sl->buf, cb_ + gb_ + S * 8 + 64)) != hipSuccess) return hip_fail(e, "supermer planes");
+  sl->codes = sl->buf.as<uint64_t>();
+  sl->good = (uint32_t *)(sl->buf.as<char>() + cb_);
+  sl->desc = (uint64_t *)(sl->buf.as<char>() + cb_ + gb_);
+  for (int d = 0; d < g; d++) {  // cursors: each destination's span starts at its exclusive prefix
+    hc[2 * g + 2 * d] = sl->swb[d];
+    hc[2 * g + 2 * d + 1] = sl->ssb[d];
+  }
+  if ((e = hipMemcpyAsync(cur, hc + 2 * g, (size_t)g * 16, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(e, "supermer cursors");
+  sp.codes = sl->codes;
+  sp.good = sl->good;
+  sp.desc = sl->desc;
+  sp.n_words = W;
+  sp.n_smer = S;
+  prof_begin(MHMKC_STAGE_ESCAT);
+  e = mhm::launch_smer_pack(sp, nl, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "smer_pack");
+  sl->n = sl->wins;
+  sl->pending = false;
+  st.smer_words += W;
+  st.smer_count += S;
+  // the pinned counters are read back into the host vectors above; the pack's cursor copy must land before the
+  // next slab reuses them (one pinned buffer per slab: no reuse within a round)
+  return MHMKC_OK;
+}
+
+int mhmkc::smer_exchange(std::vector<Source> &srcs) {
+  const int g = G(), me = cfg.rank;
+  int rc;
+  hipError_t e;
+  // 1. every rank's per-slab span sizes (words, supermers per destination)
+  uint64_t my_slabs = n_slabs;
+  std::vector<uint64_t> slabs_of(g);
+  if ((rc = allgather_host(&my_slabs, slabs_of.data(), 8))) return rc;
+  const uint64_t ms = std::max<uint64_t>(1, *std::max_element(slabs_of.begin(), slabs_of.end()));
+  const size_t per = 2 * (size_t)g;
+  std::vector<uint64_t> mine(ms * per, 0), all((size_t)g * ms * per, 0);
+  for (size_t s = 0; s < n_slabs; s++)
+    for (int d = 0; d < g; d++) {
+      mine[s * per + 2 * d] = slabs[s]->sw[d];
+      mine[s * per + 2 * d + 1] = slabs[s]->ss[d];
+    }
+  if ((rc = allgather_host(mine.data(), all.data(), 8 * ms * per))) return rc;
+  auto W_of = [&](int p, uint64_t s) { return all[((size_t)p * ms + s) * per + 2 * me]; };
+  auto S_of = [&](int p, uint64_t s) { return all[((size_t)p * ms + s) * per + 2 * me + 1]; };
+  // 2. the received spans back to back in (peer, slab) order, this rank's own among them
+  // a descriptor's word offset counts from the start of its sender's slab planes, where this rank's span starts
+  // after the spans of the lower destinations (sb)
+  struct Span {
+    int peer;
+    uint64_t slab, w0, s0, nw, ns, sb;
+  };
+  std::vector<Span> spans;
+  uint64_t Wt = 0, St = 0;
+  for (int p = 0; p < g; p++)
+    for (uint64_t s = 0; s < slabs_of[p]; s++) {
+      const uint64_t nw = W_of(p, s), ns = S_of(p, s);
+      uint64_t sb = 0;
+      for (int d = 0; d < me; d++) sb += all[((size_t)p * ms + s) * per + 2 * d];
+      if (ns) spans.push_back({p, s, Wt, St, nw, ns, sb});
+      Wt += nw;
+      St += ns;
+    }
+  if ((e = grow(d_rcodes, Wt * 8 + 64)) != hipSuccess || (e = grow(d_rgood, Wt * 4 + 64)) != hipSuccess ||
+      (e = grow(d_rdesc, St * 8 + 64)) != hipSuccess || (e = grow(d_rnwin, (St + 1) * 8 + 64)) != hipSuccess ||
+      (e = grow(d_rwpre, (St + 1) * 8 + 64)) != hipSuccess)
+    return hip_fail(e, "supermer receive buffers");
+  uint64_t *rcodes = d_rcodes.as<uint64_t>(), *rdesc = d_rdesc.as<uint64_t>();
+  uint32_t *rgood = d_rgood.as<uint32_t>();
+  std::vector<Xfer> snd, rcv;
+  for (int p = 0; p < g; p++) {
+    if (p == me) continue;
+    for (size_t s = 0; s < n_slabs; s++) {
+      const Slab *sl = slabs[s];
+      if (!sl->ss[p]) continue;
+      snd.push_back({p, sl->codes + sl->swb[p], sl->sw[p] * 8});
+      snd.push_back({p, sl->good + sl->swb[p], sl->sw[p] * 4});
+      snd.push_back({p, sl->desc + sl->ssb[p], sl->ss[p] * 8});
+    }
+  }
+  for (const Span &sp : spans) {
+    if (sp.peer == me) {  // this rank's own supermers: device copies
+      const Slab *sl = slabs[sp.slab];
+      if ((e = hipMemcpyAsync(rcodes + sp.w0, sl->codes + sl->swb[me], sp.nw * 8, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(rgood + sp.w0, sl->good + sl->swb[me], sp.nw * 4, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(rdesc + sp.s0, sl->desc + sl->ssb[me], sp.ns * 8, hipMemcpyDeviceToDevice, stream)) != hipSuccess)
+        return hip_fail(e, "own supermers");
+      continue;
+    }
+    rcv.push_back({sp.peer, rcodes + sp.w0, sp.nw * 8});
+    rcv.push_back({sp.peer, rgood + sp.w0, sp.nw * 4});
+    rcv.push_back({sp.peer, rdesc + sp.s0, sp.ns * 8});
+  }
+  prof_begin(MHMKC_STAGE_XCHG);
+  rc = move(snd, rcv);
+  prof_end();
+  if (rc) return rc;
+  // 3. descriptors rebased to the concatenated stream, the window prefix, the tile index
+  unsigned long long *nwin = d_rnwin.as<unsigned long long>(), *wpre = d_rwpre.as<unsigned long long>();
+  prof_begin(MHMKC_STAGE_OTHER);
+  for (const Span &sp : spans)
+    if ((e = mhm::launch_smer_rebase(rdesc + sp.s0, sp.ns, sp.w0 - sp.sb, nwin + sp.s0, stream)) != hipSuccess) break;
+  if (e == hipSuccess) e = hipMemsetAsync(nwin + St, 0, 8, stream);
+  const size_t tb = mhm::fq_scan_tmp_bytes(St + 1);
+  if (e == hipSuccess) e = grow(d_rtmp, tb + 64);
+  if (e == hipSuccess) e = mhm::fq_scan(d_rtmp.p, tb, nwin, wpre, St + 1, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "supermer descriptors");
+  unsigned long long n_win = 0;
+  if ((e = hipMemcpyAsync(&n_win, wpre + St, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess)
+    return hip_fail(e, "supermer windows");
+  const int T = mhm::tile_bases(nl);
+  const uint64_t tiles64 = (n_win + T - 1) / T;
+  if (tiles64 >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many received windows in one round");
+  if ((e = grow(d_rtiles, (tiles64 + 2) * 8)) != hipSuccess) return hip_fail(e, "supermer tiles");
+  prof_begin(MHMKC_STAGE_TILEIDX);
+  e = mhm::launch_smer_tiles((const uint64_t *)wpre, St, d_rtiles.as<uint64_t>(), (uint32_t)tiles64, T, stream);
+  prof_end();
+  if (e != hipSuccess) return hip_fail(e, "supermer tiles");
+  rsrc = mhm::SmerSource{rcodes, rgood, rdesc, (const uint64_t *)wpre, d_rtiles.as<uint64_t>(), St, n_win, Wt + 2};
+  // 4. the received windows' records, as one more slab (capped layout; an overflow reruns it exactly)
+  const size_t n_read_slabs = n_slabs;
+  if (n_win) {
+    Slab *rs = new_slab();
+    rs->recv = true;
+    rs->rv = mhm::ReadsView{};
+    rs->wins = n_win;
+    rs->tiles = (uint32_t)tiles64;
+    rs->qcut = cfg.qual_cutoff;
+    rs->n = 0;
+    if ((rc = extract(rs, getenv("MHMKC_DEBUG_EXACT") != nullptr))) return rc;
+    if ((rc = resolve_slabs())) return rc;
+    Source src;
+    src.planes = rs->planes;
+    src.start.assign(rs->bases.begin(), rs->bases.begin() + (size_t)nb * NSUB);
+    src.count = rs->counts;
+    srcs.push_back(std::move(src));
+  }
+  (void)n_read_slabs;
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 // contig pass: extract, fold and bucket the contig k-mers (kcount_ctg.hip); k_count applies them
 
 // With several ranks every rank needs the contigs of all ranks, in one order, for the k-mers of its hash
@@ -820,7 +1031,8 @@ int mhmkc::prepare_ctgs() {
   prof_begin(MHMKC_STAGE_OTHER);
   // the synchronous copies above keep the host vectors alive long enough: ctg_prepare waits for its
   // fold count before returning
-  e = mhm::ctg_prepare(cv, k, nl, mixed(), 1, dmin, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, own_hi,
+  const mhm::CtgOwner ow{smer ? G() : 0, cfg.rank, mlen};  // supermer exchange: keep this rank's target k-mers
+  e = mhm::ctg_prepare(cv, k, nl, mixed(), 1, dmin, 1.0 - cfg.dyn_min_depth, cb, fb, own_lo, own_hi, ow,
                        d_ctg_scratch.p, sb, keys, d_ctg_state.as<uint32_t>(), d_ctg_bucket.as<uint32_t>(), &ctg_n,
                        d_err.as<unsigned int>(), stream);
   prof_end();
@@ -940,7 +1152,9 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   hipError_t e;
   const uint32_t no = n_owned();
   std::vector<Source> srcs;
-  if (G() > 1) {
+  if (smer) {
+    if ((rc = smer_exchange(srcs))) return rc;
+  } else if (G() > 1) {
     if ((rc = exchange(srcs))) return rc;
   } else {
     for (size_t s = 0; s < n_slabs; s++) {
@@ -1196,6 +1410,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if (hipEventElapsedTime(&ms, ev_begin, ev_end) == hipSuccess) st.ms_total = ms;
   finished = true;
   if (errf & 1u) return fail(MHMKC_EBADCHAR, "input byte with a base code > 4 (not A,C,G,T,N)");
+  if (errf & 8u) return fail(MHMKC_EHIP, "internal: supermer spans inconsistent");
   if (stats[mhm::STAT_N - 1]) return fail(MHMKC_EHIP, "internal: LDS probe bound exceeded");
   if (getenv("MHMKC_PRINT_STAMPS")) {  // k_count phase cycles of an MHMKC_STAMP build (diagnostics)
     const char *names[6] = {"clear", "loadwait", "insert", "barrier", "overflow", "finalize"};
@@ -1215,7 +1430,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   st.dropped = 0;
   n_out = st.n_out;
   if (n_out > out_cap) return fail(MHMKC_EHIP, "internal: output overflow");
-  if (cfg.output_owner == MHMKC_OWNER_MINIMIZER && G() > 1) {
+  if (cfg.output_owner == MHMKC_OWNER_MINIMIZER && G() > 1 && !smer) {  // (supermers already went to that owner)
     if ((rc = handoff())) return rc;
   }
   prof_collect();
@@ -1295,10 +1510,11 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     g_create_error = "dyn_min_depth must be in [0, 1]";
     return MHMKC_EINVAL;
   }
-  // up to 8 ranks (one node): the coarse partition then has <= 2^11 bins, what a scatter workgroup keeps
-  // in registers (scatter_staged)
-  if (cfg->n_ranks < 1 || cfg->n_ranks > 8 || cfg->rank < 0 || cfg->rank >= cfg->n_ranks) {
-    g_create_error = "bad rank / n_ranks (1..8 ranks, one per GPU of a node)";
+  // up to 255 ranks: the coarse partition has at most 2^11 bins (what a scatter workgroup keeps in registers,
+  // scatter_staged), so beyond 8 ranks a rank owns 2048 / n_ranks of them (equal hash ranges when n_ranks divides
+  // 2048); the supermer exchange keeps owners in bytes
+  if (cfg->n_ranks < 1 || cfg->n_ranks > 255 || cfg->rank < 0 || cfg->rank >= cfg->n_ranks) {
+    g_create_error = "bad rank / n_ranks (1..255 ranks)";
     return MHMKC_EINVAL;
   }
   if (cfg->output_owner != MHMKC_OWNER_HASH && cfg->output_owner != MHMKC_OWNER_MINIMIZER) {
@@ -1320,8 +1536,14 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   h->qcut_pending = cfg->qual_cutoff;
   h->packed = mhm::ext_packs(k, nl);
   h->hbits = mhm::stored_hash_bits(k, nl, h->packed);
+  // supermer exchange: the reference's owner (MHMKC_OWNER_MINIMIZER) with keys of two or more
+  // words is reached by shipping supermers, each rank then counting all of its k-mers over the whole hash range;
+  // MHMKC_SMER=0 keeps the record exchange + hand-off (A/B, tests)
+  const char *smer_env = getenv("MHMKC_SMER");
+  h->smer = cfg->output_owner == MHMKC_OWNER_MINIMIZER && cfg->n_ranks > 1 && nl >= 2 && !(smer_env && !atoi(smer_env));
   int extra = 0;
-  while ((1 << extra) < cfg->n_ranks) extra++;
+  while ((1 << extra) < cfg->n_ranks && extra < 3) extra++;
+  if (h->smer) extra = 0;
 #ifndef MHMKC_CB0
 #define MHMKC_CB0 8
 #endif
@@ -1337,8 +1559,8 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     h->hbits = 0;
   }
   h->nb = 1u << h->cb;
-  h->own_lo = h->owner_lo(cfg->rank);
-  h->own_hi = h->owner_lo(cfg->rank + 1);
+  h->own_lo = h->smer ? 0 : h->owner_lo(cfg->rank);
+  h->own_hi = h->smer ? h->nb : h->owner_lo(cfg->rank + 1);
   hipError_t e;
   if (cfg->device >= 0) {
     if ((e = hipSetDevice(cfg->device)) != hipSuccess) {
@@ -1404,6 +1626,8 @@ void mhmkc_destroy(mhmkc_t h) {
                     &h->d_out_keys, &h->d_out_counts, &h->d_out_left,   &h->d_out_right,  &h->d_out_cursor,
                     &h->d_recv,     &h->d_xg,         &h->d_hll,        &h->d_dest,       &h->d_ohist,
                     &h->d_out2_keys, &h->d_out2_counts, &h->d_out2_left, &h->d_out2_right, &h->d_mh, &h->d_ord,
+                    &h->d_owners, &h->d_rcodes, &h->d_rgood, &h->d_rdesc, &h->d_rnwin, &h->d_rwpre, &h->d_rtiles,
+                    &h->d_rtmp,
                     &h->d_fqa_bytes, &h->d_fqa_offs,
                     &h->d_fq_text,  &h->d_fq_chunk,   &h->d_fq_lines,   &h->d_fq_len,     &h->d_fq_tmp,
                     &h->d_fq_bytes, &h->d_fq_offs,    &h->d_fq_err};

@@ -499,6 +499,104 @@ class TorchDistTransport:
             return 1
 
 
+class SharedGpuCounter:
+    """Several host ranks over fewer GPU counters: the reference's launch runs one rank per core and maps rank r to
+    GPU r % n_devices (gpu_utils::set_gpu_device, src/gpu-utils/gpu_utils.cpp:68-75; src/devices_gpu.cpp:61), while
+    one GPU holds one counter. Rank r belongs to counter group g = r % n_counters; the group's leader (rank g) owns
+    the counter (KmerCounter rank g of n_counters, MHMKC_OWNER_MINIMIZER, the leaders exchanging through the host
+    transport over their own process group), the other members hand their PackedReads to it, and after the finish
+    the leader sends every member the rows it owns. With n_counters dividing the number of ranks, the rows of
+    counter g (get_kmer_target_rank % n_counters == g) are exactly those whose get_kmer_target_rank over all ranks
+    is a member of group g (t % n_ranks = r implies t % n_counters = r % n_counters), so every rank ends with the
+    table the reference's KmerDHT would hold (kmer_dht.cpp:193-196). Non-leaders never touch a GPU.
+
+    Collective over the default torch.distributed process group (gloo: CPU tensors); every rank creates it."""
+
+    def __init__(self, k: int, n_counters: int, *, device: int = 0, **counter_kwargs):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.k, self.world, self.rank = k, dist.get_world_size(), dist.get_rank()
+        if n_counters < 1 or self.world % n_counters:
+            raise ValueError("n_counters must divide the number of ranks")
+        self.n_counters = n_counters
+        self.group_id = self.rank % n_counters
+        self.leader = self.group_id
+        self.members = list(range(self.group_id, self.world, n_counters))
+        # every rank takes part in creating every group (torch.distributed.new_group is collective)
+        leaders = dist.new_group(list(range(n_counters)))
+        self.counter = None
+        if self.rank == self.leader:
+            self.counter = KmerCounter(k, device=device, rank=self.group_id, n_ranks=n_counters,
+                                       transport=TorchDistTransport(leaders) if n_counters > 1 else None,
+                                       output_owner=N.MHMKC_OWNER_MINIMIZER, **counter_kwargs)
+        self._reads = []
+
+    def add_packed_reads(self, packed_bytes: np.ndarray, offsets: np.ndarray) -> None:
+        self._reads.append((np.ascontiguousarray(packed_bytes, dtype=np.uint8),
+                            np.ascontiguousarray(offsets, dtype=np.uint64)))
+
+    def _send_arrays(self, arrays, dst: int) -> None:
+        import torch
+
+        sizes = torch.tensor([a.nbytes for a in arrays], dtype=torch.int64)
+        self.dist.send(torch.tensor([len(arrays)], dtype=torch.int64), dst)
+        self.dist.send(sizes, dst)
+        for a in arrays:
+            if a.nbytes:
+                self.dist.send(torch.from_numpy(a.view(np.uint8).reshape(-1).copy()), dst)
+
+    def _recv_arrays(self, src: int) -> list:
+        import torch
+
+        n = torch.zeros(1, dtype=torch.int64)
+        self.dist.recv(n, src)
+        sizes = torch.zeros(int(n.item()), dtype=torch.int64)
+        self.dist.recv(sizes, src)
+        out = []
+        for sz in sizes.tolist():
+            t = torch.empty(sz, dtype=torch.uint8)
+            if sz:
+                self.dist.recv(t, src)
+            out.append(t.numpy())
+        return out
+
+    def finish(self) -> KmerTable:
+        """Count every member's reads on the group's GPU, exchange between the counters, and return this rank's
+        rows (the k-mers whose get_kmer_target_rank over all ranks is this rank)."""
+        nl = n_longs_for(self.k)
+        if self.rank != self.leader:  # members: reads to the leader, then this rank's rows back
+            flat = [a for pair in self._reads for a in pair]
+            self._send_arrays(flat, self.leader)
+            keys, counts, left, right = self._recv_arrays(self.leader)
+            return KmerTable(self.k, keys.view(np.uint64).reshape(-1, nl), counts.view(np.uint16), left, right)
+        c = self.counter
+        for b, o in self._reads:
+            c.add_packed_reads(b, o)
+        for m in self.members[1:]:
+            got = self._recv_arrays(m)
+            for i in range(0, len(got), 2):
+                c.add_packed_reads(got[i], got[i + 1].view(np.uint64))
+        c.finish()
+        t = c.fetch()
+        owner = c.target_ranks(t.keys, self.world) if len(t) else np.zeros(0, np.int64)
+        mine = None
+        for m in self.members:
+            sel = np.flatnonzero(owner == m)
+            part = [np.ascontiguousarray(t.keys[sel]), np.ascontiguousarray(t.counts[sel]),
+                    np.ascontiguousarray(t.left[sel]), np.ascontiguousarray(t.right[sel])]
+            if m == self.rank:
+                mine = KmerTable(self.k, *part)
+            else:
+                self._send_arrays(part, m)
+        return mine
+
+    def close(self) -> None:
+        if self.counter is not None:
+            self.counter.close()
+            self.counter = None
+
+
 def comm_id() -> bytes:
     """RCCL unique id for multi-rank counters (rank 0 creates it and broadcasts it)."""
     buf = C.create_string_buffer(N.MHMKC_COMM_ID_BYTES)

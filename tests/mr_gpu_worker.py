@@ -28,9 +28,9 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     from common import ctg_set, synth_set
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     for key, val in opts.get("env", {}).items():
         os.environ[key] = val
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     if opts.get("contigs"):
         b, o, seqs, depths = ctg_set(seed=opts["seed"], n_reads=opts.get("n_reads", 300))
     else:
@@ -57,7 +57,28 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
              bytes_sent=st["bytes_sent"], bytes_recv=st["bytes_recv"], occurrences=st["occurrences"],
              owned=st["owned_records"], count_sum=st["count_sum"], distinct=st["distinct"], purged=st["purged"],
              n_out=st["n_out"], handoff_sent=st["handoff_sent"], handoff_recv=st["handoff_recv"],
-             ctg_kmers=st["ctg_kmers"])
+             ctg_kmers=st["ctg_kmers"], smer_count=st["smer_count"], smer_words=st["smer_words"])
     c.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_shared(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
+    """One host rank of a SharedGpuCounter: world ranks over opts["counters"] counters on the one GPU."""
+    import torch.distributed as dist
+
+    import mhm2_proxy_amd as m
+    from common import synth_set
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, o = synth_set(opts.get("n_reads", 1200), opts.get("genome", 9000), opts["seed"])
+    lo, hi = shard(o.size - 1, rank, world)
+    sc = m.SharedGpuCounter(k, opts["counters"], device=0)
+    sc.add_packed_reads(b[int(o[lo]):int(o[hi])], (o[lo:hi + 1] - o[lo]).astype(np.uint64))
+    t = sc.finish()
+    np.savez(Path(out_dir) / f"rank{rank}.npz", keys=t.keys, counts=t.counts, left=t.left, right=t.right,
+             leader=int(sc.counter is not None))
+    sc.close()
     dist.barrier()
     dist.destroy_process_group()
