@@ -1083,10 +1083,13 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_smer_owner(SmerParams p) {
   uint32_t *gown = (uint32_t *)(p.owners + (uint64_t)tile * T);
   for (int i = threadIdx.x; i < T / 4; i += ET) gown[i] = ((const uint32_t *)own)[i];
   __syncthreads();
+  // counters per (destination, slice): consecutive tiles add to different words (with a handful of ranks one word
+  // per destination took every workgroup's atomics: 16 ms for 2M reads)
+  unsigned long long *h = p.hist + 2 * (uint64_t)(blockIdx.x % SMER_SLICES);
   for (int d = threadIdx.x; d < G; d += ET) {
     if (dcnt[2 * d + 1]) {
-      atomicAdd(&p.hist[2 * d], (unsigned long long)dcnt[2 * d]);
-      atomicAdd(&p.hist[2 * d + 1], (unsigned long long)dcnt[2 * d + 1]);
+      atomicAdd(&h[2 * SMER_SLICES * d], (unsigned long long)dcnt[2 * d]);
+      atomicAdd(&h[2 * SMER_SLICES * d + 1], (unsigned long long)dcnt[2 * d + 1]);
     }
   }
 }
@@ -1126,10 +1129,11 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_smer_pack(SmerParams p) {
     }
   }
   __syncthreads();
+  unsigned long long *cur = p.cursor + 2 * (uint64_t)(blockIdx.x % SMER_SLICES);  // this tile's slice (k_smer_owner)
   for (int d = threadIdx.x; d < G; d += ET) {
     const uint32_t nw = dcnt[2 * d], ns = dcnt[2 * d + 1];
-    goff[2 * d] = ns ? atomicAdd(&p.cursor[2 * d], (unsigned long long)nw) : 0ull;
-    goff[2 * d + 1] = ns ? atomicAdd(&p.cursor[2 * d + 1], (unsigned long long)ns) : 0ull;
+    goff[2 * d] = ns ? atomicAdd(&cur[2 * SMER_SLICES * d], (unsigned long long)nw) : 0ull;
+    goff[2 * d + 1] = ns ? atomicAdd(&cur[2 * SMER_SLICES * d + 1], (unsigned long long)ns) : 0ull;
   }
   __syncthreads();
   // the staged words past the tile read as zero (they only fill masked bits of a supermer's last word)

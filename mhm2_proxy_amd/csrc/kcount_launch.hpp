@@ -46,6 +46,7 @@ struct ExtractParams {
   unsigned int *ovf;                // bit 1: a capped bin of this slab overflowed (per slab)
 };
 
+constexpr int SMER_SLICES = 64;  // counter slices per destination (spread the workgroups' atomics)
 // Supermer exchange (kcount_kernels.hip). Sender side, per read slab: owners and per-destination
 // counts (k_smer_owner), then the supermers packed into exact per-destination spans (k_smer_pack).
 struct SmerParams {
@@ -54,8 +55,9 @@ struct SmerParams {
   uint32_t n_tiles;
   int k, m, n_ranks, qual_cutoff;
   uint8_t *owners;              // [n_tiles * tile]: owner of the window at each tile position, 0xFF: not counted
-  unsigned long long *hist;     // [2 n_ranks]: words, supermers per destination (k_smer_owner adds)
-  unsigned long long *cursor;   // [2 n_ranks]: word cursor, supermer cursor per destination (k_smer_pack)
+  unsigned long long *hist;     // [n_ranks][SMER_SLICES][2]: words, supermers per destination and slice of tiles
+                                // (tile % SMER_SLICES; k_smer_owner adds)
+  unsigned long long *cursor;   // the same layout: word and supermer cursors (k_smer_pack)
   uint64_t *codes;              // supermer bases, 2-bit codes, 32 per word (MSB first)
   uint32_t *good;               // their "extension countable" bits, 32 per word
   uint64_t *desc;               // per supermer: first word << 16 | windows

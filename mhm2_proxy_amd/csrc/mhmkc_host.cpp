@@ -761,9 +761,11 @@ int mhmkc::smer_build(Slab *sl) {
   hipError_t e;
   if ((e = grow(d_tiles, (size_t)sl->tiles * 4 + 64)) != hipSuccess) return hip_fail(e, "tile index");
   if ((e = grow(d_owners, (size_t)sl->tiles * T + 64)) != hipSuccess) return hip_fail(e, "supermer owners");
-  if ((e = sl->meta.ensure((size_t)g * 32 + 64)) != hipSuccess) return hip_fail(e, "supermer counters");
-  if ((e = sl->pin.ensure((size_t)g * 32 + 64)) != hipSuccess) return hip_fail(e, "supermer counters (host)");
-  unsigned long long *hist = sl->meta.as<unsigned long long>(), *cur = hist + 2 * g;
+  constexpr int NS = mhm::SMER_SLICES;
+  const size_t nc = 2 * (size_t)g * NS;  // [destination][slice][words, supermers]
+  if ((e = sl->meta.ensure(nc * 16 + 64)) != hipSuccess) return hip_fail(e, "supermer counters");
+  if ((e = sl->pin.ensure(nc * 16 + 64)) != hipSuccess) return hip_fail(e, "supermer counters (host)");
+  unsigned long long *hist = sl->meta.as<unsigned long long>(), *cur = hist + nc;
   mhm::SmerParams sp{};
   sp.reads = sl->rv;
   sp.tile_first_read = d_tiles.as<uint32_t>();
@@ -779,20 +781,29 @@ int mhmkc::smer_build(Slab *sl) {
   prof_begin(MHMKC_STAGE_TILEIDX);
   e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
   prof_end();
-  if (e == hipSuccess) e = hipMemsetAsync(hist, 0, (size_t)g * 16, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(hist, 0, nc * 8, stream);
   if (e != hipSuccess) return hip_fail(e, "supermer owners");
   prof_begin(MHMKC_STAGE_EHIST);
   e = mhm::launch_smer_owner(sp, nl, stream);
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "smer_owner");
   uint64_t *hc = sl->pin.as<uint64_t>();
-  if ((e = hipMemcpyAsync(hc, hist, (size_t)g * 16, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(hc, hist, nc * 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
       (e = hipStreamSynchronize(stream)) != hipSuccess)
     return hip_fail(e, "supermer counts");
   sl->sw.assign(g, 0), sl->ss.assign(g, 0), sl->swb.assign(g + 1, 0), sl->ssb.assign(g + 1, 0);
+  uint64_t *hcur = hc + nc;  // cursors: destination-major spans, each cut into its slices in order
+  uint64_t wacc = 0, sacc = 0;
   for (int d = 0; d < g; d++) {
-    sl->sw[d] = hc[2 * d];
-    sl->ss[d] = hc[2 * d + 1];
+    for (int q = 0; q < NS; q++) {
+      const size_t i = 2 * ((size_t)d * NS + q);
+      hcur[i] = wacc;
+      hcur[i + 1] = sacc;
+      wacc += hc[i];
+      sacc += hc[i + 1];
+      sl->sw[d] += hc[i];
+      sl->ss[d] += hc[i + 1];
+    }
     sl->swb[d + 1] = sl->swb[d] + sl->sw[d];
     sl->ssb[d + 1] = sl->ssb[d] + sl->ss[d];
   }
@@ -802,11 +813,7 @@ int mhmkc::smer_build(Slab *sl) {
   sl->codes = sl->buf.as<uint64_t>();
   sl->good = (uint32_t *)(sl->buf.as<char>() + cb_);
   sl->desc = (uint64_t *)(sl->buf.as<char>() + cb_ + gb_);
-  for (int d = 0; d < g; d++) {  // cursors: each destination's span starts at its exclusive prefix
-    hc[2 * g + 2 * d] = sl->swb[d];
-    hc[2 * g + 2 * d + 1] = sl->ssb[d];
-  }
-  if ((e = hipMemcpyAsync(cur, hc + 2 * g, (size_t)g * 16, hipMemcpyHostToDevice, stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(cur, hcur, nc * 8, hipMemcpyHostToDevice, stream)) != hipSuccess)
     return hip_fail(e, "supermer cursors");
   sp.codes = sl->codes;
   sp.good = sl->good;

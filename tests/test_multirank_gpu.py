@@ -163,3 +163,34 @@ def test_ranks_sharing_gpu_counters(k, tmp_path):
         keys = np.ascontiguousarray(p["keys"][:, :nl], dtype=np.uint64)
         assert len(keys) > 0
         assert all(L.orc_kmer_target_rank(keys[i].ctypes.data, k, nl, world) == r for i in range(len(keys)))
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(1500)
+@pytest.mark.parametrize("k,reads_per_rank,owner", [(21, 12_500_000, "hash"), (63, 6_250_000, "minimizer")])
+def test_c3_c4_rank_share_vs_cpu_restatement(k, reads_per_rank, owner, tmp_path):
+    """two ranks on the one GPU, each with a C3 / C4 per-rank share (12.5M reads is C3's share at
+    8 GPUs; k = 63 with 6.25M, C4's share at 16) of the 500 Mbp C3 read set (seed 3), exchanged over the host
+    transport; the union of the two tables is compared row by row with the multi-threaded CPU restatement
+    (oracle/kcount_mt.c) of all their reads."""
+    import torch.multiprocessing as mp
+
+    import mr_gpu_worker
+
+    world = 2
+    opts = {"reads_per_rank": reads_per_rank, "genome": 500_000_000, "seed": 3, "owner": owner}
+    mp.spawn(mr_gpu_worker.run_share, args=(world, free_port(), k, str(tmp_path), opts), nprocs=world, join=True)
+    stats = [dict(np.load(tmp_path / f"rank{r}_stats.npz")) for r in range(world)]
+    assert sum(int(s["owned_records"]) for s in stats) == sum(int(s["occurrences"]) for s in stats)
+    assert sum(int(s["bytes_sent"]) for s in stats) == sum(int(s["bytes_recv"]) for s in stats) > 0
+    parts = [{n: np.load(tmp_path / f"rank{r}_{n}.npy") for n in ("keys", "counts", "left", "right")}
+             for r in range(world)]
+    got = union(parts, k)
+    del parts
+    g = m.synth_genome(500_000_000, 3)
+    b, o = m.synth_reads(g, world * reads_per_rank, 150, 3)
+    del g
+    t = O.kcount_mt(b, o, k, threads=16)
+    del b, o
+    keys, c, l, r = t.fetch()
+    assert_tables_equal(got, m.KmerTable(k, keys, c, l, r), f"C3/C4 share x{world}, k={k}, {owner}")
