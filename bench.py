@@ -559,6 +559,12 @@ def main():
                           "wire": ("supermers (2-bit codes + extension bits in 32-base words + a descriptor)"
                                    if st["smer_count"] else "records"),
                           "handoff_rows_sent_rank0": st["handoff_sent"],
+                          "pipelined": bool(st["xchg_rounds"]),
+                          "rounds_rank0": st["xchg_rounds"],
+                          # pipelined: device time of the rounds' transfers, and the part of it after the last
+                          # extraction ended (the rest overlapped extraction)
+                          "ms_transfers_rank0": round(st["ms_xchg"], 3) if st["xchg_rounds"] else None,
+                          "ms_exposed_rank0": round(st["ms_xchg_exposed"], 3) if st["xchg_rounds"] else None,
                           "GBps_rank0": round(st["bytes_sent"] / (per_step["exchange"] * 1e-3) / 1e9, 2)
                           if per_step.get("exchange") else None}
                          if world > 1 and st else None),

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 9
+#define MHMKC_ABI_VERSION 10
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -121,6 +121,9 @@ typedef struct {
   uint64_t fq_file_blocks; /* mhmkc_add_fastq[_pairs]_file: blocks of the last call */
   uint64_t smer_count;     /* supermer exchange: supermers this rank built (all destinations, itself included) */
   uint64_t smer_words;     /* ... their 32-base words (each a u64 of 2-bit codes + a u32 of extension bits) */
+  uint64_t xchg_rounds;    /* pipelined record exchange: rounds (one per slab of the rank with the most slabs) */
+  double ms_xchg;          /* ... device time of the rounds' transfers (exchange stream events, summed) */
+  double ms_xchg_exposed;  /* ... of it after the last extraction ended (what the overlap did not hide) */
 } mhmkc_stats;
 
 enum {

@@ -106,6 +106,9 @@ class MhmkcStats(C.Structure):
         ("fq_file_blocks", C.c_uint64),
         ("smer_count", C.c_uint64),
         ("smer_words", C.c_uint64),
+        ("xchg_rounds", C.c_uint64),
+        ("ms_xchg", C.c_double),
+        ("ms_xchg_exposed", C.c_double),
     ]
 
     def as_dict(self) -> dict:

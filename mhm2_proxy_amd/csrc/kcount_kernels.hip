@@ -1701,6 +1701,12 @@ constexpr int G_FULL = -8, G_BUSY = -9;
 #ifndef MHMKC_EXAM2
 #define MHMKC_EXAM2 1
 #endif
+// Compact keys in a cold sweep take a phase A with all claims in flight together (MHMKC_FASTA=0: the general one).
+#ifndef MHMKC_FASTA
+#define MHMKC_FASTA 1
+#endif
+constexpr bool kFastA = MHMKC_FASTA != 0;
+
 template <int NL, typename K>
 __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_t *key, int g, const K (&v)[4]) {
   const K kl = (K)key[NL - 1];
@@ -2310,6 +2316,41 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         //    reads of a batch in flight together), then found records are counted, missed ones listed.
         uint32_t old[R], defer = 0, okm = 0, missm = 0;
         int slot[R], g[R];
+        if constexpr (RK::C32 && COLD && WQ && kFastA) {
+          // compact keys in a cold sweep: the R home groups read back to back and examined, every claim CAS
+          // issued before the first one is waited for (the general path below waits for each in turn), then the
+          // non-returning adds; misses join the wave queue below. Same verdicts as the general path.
+          K gv[R][4];
+          uint32_t res[R];
+#pragma unroll
+          for (int j = 0; j < R; j++) {
+            g[j] = cmp_group((uint32_t)ck[j][0], kshl, (uint32_t)ng);
+            read_group(last, g[j], gv[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < R; j++) slot[j] = examine_group<NL>(t, ck[j], g[j], gv[j]);
+#pragma unroll
+          for (int j = 0; j < R; j++) {
+            res[j] = 0u;
+            if (ce[j] != NONE && slot[j] < 0 && slot[j] > G_FULL)  // slot -1 - r of the home group was empty: claim it
+              res[j] = atomicCAS((unsigned int *)&last[4 * g[j] - 1 - slot[j]], 0xffffffffu, (uint32_t)ck[j][0]);
+          }
+#pragma unroll
+          for (int j = 0; j < R; j++) {
+            old[j] = 0;
+            int r = slot[j];
+            if (r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = 4 * g[j] - 1 - r;
+            if (ce[j] == NONE) {
+              slot[j] = -3;
+            } else if (r >= 0) {
+              slot[j] = r;
+              lds_add_nr(t, r, ce[j], &s_wave[wid]);
+              okm |= 1u << j;
+            } else {  // a full home group, or a lost claim (lds_insert re-examines the group)
+              missm |= 1u << j;
+            }
+          }
+        } else {
 #pragma unroll
         for (int j0 = 0; j0 < R; j0 += C_BATCH) {
           K v[C_BATCH][4];
@@ -2384,6 +2425,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #endif
           okm |= 1u << j;
         }
+        }  // general phase A
         if constexpr (WQ) {
           // this wave's misses join its own queue (ballot + prefix: no LDS atomic); a queue without room for
           // them inserts in place, as a full shared list did

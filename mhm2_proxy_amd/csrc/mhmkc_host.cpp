@@ -105,6 +105,7 @@ struct Slab {
   uint32_t tiles = 0;
   int qcut = 20;         // quality cutoff of its batch (mhmkc_add_seqs encodes quality as case: cutoff 1)
   bool pending = false;  // final cursors not read yet
+  hipEvent_t ev = nullptr;  // recorded after the extraction and its cursor D2H (the pipelined exchange waits on it)
   std::vector<uint64_t> counts;  // [nb * NSUB]
   std::vector<uint64_t> bases;   // [nb * NSUB + 1] segment starts, bases[nb * NSUB] = end of the slab
   // supermer exchange: a read slab's supermers per destination (words and supermers, their exact spans), or
@@ -118,6 +119,19 @@ struct Slab {
 // Device copy of one host batch (mhmkc_add_reads); it lives until finish (a slab may be re-extracted).
 struct Arena {
   DevBuf bytes, offs;
+};
+
+// Records received in one round of the pipelined exchange: one span per sending peer, each with
+// the peer's segment starts / counts of this rank's owned range.
+struct RecvPart {
+  DevBuf buf;
+  mhm::PlaneSet planes{};
+  struct Span {
+    uint64_t off;                 // first record of the span in planes
+    std::vector<uint64_t> start;  // [n_owned * NSUB], relative to the planes
+    std::vector<uint64_t> count;  // [n_owned * NSUB]
+  };
+  std::vector<Span> spans;
 };
 
 // A source of owned records for the fine partition: per owned coarse bucket (local index) and segment.
@@ -167,6 +181,21 @@ struct mhmkc {
   size_t n_slabs = 0;
   std::vector<Arena *> arenas;  // pool; first n_arenas are in use
   size_t n_arenas = 0;
+  // pipelined exchange (xpipe): slabs [0, xq) have been sent, one round per slab, on xstream while
+  // the next slab is extracted; received records land in parts [0, n_parts)
+  bool xpipe = false;
+  int xpieces = 4;  // a device batch is cut into this many slabs (so that there is a next slab to overlap)
+  hipStream_t xstream = nullptr;
+  std::vector<RecvPart *> parts;
+  size_t n_parts = 0, xq = 0;
+  uint64_t x_rounds = 0;
+  bool x_all_done = false;
+  double x_ms = 0;
+  hipEvent_t ev_xdone = nullptr, ev_xext = nullptr;
+  std::vector<hipEvent_t> x_ev;  // per round: start / end of the round's transfer on xstream
+  int xround(Slab *sl, bool done);
+  int pump();
+  int resolve_one(Slab *sl, bool &redo);
   std::vector<hipEvent_t> chunk_ev;  // one per H2D chunk in flight (pool)
   DevBuf d_hist, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
@@ -310,8 +339,8 @@ struct mhmkc {
   int extract(Slab *sl, bool exact);
   int resolve_slabs();
   int add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut);
-  int allgather_host(const void *send, void *recv, size_t bytes);
-  int move(const std::vector<Xfer> &snd, const std::vector<Xfer> &rcv);
+  int allgather_host(const void *send, void *recv, size_t bytes, hipStream_t xs = nullptr);
+  int move(const std::vector<Xfer> &snd, const std::vector<Xfer> &rcv, hipStream_t xs = nullptr);
   int exchange(std::vector<Source> &srcs);
   int gather_ctgs(std::vector<uint8_t> &gb, std::vector<uint64_t> &go, std::vector<uint64_t> &gw,
                   std::vector<uint16_t> &gd);
@@ -438,6 +467,8 @@ int mhmkc::extract(Slab *sl, bool exact) {
 #endif
   if ((e = hipMemcpyAsync(hc, dcur, (size_t)nseg * 8 + 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
     return hip_fail(e, "cursor D2H");
+  if (!sl->ev && (e = hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "slab event");
+  if ((e = hipEventRecord(sl->ev, stream)) != hipSuccess) return hip_fail(e, "slab event");
   sl->pending = true;
   return MHMKC_OK;
 }
@@ -475,43 +506,45 @@ int mhmkc::add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known) {
   st.occurrences += wins;
   st.slabs++;
   if (smer) return smer_build(sl);
-  return extract(sl, getenv("MHMKC_DEBUG_EXACT") != nullptr);  // tests force the exact layout
+  int rc = extract(sl, getenv("MHMKC_DEBUG_EXACT") != nullptr);  // tests force the exact layout
+  return rc ? rc : pump();
 }
 
-// Read the final cursors of every pending slab (one wait for all of them); a slab whose capped segment
-// overflowed (skewed input: very repetitive reads) is extracted again with exact sizes.
-int mhmkc::resolve_slabs() {
-  bool any = false;
-  for (size_t s = 0; s < n_slabs; s++) any |= slabs[s]->pending;
-  if (!any) return MHMKC_OK;
-  hipError_t e;
+// The final cursors of a pending slab (its event: the extraction and the cursor D2H are done). A slab whose capped
+// segment overflowed (skewed input: very repetitive reads) is extracted again with exact sizes (redo: read it again).
+int mhmkc::resolve_one(Slab *sl, bool &redo) {
   const uint32_t nseg = nb * NSUB;
-  for (int pass = 0; pass < 2; pass++) {
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "extract");
-    bool redo = false;
-    for (size_t s = 0; s < n_slabs; s++) {
-      Slab *sl = slabs[s];
-      if (!sl->pending) continue;
-      const uint64_t *hc = sl->pin.as<uint64_t>();
-      if (hc[nseg] & 2u) {  // a capped segment overflowed: its excess records were not written
-        if (pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
-        st.exact_reruns++;
-        int rc = extract(sl, true);
-        if (rc) return rc;
-        redo = true;
-        continue;
-      }
-      uint64_t tot = 0;
-      for (uint32_t i = 0; i < nseg; i++) {
-        sl->counts[i] = hc[(size_t)(i % NSUB) * nb + i / NSUB] - sl->bases[i];
-        tot += sl->counts[i];
-      }
-      if (tot != sl->wins) return fail(MHMKC_EHIP, "internal: slab holds %llu records, expected %llu",
-                                       (unsigned long long)tot, (unsigned long long)sl->wins);
-      sl->n = tot;
-      sl->pending = false;
+  hipError_t e;
+  redo = false;
+  if ((e = hipEventSynchronize(sl->ev)) != hipSuccess) return hip_fail(e, "extract");
+  const uint64_t *hc = sl->pin.as<uint64_t>();
+  if (hc[nseg] & 2u) {  // a capped segment overflowed: its excess records were not written
+    st.exact_reruns++;
+    redo = true;
+    return extract(sl, true);
+  }
+  uint64_t tot = 0;
+  for (uint32_t i = 0; i < nseg; i++) {
+    sl->counts[i] = hc[(size_t)(i % NSUB) * nb + i / NSUB] - sl->bases[i];
+    tot += sl->counts[i];
+  }
+  if (tot != sl->wins) return fail(MHMKC_EHIP, "internal: slab holds %llu records, expected %llu",
+                                   (unsigned long long)tot, (unsigned long long)sl->wins);
+  sl->n = tot;
+  sl->pending = false;
+  return MHMKC_OK;
+}
+
+// Read the final cursors of every pending slab (in order; the last one's event covers the others).
+int mhmkc::resolve_slabs() {
+  for (size_t s = 0; s < n_slabs; s++) {
+    Slab *sl = slabs[s];
+    for (int pass = 0; sl->pending; pass++) {
+      bool redo = false;
+      int rc = resolve_one(sl, redo);
+      if (rc) return rc;
+      if (redo && pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
     }
-    if (!redo) break;
   }
   return MHMKC_OK;
 }
@@ -593,7 +626,8 @@ int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads
 // ------------------------------------------------------------------------------------------------
 // collectives between ranks: RCCL over xGMI (comm) or the caller's host transport (xp)
 
-int mhmkc::allgather_host(const void *send, void *recv, size_t bytes) {
+int mhmkc::allgather_host(const void *send, void *recv, size_t bytes, hipStream_t xs) {
+  if (!xs) xs = stream;
   if (has_xp) {
     if (!xp.allgather || xp.allgather(xp.ctx, send, recv, bytes) != 0)
       return fail(MHMKC_ETRANSPORT, "transport allgather failed");
@@ -605,11 +639,11 @@ int mhmkc::allgather_host(const void *send, void *recv, size_t bytes) {
   ncclResult_t nr;
   if ((e = grow(d_xg, bytes * (g + 1) + 64)) != hipSuccess) return hip_fail(e, "allgather buffer");
   char *d = d_xg.as<char>();
-  if ((e = hipMemcpyAsync(d, send, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess) return hip_fail(e, "allgather H2D");
-  if ((nr = ncclAllGather(d, d + bytes, bytes, ncclUint8, comm, stream)) != ncclSuccess)
+  if ((e = hipMemcpyAsync(d, send, bytes, hipMemcpyHostToDevice, xs)) != hipSuccess) return hip_fail(e, "allgather H2D");
+  if ((nr = ncclAllGather(d, d + bytes, bytes, ncclUint8, comm, xs)) != ncclSuccess)
     return fail(MHMKC_ERCCL, "ncclAllGather: %s", ncclGetErrorString(nr));
-  if ((e = hipMemcpyAsync(recv, d + bytes, bytes * g, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-      (e = hipStreamSynchronize(stream)) != hipSuccess)
+  if ((e = hipMemcpyAsync(recv, d + bytes, bytes * g, hipMemcpyDeviceToHost, xs)) != hipSuccess ||
+      (e = hipStreamSynchronize(xs)) != hipSuccess)
     return hip_fail(e, "allgather D2H");
   return MHMKC_OK;
 }
@@ -617,8 +651,9 @@ int mhmkc::allgather_host(const void *send, void *recv, size_t bytes) {
 // Point-to-point transfers of device buffers, given per peer in the same order on both sides (snd and rcv
 // sorted by peer). RCCL: one group of ncclSend/ncclRecv. Host transport: staged through pinned memory,
 // one alltoallv call.
-int mhmkc::move(const std::vector<Xfer> &snd, const std::vector<Xfer> &rcv) {
+int mhmkc::move(const std::vector<Xfer> &snd, const std::vector<Xfer> &rcv, hipStream_t xs) {
   const int g = G();
+  if (!xs) xs = stream;
   hipError_t e;
   for (auto &x : snd) st.bytes_sent += x.bytes;
   for (auto &x : rcv) st.bytes_recv += x.bytes;
@@ -632,30 +667,30 @@ int mhmkc::move(const std::vector<Xfer> &snd, const std::vector<Xfer> &rcv) {
     char *hs = x_send.as<char>(), *hr = x_recv.as<char>();
     uint64_t o = 0;
     for (auto &x : snd) {
-      if (x.bytes && (e = hipMemcpyAsync(hs + o, x.ptr, x.bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+      if (x.bytes && (e = hipMemcpyAsync(hs + o, x.ptr, x.bytes, hipMemcpyDeviceToHost, xs)) != hipSuccess)
         return hip_fail(e, "exchange D2H");
       o += x.bytes;
     }
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange D2H");
+    if ((e = hipStreamSynchronize(xs)) != hipSuccess) return hip_fail(e, "exchange D2H");
     if (!xp.alltoallv || xp.alltoallv(xp.ctx, hs, sb.data(), hr, rb.data()) != 0)
       return fail(MHMKC_ETRANSPORT, "transport alltoallv failed");
     o = 0;
     for (auto &x : rcv) {
-      if (x.bytes && (e = hipMemcpyAsync(x.ptr, hr + o, x.bytes, hipMemcpyHostToDevice, stream)) != hipSuccess)
+      if (x.bytes && (e = hipMemcpyAsync(x.ptr, hr + o, x.bytes, hipMemcpyHostToDevice, xs)) != hipSuccess)
         return hip_fail(e, "exchange H2D");
       o += x.bytes;
     }
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "exchange H2D");  // x_recv is reused
+    if ((e = hipStreamSynchronize(xs)) != hipSuccess) return hip_fail(e, "exchange H2D");  // x_recv is reused
     return MHMKC_OK;
   }
   if (!comm) return fail(MHMKC_ETRANSPORT, "n_ranks > 1 needs comm_id or mhmkc_set_transport");
   ncclResult_t nr;
   if ((nr = ncclGroupStart()) != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupStart: %s", ncclGetErrorString(nr));
   for (auto &x : snd)
-    if (x.bytes && (nr = ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, comm, stream)) != ncclSuccess) break;
+    if (x.bytes && (nr = ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, comm, xs)) != ncclSuccess) break;
   if (nr == ncclSuccess)
     for (auto &x : rcv)
-      if (x.bytes && (nr = ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, comm, stream)) != ncclSuccess) break;
+      if (x.bytes && (nr = ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, comm, xs)) != ncclSuccess) break;
   ncclResult_t ne = ncclGroupEnd();
   if (nr != ncclSuccess) return fail(MHMKC_ERCCL, "ncclSend/Recv: %s", ncclGetErrorString(nr));
   if (ne != ncclSuccess) return fail(MHMKC_ERCCL, "ncclGroupEnd: %s", ncclGetErrorString(ne));
@@ -746,6 +781,112 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
       src.count[i] = cnt(sg.peer, sg.slab, own_lo * NSUB + i);
     }
     srcs.push_back(std::move(src));
+  }
+  return MHMKC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// pipelined hash-range exchange: one round per slab, its transfers on xstream while the main stream
+// extracts the next slab (the reference ships supermers to their owners from process_seq, kmer_dht.cpp:222-224, and
+// quiesces once at the end, :227-231). A round is collective: every rank takes part with its next unsent slab or with
+// none, and says whether it is done (in finish, nothing left to add); rounds go on until every rank is done, so ranks
+// with different numbers of slabs stay in step.
+
+int mhmkc::xround(Slab *sl, bool done) {
+  const int g = G(), me = cfg.rank;
+  const uint32_t nseg = nb * NSUB, no = n_owned();
+  int rc;
+  hipError_t e;
+  for (int pass = 0; sl && sl->pending; pass++) {
+    bool redo = false;
+    if ((rc = resolve_one(sl, redo))) return rc;
+    if (redo && pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
+  }
+  // 1. every rank's flags (done, has a slab) and its slab's segment counts and starts (capped slabs have gaps)
+  const size_t per = 2 * (size_t)nseg + 3;
+  std::vector<uint64_t> mine(per, 0), all((size_t)g * per, 0);
+  mine[0] = done;
+  mine[1] = sl != nullptr;
+  if (sl) {
+    std::copy(sl->counts.begin(), sl->counts.end(), mine.begin() + 2);
+    std::copy(sl->bases.begin(), sl->bases.end(), mine.begin() + 2 + nseg);
+  }
+  if ((rc = allgather_host(mine.data(), all.data(), 8 * per, xstream))) return rc;
+  auto row = [&](int r) { return all.data() + (size_t)r * per; };
+  bool all_done = true;
+  for (int p = 0; p < g; p++) all_done &= row(p)[0] != 0;
+  // 2. receive layout: one span per peer with a slab this round, its records of my owned range
+  std::vector<std::pair<int, uint64_t>> rsp;
+  uint64_t recv_total = 0;
+  for (int p = 0; p < g; p++) {
+    if (p == me || !row(p)[1]) continue;
+    const uint64_t *pb = row(p) + 2 + nseg;
+    const uint64_t n = pb[own_hi * NSUB] - pb[own_lo * NSUB];
+    rsp.push_back({p, n});
+    recv_total += n;
+  }
+  if (n_parts == parts.size()) parts.push_back(new RecvPart());
+  RecvPart *rp = parts[n_parts++];
+  rp->spans.clear();
+  if ((rc = set_planes(rp->buf, recv_total, rp->planes))) return rc;
+  uint64_t off = 0;
+  for (auto &pn : rsp) {
+    RecvPart::Span sp;
+    sp.off = off;
+    sp.start.resize((size_t)no * NSUB);
+    sp.count.resize((size_t)no * NSUB);
+    const uint64_t *pc = row(pn.first) + 2, *pb = row(pn.first) + 2 + nseg;
+    for (uint32_t i = 0; i < no * NSUB; i++) {
+      sp.start[i] = off + (pb[own_lo * NSUB + i] - pb[own_lo * NSUB]);
+      sp.count[i] = pc[own_lo * NSUB + i];
+    }
+    rp->spans.push_back(std::move(sp));
+    off += pn.second;
+  }
+  // 3. transfers, per peer in plane order on both sides (as exchange())
+  const bool aos = mixed2 && MHMKC_M2AOS;
+  const int np = (compact || aos) ? 1 : nl;
+  const size_t wb = compact ? 4 : aos ? 16 : 8;
+  std::vector<Xfer> snd, rcv;
+  if (sl) {
+    for (int p = 0; p < g; p++) {
+      if (p == me) continue;
+      const uint32_t lo = owner_lo(p), hi = owner_lo(p + 1);
+      const uint64_t a = sl->bases[lo * NSUB], b = sl->bases[hi * NSUB];
+      if (b == a) continue;
+      for (int w = 0; w < np; w++) snd.push_back({p, (char *)sl->planes.w[w] + a * wb, (b - a) * wb});
+      if (sl->planes.ext) snd.push_back({p, sl->planes.ext + a, b - a});
+    }
+  }
+  off = 0;
+  for (auto &pn : rsp) {
+    if (pn.second) {
+      for (int w = 0; w < np; w++) rcv.push_back({pn.first, (char *)rp->planes.w[w] + off * wb, pn.second * wb});
+      if (rp->planes.ext) rcv.push_back({pn.first, rp->planes.ext + off, pn.second});
+    }
+    off += pn.second;
+  }
+  // 4. on xstream, after the slab's extraction (not after what the main stream was given since)
+  while (x_ev.size() < 2 * (x_rounds + 1)) {
+    hipEvent_t ev = nullptr;
+    if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "exchange event");
+    x_ev.push_back(ev);
+  }
+  if (sl && (e = hipStreamWaitEvent(xstream, sl->ev, 0)) != hipSuccess) return hip_fail(e, "exchange wait");
+  (void)hipEventRecord(x_ev[2 * x_rounds], xstream);
+  if ((rc = move(snd, rcv, xstream))) return rc;
+  (void)hipEventRecord(x_ev[2 * x_rounds + 1], xstream);
+  x_rounds++;
+  x_all_done = all_done;
+  return MHMKC_OK;
+}
+
+// Send every slab but the newest (whose extraction is what the next round overlaps).
+int mhmkc::pump() {
+  while (xpipe && n_slabs >= xq + 2) {
+    int rc = xround(slabs[xq], false);
+    if (rc) return rc;
+    xq++;
   }
   return MHMKC_OK;
 }
@@ -1161,6 +1302,44 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   std::vector<Source> srcs;
   if (smer) {
     if ((rc = smer_exchange(srcs))) return rc;
+  } else if (G() > 1 && xpipe) {
+    (void)hipEventRecord(ev_xext, stream);  // every extraction is enqueued: the exchange's exposed time starts here
+    for (; xq < n_slabs; xq++)
+      if ((rc = xround(slabs[xq], xq + 1 == n_slabs))) return rc;
+    while (!x_all_done)
+      if ((rc = xround(nullptr, true))) return rc;
+    (void)hipEventRecord(ev_xdone, xstream);
+    if ((e = hipStreamWaitEvent(stream, ev_xdone, 0)) != hipSuccess || (e = hipEventSynchronize(ev_xdone)) != hipSuccess)
+      return hip_fail(e, "exchange");
+    x_ms = 0;
+    for (uint64_t r = 0; r < x_rounds; r++) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, x_ev[2 * r], x_ev[2 * r + 1]) == hipSuccess) x_ms += ms;
+    }
+    float exposed = 0;
+    if (hipEventElapsedTime(&exposed, ev_xext, ev_xdone) != hipSuccess || exposed < 0) exposed = 0;
+    st.xchg_rounds = x_rounds;
+    st.ms_xchg = x_ms;
+    st.ms_xchg_exposed = exposed;
+    if (profiling) {
+      st.ms_kernel[MHMKC_STAGE_XCHG] += x_ms;
+      st.launches[MHMKC_STAGE_XCHG] += x_rounds;
+    }
+    for (size_t s = 0; s < n_slabs; s++) {  // local slabs: the owned range in place
+      Source src;
+      src.planes = slabs[s]->planes;
+      src.start.assign(slabs[s]->bases.begin() + own_lo * NSUB, slabs[s]->bases.begin() + own_hi * NSUB);
+      src.count.assign(slabs[s]->counts.begin() + own_lo * NSUB, slabs[s]->counts.begin() + own_hi * NSUB);
+      srcs.push_back(std::move(src));
+    }
+    for (size_t q = 0; q < n_parts; q++)
+      for (auto &sp : parts[q]->spans) {
+        Source src;
+        src.planes = parts[q]->planes;
+        src.start = sp.start;
+        src.count = sp.count;
+        srcs.push_back(std::move(src));
+      }
   } else if (G() > 1) {
     if ((rc = exchange(srcs))) return rc;
   } else {
@@ -1597,6 +1776,16 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     mhmkc_destroy(h);
     return MHMKC_EHIP;
   }
+  // pipelined record exchange (MHMKC_XPIPE=0: one exchange at finish; MHMKC_XPIECES: slabs per device batch)
+  const char *xp_env = getenv("MHMKC_XPIPE");
+  h->xpipe = cfg->n_ranks > 1 && !h->smer && !(xp_env && !atoi(xp_env));
+  if (const char *env = getenv("MHMKC_XPIECES")) h->xpieces = std::max(1, std::min(64, atoi(env)));
+  if (h->xpipe && ((e = hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking)) != hipSuccess ||
+                   (e = hipEventCreate(&h->ev_xdone)) != hipSuccess || (e = hipEventCreate(&h->ev_xext)) != hipSuccess)) {
+    g_create_error = std::string("exchange stream: ") + hipGetErrorString(e);
+    mhmkc_destroy(h);
+    return MHMKC_EHIP;
+  }
   if (cfg->n_ranks > 1 && cfg->comm_id) {
     ncclUniqueId id;
     memcpy(&id, cfg->comm_id, sizeof id);
@@ -1616,8 +1805,18 @@ void mhmkc_destroy(mhmkc_t h) {
   if (!h) return;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
+  if (h->xstream) (void)hipStreamSynchronize(h->xstream);
   if (h->comm) ncclCommDestroy(h->comm);
+  for (RecvPart *q : h->parts) {
+    q->buf.release();
+    delete q;
+  }
+  for (hipEvent_t ev : h->x_ev) (void)hipEventDestroy(ev);
+  if (h->ev_xdone) (void)hipEventDestroy(h->ev_xdone);
+  if (h->ev_xext) (void)hipEventDestroy(h->ev_xext);
+  if (h->xstream) (void)hipStreamDestroy(h->xstream);
   for (Slab *s : h->slabs) {
+    if (s->ev) (void)hipEventDestroy(s->ev);
     s->buf.release();
     s->meta.release();
     s->pin.release();
@@ -1671,6 +1870,31 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_
   if (n_reads == 0) return MHMKC_OK;
   if (n_reads >= 0xffffffffull) return h->fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
   h->qcut_pending = h->cfg.qual_cutoff;
+  const uint64_t P = (uint64_t)h->xpieces;
+  if (h->xpipe && P > 1 && n_reads >= 64 * P) {
+    // pipelined exchange: the batch as xpieces slabs of whole reads, so that each one's round overlaps the next
+    // one's extraction (the cut points' offsets come from the device)
+    std::vector<uint64_t> cut(P + 1);
+    hipError_t e = hipSuccess;
+    for (uint64_t i = 0; i <= P && e == hipSuccess; i++)
+      e = hipMemcpyAsync(&cut[i], d_offs + n_reads * i / P, 8, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return h->hip_fail(e, "read offsets");
+    for (uint64_t i = 0; i < P; i++) {
+      const uint64_t r0 = n_reads * i / P, r1 = n_reads * (i + 1) / P;
+      if (cut[i + 1] < cut[i] || cut[P] != n_bases)
+        return h->fail(MHMKC_EINVAL, "device read offsets are not a PackedReads CSR (offs[n_reads] == n_bases)");
+      mhm::ReadsView rv{};
+      rv.obase = cut[i] & ~15ull;
+      rv.head = (uint32_t)(cut[i] - rv.obase);
+      rv.bytes = d_bytes + rv.obase;
+      rv.offs = d_offs + r0;
+      rv.n_reads = r1 - r0;
+      rv.n_bases = cut[i + 1] - rv.obase;
+      if ((rc = h->add_view(rv, 0, false))) return rc;
+    }
+    return MHMKC_OK;
+  }
   mhm::ReadsView rv{d_bytes, d_offs, n_reads, n_bases, 0, 0, 0};
   return h->add_view(rv, 0, false);
 }
@@ -2223,9 +2447,14 @@ int mhmkc_get_stats(mhmkc_t h, mhmkc_stats *s) {
 int mhmkc_reset(mhmkc_t h) {
   if (!h) return MHMKC_EINVAL;
   hipError_t e = hipStreamSynchronize(h->stream);
+  if (e == hipSuccess && h->xstream) e = hipStreamSynchronize(h->xstream);
   if (e != hipSuccess) return h->hip_fail(e, "reset");
   h->prof_collect();
   h->n_slabs = 0;
+  h->n_parts = 0;
+  h->xq = 0;
+  h->x_rounds = 0;
+  h->x_all_done = false;
   h->n_arenas = 0;
   h->ctg_bytes.clear();
   h->ctg_offs.assign(1, 0);

@@ -134,6 +134,56 @@ def assert_tables_equal(a: m.KmerTable, b: m.KmerTable, what: str = ""):
                              f"{chr(a.right[i])} vs {kb} {b.counts[i]} {chr(b.left[i])} {chr(b.right[i])}")
 
 
+def _mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64's finalizer over a uint64 array (wrapping arithmetic)."""
+    x = x ^ (x >> np.uint64(30))
+    x *= np.uint64(0xBF58476D1CE4E5B9)
+    x ^= x >> np.uint64(27)
+    x *= np.uint64(0x94D049BB133111EB)
+    x ^= x >> np.uint64(31)
+    return x
+
+
+def table_digest(t: m.KmerTable, sample_bits: int = 8) -> dict:
+    """Order-independent digest of a (large) table for the tests whose tables hold hundreds of millions of rows:
+    the row count, two wrapping sums of independent 64-bit row fingerprints (key words, count, left, right), and the
+    rows whose key fingerprint has its top sample_bits bits zero (a fixed 1/2^sample_bits subsample of the key space,
+    the same keys on both sides, for a row-by-row check). Two tables with equal digests hold the same multiset of
+    rows except with probability ~2^-64; the sample is compared exactly (assert_digests_equal)."""
+    keys = np.ascontiguousarray(t.keys, dtype=np.uint64)
+    kf = _mix64(keys[:, 0] ^ np.uint64(0x9E3779B97F4A7C15))
+    for w in range(1, keys.shape[1]):
+        kf = _mix64(kf ^ keys[:, w])
+    v = (t.counts.astype(np.uint64) | (t.left.astype(np.uint64) << np.uint64(32)) |
+         (t.right.astype(np.uint64) << np.uint64(40)))
+    rf = _mix64(kf ^ v)
+    s1 = int(rf.sum(dtype=np.uint64))
+    rf ^= np.uint64(0xD6E8FEB86659FD93)
+    s2 = int(_mix64(rf).sum(dtype=np.uint64))
+    del rf, v
+    sel = (kf >> np.uint64(64 - sample_bits)) == 0
+    return {"n": len(t), "s1": s1, "s2": s2, "keys": keys[sel], "counts": t.counts[sel], "left": t.left[sel],
+            "right": t.right[sel]}
+
+
+def merge_digests(ds: list) -> dict:
+    """The digest of the union of disjoint tables (e.g. the owners' parts of one table)."""
+    mask = (1 << 64) - 1
+    out = {"n": sum(int(d["n"]) for d in ds), "s1": sum(int(d["s1"]) for d in ds) & mask,
+           "s2": sum(int(d["s2"]) for d in ds) & mask}
+    for f in ("keys", "counts", "left", "right"):
+        out[f] = np.concatenate([np.asarray(d[f]) for d in ds])
+    return out
+
+
+def assert_digests_equal(a: dict, b: dict, k: int, what: str = ""):
+    assert int(a["n"]) == int(b["n"]), f"{what}: {int(a['n'])} vs {int(b['n'])} k-mers"
+    sa = m.KmerTable(k, a["keys"], a["counts"], a["left"], a["right"])
+    sb = m.KmerTable(k, b["keys"], b["counts"], b["left"], b["right"])
+    assert_tables_equal(sa, sb, f"{what} (sampled rows)")
+    assert (int(a["s1"]), int(a["s2"])) == (int(b["s1"]), int(b["s2"])), f"{what}: row fingerprints differ"
+
+
 def read_reads_file(path: Path):
     """'seq qual' lines (BASELINE.md input format) -> PackedRead bytes + offsets."""
     seqs = []

@@ -86,11 +86,19 @@ def run_shared(rank: int, world: int, port: int, k: int, out_dir: str, opts: dic
 
 def run_share(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     """One rank of a C3 / C4 per-rank share: reads [rank * R, (rank + 1) * R) of the config's global read set
-    (genome opts["genome"], seed opts["seed"]) counted with opts["owner"], exchanged over the host transport; the
-    table goes to raw .npy files (keys, counts, left, right) for the parent's row-by-row comparison."""
+    (genome opts["genome"], seed opts["seed"]) counted with opts["owner"], exchanged over the host transport. The
+    owner's part of the table (hundreds of millions of rows) is reduced to its table_digest for the parent."""
+    import time
+
     import torch.distributed as dist
 
     import mhm2_proxy_amd as m
+    from common import table_digest
+
+    t0 = time.time()
+
+    def say(what):
+        print(f"[rank {rank} {time.time() - t0:6.1f}s] {what}", flush=True)
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -98,18 +106,22 @@ def run_share(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict
     g = m.synth_genome(opts["genome"], opts["seed"])
     b, o = m.synth_reads(g, R, 150, opts["seed"], first_read=rank * R)
     del g
+    say(f"{R} reads")
     owner = m.MHMKC_OWNER_MINIMIZER if opts.get("owner") == "minimizer" else m.MHMKC_OWNER_HASH
     c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner)
     c.add_packed_reads(b, o)
     del b, o
     c.finish()
+    say("counted")
     t = c.fetch()
     st = c.stats()
-    out = Path(out_dir)
-    for name in ("keys", "counts", "left", "right"):
-        np.save(out / f"rank{rank}_{name}.npy", getattr(t, name))
-    np.savez(out / f"rank{rank}_stats.npz", **{key: st[key] for key in ("occurrences", "owned_records", "bytes_sent",
-                                                                        "bytes_recv", "exact_reruns", "smer_count")})
     c.close()
+    say(f"fetched {len(t)} rows")
+    d = table_digest(t)
+    del t
+    say(f"digest ({d['keys'].shape[0]} sampled rows)")
+    np.savez(Path(out_dir) / f"rank{rank}_digest.npz", **d)
+    np.savez(Path(out_dir) / f"rank{rank}_stats.npz", **{key: st[key] for key in ("occurrences", "owned_records", "bytes_sent",
+                                                                                 "bytes_recv", "exact_reruns", "smer_count")})
     dist.barrier()
     dist.destroy_process_group()
