@@ -292,6 +292,10 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     host_xp = world > 1 and args.transport == "host"
+    # the pipelined record exchange: a step goes from its adds to finish with no other collective
+    # in between, which is the contract MHMKC_XPIPE asks for (MHMKC_XPIPE=0 in the environment: one exchange at finish)
+    if world > 1:
+        os.environ.setdefault("MHMKC_XPIPE", "1")
     n_dev = torch.cuda.device_count()
     if n_dev < 1:
         raise SystemExit("bench.py: no GPU visible")

@@ -1776,9 +1776,11 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     mhmkc_destroy(h);
     return MHMKC_EHIP;
   }
-  // pipelined record exchange (MHMKC_XPIPE=0: one exchange at finish; MHMKC_XPIECES: slabs per device batch)
+  // pipelined record exchange (MHMKC_XPIPE=1; MHMKC_XPIECES: slabs per device batch). Opt-in: its
+  // rounds are collectives inside the mhmkc_add_* calls, so every rank must go from its adds to mhmkc_finish with no
+  // other collective of the same ranks in between; without it the exchange runs once, in finish.
   const char *xp_env = getenv("MHMKC_XPIPE");
-  h->xpipe = cfg->n_ranks > 1 && !h->smer && !(xp_env && !atoi(xp_env));
+  h->xpipe = cfg->n_ranks > 1 && !h->smer && xp_env && atoi(xp_env);
   if (const char *env = getenv("MHMKC_XPIECES")) h->xpieces = std::max(1, std::min(64, atoi(env)));
   if (h->xpipe && ((e = hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking)) != hipSuccess ||
                    (e = hipEventCreate(&h->ev_xdone)) != hipSuccess || (e = hipEventCreate(&h->ev_xext)) != hipSuccess)) {

@@ -30,6 +30,8 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     for key, val in opts.get("env", {}).items():
         os.environ[key] = val
+    for key, val in opts.get("env_by_rank", {}).get(rank, {}).items():
+        os.environ[key] = val
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if opts.get("contigs"):
         b, o, seqs, depths = ctg_set(seed=opts["seed"], n_reads=opts.get("n_reads", 300))
@@ -38,6 +40,11 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
         seqs, depths = [], np.zeros(0, np.uint16)
     n = o.size - 1
     lo, hi = shard(n, rank, world)
+    idle = opts.get("idle_rank")  # this rank adds nothing; its share goes to the next rank (idle < world - 1)
+    if idle is not None and rank == idle:
+        lo = hi
+    elif idle is not None and rank == idle + 1:
+        lo = shard(n, idle, world)[0]
     owner = m.MHMKC_OWNER_MINIMIZER if opts.get("minimizer") else m.MHMKC_OWNER_HASH
     c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner,
                       dmin_thres=opts.get("dmin", 2))
@@ -57,7 +64,8 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
              bytes_sent=st["bytes_sent"], bytes_recv=st["bytes_recv"], occurrences=st["occurrences"],
              owned=st["owned_records"], count_sum=st["count_sum"], distinct=st["distinct"], purged=st["purged"],
              n_out=st["n_out"], handoff_sent=st["handoff_sent"], handoff_recv=st["handoff_recv"],
-             ctg_kmers=st["ctg_kmers"], smer_count=st["smer_count"], smer_words=st["smer_words"])
+             ctg_kmers=st["ctg_kmers"], smer_count=st["smer_count"], smer_words=st["smer_words"],
+             xchg_rounds=st["xchg_rounds"])
     c.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -100,7 +108,7 @@ def run_share(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict
     def say(what):
         print(f"[rank {rank} {time.time() - t0:6.1f}s] {what}", flush=True)
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MHMKC_XPIPE=opts.get("xpipe", "1"))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     R = opts["reads_per_rank"]
     g = m.synth_genome(opts["genome"], opts["seed"])

@@ -100,6 +100,25 @@ def test_supermer_exchange_variants(k, world, env, tmp_path):
     assert (sum(int(p["handoff_sent"]) for p in parts) > 0) == (not smer)
 
 
+@pytest.mark.parametrize("k,world,opts", [
+    (21, 2, {}), (33, 3, {}), (63, 2, {}), (99, 2, {}), (21, 3, {"minimizer": True}),
+    (21, 2, {"env_by_rank": {0: {"MHMKC_CHUNK_BYTES": "2000"}}}),   # rank 0: ~20 slabs, rank 1: a few
+    (63, 3, {"idle_rank": 0}),                                          # a rank with no slab at all
+    (21, 2, {"env": {"MHMKC_DEBUG_EXACT": "1"}}),
+    (33, 2, {"env": {"MHMKC_XPIECES": "7"}, "n_reads": 3000, "genome": 20000})])
+def test_pipelined_exchange(k, world, opts, tmp_path):
+    """The pipelined record exchange (MHMKC_XPIPE=1): one collective round per slab inside the add
+    calls, ranks with different slab counts (or none) kept in step by empty rounds; the union equals the oracle."""
+    env = dict(opts.get("env", {}), MHMKC_XPIPE="1")
+    o2 = {key: v for key, v in opts.items() if key != "env"}
+    seed = 1300 + k + world
+    parts = run_ranks(k, world, tmp_path, seed=seed, env=env, **o2)
+    b, o = synth_set(o2.get("n_reads", 1200), o2.get("genome", 9000), seed)
+    check_parts(parts, k, oracle_table(b, o, k), f"pipelined exchange {opts}, k={k}")
+    assert all(int(p["xchg_rounds"]) >= 2 for p in parts)
+    assert len({int(p["xchg_rounds"]) for p in parts}) == 1  # every rank took part in every round
+
+
 def test_supermer_bytes_per_kmer(tmp_path):
     """The wire volume of the supermer exchange at k = 63 against the 16-byte records it replaces."""
     parts = run_ranks(63, 2, tmp_path, seed=963, minimizer=True, n_reads=4000, genome=40000)
