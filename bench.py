@@ -71,10 +71,13 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--kmermap-sample-rows", type=int, default=-1,
                     help="rows of the fetched table put into the C++ adapter's KmerMap to time it (-1: all, 0: skip)")
-    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+    ap.add_argument("--transport", choices=("rccl", "host", "rccl-same-gpu"), default="rccl",
                     help="exchange between ranks (N > 1): rccl = one rank per GPU, RCCL grouped send/recv over xGMI; "
                          "host = mhmkc_set_transport over a gloo process group (pinned D2H, gloo, H2D), ranks share "
-                         "the visible GPUs round-robin (a rehearsal of the multi-rank path on one GPU)")
+                         "the visible GPUs round-robin (a rehearsal of the multi-rank path on one GPU); rccl-same-gpu = "
+                         "libmhmkc's RCCL path with the ranks sharing the visible GPUs (a per-rank NCCL_HOSTID makes "
+                         "RCCL accept them and move the data over its socket transport on loopback: a rehearsal of the "
+                         "8-GPU run's code path, not of its speed)")
     ap.add_argument("--owner", choices=("hash", "minimizer"), default="hash",
                     help="N > 1: where a finished k-mer lives: hash = the counting hash range (record exchange); "
                          "minimizer = the reference's get_kmer_target_rank (k >= 33: supermer exchange, DESIGN.md "
@@ -292,6 +295,10 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     host_xp = world > 1 and args.transport == "host"
+    same_gpu = world > 1 and args.transport == "rccl-same-gpu"
+    if same_gpu:  # before anything initialises RCCL in this process
+        os.environ.update(NCCL_HOSTID=f"mhmkc-rehearsal-{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                          NCCL_NET="Socket")
     # the pipelined record exchange: a step goes from its adds to finish with no other collective
     # in between, which is the contract MHMKC_XPIPE asks for (MHMKC_XPIPE=0 in the environment: one exchange at finish)
     if world > 1:
@@ -299,18 +306,19 @@ def main():
     n_dev = torch.cuda.device_count()
     if n_dev < 1:
         raise SystemExit("bench.py: no GPU visible")
-    if not host_xp and local >= n_dev:
+    shared = host_xp or same_gpu  # ranks share the visible GPUs round-robin
+    if not shared and local >= n_dev:
         raise SystemExit(f"bench.py: rank {rank} needs GPU {local} (one rank per GPU, RCCL), but {n_dev} visible; "
                          "use --transport host to run several ranks on one GPU")
-    local_dev = local % n_dev if host_xp else local
+    local_dev = local % n_dev if shared else local
     torch.cuda.set_device(local_dev)
     dist = None
-    cdev = torch.device("cpu") if host_xp else torch.device("cuda", local_dev)  # where the timing reductions run
+    cdev = torch.device("cpu") if shared else torch.device("cuda", local_dev)  # where the timing reductions run
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if host_xp:
+        if shared:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_dev))
@@ -527,7 +535,7 @@ def main():
                        "k": k, "reads_total": total, "reads_per_gpu": R, "read_len": L, "genome_len": G,
                        "occurrences_per_step": occ_total // steps, "parallelism": f"hash-range x{world}",
                        "transport": args.transport if world > 1 else None,
-                       "physical_gpus": min(world, n_dev) if host_xp else world},
+                       "physical_gpus": min(world, n_dev) if shared else world},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "stages_ms_per_step": {s_: round(v, 3) for s_, v in per_step.items() if launches.get(s_)},
@@ -555,7 +563,10 @@ def main():
             "bytes_sent_rank0": st["bytes_sent"] if st else None,
             "exchange": ({"transport": ("host-staged (mhmkc_set_transport over gloo: pinned D2H, gloo all-to-all-v, "
                                         f"H2D), {world} ranks on {min(world, n_dev)} physical GPU(s)")
-                          if host_xp else "RCCL grouped ncclSend/ncclRecv over xGMI, one rank per GPU",
+                          if host_xp else
+                          (f"RCCL grouped ncclSend/ncclRecv, {world} ranks on {min(world, n_dev)} physical GPU(s) "
+                           "(per-rank NCCL_HOSTID: RCCL's socket transport on loopback)") if same_gpu else
+                          "RCCL grouped ncclSend/ncclRecv over xGMI, one rank per GPU",
                           "ms_per_step_rank0": round(per_step.get("exchange", 0.0), 3),
                           "bytes_sent_per_step_rank0": st["bytes_sent"], "bytes_recv_per_step_rank0": st["bytes_recv"],
                           "bytes_sent_per_occurrence": round(st["bytes_sent"] / max(1, st["occurrences"]), 3),

@@ -1675,16 +1675,42 @@ constexpr int C_PROBE = MHMKC_CPROBE;
 #define MHMKC_CBATCH 2
 #endif
 
-// The last key words of one 4-slot group (two ds_read_b128; the group is 32-byte aligned).
-__device__ __forceinline__ void read_group(const uint64_t *last, int g, uint64_t (&v)[4]) {
-  const ulonglong2 *q = (const ulonglong2 *)(last + 4 * g);
-  const ulonglong2 a = q[0], b = q[1];
-  v[0] = a.x, v[1] = a.y, v[2] = b.x, v[3] = b.y;
+// Slots per probe group of k_count's table. A lane's home lookup reads one group with one LDS read: 4 slots = one
+// ds_read_b128 of 32-bit keys (two of 64-bit keys), 2 slots = one ds_read_b64 (one ds_read_b128). Random-address
+// ds_read_b64 runs at 3.5x the lane rate of ds_read_b128 on this part (profiles/r01_lds_microbench.txt: its two
+// 32-lane halves over 64 banks against four 16-lane groups), at the price of more home groups that are full.
+#ifndef MHMKC_GS_C
+#define MHMKC_GS_C 4  // compact (32-bit) keys
+#endif
+#ifndef MHMKC_GS_M2
+#define MHMKC_GS_M2 4  // mixed two-word keys (the last word, 64-bit, is the one read)
+#endif
+template <int NL, bool C32, bool M2>
+constexpr int group_slots() {
+  return C32 ? MHMKC_GS_C : M2 ? MHMKC_GS_M2 : 4;
 }
-// 32-bit keys: one ds_read_b128 per group
-__device__ __forceinline__ void read_group(const uint32_t *last, int g, uint32_t (&v)[4]) {
-  const uint4 a = *(const uint4 *)(last + 4 * g);
-  v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
+
+// The last key words of one group (4 x u64: two ds_read_b128, the group 32-byte aligned; 2 x u64: one)
+template <int GS>
+__device__ __forceinline__ void read_group(const uint64_t *last, int g, uint64_t (&v)[GS]) {
+  const ulonglong2 *q = (const ulonglong2 *)(last + GS * g);
+  const ulonglong2 a = q[0];
+  v[0] = a.x, v[1] = a.y;
+  if constexpr (GS == 4) {
+    const ulonglong2 b = q[1];
+    v[2] = b.x, v[3] = b.y;
+  }
+}
+// 32-bit keys: one ds_read_b128 per 4-slot group, one ds_read_b64 per 2-slot group
+template <int GS>
+__device__ __forceinline__ void read_group(const uint32_t *last, int g, uint32_t (&v)[GS]) {
+  if constexpr (GS == 4) {
+    const uint4 a = *(const uint4 *)(last + 4 * g);
+    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
+  } else {
+    const uint2 a = *(const uint2 *)(last + 2 * g);
+    v[0] = a.x, v[1] = a.y;
+  }
 }
 
 template <int NL, typename K>
@@ -1707,25 +1733,25 @@ constexpr int G_FULL = -8, G_BUSY = -9;
 #endif
 constexpr bool kFastA = MHMKC_FASTA != 0;
 
-template <int NL, typename K>
-__device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_t *key, int g, const K (&v)[4]) {
+template <int NL, int GS, typename K>
+__device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_t *key, int g, const K (&v)[GS]) {
   const K kl = (K)key[NL - 1];
   if constexpr (NL == 1) {  // single-word keys: eight compares and selects, no branch (a key is never EMPTY)
     int r = G_FULL;
 #pragma unroll
-    for (int i = 3; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;  // the first empty slot
+    for (int i = GS - 1; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;  // the first empty slot
 #pragma unroll
-    for (int i = 3; i >= 0; i--) r = v[i] == kl ? 4 * g + i : r;  // the key itself takes precedence
+    for (int i = GS - 1; i >= 0; i--) r = v[i] == kl ? GS * g + i : r;  // the key itself takes precedence
     return r;
   }
   if constexpr (NL == 2 && MHMKC_EXAM2) {  // the same on the last word, then one read of the first word
     int r = G_FULL;
 #pragma unroll
-    for (int i = 3; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;
+    for (int i = GS - 1; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;
 #pragma unroll
-    for (int i = 3; i >= 0; i--) r = v[i] == (K)KEY_BUSY ? G_BUSY : r;
+    for (int i = GS - 1; i >= 0; i--) r = v[i] == (K)KEY_BUSY ? G_BUSY : r;
 #pragma unroll
-    for (int i = 3; i >= 0; i--) r = v[i] == kl ? 4 * g + i : r;
+    for (int i = GS - 1; i >= 0; i--) r = v[i] == kl ? GS * g + i : r;
     // a slot holding the last word: the key iff its first word matches too (a second slot of the group with
     // the same last word is possible, so a mismatch falls back to the full examination below)
     if (r < 0 || t.keys[r] == (K)key[0]) return r;
@@ -1733,12 +1759,12 @@ __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_
   int found = -1, empty = -1;
   bool busy = false;
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    if (found < 0 && v[i] == kl && (NL == 1 || rest_equal<NL>(t, 4 * g + i, key))) found = i;
+  for (int i = 0; i < GS; i++) {
+    if (found < 0 && v[i] == kl && (NL == 1 || rest_equal<NL>(t, GS * g + i, key))) found = i;
     if (v[i] == (K)KEY_EMPTY && empty < 0) empty = i;
     if (NL > 1 && v[i] == (K)KEY_BUSY) busy = true;
   }
-  if (found >= 0) return 4 * g + found;
+  if (found >= 0) return GS * g + found;
   if (busy) return G_BUSY;
   return empty >= 0 ? -1 - empty : G_FULL;
 }
@@ -1754,19 +1780,19 @@ __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_
 // the key nor an empty slot; slots only fill, so the key can never be inserted later in the sweep, and had
 // it been inserted earlier this lookup would have found it. Every occurrence of a key is therefore counted
 // in the same sweep; no occupancy counter is needed.
-template <int NL, typename K>
+template <int NL, int GS, typename K>
 __device__ int lds_insert(const CountLds<K> &t, const uint64_t *key, int g, int r) {
   K *last = t.keys + (NL - 1) * t.cap;
-  const int ng = t.cap >> 2;
+  const int ng = t.cap / GS;
   const K kl = (K)key[NL - 1];
   int probed = 0;
   for (int iter = 0; iter < (1 << 20); iter++) {
     if (r >= 0) return r;
     if (r == G_FULL) {
-      if (++probed == C_PROBE) return -1;
+      if (++probed == C_PROBE * 4 / GS) return -1;  // C_PROBE 4-slot groups' worth of slots
       g = (g + 1 == ng) ? 0 : g + 1;
     } else if (r != G_BUSY) {
-      const int sl = 4 * g + (-1 - r);
+      const int sl = GS * g + (-1 - r);
       const K want = (NL == 1) ? kl : (K)KEY_BUSY;
       K old;
       if constexpr (sizeof(K) == 4)
@@ -1784,9 +1810,9 @@ __device__ int lds_insert(const CountLds<K> &t, const uint64_t *key, int g, int 
       if (NL == 1 && old == kl) return sl;  // the winner inserted this very key
       // otherwise the slot was just taken: look at the group again
     }
-    K v[4];
-    read_group(last, g, v);
-    r = examine_group<NL>(t, key, g, v);
+    K v[GS];
+    read_group<GS>(last, g, v);
+    r = examine_group<NL, GS>(t, key, g, v);
   }
   return -2;
 }
@@ -1807,10 +1833,10 @@ constexpr bool kClaimA = MHMKC_CLAIMA != 0;
 #define MHMKC_PROBE2 0
 #endif
 constexpr bool kProbe2 = MHMKC_PROBE2 != 0;
-template <int NL, typename K>
+template <int NL, int GS, typename K>
 __device__ __forceinline__ int claim_home(const CountLds<K> &t, const uint64_t *key, int g, int r) {
   K *last = t.keys + (NL - 1) * t.cap;
-  const int sl = 4 * g + (-1 - r);
+  const int sl = GS * g + (-1 - r);
   const K kl = (K)key[NL - 1];
   if constexpr (NL == 1) {
     K old;
@@ -1970,7 +1996,8 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
   }
   __syncthreads();
   const uint64_t q0 = s_range[0], q1 = s_range[1];
-  const int ng = t.cap >> 2;
+  constexpr int GS = group_slots<NL, RecKind<NL, CMP>::C32, RecKind<NL, CMP>::M2>();
+  const int ng = t.cap / GS;
   const K *last = t.keys + (NL - 1) * t.cap;
   for (uint64_t q = q0 + tid; q < q1; q += C_THREADS) {
     if (p.ctg_done[q]) continue;
@@ -1995,10 +2022,10 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
             : RecKind<NL, CMP>::M2 ? cmp_group((uint32_t)tkey[NL - 1], 16, (uint32_t)ng)
                                    : (int)__umulhi(slot_hash<NL>(tkey), (uint32_t)ng);
     int slot = -1;
-    for (int pr = 0; pr < C_PROBE; pr++) {  // find only: a key in the table is within its probe window
-      K v[4];
-      read_group(last, g, v);
-      const int e = examine_group<NL>(t, tkey, g, v);
+    for (int pr = 0; pr < C_PROBE * 4 / GS; pr++) {  // find only: a key in the table is within its probe window
+      K v[GS];
+      read_group<GS>(last, g, v);
+      const int e = examine_group<NL, GS>(t, tkey, g, v);
       if (e >= 0) {
         slot = e;
         break;
@@ -2129,7 +2156,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   constexpr int CB0 = NL == 2 ? MHMKC_CBATCH2 : MHMKC_CBATCH;
   constexpr int C_BATCH = CB0 < R ? CB0 : R;
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
-  const int ng = t.cap >> 2;
+  constexpr int GS = group_slots<NL, RK::C32, RK::M2>();  // slots per probe group
+  const int ng = t.cap / GS;
   const K *last = t.keys + (NL - 1) * t.cap;
   // cmp_group: compact keys from their top stored bits; mixed two-word keys from the low 16 bits of R' (the
   // table's last word)
@@ -2320,26 +2348,26 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           // compact keys in a cold sweep: the R home groups read back to back and examined, every claim CAS
           // issued before the first one is waited for (the general path below waits for each in turn), then the
           // non-returning adds; misses join the wave queue below. Same verdicts as the general path.
-          K gv[R][4];
+          K gv[R][GS];
           uint32_t res[R];
 #pragma unroll
           for (int j = 0; j < R; j++) {
             g[j] = cmp_group((uint32_t)ck[j][0], kshl, (uint32_t)ng);
-            read_group(last, g[j], gv[j]);
+            read_group<GS>(last, g[j], gv[j]);
           }
 #pragma unroll
-          for (int j = 0; j < R; j++) slot[j] = examine_group<NL>(t, ck[j], g[j], gv[j]);
+          for (int j = 0; j < R; j++) slot[j] = examine_group<NL, GS>(t, ck[j], g[j], gv[j]);
 #pragma unroll
           for (int j = 0; j < R; j++) {
             res[j] = 0u;
             if (ce[j] != NONE && slot[j] < 0 && slot[j] > G_FULL)  // slot -1 - r of the home group was empty: claim it
-              res[j] = atomicCAS((unsigned int *)&last[4 * g[j] - 1 - slot[j]], 0xffffffffu, (uint32_t)ck[j][0]);
+              res[j] = atomicCAS((unsigned int *)&last[GS * g[j] - 1 - slot[j]], 0xffffffffu, (uint32_t)ck[j][0]);
           }
 #pragma unroll
           for (int j = 0; j < R; j++) {
             old[j] = 0;
             int r = slot[j];
-            if (r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = 4 * g[j] - 1 - r;
+            if (r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = GS * g[j] - 1 - r;
             if (ce[j] == NONE) {
               slot[j] = -3;
             } else if (r >= 0) {
@@ -2353,15 +2381,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         } else {
 #pragma unroll
         for (int j0 = 0; j0 < R; j0 += C_BATCH) {
-          K v[C_BATCH][4];
+          K v[C_BATCH][GS];
 #pragma unroll
           for (int j = j0; j < j0 + C_BATCH; j++) {
             g[j] = CMP ? cmp_group((uint32_t)ck[j][NL - 1], kshl, (uint32_t)ng)
                        : (int)__umulhi(slot_hash<NL>(ck[j]), (uint32_t)ng);
-            read_group(last, g[j], v[j - j0]);  // also for an invalid lane: harmless, keeps the batch uniform
+            read_group<GS>(last, g[j], v[j - j0]);  // also for an invalid lane: harmless, keeps the batch uniform
           }
 #pragma unroll
-          for (int j = j0; j < j0 + C_BATCH; j++) slot[j] = examine_group<NL>(t, ck[j], g[j], v[j - j0]);
+          for (int j = j0; j < j0 + C_BATCH; j++) slot[j] = examine_group<NL, GS>(t, ck[j], g[j], v[j - j0]);
         }
 #pragma unroll
         for (int j = 0; j < R; j++) {
@@ -2372,8 +2400,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           }
           int r = slot[j];
           if (kClaimA && r < 0 && r > G_FULL) {  // -1 - i: slot i of the home group was empty
-            const int sl = 4 * g[j] + (-1 - r);
-            r = claim_home<NL>(t, ck[j], g[j], r);
+            const int sl = GS * g[j] + (-1 - r);
+            r = claim_home<NL, GS>(t, ck[j], g[j], r);
             if (NL > 1 && r < 0) {  // lost: the winner may have claimed it for this very key (a lane of this
                                     // wave has published it by now; another wave's is left to phase B)
               const K v = __hip_atomic_load(&last[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2383,12 +2411,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           }
           if (kProbe2 && r == G_FULL) {  // a full home group: look at the next one before listing the record
             const int g2 = (g[j] + 1 == ng) ? 0 : g[j] + 1;
-            K v2[4];
-            read_group(last, g2, v2);
-            r = examine_group<NL>(t, ck[j], g2, v2);
+            K v2[GS];
+            read_group<GS>(last, g2, v2);
+            r = examine_group<NL, GS>(t, ck[j], g2, v2);
             if (kClaimA && r < 0 && r > G_FULL) {
-              const int sl = 4 * g2 + (-1 - r);
-              r = claim_home<NL>(t, ck[j], g2, r);
+              const int sl = GS * g2 + (-1 - r);
+              r = claim_home<NL, GS>(t, ck[j], g2, r);
               if (NL > 1 && r < 0) {
                 const K v = __hip_atomic_load(&last[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (v == (K)ck[j][NL - 1] && rest_equal<NL>(t, sl, ck[j])) r = sl;
@@ -2411,7 +2439,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
               slot[j] = -3;
               continue;
             }
-            r = lds_insert<NL>(t, ck[j], g[j], r);  // list full (first rounds of a bucket): in place
+            r = lds_insert<NL, GS>(t, ck[j], g[j], r);  // list full (first rounds of a bucket): in place
             if (r == -1) defer |= 1u << j;
             if (r == -2) s_err = 1;
             slot[j] = r;
@@ -2445,7 +2473,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
               }
               wq_n += tot;
             } else if (mj) {
-              const int r = lds_insert<NL>(t, ck[j], g[j], slot[j]);
+              const int r = lds_insert<NL, GS>(t, ck[j], g[j], slot[j]);
               if (r == -1) defer |= 1u << j;
               if (r == -2) s_err = 1;
               slot[j] = r;
@@ -2499,9 +2527,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
               const uint32_t e = s_me[q];
               const int g = CMP ? cmp_group((uint32_t)key[NL - 1], kshl, (uint32_t)ng)
                                 : (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
-              K v[4];
-              read_group(last, g, v);
-              const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
+              K v[GS];
+              read_group<GS>(last, g, v);
+              const int r = lds_insert<NL, GS>(t, key, g, examine_group<NL, GS>(t, key, g, v));
               if (r >= 0) {
                 if (COLD)
                   lds_add_nr(t, r, e, &s_wave[wid]);
@@ -2539,9 +2567,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           const uint32_t e = me[q];
           const int g = CMP ? cmp_group((uint32_t)key[NL - 1], kshl, (uint32_t)ng)
                             : (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
-          K v[4];
-          read_group(last, g, v);
-          const int r = lds_insert<NL>(t, key, g, examine_group<NL>(t, key, g, v));
+          K v[GS];
+          read_group<GS>(last, g, v);
+          const int r = lds_insert<NL, GS>(t, key, g, examine_group<NL, GS>(t, key, g, v));
           if (r >= 0) {
             if (COLD)
               lds_add_nr(t, r, e, &s_wave[wid]);

@@ -20,6 +20,13 @@ def shard(n: int, rank: int, world: int):
     return n * rank // world, n * (rank + 1) // world
 
 
+def rccl_same_gpu_env(rank: int):
+    """RCCL refuses two ranks of one communicator on one GPU ("Duplicate GPU detected"), unless the ranks look like
+    different hosts: a per-rank NCCL_HOSTID, the socket network transport over loopback, no InfiniBand."""
+    os.environ.update(NCCL_HOSTID=f"mhmkc-rehearsal-{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                      NCCL_NET="Socket")
+
+
 def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     import torch
     import torch.distributed as dist
@@ -46,8 +53,18 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     elif idle is not None and rank == idle + 1:
         lo = shard(n, idle, world)[0]
     owner = m.MHMKC_OWNER_MINIMIZER if opts.get("minimizer") else m.MHMKC_OWNER_HASH
-    c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner,
-                      dmin_thres=opts.get("dmin", 2))
+    if opts.get("rccl"):
+        # libmhmkc's RCCL path (ncclCommInitRank, ncclAllGather, grouped ncclSend/ncclRecv) with the ranks on one GPU:
+        # each rank gets its own NCCL_HOSTID, so RCCL sees one GPU per "host" (no duplicate-GPU refusal) and moves
+        # the data over its socket transport on loopback
+        rccl_same_gpu_env(rank)
+        obj = [m.comm_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, comm_id=obj[0], output_owner=owner,
+                          dmin_thres=opts.get("dmin", 2))
+    else:
+        c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner,
+                          dmin_thres=opts.get("dmin", 2))
     # two batches per rank: the first from host memory (chunked H2D), the second from device tensors
     mid = (lo + hi) // 2
     c.add_packed_reads(b[int(o[lo]):int(o[mid])], (o[lo:mid + 1] - o[lo]).astype(np.uint64))

@@ -119,6 +119,29 @@ def test_pipelined_exchange(k, world, opts, tmp_path):
     assert len({int(p["xchg_rounds"]) for p in parts}) == 1  # every rank took part in every round
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("k,world,opts", [
+    (21, 2, {}), (21, 2, {"env": {"MHMKC_XPIPE": "1"}}), (33, 3, {"env": {"MHMKC_XPIPE": "1"}}),
+    (63, 2, {"minimizer": True}), (21, 3, {"minimizer": True}), (99, 2, {"env": {"MHMKC_XPIPE": "1"}})])
+def test_rccl_ranks_on_one_gpu(k, world, opts, tmp_path):
+    """The RCCL exchange itself (ncclCommInitRank from mhmkc_comm_id, ncclAllGather, grouped ncclSend/ncclRecv on the
+    library's streams), which the 8-GPU driver run takes: the ranks share the one GPU, each with its own NCCL_HOSTID so
+    RCCL accepts them (tests/mr_gpu_worker.rccl_same_gpu_env). Record exchange at finish and pipelined, the supermer
+    exchange, the one-word hand-off; the union equals the oracle."""
+    seed = 1500 + k + world
+    parts = run_ranks(k, world, tmp_path, seed=seed, rccl=True, **opts)
+    b, o = synth_set(1200, 9000, seed)
+    check_parts(parts, k, oracle_table(b, o, k), f"RCCL, {world} ranks on one GPU, {opts}, k={k}")
+    if opts.get("env", {}).get("MHMKC_XPIPE") == "1":
+        assert all(int(p["xchg_rounds"]) >= 2 for p in parts)
+    if opts.get("minimizer"):
+        nl = k // 32 + 1
+        L = O.oracle()
+        for r, p in enumerate(parts):
+            keys = np.ascontiguousarray(p["keys"][:, :nl], dtype=np.uint64)
+            assert all(L.orc_kmer_target_rank(keys[i].ctypes.data, k, nl, world) == r for i in range(len(keys)))
+
+
 def test_supermer_bytes_per_kmer(tmp_path):
     """The wire volume of the supermer exchange at k = 63 against the 16-byte records it replaces."""
     parts = run_ranks(63, 2, tmp_path, seed=963, minimizer=True, n_reads=4000, genome=40000)
