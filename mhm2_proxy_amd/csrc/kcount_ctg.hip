@@ -161,6 +161,10 @@ __global__ __launch_bounds__(G_THREADS) void k_ctg_fold(PlaneSet keys, const uin
       uint64_t L, R;
       m2_mix(key, cmpB / 2, L, R);
       h = L << (64 - cmpB / 2);
+    } else if (NL >= 3 && cmpB) {  // mixed three- and four-word records: w0' of mx_mix
+      uint64_t r[NL];
+      mx_mix<NL>(key, r);
+      h = r[0];
     } else {
       h = part_hash<NL>(key);
     }

@@ -28,7 +28,7 @@ constexpr int kTile() {  // bases per extract tile
 }
 template <int NL>
 constexpr int kEThreads() {  // threads per extract workgroup
-  return NL == 1 ? MHMKC_ETHREADS1 : MHMKC_ETHREADS2;
+  return NL == 1 ? MHMKC_ETHREADS1 : NL == 2 ? MHMKC_ETHREADS2 : MHMKC_ETHREADS3;
 }
 template <int NL>
 constexpr int kPTile() {  // records per partition chunk (E_THREADS threads)
@@ -465,16 +465,26 @@ __device__ __forceinline__ uint64_t window_hash(const uint64_t *key, int k) {
     m2_mix(key, k, L, R);
     return L << (64 - k);
   }
+  if (CMP && NL >= 3) {  // mixed three- and four-word records: w0' of mx_mix
+    uint64_t r[NL];
+    mx_mix<NL>(key, r);
+    return r[0];
+  }
   return part_hash<NL>(key);
 }
 
-// Record layout traits: compact (one u32 word, NL = 1) and mixed two-word records (NL = 2, ext code in w[0],
-// kmer_ops.hpp m2_mix) are the two kinds of "mixed" records (CMP) whose bucket digits are implicit.
+// Record layout traits: compact (one u32 word, NL = 1), mixed two-word records (NL = 2, ext code in w[0],
+// kmer_ops.hpp m2_mix) and mixed three- and four-word records (NL = 3, 4, ext code in w[0], mx_mix) are the kinds
+// of "mixed" records (CMP) whose bucket digits are implicit. LW: bits of the mixed first word whose top bits are the
+// digits (L' of k bits, w0' of 64).
 template <int NL, bool CMP>
 struct RecKind {
   static constexpr bool C32 = CMP && NL == 1;
   static constexpr bool M2 = CMP && NL == 2;
-  static constexpr int XW = M2 ? 0 : NL - 1;  // the word holding the ext code of a packed record
+  static constexpr bool MX = CMP && NL >= 3;
+  static constexpr bool MW = M2 || MX;  // multi-word mixed: w[0] = (first mixed word below the digits) << 6 | ext
+  static constexpr int XW = MW ? 0 : NL - 1;  // the word holding the ext code of a packed record
+  static __host__ __device__ constexpr int lw(int k) { return M2 ? k : 64; }
 };
 
 template <int NL, bool PACKED, bool CMP>
@@ -906,6 +916,19 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
   } else
   walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk,
                    [&](int i, const uint64_t *key, uint32_t e, bool valid) {
+                     if constexpr (RecKind<NL, CMP>::MX) {  // (w0' below the coarse digit) << 6 | ext, r[1..]
+                       uint64_t r[NL];
+                       mx_mix<NL>(key, r);
+                       const int xsh = 64 - p.coarse_bits;
+                       rk[i][0] = ((r[0] & ((1ull << xsh) - 1)) << EXT_BITS) | e;
+#pragma unroll
+                       for (int w = 1; w < NL; w++) rk[i][w] = r[w];
+                       inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(r[0] >> xsh) : 0u;
+#pragma unroll
+                       for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[i][w]));
+                       asm volatile("" : "+v"(inf[i]));
+                       return;
+                     }
                      if constexpr (RecKind<NL, CMP>::M2) {  // (L' below the coarse digit) << 6 | ext, R'
                        uint64_t L, R;
                        m2_mix(key, kk, L, R);
@@ -1186,6 +1209,16 @@ __device__ __forceinline__ void window_record(const uint64_t *key, uint32_t e, b
     inf = valid ? (1u << 31) | (e << 16) | (uint32_t)(L >> m2_csh) : 0u;
     return;
   }
+  if constexpr (RecKind<NL, CMP>::MX) {
+    const int xsh = 64 - p.coarse_bits;
+    uint64_t r[NL];
+    mx_mix<NL>(key, r);
+    rk[0] = ((r[0] & ((1ull << xsh) - 1)) << EXT_BITS) | e;
+#pragma unroll
+    for (int w = 1; w < NL; w++) rk[w] = r[w];
+    inf = valid ? (1u << 31) | (e << 16) | (uint32_t)(r[0] >> xsh) : 0u;
+    return;
+  }
   const uint64_t h = window_hash<NL, CMP>(key, kk);
 #pragma unroll
   for (int w = 0; w < NL; w++) rk[w] = key[w];
@@ -1338,6 +1371,7 @@ __device__ __forceinline__ uint32_t fine_digit(const uint64_t *rk, const Partiti
   const uint64_t fmask = (1ull << p.fine_bits) - 1;
   if (CMP && NL == 1) return (uint32_t)((rk[0] >> (EXT_BITS + 2 * p.k - p.coarse_bits - p.fine_bits)) & fmask);
   if (CMP && NL == 2) return (uint32_t)((rk[0] >> (EXT_BITS + p.k - p.coarse_bits - p.fine_bits)) & fmask);
+  if (CMP && NL >= 3) return (uint32_t)((rk[0] >> (EXT_BITS + 64 - p.coarse_bits - p.fine_bits)) & fmask);
   if (PACKED && p.hbits >= p.fine_bits) {
     const uint64_t stored = (rk[NL - 1] >> EXT_BITS) & ((1ull << p.hbits) - 1);
     return (uint32_t)((stored >> (p.hbits - p.fine_bits)) & fmask);
@@ -1455,7 +1489,8 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
   load_chunk<NL, PACKED, CMP, W>(src, ch, rk, re);
   // compact: the fine record keeps the bits below the fine digit (+ the ext code), <= 32 bits; mixed
   // two-word: w[0] keeps L' below the fine digit (+ the ext code)
-  const uint64_t cmask = (1ull << (EXT_BITS + (NL == 1 ? 2 * p.k : p.k) - p.coarse_bits - p.fine_bits)) - 1;
+  const uint64_t cmask =
+      (1ull << (EXT_BITS + (NL == 1 ? 2 * p.k : RecKind<NL, CMP>::lw(p.k)) - p.coarse_bits - p.fine_bits)) - 1;
 #pragma unroll
   for (int j = 0; j < W; j++) {
     inf[j] = (threadIdx.x + j * E_THREADS < ch.count)
@@ -1529,24 +1564,40 @@ __global__ void k_init_fine(const unsigned long long *coarse_base, const unsigne
 // sum over reads of max(0, L - k - 1): the counted windows of a batch
 // and the CSR checks of mhmkc_add_reads (offsets non-decreasing, reads <= 65535 bases: PackedRead's
 // read_len is a uint16, src/packed_reads.hpp:60-80) for device-resident offsets
+// (4 reads per lane per iteration, their loads issued together, and one global atomic per workgroup: the first
+// version's two dependent loads per read took 0.11 ms at C2, and one atomic per wave over a 64k-workgroup grid 1.9 ms)
 __global__ __launch_bounds__(256) void k_count_windows(ReadsView rv, int k, unsigned long long *out, unsigned int *err) {
+  __shared__ unsigned long long s_acc[4];
   unsigned long long acc = 0;
   bool bad = false;
-  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rv.n_reads; r += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t a = rv.offs[r], b = rv.offs[r + 1];
-    bad |= b < a || b - a > 65535;
-    const uint64_t L = b - a;
-    if (b >= a && L > (uint64_t)k + 1) acc += L - k - 1;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r0 < rv.n_reads; r0 += 4 * stride) {
+    uint64_t a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint64_t r = r0 + u * stride, rr = r < rv.n_reads ? r : rv.n_reads - 1;
+      a[u] = rv.offs[rr];
+      b[u] = rv.offs[rr + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (r0 + u * stride >= rv.n_reads) break;
+      bad |= b[u] < a[u] || b[u] - a[u] > 65535;
+      const uint64_t L = b[u] - a[u];
+      acc += (b[u] >= a[u] && L > (uint64_t)k + 1) ? L - k - 1 : 0;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0)
     bad |= rv.offs[0] != rv.obase + rv.head || rv.offs[rv.n_reads] - rv.obase != rv.n_bases;
   if (bad) atomicOr(err, 4u);
   acc = wave_sum_u64(acc);
-  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+  if ((threadIdx.x & 63) == 0) s_acc[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = s_acc[0] + s_acc[1] + s_acc[2] + s_acc[3];
+    if (t) atomicAdd(out, t);
+  }
 }
-
-// ------------------------------------------------------------------------------------------------
-// exclusive scan of bucket counts (one workgroup)
 
 __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, unsigned long long *base,
                                                unsigned long long *cursor, uint32_t n) {
@@ -1744,7 +1795,7 @@ __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_
     for (int i = GS - 1; i >= 0; i--) r = v[i] == kl ? GS * g + i : r;  // the key itself takes precedence
     return r;
   }
-  if constexpr (NL == 2 && MHMKC_EXAM2) {  // the same on the last word, then one read of the first word
+  if constexpr (NL >= 2 && MHMKC_EXAM2) {  // the same on the last word, then one read of the other words
     int r = G_FULL;
 #pragma unroll
     for (int i = GS - 1; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;
@@ -1752,9 +1803,9 @@ __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_
     for (int i = GS - 1; i >= 0; i--) r = v[i] == (K)KEY_BUSY ? G_BUSY : r;
 #pragma unroll
     for (int i = GS - 1; i >= 0; i--) r = v[i] == kl ? GS * g + i : r;
-    // a slot holding the last word: the key iff its first word matches too (a second slot of the group with
+    // a slot holding the last word: the key iff its other words match too (a second slot of the group with
     // the same last word is possible, so a mismatch falls back to the full examination below)
-    if (r < 0 || t.keys[r] == (K)key[0]) return r;
+    if (r < 0 || rest_equal<NL>(t, r, key)) return r;
   }
   int found = -1, empty = -1;
   bool busy = false;
@@ -1900,6 +1951,26 @@ __device__ __forceinline__ void lds_add_nr(const CountLds<K> &t, int slot, uint3
   if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
 }
 
+// lds_add_nr without branches (the compact cold fast path): word offsets and addends from nibble tables indexed by
+// the ext code, so every lane issues its two adds and a lane with nothing to count adds 0. Left: ext plane l >> 1
+// (offset cap * (1 + (l >> 1)) from the count word) adding 1 or 0x10000, or for a left neighbour that is no
+// countable base the count word itself, adding 1; right: ext plane 2 + (r >> 1) (offset cap * (3 + (r >> 1))), or
+// 0 added to the count word (lds_add_nr's dummy word). Needs t.ext == t.cnt + t.cap.
+#ifndef MHMKC_ADDBF
+#define MHMKC_ADDBF 0  // measured slower: count 4.85 -> 5.04 ms at C2 (LDS adds of 0 by every lane that misses)
+#endif
+template <typename K>
+__device__ __forceinline__ void lds_add_nr_bf(const CountLds<K> &t, int slot, uint32_t e, bool ok) {
+  uint32_t *base = t.cnt + slot;
+  const uint32_t sl = (e >> 1) & 0x1Cu, sr = (e << 2) & 0x1Cu;  // 4 * l, 4 * r
+  const uint32_t fl = __builtin_amdgcn_ubfe(0x02211u, sl, 4), fr = __builtin_amdgcn_ubfe(0x04433u, sr, 4);
+  const uint32_t cr = __builtin_amdgcn_ubfe(0x02121u, sr, 4);  // right: 0 none, 1 low half, 2 high half
+  const uint32_t vl = ok ? __umul24((e >> 3) & 1u, 0xFFFFu) + 1u : 0u;
+  const uint32_t vr = ok ? __umul24(cr >> 1, 0xFFFEu) + cr : 0u;
+  atomicAdd(base + __umul24(fl, (uint32_t)t.cap), vl);
+  atomicAdd(base + __umul24(fr, (uint32_t)t.cap), vr);
+}
+
 // The count of an occupied slot (see lds_add_nr for the cold-sweep encoding).
 template <typename K>
 __device__ __forceinline__ uint32_t slot_count(const CountLds<K> &t, int slot, bool cold) {
@@ -2017,9 +2088,15 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
       m2_mix(key, p.k, L, R);
       tkey[0] = (L & ((1ull << (p.k - p.coarse_bits - p.fine_bits)) - 1)) << EXT_BITS;
       tkey[NL - 1] = R;
+    } else if (RecKind<NL, CMP>::MX) {  // mixed three- and four-word: w0' below the bucket digits << 6, r[1..]
+      uint64_t r[NL];
+      mx_mix<NL>(key, r);
+      tkey[0] = (r[0] & ((1ull << (64 - p.coarse_bits - p.fine_bits)) - 1)) << EXT_BITS;
+#pragma unroll
+      for (int w = 1; w < NL; w++) tkey[w] = r[w];
     }
     int g = RecKind<NL, CMP>::C32 ? cmp_group((uint32_t)tkey[0], 26 - (2 * p.k - p.coarse_bits - p.fine_bits), (uint32_t)ng)
-            : RecKind<NL, CMP>::M2 ? cmp_group((uint32_t)tkey[NL - 1], 16, (uint32_t)ng)
+            : RecKind<NL, CMP>::MW ? cmp_group((uint32_t)tkey[NL - 1], 16, (uint32_t)ng)
                                    : (int)__umulhi(slot_hash<NL>(tkey), (uint32_t)ng);
     int slot = -1;
     for (int pr = 0; pr < C_PROBE * 4 / GS; pr++) {  // find only: a key in the table is within its probe window
@@ -2297,11 +2374,16 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         STAMP(t_r0);
         uint64_t ck[R][NL];
         uint32_t ce[R];
+        // record j of this lane is valid iff j * vstep < vrem: the records left from this lane's first one (a dense
+        // sweep: [r0, n) in thread order; a re-sweep: this wave's own nw positions), saturated at 0
+        const uint32_t vfirst = nw == NONE ? r0 + (RK::C32 ? 4u * (uint32_t)tid : (uint32_t)tid)
+                                           : (uint32_t)rnd * (uint32_t)(64 * R) + (RK::C32 ? 4u * (uint32_t)lane : (uint32_t)lane);
+        const uint32_t vend = nw == NONE ? n : nw;
+        const uint32_t vrem = (vend > vfirst ? vend : vfirst) - vfirst;
+        const uint32_t vstep = RK::C32 ? 1u : nw == NONE ? (uint32_t)C_THREADS : 64u;
 #pragma unroll
         for (int j = 0; j < R; j++) {
-          const bool valid =
-              nw == NONE ? (RK::C32 ? r0 + 4u * (uint32_t)tid + (uint32_t)j : r0 + (uint32_t)tid + (uint32_t)j * C_THREADS) < n
-                         : (uint32_t)rnd * (uint32_t)(64 * R) + (uint32_t)(RK::C32 ? 4 * lane + j : 64 * j + lane) < nw;
+          const bool valid = (uint32_t)j * vstep < vrem;
 #pragma unroll
           for (int w = 0; w < NL; w++) ck[j][w] = nk[j][w];
           if (PACKED) {
@@ -2368,6 +2450,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             old[j] = 0;
             int r = slot[j];
             if (r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = GS * g[j] - 1 - r;
+            if (MHMKC_ADDBF && kCold2) {  // every lane adds (0 when it has nothing to count): no branch per record
+              const bool valid = ce[j] != NONE, ok = valid && r >= 0;
+              lds_add_nr_bf(t, ok ? r : GS * g[j], ce[j], ok);  // (adds of 0 spread over the home groups: one common
+                                                                // dummy address serialised them, count 4.84 -> 5.07 ms)
+              slot[j] = valid ? r : -3;
+              okm |= (uint32_t)ok << j;
+              missm |= (uint32_t)(valid && r < 0) << j;  // a full home group, or a lost claim
+              continue;
+            }
             if (ce[j] == NONE) {
               slot[j] = -3;
             } else if (r >= 0) {
@@ -2634,9 +2725,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
     for (int j = 0; j < QPT; j++) {
       const int qd = tid + j * C_THREADS;
+      uint32_t c[4] = {0, 0, 0, 0};
       if (4 * qd < t.cap) {
         const uint4 c4 = *(const uint4 *)(t.cnt + 4 * qd);
-        uint32_t c[4] = {c4.x, c4.y, c4.z, c4.w};
+        c[0] = c4.x, c[1] = c4.y, c[2] = c4.z, c[3] = c4.w;
         if (kCold2 && cold) {  // slot_count's cold encoding, four at a time
           const uint4 a4 = *(const uint4 *)(t.ext + 4 * qd), b4 = *(const uint4 *)(t.ext + t.cap + 4 * qd);
           const uint32_t a[4] = {a4.x, a4.y, a4.z, a4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
@@ -2645,12 +2737,29 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             c[i] = (c[i] >> 31) ? c[i] & 0x7fffffffu
                                 : c[i] + (a[i] & 0xffffu) + (a[i] >> 16) + (bb[i] & 0xffffu) + (bb[i] >> 16);
         }
+      }
+      // the wave's listed slots take one reservation (ballots + lane prefixes), not one LDS atomic each on the
+      // same word
+      uint64_t bal[4];
+      uint32_t pre[4], tot = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          occ += c[i] != 0u;
-          sum += c[i];
-          if (c[i] >= 2) flist[atomicAdd(&s_fin[0], 1u)] = (uint16_t)(4 * qd + i);
-        }
+      for (int i = 0; i < 4; i++) {
+        occ += c[i] != 0u;
+        sum += c[i];
+        bal[i] = __ballot(c[i] >= 2);
+        pre[i] = tot;
+        tot += (uint32_t)__popcll(bal[i]);
+      }
+      if (tot) {
+        uint32_t fb = 0;
+        if (lane == 0) fb = atomicAdd(&s_fin[0], tot);
+        fb = __builtin_amdgcn_readfirstlane(fb);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (c[i] >= 2)
+            flist[fb + pre[i] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[i] >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal[i], 0u))] =
+                (uint16_t)(4 * qd + i);
       }
     }
 #else
@@ -2675,15 +2784,24 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       const uint32_t i = (uint32_t)tid + (uint32_t)j * C_THREADS;
       spos[j] = 0;
       fslot[j] = 0;
+      bool sv = false;
       if (i < n_list) {
         const int slot = flist[i];
         fslot[j] = (uint16_t)slot;
 #if !MHMKC_EXP_NOFIN
-        if (slot_survives(t, slot, p, slot_count(t, slot, cold), c16[j], L[j], R_[j])) {
-          surv_mask |= 1u << j;
-          spos[j] = atomicAdd(&s_fin[1], 1u);
-        }
+        sv = slot_survives(t, slot, p, slot_count(t, slot, cold), c16[j], L[j], R_[j]);
 #endif
+      }
+      // one reservation per wave for its survivors (ballot + lane prefix)
+      const uint64_t bal = __ballot(sv);
+      if (bal) {
+        uint32_t sb = 0;
+        if (lane == 0) sb = atomicAdd(&s_fin[1], (uint32_t)__popcll(bal));
+        sb = __builtin_amdgcn_readfirstlane(sb);
+        if (sv) {
+          surv_mask |= 1u << j;
+          spos[j] = sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        }
       }
     }
     const uint32_t mine = __popc(surv_mask);
@@ -2713,6 +2831,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           m2_unmix(L, t.keys[t.cap + slot], p.k, kw);
           ok[0] = kw[0];
           ok[1] = kw[1];
+        } else if (RK::MX) {  // key = mx_unmix(global fine bucket digits | stored w0' bits, r[1..])
+          const int rb = 64 - p.coarse_bits - p.fine_bits;
+          uint64_t r[NL], kw[NL];
+          r[0] = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+#pragma unroll
+          for (int w = 1; w < NL; w++) r[w] = t.keys[w * t.cap + slot];
+          mx_unmix<NL>(r, kw);
+#pragma unroll
+          for (int w = 0; w < NL; w++) ok[w] = kw[w];
         } else {
 #pragma unroll
           for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
@@ -2780,6 +2907,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           m2_unmix(L, t.keys[t.cap + slot], p.k, kw);
           ok[0] = kw[0];
           ok[1] = kw[1];
+        } else if (RK::MX) {  // key = mx_unmix(global fine bucket digits | stored w0' bits, r[1..])
+          const int rb = 64 - p.coarse_bits - p.fine_bits;
+          uint64_t r[NL], kw[NL];
+          r[0] = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+#pragma unroll
+          for (int w = 1; w < NL; w++) r[w] = t.keys[w * t.cap + slot];
+          mx_unmix<NL>(r, kw);
+#pragma unroll
+          for (int w = 0; w < NL; w++) ok[w] = kw[w];
         } else {
 #pragma unroll
           for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
@@ -2868,6 +3004,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     case 9: return FN<4, true> ARGS;         \
     default: return hipErrorInvalidValue;    \
   }
+// mixed records (compact, two-, three- and four-word): <NL, packed, mixed>
+#define MHM_DISPATCH_MIXED(nl, FN, ARGS)                                                                \
+  ((nl) == 1 ? FN<1, true, true> ARGS : (nl) == 2 ? FN<2, true, true> ARGS : (nl) == 3 ? FN<3, true, true> ARGS \
+             : (nl) == 4 ? FN<4, true, true> ARGS : hipErrorInvalidValue)
 
 template <typename K>
 static hipError_t allow_lds(K kernel, size_t lds) {
@@ -2935,7 +3075,7 @@ hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_
 
 hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, unsigned int *err, hipStream_t s) {
   if (!r.n_reads) return hipSuccess;
-  const uint64_t blocks = std::min<uint64_t>(2048, (r.n_reads + 255) / 256);
+  const uint64_t blocks = std::min<uint64_t>(2048, (r.n_reads + 1023) / 1024);
   k_count_windows<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, k, out, err);
   return hipGetLastError();
 }
@@ -2952,25 +3092,25 @@ hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigne
 
 hipError_t launch_extract_hist(const ExtractParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_tiles) return hipSuccess;
-  if (p.compact) return nl == 2 ? do_extract_hist<2, true, true>(p, s) : do_extract_hist<1, true, true>(p, s);
+  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_extract_hist, (p, s));
   MHM_DISPATCH(nl, packed, do_extract_hist, (p, s));
 }
 
 hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_tiles) return hipSuccess;
-  if (p.compact) return nl == 2 ? do_extract_scatter<2, true, true>(p, s) : do_extract_scatter<1, true, true>(p, s);
+  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_extract_scatter, (p, s));
   MHM_DISPATCH(nl, packed, do_extract_scatter, (p, s));
 }
 
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_chunks) return hipSuccess;
-  if (p.compact) return nl == 2 ? do_part_hist<2, true, true>(p, s) : do_part_hist<1, true, true>(p, s);
+  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_part_hist, (p, s));
   MHM_DISPATCH(nl, packed, do_part_hist, (p, s));
 }
 
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_chunks) return hipSuccess;
-  if (p.compact) return nl == 2 ? do_part_scatter<2, true, true>(p, s) : do_part_scatter<1, true, true>(p, s);
+  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_part_scatter, (p, s));
   MHM_DISPATCH(nl, packed, do_part_scatter, (p, s));
 }
 
@@ -2989,7 +3129,7 @@ static hipError_t do_sketch(const PartitionParams &p, uint32_t n, unsigned int *
 hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
                          hipStream_t s) {
   if (!n_chunks) return hipSuccess;
-  if (p.compact) return nl == 2 ? do_sketch<2, true, true>(p, n_chunks, hll, s) : do_sketch<1, true, true>(p, n_chunks, hll, s);
+  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_sketch, (p, n_chunks, hll, s));
   MHM_DISPATCH(nl, packed, do_sketch, (p, n_chunks, hll, s));
 }
 
@@ -3001,7 +3141,7 @@ hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, u
 
 hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s) {
   if (!p.n_buckets) return hipSuccess;
-  if (p.compact) return nl == 2 ? do_count<2, true, true>(p, s) : do_count<1, true, true>(p, s);
+  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_count, (p, s));
   MHM_DISPATCH(nl, packed, do_count, (p, s));
 }
 
@@ -3061,7 +3201,9 @@ static hipError_t do_smer_extract(const ExtractParams &p, const SmerSource &src,
 
 template <bool HIST>
 static hipError_t smer_extract_nl(const ExtractParams &p, const SmerSource &src, int nl, bool packed, hipStream_t s) {
-  if (p.compact) return nl == 2 ? do_smer_extract<2, true, true, HIST>(p, src, s) : hipErrorInvalidValue;
+  if (p.compact)
+    return nl == 2 ? do_smer_extract<2, true, true, HIST>(p, src, s) : nl == 3 ? do_smer_extract<3, true, true, HIST>(p, src, s)
+         : nl == 4 ? do_smer_extract<4, true, true, HIST>(p, src, s) : hipErrorInvalidValue;
   switch (nl * 2 + (packed ? 1 : 0)) {
     case 4: return do_smer_extract<2, false, false, HIST>(p, src, s);
     case 5: return do_smer_extract<2, true, false, HIST>(p, src, s);

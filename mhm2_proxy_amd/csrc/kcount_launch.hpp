@@ -253,6 +253,9 @@ inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : nl == 2 ? MHMKC_T
 #ifndef MHMKC_ETHREADS2
 #define MHMKC_ETHREADS2 E_THREADS
 #endif
+#ifndef MHMKC_ETHREADS3
+#define MHMKC_ETHREADS3 MHMKC_ETHREADS2  // three- and four-word keys
+#endif
 // records per partition chunk (one E_THREADS workgroup)
 #ifndef MHMKC_PTILE1
 #define MHMKC_PTILE1 4096

@@ -284,6 +284,56 @@ MHM_HD void m2_unmix(uint64_t L, uint64_t R, int k, uint64_t *w) {
   w[1] = R << (128 - 2 * k);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Mixed three- and four-word records (64 < k < 128, k % 32 != 0, NL = 3, 4). Two Feistel rounds
+// over the key words w[0..NL-1] (Kmer layout; the tail word w[NL-1] holds the last k - 32 (NL - 1) bases):
+//   w0' = w0 ^ (h1(w[1..NL-1]) << 32)     the bucket digits are the top bits of w0'
+//   X   = w[NL-2] ^ h2(w0')                a full 64-bit word: k_count's examined (last) table word, home group
+//                                          from its low bits
+// Mixed words r[0] = w0', r[1..NL-3] = w[1..NL-3], r[NL-2] = w[NL-1] (the tail), r[NL-1] = X; a record keeps
+// r[0] below the bucket digits << 6 | ext code in its first word (like §3.7b's L'), so three- and four-word keys drop
+// the 16 stored MurmurHash3 bits and MurmurHash3 itself (about ten quarter-rate 64-bit multiplies per window in the
+// extraction, and a 64-bit slot hash per lookup in k_count). h1 and h2 use full-rate 24-bit multiplies (m2_h).
+constexpr uint32_t MX_C[8] = {0x9E3779u, 0x85EBCBu, 0xC2B2AFu, 0x27D4EBu, 0x165667u, 0x3A2659u, 0xD3A2E5u, 0x6B43A9u};
+MHM_HD bool mixed3_ok(int k, int nl) { return (nl == 3 || nl == 4) && k % 32 != 0 && k < 32 * nl; }
+MHM_HD uint32_t mx_stir(uint32_t u, uint32_t c1, uint32_t c2) {
+  u ^= u >> 16;
+  u = mul24(u, c1);
+  u ^= u >> 15;
+  u = mul24(u, c2);
+  u ^= u >> 16;
+  return u;
+}
+MHM_HD uint32_t fold64(uint64_t v) {
+  const uint32_t hi = (uint32_t)(v >> 32);
+  return (uint32_t)v ^ ((hi << 7) | (hi >> 25));
+}
+template <int NL>
+MHM_HD uint32_t mx_h1(const uint64_t *w) {  // w[1..NL-1] -> 32 bits
+  uint32_t u = mx_stir(fold64(w[1]), MX_C[0], MX_C[1]);
+#pragma unroll
+  for (int i = 2; i < NL; i++) u = mx_stir(u ^ fold64(w[i]), MX_C[2 * i - 2], MX_C[2 * i - 1]);
+  return u;
+}
+// key words -> mixed words (r[0] = w0' in full)
+template <int NL>
+MHM_HD void mx_mix(const uint64_t *w, uint64_t *r) {
+  r[0] = w[0] ^ ((uint64_t)mx_h1<NL>(w) << 32);
+#pragma unroll
+  for (int i = 1; i + 2 < NL; i++) r[i] = w[i];
+  r[NL - 2] = w[NL - 1];
+  r[NL - 1] = w[NL - 2] ^ (uint64_t)m2_h(r[0], MX_C[6], MX_C[7]);
+}
+// mixed words (r[0] = w0' in full) -> key words
+template <int NL>
+MHM_HD void mx_unmix(const uint64_t *r, uint64_t *w) {
+  w[NL - 2] = r[NL - 1] ^ (uint64_t)m2_h(r[0], MX_C[6], MX_C[7]);
+  w[NL - 1] = r[NL - 2];
+#pragma unroll
+  for (int i = 1; i + 2 < NL; i++) w[i] = r[i];
+  w[0] = r[0] ^ ((uint64_t)mx_h1<NL>(w) << 32);
+}
+
 // Reverse the order of the 32 two-bit groups of x.
 MHM_HD uint64_t rev2(uint64_t x) {
   x = __builtin_bswap64(x);

@@ -165,7 +165,8 @@ struct mhmkc {
   bool packed = true;
   bool compact = false;  // compact records (kmer_ops.hpp cmix): 5 B per coarse record, 4 B per fine record
   bool mixed2 = false;   // mixed two-word records (kmer_ops.hpp m2_mix, 33 <= k <= 63): 16 B, no byte plane
-  bool mixed() const { return compact || mixed2; }  // the kernels' "compact" flag: bucket digits implicit
+  bool mixed3 = false;   // mixed three- and four-word records (kmer_ops.hpp mx_mix, 64 < k < 128): NL words
+  bool mixed() const { return compact || mixed2 || mixed3; }  // the kernels' "compact" flag: bucket digits implicit
   int cb = 8, fb = 8, hbits = 0;
   uint32_t nb = 256, nf = 256;
   uint32_t own_lo = 0, own_hi = 256;  // owned coarse range [own_lo, own_hi)
@@ -1741,6 +1742,13 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   // mixed two-word records for 33 <= k <= 63 (the same switch keeps the plain key words)
   h->mixed2 = mhm::mixed2_ok(k, nl) && !(wide && atoi(wide));
   if (h->mixed2) {
+    h->packed = true;  // the ext code sits in w[0]
+    h->hbits = 0;
+  }
+  // mixed three- and four-word records for 64 < k < 128 (MHMKC_MIXED3=0: the key words + stored MurmurHash3 bits)
+  const char *mx_env = getenv("MHMKC_MIXED3");
+  h->mixed3 = mhm::mixed3_ok(k, nl) && !(wide && atoi(wide)) && !(mx_env && !atoi(mx_env));
+  if (h->mixed3) {
     h->packed = true;  // the ext code sits in w[0]
     h->hbits = 0;
   }

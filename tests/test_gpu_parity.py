@@ -97,7 +97,7 @@ def test_batches_equal_single(k):
     assert_tables_equal(many, one, "5 batches vs 1")
 
 
-@pytest.mark.parametrize("k,wide", [(21, True), (15, False), (17, False), (63, False), (77, False)])
+@pytest.mark.parametrize("k,wide", [(21, True), (15, False), (17, False), (63, False), (77, False), (99, False)])
 def test_forced_overflow_sweeps(k, wide, monkeypatch):
     """Tiny LDS tables force the multi-sweep path (a closed table overflows whole keys to the next sweep).
     Compact records (k <= 21) need >= 2k - 34 fine bits, so k = 15, 17 cover them with one fine bucket."""
@@ -113,7 +113,7 @@ def test_forced_overflow_sweeps(k, wide, monkeypatch):
     check_stats(st)
 
 
-@pytest.mark.parametrize("k,wide", [(15, False), (21, True), (63, False)])
+@pytest.mark.parametrize("k,wide", [(15, False), (21, True), (63, False), (77, False)])
 def test_forced_overflow_hot_sweep(k, wide, monkeypatch):
     """A hot first sweep (>= 0xC000 records: the checked round loop with its round barrier and clamp) that
     overflows a 64-slot table: the poly-A k-mer's bucket also holds ~100-200 distinct keys of the random reads,
@@ -319,11 +319,11 @@ def test_compact_overflow_at_min_fine_bits(k, monkeypatch):
     check_stats(st)
 
 
-@pytest.mark.parametrize("k", [21, 12, 33, 47, 63])
+@pytest.mark.parametrize("k", [21, 12, 33, 47, 63, 65, 77, 95, 99, 127])
 def test_compact_equals_wide_records(k, monkeypatch):
-    """The mixed record layouts (compact 4/5-byte at k <= 21, two-word m2_mix at 33 <= k <= 63; the key rebuilt
-    from the bucket digits) and the plain key-word records give the same table, through the capped and the
-    exact partition paths."""
+    """The mixed record layouts (compact 4/5-byte at k <= 21, two-word m2_mix at 33 <= k <= 63, three- and four-word
+    mx_mix at 64 < k < 128; the key rebuilt from the bucket digits) and the plain key-word records give the same
+    table, through the capped and the exact partition paths."""
     b, o = synth_set(20000, 300000, 31)
     cmp_t, st_c = hip_table(b, o, k)
     monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")

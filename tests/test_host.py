@@ -82,8 +82,8 @@ def test_table_lines_dump_format(tmp_path):
 
 
 def test_mixed_record_bijection_and_flatness(tmp_path):
-    """kmer_ops.hpp cmix / m2_mix and their inverses (mixed records): round trips at every k
-    in 10..21 and 33..63,
+    """kmer_ops.hpp cmix / m2_mix / mx_mix and their inverses (mixed records): round
+    trips at every k in 10..21, 33..63 and 65..127 (k % 32 != 0),
     and flat bucket digits and home groups over the consecutive (correlated) canonical windows of one sequence."""
     import shutil
     import subprocess
@@ -97,7 +97,7 @@ def test_mixed_record_bijection_and_flatness(tmp_path):
     out = subprocess.run([str(exe), "2000000"], capture_output=True, text=True, check=True).stdout
     assert "roundtrip ok" in out
     rows = [ln.split() for ln in out.splitlines() if ln.startswith("k ")]
-    assert len(rows) == 6
+    assert len(rows) == 11
     for r in rows:
         coarse, fine, group = float(r[3]), float(r[5]), float(r[7])
         # 256 coarse bins of ~7800 windows, up to 2^17 fine bins of ~15 (Poisson max), 1000 groups of 2000

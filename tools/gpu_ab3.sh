@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B of library variants (exp/libmhmkc_<v>.so, VARIANTS) at the k values in KS, after each variant's parity tests
+# (PARITY_K selects them). Each GPU step has its own limit; an abnormal end stops the call.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for v in $VARIANTS; do
+  MHMKC_LIB=exp/libmhmkc_$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -m "gpu and not slow" -k "${PARITY_K:-not nothing}" --timeout 300 --timeout-method thread > gpurun_out/pytest_parity_$v.log 2>&1; rc=$?
+  echo "$v parity: $(tail -n 1 gpurun_out/pytest_parity_$v.log)"
+  if [ $rc -ne 0 ]; then echo "variant $v parity failed ($rc)"; grep -E "FAILED|Error" gpurun_out/pytest_parity_$v.log | head; exit 1; fi
+done
+specs=("base|MHMKC_X=0")
+for v in $VARIANTS; do specs+=("$v|MHMKC_LIB=exp/libmhmkc_$v.so"); done
+for k in ${KS:-21 63}; do
+  echo "== k=$k"; BENCH_ARGS="--k $k" bash tools/ab_env.sh "${specs[@]}" || exit $?
+done
+echo done

@@ -4,7 +4,12 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-if [ -z "$SKIP_L" ]; then bash tools/gpu_r03l.sh || exit $?; fi
+if [ -z "$SKIP_L" ]; then bash tools/gpu_r03l.sh || exit $?
+elif [ -z "$SKIP_T" ]; then
+  timeout -k 10 700 python -u -m pytest tests -q -m "gpu and not slow" --timeout 300 --timeout-method thread > gpurun_out/pytest_main.log 2>&1; rc=$?
+  echo "main: $(tail -n 1 gpurun_out/pytest_main.log)"
+  if [ $rc -ne 0 ]; then echo "main tests failed ($rc)"; grep -E "FAILED|Error" gpurun_out/pytest_main.log | head; exit 1; fi
+fi
 for v in $VARIANTS; do
   MHMKC_LIB=exp/libmhmkc_$v.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -m "gpu and not slow" --timeout 300 --timeout-method thread > gpurun_out/pytest_parity_$v.log 2>&1; rc=$?
   echo "$v parity: $(tail -n 1 gpurun_out/pytest_parity_$v.log)"
