@@ -1734,7 +1734,7 @@ constexpr int C_PROBE = MHMKC_CPROBE;
 #define MHMKC_GS_C 4  // compact (32-bit) keys
 #endif
 #ifndef MHMKC_GS_M2
-#define MHMKC_GS_M2 4  // mixed two-word keys (the last word, 64-bit, is the one read)
+#define MHMKC_GS_M2 2  // mixed two-word keys (the last word, 64-bit, is the one read): k = 63 count 9.32 -> 9.09 ms
 #endif
 template <int NL, bool C32, bool M2>
 constexpr int group_slots() {

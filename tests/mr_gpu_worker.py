@@ -1,9 +1,10 @@
 """Worker of the multi-rank GPU tests (TEST INFRASTRUCTURE): one rank of libmhmkc's own multi-GPU path.
 
-Every rank is a process with its own counter on the same GPU (RCCL refuses two ranks on one device, so the
-exchange goes through the host-staged transport, mhmkc_set_transport, driven by a gloo process group). The
-rank counts its shard of the reads (and adds its share of the contigs); mhmkc_finish then runs the real
-exchange code (exchange(), the contig all-gather and, with MHMKC_OWNER_MINIMIZER, the owner hand-off).
+Every rank is a process with its own counter on the same GPU. The exchange goes through the host-staged transport
+(mhmkc_set_transport, driven by a gloo process group), or with opts["rccl"] through libmhmkc's RCCL path (each rank
+with its own NCCL_HOSTID: RCCL refuses two ranks of one communicator on one device otherwise). The rank counts its
+shard of the reads (and adds its share of the contigs); mhmkc_finish then runs the real exchange code (exchange(),
+the contig all-gather and, with MHMKC_OWNER_MINIMIZER, the owner hand-off or the supermer exchange).
 """
 import os
 import sys
@@ -42,11 +43,18 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if opts.get("contigs"):
         b, o, seqs, depths = ctg_set(seed=opts["seed"], n_reads=opts.get("n_reads", 300))
+    elif opts.get("hot"):  # common.hot_set: random reads first, then the poly-A reads
+        from common import hot_set
+
+        b, o = hot_set()
+        seqs, depths = [], np.zeros(0, np.uint16)
     else:
         b, o = synth_set(opts.get("n_reads", 1200), opts.get("genome", 9000), opts["seed"])
         seqs, depths = [], np.zeros(0, np.uint16)
     n = o.size - 1
     lo, hi = shard(n, rank, world)
+    if opts.get("cuts"):  # explicit read ranges: rank r takes [cuts[r], cuts[r + 1])
+        lo, hi = opts["cuts"][rank], opts["cuts"][rank + 1]
     idle = opts.get("idle_rank")  # this rank adds nothing; its share goes to the next rank (idle < world - 1)
     if idle is not None and rank == idle:
         lo = hi
@@ -73,6 +81,8 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     c.add_tensors(bt, ot)
     if len(seqs):
         a, z = shard(len(seqs), rank, world)
+        if opts.get("ctg_rank") is not None:  # all contigs on one rank
+            a, z = (0, len(seqs)) if rank == opts["ctg_rank"] else (0, 0)
         c.add_ctgs(seqs[a:z], depths[a:z])
     c.finish()
     t = c.fetch()
@@ -82,7 +92,7 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
              owned=st["owned_records"], count_sum=st["count_sum"], distinct=st["distinct"], purged=st["purged"],
              n_out=st["n_out"], handoff_sent=st["handoff_sent"], handoff_recv=st["handoff_recv"],
              ctg_kmers=st["ctg_kmers"], smer_count=st["smer_count"], smer_words=st["smer_words"],
-             xchg_rounds=st["xchg_rounds"])
+             xchg_rounds=st["xchg_rounds"], exact_reruns=st["exact_reruns"])
     c.close()
     dist.barrier()
     dist.destroy_process_group()

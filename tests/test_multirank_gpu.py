@@ -176,6 +176,33 @@ def test_multirank_contig_pass(k, world, minimizer, tmp_path):
             assert all(L.orc_kmer_target_rank(keys[i].ctypes.data, k, nl, world) == r for i in range(len(keys)))
 
 
+@pytest.mark.parametrize("k,xpipe,rccl", [(21, "0", False), (21, "1", False), (63, "1", False), (21, "1", True)])
+def test_hot_kmer_on_one_rank(k, xpipe, rccl, tmp_path):
+    """the poly-A reads (one k-mer past 65535 occurrences) all on rank 1, so rank 1's capped
+    extraction overflows and is redone exactly while rank 0's is not, with the exchange at finish and pipelined
+    (a rerun inside a collective round), over the host transport and over RCCL; the union equals the oracle."""
+    from common import hot_set
+
+    world = 2
+    parts = run_ranks(k, world, tmp_path, seed=0, hot=True, cuts=[0, 200, 1200], rccl=rccl, env={"MHMKC_XPIPE": xpipe})
+    b, o = hot_set()
+    exp = oracle_table(b, o, k)
+    assert (exp.counts == 65535).any()
+    check_parts(parts, k, exp, f"hot k-mer on rank 1, k={k}, xpipe={xpipe}")
+    assert int(parts[1]["exact_reruns"]) >= 1
+
+
+@pytest.mark.parametrize("k,world,minimizer", [(21, 2, False), (63, 3, True), (33, 3, False)])
+def test_contigs_on_one_rank(k, world, minimizer, tmp_path):
+    """every contig added on rank 0 only (the others add none): still applied in that one order
+    everywhere, the union equals a single rank given all reads and contigs."""
+    seed = 850 + k
+    parts = run_ranks(k, world, tmp_path, seed=seed, contigs=True, minimizer=minimizer, ctg_rank=0)
+    b, o, seqs, depths = ctg_set(seed=seed)
+    assert sum(int(p["ctg_kmers"]) for p in parts) > 0
+    check_parts(parts, k, oracle_ctg_table(b, o, seqs, depths, k), f"contigs on rank 0 of {world}, k={k}")
+
+
 def test_multirank_dmin_and_many_chunks(tmp_path):
     """Two ranks, each host batch cut into ~45 H2D chunks (slice views with a head offset), dmin_thres = 3."""
     parts = run_ranks(21, 2, tmp_path, seed=9, dmin=3, n_reads=1200, genome=20000,
