@@ -438,29 +438,36 @@ def main():
             pmc = {}
     # measured for this workload only (the config's own sizes)
     pmc = {} if (args.reads_per_gpu or args.reads_total) else pmc.get("configs", {}).get(f"{args.config}/k{k}", {})
-    if dom and launches.get(dom):
-        ms_launch = stage_ms[dom] / launches[dom]
-        alg = algorithmic_bytes(dom, st, k) / max(1, launches[dom] // steps)
+    def roofline_of(stage):
+        """The roofline object of one stage's kernel: k_count against its LDS floor (its HBM figures beside it), the
+        streaming kernels against HBM."""
+        ms_launch = stage_ms[stage] / launches[stage]
+        alg = algorithmic_bytes(stage, st, k) / max(1, launches[stage] // steps)
         hbm = {"achieved": round(alg / (ms_launch * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                "frac": round(alg / (ms_launch * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "algorithmic_bytes": int(alg)}
-        traffic = pmc.get("per_launch_bytes", {}).get(dom)
-        if dom == "count":
+        traffic = pmc.get("per_launch_bytes", {}).get(stage)
+        if stage == "count":
             # k_count keeps its hash table in LDS and is bound there (DESIGN.md §4): the roofline is its LDS
             # time floor at the measured random-access LDS rates; achieved / peak are the LDS bytes of its
             # table operations over the measured time / over that floor
             t_floor, lds_b = lds_floor_seconds(st, k)
-            roofline = {"bound": "lds", "kernel": "k_count", "achieved": round(lds_b / (ms_launch * 1e-3) / 1e12, 3),
-                        "peak": round(lds_b / t_floor / 1e12, 3), "unit": "TB/s",
-                        "frac": round(t_floor / (ms_launch * 1e-3), 4), "traffic": traffic,
-                        "traffic_source": pmc.get("source"), "avg_launch_ms": round(ms_launch, 4),
-                        "lds_floor_ms": round(t_floor * 1e3, 4),
-                        "lds_ops": {"records": st["owned_records"], "phase_b_records": st["lds_misses"],
-                                    "ext_adds": st["lds_ext_adds"]},
-                        "hbm": hbm}
-        else:
-            roofline = {"bound": "hbm", "kernel": dom, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBPS,
-                        "unit": "GB/s", "frac": hbm["frac"], "traffic": traffic, "traffic_source": pmc.get("source"),
-                        "algorithmic_bytes": int(alg), "avg_launch_ms": round(ms_launch, 4)}
+            return {"bound": "lds", "kernel": "k_count", "achieved": round(lds_b / (ms_launch * 1e-3) / 1e12, 3),
+                    "peak": round(lds_b / t_floor / 1e12, 3), "unit": "TB/s",
+                    "frac": round(t_floor / (ms_launch * 1e-3), 4), "traffic": traffic,
+                    "traffic_source": pmc.get("source"), "avg_launch_ms": round(ms_launch, 4),
+                    "lds_floor_ms": round(t_floor * 1e3, 4),
+                    "lds_ops": {"records": st["owned_records"], "phase_b_records": st["lds_misses"],
+                                "ext_adds": st["lds_ext_adds"]},
+                    "hbm": hbm}
+        return {"bound": "hbm", "kernel": "k_" + stage, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": hbm["frac"], "traffic": traffic, "traffic_source": pmc.get("source"),
+                "algorithmic_bytes": int(alg), "avg_launch_ms": round(ms_launch, 4)}
+
+    if dom and launches.get(dom):
+        roofline = roofline_of(dom)
+    # every main kernel's roofline (at k = 21 extraction and counting take about the same time, so the dominant one
+    # changes from run to run)
+    rooflines = {s_: roofline_of(s_) for s_ in ("extract_scatter", "part_scatter", "count") if launches.get(s_)}
 
     # D2H of the finished table (the KmerMap fill starts from it)
     t1 = time.perf_counter()
@@ -537,6 +544,7 @@ def main():
                        "transport": args.transport if world > 1 else None,
                        "physical_gpus": min(world, n_dev) if shared else world},
             "roofline": roofline,
+            "rooflines": rooflines,
             "cpu_baseline": cpu,
             "stages_ms_per_step": {s_: round(v, 3) for s_, v in per_step.items() if launches.get(s_)},
             "achieved_measured_GBps_whole_step": round(

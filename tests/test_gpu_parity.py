@@ -488,11 +488,12 @@ def test_capped_overflow_in_last_bucket(k):
 
 @pytest.mark.slow
 @pytest.mark.timeout(1200)
-@pytest.mark.parametrize("k", [21, 63])
+@pytest.mark.parametrize("k", [21, 63, 99])
 def test_c2_full_table_vs_cpu_restatement(k):
     """config C2 at full size (10M x 150 bp, G = 50 Mbp, seed 2) through the host path
     (chunked H2D), every row of the table compared with the multi-threaded CPU restatement (oracle/kcount_mt.c,
-    itself pinned to the single-threaded oracle and the golden fixtures); k = 21 and the C4 k = 63."""
+    itself pinned to the single-threaded oracle and the golden fixtures); k = 21, the C4 k = 63 and k = 99 (mixed
+    four-word records)."""
     g = m.synth_genome(50_000_000, 2)
     b, o = m.synth_reads(g, 10_000_000, 150, 2, threads=16)
     del g
