@@ -24,7 +24,7 @@ namespace mhm {
 
 template <int NL>
 constexpr int kTile() {  // bases per extract tile
-  return NL == 1 ? MHMKC_TILE1 : NL == 2 ? MHMKC_TILE2 : MHMKC_TILE3;
+  return NL == 1 ? MHMKC_TILE1 : NL == 2 ? MHMKC_TILE2 : NL == 3 ? MHMKC_TILE3 : MHMKC_TILE4;
 }
 template <int NL>
 constexpr int kEThreads() {  // threads per extract workgroup
@@ -32,7 +32,7 @@ constexpr int kEThreads() {  // threads per extract workgroup
 }
 template <int NL>
 constexpr int kPTile() {  // records per partition chunk (E_THREADS threads)
-  return NL == 1 ? MHMKC_PTILE1 : MHMKC_PTILE2;
+  return NL == 1 ? MHMKC_PTILE1 : NL == 2 ? MHMKC_PTILE2 : MHMKC_PTILE3;
 }
 template <int NL>
 constexpr int kGroups() {
@@ -703,6 +703,15 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
 #define MHMKC_ESTAGE 1
 #endif
 constexpr bool kEStaged = MHMKC_ESTAGE != 0;
+// three- and four-word keys: a 2048-base tile at k >= 65 makes ~3 records per coarse bin, so staging gains little
+// coalescing and its 48-64 KB of LDS per workgroup cost occupancy (MHMKC_ESTAGE3=0: register scatter for NL >= 3)
+#ifndef MHMKC_ESTAGE3
+#define MHMKC_ESTAGE3 1
+#endif
+template <int NL>
+constexpr bool kEStagedNL() {
+  return NL >= 3 ? (kEStaged && MHMKC_ESTAGE3 != 0) : kEStaged;
+}
 
 #ifndef MHMKC_PSTAGE
 #define MHMKC_PSTAGE 1
@@ -876,7 +885,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
   uint64_t *fwd;
   uint32_t *good, *start;
   unsigned char *smem, *area;
-  if (kEStaged) {  // counters first, then the tile aliased by the stage area
+  if (kEStagedNL<NL>()) {  // counters first, then the tile aliased by the stage area
     smem = smem0;
     area = smem0 + staged_cnt_bytes(p.n_bins);
     carve_tile<NL>(area, fwd, good, start);
@@ -907,7 +916,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
     walk_c32<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, rk, inf);
   } else if constexpr (RecKind<NL, CMP>::M2 && kMixedWalk && !kM2Walk) {
     walk_m2<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, rk, inf);
-  } else if constexpr (RecKind<NL, CMP>::M2 && kM2Walk && kEStaged) {
+  } else if constexpr (RecKind<NL, CMP>::M2 && kM2Walk && kEStagedNL<NL>()) {
     m2_walk_valid<W>(p, tile, fwd, good, start, area + tile_lds_bytes<NL>(), rk, inf
 #ifdef MHMKC_ESTAMP
                      , es2
@@ -962,7 +971,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
   const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
   constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
-  if (kEStaged)
+  if (kEStagedNL<NL>())
     scatter_staged<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
                                       p.ovf);
   else
@@ -3029,7 +3038,7 @@ template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
   constexpr int T = kTile<NL>();
   const size_t tile_b = tile_lds_bytes<NL>() + (RecKind<NL, CMP>::M2 && kM2Walk ? m2walk_lds_bytes() : 0);
-  const size_t lds = kEStaged ? staged_cnt_bytes(p.n_bins) + std::max(tile_b, staged_area_bytes(NL, T, PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
+  const size_t lds = kEStagedNL<NL>() ? staged_cnt_bytes(p.n_bins) + std::max(tile_b, staged_area_bytes(NL, T, PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
                               : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;

@@ -242,10 +242,18 @@ inline int stored_hash_bits(int k, int nl, bool packed) {
 #ifndef MHMKC_TILE2
 #define MHMKC_TILE2 4096
 #endif
+// three-word keys: 1536-base tiles, so that the staged 24-byte records of three workgroups fit a CU's LDS (2048: two
+// workgroups, k = 77 extract 14.70 -> 13.05 ms); four-word keys keep 2048 (1536 still leaves two workgroups of
+// 32-byte records: 16.08 -> 19.09 ms; 1024: 16.03)
 #ifndef MHMKC_TILE3
-#define MHMKC_TILE3 2048
+#define MHMKC_TILE3 1536
 #endif
-inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : nl == 2 ? MHMKC_TILE2 : MHMKC_TILE3; }
+#ifndef MHMKC_TILE4
+#define MHMKC_TILE4 2048
+#endif
+inline int tile_bases(int nl) {
+  return nl == 1 ? MHMKC_TILE1 : nl == 2 ? MHMKC_TILE2 : nl == 3 ? MHMKC_TILE3 : MHMKC_TILE4;
+}
 // threads of an extract workgroup (tile_bases / threads windows each)
 #ifndef MHMKC_ETHREADS1
 #define MHMKC_ETHREADS1 E_THREADS
@@ -263,7 +271,10 @@ inline int tile_bases(int nl) { return nl == 1 ? MHMKC_TILE1 : nl == 2 ? MHMKC_T
 #ifndef MHMKC_PTILE2
 #define MHMKC_PTILE2 2048
 #endif
-inline int chunk_records(int nl) { return nl == 1 ? MHMKC_PTILE1 : MHMKC_PTILE2; }
+#ifndef MHMKC_PTILE3
+#define MHMKC_PTILE3 MHMKC_PTILE2  // three- and four-word keys
+#endif
+inline int chunk_records(int nl) { return nl == 1 ? MHMKC_PTILE1 : nl == 2 ? MHMKC_PTILE2 : MHMKC_PTILE3; }
 // Mixed two-word records (33 <= k <= 63) as one 16-byte record in the first of their two planes' space, in the
 // coarse slabs and the fine buckets (0: two u64 planes)
 #ifndef MHMKC_M2AOS
