@@ -132,7 +132,7 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // Group g of the tile is global group tile*T/32 - 1 + g (one group of left halo).
 template <int NL>
 __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_read, int qcut, uint64_t *fwd,
-                          uint32_t *good, uint32_t *start, unsigned int *err) {
+                          uint32_t *good, uint32_t *start, unsigned int *err, const uint32_t *tile_starts = nullptr) {
   constexpr int T = kTile<NL>(), NG = kGroups<NL>();
   const int64_t gA = (int64_t)tile * (T / 32) - 1;
   for (int g = threadIdx.x; g < NG; g += blockDim.x) {
@@ -180,9 +180,10 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
     }
     fwd[g] = f;
     good[g] = gd;
-    start[g] = 0;
+    start[g] = tile_starts ? gload(tile_starts + (uint64_t)tile * NG + g) : 0u;
   }
   __syncthreads();
+  if (tile_starts) return;  // (uniform) the bitmap came precomputed: no dependent load of the tile's first read
   const int64_t lo = gA * 32, hi = (gA + NG) * 32;
   for (uint64_t r = (uint64_t)first_read + threadIdx.x; r <= rv.n_reads; r += blockDim.x) {
     const int64_t s = (int64_t)(rv.offs[r] - rv.obase);
@@ -452,6 +453,37 @@ __global__ void k_tile_first_read(ReadsView rv, uint32_t *out, uint32_t n_tiles,
   out[t] = (uint32_t)a;
 }
 
+// Read-start bitmaps of the extraction tiles (what load_tile builds from the offsets: bit 31 - (d & 31) of word d >> 5
+// for a read start at tile-local position d of the kGroups<NL>() staged groups), one wave per tile. The extraction
+// then loads its tile's bitmap beside the bases instead of first loading the tile's first read and then the offsets
+// after it: two dependent global round trips per tile that four workgroups per CU did not hide. This kernel has the
+// same chain, but one wave per tile and little LDS, so many tiles are in flight.
+template <int NL>
+__global__ __launch_bounds__(256) void k_tile_starts(ReadsView rv, const uint32_t *tile_first, uint32_t *out,
+                                                     uint32_t n_tiles) {
+  constexpr int T = kTile<NL>(), NG = kGroups<NL>();
+  __shared__ uint32_t w[4][NG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t tile = blockIdx.x * 4 + wv;
+  for (int g = lane; g < NG; g += 64) w[wv][g] = 0;
+  __syncthreads();
+  if (tile < n_tiles) {
+    const int64_t gA = (int64_t)tile * (T / 32) - 1;
+    const int64_t lo = gA * 32, hi = (gA + NG) * 32;
+    for (uint64_t r = (uint64_t)tile_first[tile] + lane; r <= rv.n_reads; r += 64) {
+      const int64_t s = (int64_t)(rv.offs[r] - rv.obase);
+      if (s >= hi) break;
+      if (s >= lo) {
+        const int64_t d = s - lo;
+        atomicOr(&w[wv][d >> 5], 1u << (31 - (d & 31)));
+      }
+    }
+  }
+  __syncthreads();
+  if (tile < n_tiles)
+    for (int g = lane; g < NG; g += 64) out[(uint64_t)tile * NG + g] = w[wv][g];
+}
+
 // ------------------------------------------------------------------------------------------------
 // extract: histogram
 
@@ -497,7 +529,8 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_hist(ExtractParams 
   uint32_t *hist = (uint32_t *)rest;
   for (uint32_t b = threadIdx.x; b < p.n_bins; b += ET) hist[b] = 0;
   const uint32_t tile = blockIdx.x;
-  load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
+  load_tile<NL>(p.reads, tile, p.tile_starts ? 0u : p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err,
+                p.tile_starts);
   const int sh = 64 - p.coarse_bits;
   walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, p.k, [&](int, const uint64_t *key, uint32_t, bool valid) {
     if (valid) atomicAdd(&hist[(uint32_t)(window_hash<NL, CMP>(key, p.k) >> sh)], 1u);
@@ -898,7 +931,8 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
 #endif
   scatter_clear<ET>((uint32_t *)smem, p.n_bins);
   const uint32_t tile = blockIdx.x;
-  load_tile<NL>(p.reads, tile, p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err);
+  load_tile<NL>(p.reads, tile, p.tile_starts ? 0u : p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err,
+                p.tile_starts);
 #ifdef MHMKC_ESTAMP
   const uint64_t es1 = __builtin_amdgcn_s_memtime();
   uint64_t es2 = es1;
@@ -3079,6 +3113,24 @@ static hipError_t do_count(const CountParams &p, hipStream_t s) {
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s) {
   if (!n_tiles) return hipSuccess;
   k_tile_first_read<<<dim3((n_tiles + 255) / 256), dim3(256), 0, s>>>(r, out, n_tiles, tile);
+  return hipGetLastError();
+}
+
+size_t tile_starts_words(int nl) {
+  return nl == 1 ? kGroups<1>() : nl == 2 ? kGroups<2>() : nl == 3 ? kGroups<3>() : kGroups<4>();
+}
+
+hipError_t launch_tile_starts(const ReadsView &r, const uint32_t *tile_first, uint32_t *out, uint32_t n_tiles, int nl,
+                              hipStream_t s) {
+  if (!n_tiles) return hipSuccess;
+  const dim3 grid((n_tiles + 3) / 4), block(256);
+  switch (nl) {
+    case 1: k_tile_starts<1><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
+    case 2: k_tile_starts<2><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
+    case 3: k_tile_starts<3><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
+    case 4: k_tile_starts<4><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -44,6 +44,8 @@ struct ExtractParams {
   PlaneSet out;                     // (E-scatter)
   unsigned int *err;                // bit 0: input byte with code > 4
   unsigned int *ovf;                // bit 1: a capped bin of this slab overflowed (per slab)
+  const uint32_t *tile_starts;      // per tile: its read-start bitmap (k_tile_starts, kGroups words), or nullptr:
+                                    // load_tile builds it from the offsets
 };
 
 constexpr int SMER_SLICES = 64;  // counter slices per destination (spread the workgroups' atomics)
@@ -305,6 +307,10 @@ static_assert(count_lds_bytes(1) <= C_LDS && count_lds_bytes(2) <= C_LDS && coun
               "k_count LDS budget");
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);
+// per extraction tile its read-start bitmap (tile_starts_words(nl) u32 per tile), from tile_first_read
+hipError_t launch_tile_starts(const ReadsView &r, const uint32_t *tile_first, uint32_t *out, uint32_t n_tiles, int nl,
+                              hipStream_t s);
+size_t tile_starts_words(int nl);
 // total counted windows sum(max(0, L - k - 1)) of a batch, added to *out; err bit 2 (4) when the offsets are
 // not a valid PackedReads CSR (offs[0] != 0, decreasing, a read longer than 65535, offs[n] != n_bases)
 hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, unsigned int *err, hipStream_t s);

@@ -198,7 +198,7 @@ struct mhmkc {
   int pump();
   int resolve_one(Slab *sl, bool &redo);
   std::vector<hipEvent_t> chunk_ev;  // one per H2D chunk in flight (pool)
-  DevBuf d_hist, d_tiles, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
+  DevBuf d_hist, d_tiles, d_tsb, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
   DevBuf d_hll, d_dest, d_ohist, d_out2_keys, d_out2_counts, d_out2_left, d_out2_right, d_mh;
   DevBuf d_ord;  // mhmkc_fetch_ordered: sort keys, row indices, radix-sort scratch
@@ -408,6 +408,15 @@ int mhmkc::extract(Slab *sl, bool exact) {
   if (!sl->recv) {  // (the received supermers' tile index is made once by smer_exchange)
     prof_begin(MHMKC_STAGE_TILEIDX);
     e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
+    // the tiles' read-start bitmaps (MHMKC_TSB=0: load_tile builds them from the offsets)
+    static const bool tsb_on = !(getenv("MHMKC_TSB") && !atoi(getenv("MHMKC_TSB")));
+    if (e == hipSuccess && tsb_on) {
+      const size_t words = (size_t)sl->tiles * mhm::tile_starts_words(nl);
+      if ((e = grow(d_tsb, words * 4 + 64)) == hipSuccess) {
+        e = mhm::launch_tile_starts(sl->rv, d_tiles.as<uint32_t>(), d_tsb.as<uint32_t>(), sl->tiles, nl, stream);
+        p.tile_starts = d_tsb.as<uint32_t>();
+      }
+    }
     prof_end();
     if (e != hipSuccess) return hip_fail(e, "tile index");
   }
@@ -1734,7 +1743,15 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
 #ifndef MHMKC_CB0
 #define MHMKC_CB0 8
 #endif
-  h->cb = MHMKC_CB0 + extra;
+// coarse bits by key words: three- and four-word keys take 128 coarse buckets (half the extraction's cursor atomics
+// per record and runs twice as long at ~0.5 records per base; k = 99 38.9 -> 34.8 ms per C2 step, k = 77 31.4 -> 31.0)
+#ifndef MHMKC_CB0_2
+#define MHMKC_CB0_2 MHMKC_CB0  // two-word keys
+#endif
+#ifndef MHMKC_CB0_3
+#define MHMKC_CB0_3 7  // three- and four-word keys (cb >= 7 keeps a fine record's w0' bits + ext in 64 bits, fb >= 0)
+#endif
+  h->cb = (nl >= 3 ? MHMKC_CB0_3 : nl == 2 ? MHMKC_CB0_2 : MHMKC_CB0) + extra;
   // compact records for 10 <= k <= 21 (MHMKC_WIDE_RECORDS=1 keeps the 8-byte records: A/B and tests)
   const char *wide = getenv("MHMKC_WIDE_RECORDS");
   h->compact = mhm::compact_ok(k, nl) && 2 * k - h->cb <= 34 && !(wide && atoi(wide));
