@@ -470,7 +470,10 @@ __global__ __launch_bounds__(256) void k_tile_starts(ReadsView rv, const uint32_
   if (tile < n_tiles) {
     const int64_t gA = (int64_t)tile * (T / 32) - 1;
     const int64_t lo = gA * 32, hi = (gA + NG) * 32;
-    for (uint64_t r = (uint64_t)tile_first[tile] + lane; r <= rv.n_reads; r += 64) {
+    // (the tile's first read from k_tile_first_read: a 64-ary search across the wave here, four dependent loads per
+    // tile, made the tile-index stage 0.17 -> 0.23 ms)
+    const uint64_t first = tile_first[tile];
+    for (uint64_t r = first + lane; r <= rv.n_reads; r += 64) {
       const int64_t s = (int64_t)(rv.offs[r] - rv.obase);
       if (s >= hi) break;
       if (s >= lo) {
@@ -2485,14 +2488,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
           for (int j = 0; j < R; j++) {
             res[j] = 0u;
-            if (ce[j] != NONE && slot[j] < 0 && slot[j] > G_FULL)  // slot -1 - r of the home group was empty: claim it
+            if (kClaimA && ce[j] != NONE && slot[j] < 0 && slot[j] > G_FULL)  // slot -1 - r of the home group was empty: claim it
               res[j] = atomicCAS((unsigned int *)&last[GS * g[j] - 1 - slot[j]], 0xffffffffu, (uint32_t)ck[j][0]);
           }
 #pragma unroll
           for (int j = 0; j < R; j++) {
             old[j] = 0;
             int r = slot[j];
-            if (r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = GS * g[j] - 1 - r;
+            if (kClaimA && r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = GS * g[j] - 1 - r;
             if (MHMKC_ADDBF && kCold2) {  // every lane adds (0 when it has nothing to count): no branch per record
               const bool valid = ce[j] != NONE, ok = valid && r >= 0;
               lds_add_nr_bf(t, ok ? r : GS * g[j], ce[j], ok);  // (adds of 0 spread over the home groups: one common
