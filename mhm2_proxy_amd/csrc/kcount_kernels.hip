@@ -31,8 +31,12 @@ constexpr int kEThreads() {  // threads per extract workgroup
   return NL == 1 ? MHMKC_ETHREADS1 : NL == 2 ? MHMKC_ETHREADS2 : MHMKC_ETHREADS3;
 }
 template <int NL>
-constexpr int kPTile() {  // records per partition chunk (E_THREADS threads)
-  return NL == 1 ? MHMKC_PTILE1 : NL == 2 ? MHMKC_PTILE2 : MHMKC_PTILE3;
+constexpr int kPTile() {  // records per partition chunk (kPThreads threads)
+  return NL == 1 ? MHMKC_PTILE1 : NL == 2 ? MHMKC_PTILE2 : NL == 3 ? MHMKC_PTILE3 : MHMKC_PTILE4;
+}
+template <int NL>
+constexpr int kPThreads() {  // threads per partition workgroup
+  return NL == 1 ? MHMKC_PTHREADS1 : NL == 2 ? MHMKC_PTHREADS2 : MHMKC_PTHREADS3;
 }
 template <int NL>
 constexpr int kGroups() {
@@ -1462,13 +1466,13 @@ __global__ __launch_bounds__(256) void k_chunk_runs(const SRun *runs, uint32_t *
 // loads are unconditional (lanes past the chunk end re-read its last record) so that no use of a loaded
 // value sits inside a branch: a conditional load whose value is consumed in its own branch makes the
 // compiler wait for it there, one load after the other. Callers check i < ch.count themselves.
-template <int NL, bool PACKED, bool CMP, int W>
+template <int NL, bool PACKED, bool CMP, int W, int NT = kPThreads<NL>()>
 __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch, uint64_t (&rk)[W][NL],
                                            uint32_t (&re)[W]) {
   uint32_t rx[W];
 #pragma unroll
   for (int j = 0; j < W; j++) {
-    const uint32_t i = threadIdx.x + j * E_THREADS;
+    const uint32_t i = threadIdx.x + j * NT;
     const uint64_t idx = ch.start + (i < ch.count ? i : ch.count - 1);
     if (RecKind<NL, CMP>::C32) {  // coarse compact record: low 32 bits + high byte
       rk[j][0] = (uint64_t)gload((const uint32_t *)src.w[0] + idx);
@@ -1495,11 +1499,11 @@ __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch
 }
 
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
-  constexpr int T = kPTile<NL>(), W = T / E_THREADS;
+__global__ __launch_bounds__(kPThreads<NL>()) void k_part_hist(PartitionParams p) {
+  constexpr int NT = kPThreads<NL>(), T = kPTile<NL>(), W = T / NT;
   extern __shared__ __align__(16) uint32_t hist[];  // the only LDS object
   const uint32_t nf = 1u << p.fine_bits;
-  for (uint32_t b = threadIdx.x; b < nf; b += E_THREADS) hist[b] = 0;
+  for (uint32_t b = threadIdx.x; b < nf; b += NT) hist[b] = 0;
   uint32_t c;
   if (!xcd_chunk(p, c)) return;  // no chunk left in this workgroup's XCD class (uniform: before any barrier)
   const SChunk ch = chunk_of<T>(p, c);
@@ -1510,22 +1514,23 @@ __global__ __launch_bounds__(E_THREADS) void k_part_hist(PartitionParams p) {
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < W; j++) {
-    if (threadIdx.x + j * E_THREADS < ch.count) atomicAdd(&hist[fine_digit<NL, PACKED, CMP>(rk[j], p)], 1u);
+    if (threadIdx.x + j * NT < ch.count) atomicAdd(&hist[fine_digit<NL, PACKED, CMP>(rk[j], p)], 1u);
   }
   __syncthreads();
   unsigned long long *g = p.fine_hist + (uint64_t)ch.coarse_local * nf;
-  for (uint32_t b = threadIdx.x; b < nf; b += E_THREADS) {
+  for (uint32_t b = threadIdx.x; b < nf; b += NT) {
     const uint32_t c = hist[b];
     if (c) atomicAdd(&g[b], (unsigned long long)c);
   }
 }
 
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
-  constexpr int T = kPTile<NL>(), W = T / E_THREADS;
+__global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParams p) {
+  constexpr int NT = kPThreads<NL>(), T = kPTile<NL>(), W = T / NT;
+  static_assert(T % NT == 0 && NT % 64 == 0, "whole records per thread, whole waves");
   extern __shared__ __align__(16) unsigned char smem[];
   const uint32_t nf = 1u << p.fine_bits;
-  scatter_clear((uint32_t *)smem, nf);
+  scatter_clear<NT>((uint32_t *)smem, nf);
   uint32_t c;
   if (!xcd_chunk(p, c)) return;  // no chunk left in this workgroup's XCD class (uniform: before any barrier)
   const SChunk ch = chunk_of<T>(p, c);
@@ -1539,7 +1544,7 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
       (1ull << (EXT_BITS + (NL == 1 ? 2 * p.k : RecKind<NL, CMP>::lw(p.k)) - p.coarse_bits - p.fine_bits)) - 1;
 #pragma unroll
   for (int j = 0; j < W; j++) {
-    inf[j] = (threadIdx.x + j * E_THREADS < ch.count)
+    inf[j] = (threadIdx.x + j * NT < ch.count)
                  ? ((1u << 31) | (re[j] << 16) | fine_digit<NL, PACKED, CMP>(rk[j], p))
                  : 0u;
     if (CMP) rk[j][0] &= cmask;
@@ -1553,9 +1558,9 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
   unsigned long long *cur = p.fine_cursor + (uint64_t)ch.coarse_local * nf;
   constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C32 : (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
   if (kPStaged)
-    scatter_staged<NL, PACKED, W, SF>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
+    scatter_staged<NL, PACKED, W, SF, NT>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
   else
-    scatter_regs<NL, PACKED, W, SF>(rk, inf, nf, smem, cur, 1, p.out, lim, p.err);
+    scatter_regs<NL, PACKED, W, SF, NT>(rk, inf, nf, smem, cur, 1, p.out, lim, p.err);
 }
 
 // Distinct-key sketch (HyperLogLog, SKETCH_M registers) over the records of one coarse bucket, from which
@@ -1565,12 +1570,12 @@ __global__ __launch_bounds__(E_THREADS) void k_part_scatter(PartitionParams p) {
 // It also counts the extension adds of these records (the LDS op mix of k_count, reported in the stats as
 // a sample of the whole).
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigned int *hll) {
-  constexpr int T = kPTile<NL>(), W = T / E_THREADS;
+__global__ __launch_bounds__(kPThreads<NL>()) void k_sketch(PartitionParams p, unsigned int *hll) {
+  constexpr int NT = kPThreads<NL>(), T = kPTile<NL>(), W = T / NT;
   __shared__ unsigned int reg[SKETCH_M];
   __shared__ unsigned int s_ext;
   if (threadIdx.x == 0) s_ext = 0;
-  for (int i = threadIdx.x; i < SKETCH_M; i += E_THREADS) reg[i] = 0;
+  for (int i = threadIdx.x; i < SKETCH_M; i += NT) reg[i] = 0;
   const SChunk ch = chunk_of<T>(p, blockIdx.x);
   const PlaneSet src = p.srcs[ch.src];
   uint64_t rk[W][NL];
@@ -1581,7 +1586,7 @@ __global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigne
   uint32_t ext_adds = 0;
 #pragma unroll
   for (int j = 0; j < W; j++) {
-    if (threadIdx.x + j * E_THREADS >= ch.count) continue;
+    if (threadIdx.x + j * NT >= ch.count) continue;
     ext_adds += (uint32_t)(((re[j] >> 3) & 7u) < 4u) + (uint32_t)((re[j] & 7u) < 4u);
     uint64_t h = 0x9E3779B97F4A7C15ull;
 #pragma unroll
@@ -1591,7 +1596,7 @@ __global__ __launch_bounds__(E_THREADS) void k_sketch(PartitionParams p, unsigne
   }
   atomicAdd(&s_ext, ext_adds);
   __syncthreads();
-  for (int i = threadIdx.x; i < SKETCH_M; i += E_THREADS)
+  for (int i = threadIdx.x; i < SKETCH_M; i += NT)
     if (reg[i]) atomicMax(&hll[i], reg[i]);
   if (threadIdx.x == 0 && s_ext) atomicAdd(&hll[SKETCH_M], s_ext);  // (one add per workgroup)
 }
@@ -1782,9 +1787,12 @@ constexpr int C_PROBE = MHMKC_CPROBE;
 #ifndef MHMKC_GS_M2
 #define MHMKC_GS_M2 2  // mixed two-word keys (the last word, 64-bit, is the one read): k = 63 count 9.32 -> 9.09 ms
 #endif
-template <int NL, bool C32, bool M2>
+#ifndef MHMKC_GS_MX
+#define MHMKC_GS_MX 4  // mixed three- and four-word keys
+#endif
+template <int NL, bool C32, bool M2, bool MX = false>
 constexpr int group_slots() {
-  return C32 ? MHMKC_GS_C : M2 ? MHMKC_GS_M2 : 4;
+  return C32 ? MHMKC_GS_C : M2 ? MHMKC_GS_M2 : MX ? MHMKC_GS_MX : 4;
 }
 
 // The last key words of one group (4 x u64: two ds_read_b128, the group 32-byte aligned; 2 x u64: one)
@@ -2113,7 +2121,7 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
   }
   __syncthreads();
   const uint64_t q0 = s_range[0], q1 = s_range[1];
-  constexpr int GS = group_slots<NL, RecKind<NL, CMP>::C32, RecKind<NL, CMP>::M2>();
+  constexpr int GS = group_slots<NL, RecKind<NL, CMP>::C32, RecKind<NL, CMP>::M2, RecKind<NL, CMP>::MX>();
   const int ng = t.cap / GS;
   const K *last = t.keys + (NL - 1) * t.cap;
   for (uint64_t q = q0 + tid; q < q1; q += C_THREADS) {
@@ -2279,7 +2287,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   constexpr int CB0 = NL == 2 ? MHMKC_CBATCH2 : MHMKC_CBATCH;
   constexpr int C_BATCH = CB0 < R ? CB0 : R;
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
-  constexpr int GS = group_slots<NL, RK::C32, RK::M2>();  // slots per probe group
+  constexpr int GS = group_slots<NL, RK::C32, RK::M2, RK::MX>();  // slots per probe group
   const int ng = t.cap / GS;
   const K *last = t.keys + (NL - 1) * t.cap;
   // cmp_group: compact keys from their top stored bits; mixed two-word keys from the low 16 bits of R' (the
@@ -3088,7 +3096,7 @@ static hipError_t do_part_hist(const PartitionParams &p, hipStream_t s) {
   const size_t lds = ((size_t)1 << p.fine_bits) * 4;
   hipError_t e = allow_lds(k_part_hist<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_part_hist<NL, PK, CMP><<<dim3(p.grid), dim3(E_THREADS), lds, s>>>(p);
+  k_part_hist<NL, PK, CMP><<<dim3(p.grid), dim3(kPThreads<NL>()), lds, s>>>(p);
   return hipGetLastError();
 }
 
@@ -3099,7 +3107,7 @@ static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
                               : scatter_lds_bytes(nf);
   hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
-  k_part_scatter<NL, PK, CMP><<<dim3(p.grid), dim3(E_THREADS), lds, s>>>(p);
+  k_part_scatter<NL, PK, CMP><<<dim3(p.grid), dim3(kPThreads<NL>()), lds, s>>>(p);
   return hipGetLastError();
 }
 
@@ -3186,7 +3194,7 @@ hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_
 
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_sketch(const PartitionParams &p, uint32_t n, unsigned int *hll, hipStream_t s) {
-  k_sketch<NL, PK, CMP><<<dim3(n), dim3(E_THREADS), 0, s>>>(p, hll);
+  k_sketch<NL, PK, CMP><<<dim3(n), dim3(kPThreads<NL>()), 0, s>>>(p, hll);
   return hipGetLastError();
 }
 

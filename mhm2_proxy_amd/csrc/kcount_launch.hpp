@@ -274,9 +274,25 @@ inline int tile_bases(int nl) {
 #define MHMKC_PTILE2 2048
 #endif
 #ifndef MHMKC_PTILE3
-#define MHMKC_PTILE3 MHMKC_PTILE2  // three- and four-word keys
+#define MHMKC_PTILE3 4096  // three-word keys
 #endif
-inline int chunk_records(int nl) { return nl == 1 ? MHMKC_PTILE1 : nl == 2 ? MHMKC_PTILE2 : MHMKC_PTILE3; }
+// partition workgroup threads; three- and four-word keys take longer chunks with more threads (the chunk's runs
+// per fine bucket grow, the LDS per wave stays)
+#ifndef MHMKC_PTHREADS1
+#define MHMKC_PTHREADS1 E_THREADS
+#endif
+#ifndef MHMKC_PTHREADS2
+#define MHMKC_PTHREADS2 E_THREADS
+#endif
+#ifndef MHMKC_PTHREADS3
+#define MHMKC_PTHREADS3 512
+#endif
+#ifndef MHMKC_PTILE4
+#define MHMKC_PTILE4 3072  // four-word keys (LDS: the staged chunk + 2048 bins' counters fit 160 KB)
+#endif
+inline int chunk_records(int nl) {
+  return nl == 1 ? MHMKC_PTILE1 : nl == 2 ? MHMKC_PTILE2 : nl == 3 ? MHMKC_PTILE3 : MHMKC_PTILE4;
+}
 // Mixed two-word records (33 <= k <= 63) as one 16-byte record in the first of their two planes' space, in the
 // coarse slabs and the fine buckets (0: two u64 planes)
 #ifndef MHMKC_M2AOS
