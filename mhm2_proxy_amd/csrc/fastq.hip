@@ -487,6 +487,16 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // order and the qualities of pairs with an N go to the scratch for k_fq_merge_pack.
 constexpr int MG_WAVES = 4;
 constexpr int MG_MAXL = 2048;  // > FQ_MAX_LINE + 4 (unaligned 4-byte reads past a line stay inside)
+// Pairs whose mates are both at most MG_SHORT - 8 bases (every short-read run) go through an instance with
+// MG_SHORT-byte staging: 11 KB of LDS per workgroup instead of 42 KB, so MHMKC_MG_OCC workgroups per CU instead of
+// three hide each other's LDS and shuffle round trips; a second launch of the 2048-byte instance takes the others.
+#ifndef MHMKC_MG_SHORT
+#define MHMKC_MG_SHORT 512
+#endif
+#ifndef MHMKC_MG_OCC
+#define MHMKC_MG_OCC 6
+#endif
+constexpr int MG_SHORT = MHMKC_MG_SHORT;
 
 __device__ __forceinline__ uint32_t lds_u32(const char *p) {  // 4 bytes from any LDS byte address
   const uintptr_t a = (uintptr_t)p;
@@ -547,15 +557,18 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(64 * MG_WAVES, 3) void k_fq_merge(const char *text, const PairDesc *desc, uint64_t n_pairs,
-                                                             const unsigned long long *rec_offs, int qual_offset,
-                                                             char *scratch, uint32_t *pair_info,
-                                                             unsigned long long *out_len, unsigned long long *err,
-                                                             unsigned long long *stats) {
-  __shared__ __align__(16) char lds[MG_WAVES][4][MG_MAXL + 16];
+// MAXL < MG_MAXL: the pairs with a mate longer than MAXL - 8 are left to the MG_MAXL instance, which (with
+// long_only) takes only those.
+template <int MAXL>
+__global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) void k_fq_merge(
+    const char *text, const PairDesc *desc, uint64_t n_pairs, const unsigned long long *rec_offs, int qual_offset,
+    char *scratch, uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
+    unsigned long long *stats, bool long_only) {
+  constexpr uint32_t LONG = (uint32_t)MG_SHORT - 8;  // longest mate of a short pair
+  __shared__ __align__(16) char lds[MG_WAVES][4][MAXL + 16];
   // the bases again as 4-bit codes, 16 per word (A C G T N = 0..4, any other mate-1 character 15: it equals
   // no mate-2 base), for the fast filter's 16-base compares
-  __shared__ __align__(16) uint64_t nib[MG_WAVES][2][MG_MAXL / 16 + 4];
+  __shared__ __align__(16) uint64_t nib[MG_WAVES][2][MAXL / 16 + 4];
   // Q2Perror in LDS: a mismatch's table reads are divergent, and from constant memory each was a memory round
   // trip on the scan's critical path
   __shared__ double q2p[81];
@@ -570,13 +583,16 @@ __global__ __launch_bounds__(64 * MG_WAVES, 3) void k_fq_merge(const char *text,
   const uint64_t n_waves = (uint64_t)gridDim.x * MG_WAVES;
   if (blockIdx.x == 0 && threadIdx.x == 0) out_len[2 * n_pairs] = 0;  // the scan's last element
   for (uint64_t p = (uint64_t)blockIdx.x * MG_WAVES + w; p < n_pairs; p += n_waves) {
+    const PairDesc d = desc[p];
+    const bool is_long = d.L1 != ~0u && (d.L1 > LONG || d.L2 > LONG);
+    if (long_only && !is_long) continue;
     if (lane == 0) {
       pair_info[p] = 0;
       out_len[2 * p] = 0;
       out_len[2 * p + 1] = 0;
     }
-    const PairDesc d = desc[p];
     if (d.L1 == ~0u) continue;  // (its error is reported)
+    if (MAXL < MG_MAXL && is_long) continue;  // (the MG_MAXL instance's)
     const int L1 = (int)d.L1, L2 = (int)d.L2;
     const char *s1 = text + d.s1, *tq1 = text + d.q1, *s2 = text + d.s2, *tq2 = text + d.q2;
     // staging, four bytes per lane and step (one load round trip for reads up to 256 bases); a step may read
@@ -911,8 +927,13 @@ hipError_t launch_fq_merge(const char *text, uint64_t n, const unsigned long lon
   }
   // grid-stride over the pairs, one wave each; enough waves to fill the chip several times over
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n_pairs + MG_WAVES - 1) / MG_WAVES, 16384));
-  k_fq_merge<<<dim3((unsigned)blocks), dim3(64 * MG_WAVES), 0, s>>>(text, desc, n_pairs, rec_offs, qual_offset,
-                                                                      scratch, pair_info, out_len, err, stats);
+  k_fq_merge<MG_SHORT><<<dim3((unsigned)blocks), dim3(64 * MG_WAVES), 0, s>>>(
+      text, desc, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats, false);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || MG_SHORT >= MG_MAXL) return e;
+  // the long pairs (a pass over the descriptors when there are none)
+  k_fq_merge<MG_MAXL><<<dim3((unsigned)std::min<uint64_t>(blocks, 2048)), dim3(64 * MG_WAVES), 0, s>>>(
+      text, desc, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats, true);
   return hipGetLastError();
 }
 

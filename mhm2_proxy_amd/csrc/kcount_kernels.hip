@@ -28,7 +28,7 @@ constexpr int kTile() {  // bases per extract tile
 }
 template <int NL>
 constexpr int kEThreads() {  // threads per extract workgroup
-  return NL == 1 ? MHMKC_ETHREADS1 : NL == 2 ? MHMKC_ETHREADS2 : MHMKC_ETHREADS3;
+  return NL == 1 ? MHMKC_ETHREADS1 : NL == 2 ? MHMKC_ETHREADS2 : NL == 3 ? MHMKC_ETHREADS3 : MHMKC_ETHREADS4;
 }
 template <int NL>
 constexpr int kPTile() {  // records per partition chunk (kPThreads threads)

@@ -264,7 +264,10 @@ inline int tile_bases(int nl) {
 #define MHMKC_ETHREADS2 E_THREADS
 #endif
 #ifndef MHMKC_ETHREADS3
-#define MHMKC_ETHREADS3 MHMKC_ETHREADS2  // three- and four-word keys
+#define MHMKC_ETHREADS3 MHMKC_ETHREADS2  // three-word keys
+#endif
+#ifndef MHMKC_ETHREADS4
+#define MHMKC_ETHREADS4 512  // four-word keys: 2048-base tiles over 512 threads (k = 99 extract 13.23 -> 12.83 ms)
 #endif
 // records per partition chunk (one E_THREADS workgroup)
 #ifndef MHMKC_PTILE1
@@ -305,9 +308,15 @@ inline int chunk_records(int nl) {
 #ifndef MHMKC_CAP2
 #define MHMKC_CAP2 4000
 #endif
+#ifndef MHMKC_CAP3
+#define MHMKC_CAP3 3264
+#endif
+#ifndef MHMKC_CAP4
+#define MHMKC_CAP4 2752
+#endif
 __host__ __device__ constexpr int count_key_bytes(bool cmp) { return cmp ? 4 : 8; }
 __host__ __device__ constexpr int count_cap(int nl, bool cmp = false) {
-  return ((cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? MHMKC_CAP2 : nl == 3 ? 3264 : 2752) / C_SPLIT) & ~3;
+  return ((cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? MHMKC_CAP2 : nl == 3 ? MHMKC_CAP3 : MHMKC_CAP4) / C_SPLIT) & ~3;
 }
 __host__ __device__ constexpr size_t count_table_bytes(int nl, bool cmp = false) {
   return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 192;

@@ -351,7 +351,11 @@ struct mhmkc {
 };
 
 // Fine partition target: distinct keys per fine bucket <= FINE_LOAD x LDS table slots.
-constexpr double FINE_LOAD = 0.7;
+// (MHMKC_FINE_LOAD overrides it, for A/B runs.)
+static const double FINE_LOAD = [] {
+  const char *env = getenv("MHMKC_FINE_LOAD");
+  return env && atof(env) > 0 ? atof(env) : 0.7;
+}();
 // Load of the LDS table k_count uses per bucket, after the fine partition is fixed (0 = the whole table, the
 // default: a table fitted to 0.6-0.8 of the estimate was measured slower, 6.28 -> 7.14-10.2 ms at C2, because
 // the home-group hit rate falls with the load faster than the per-slot clear and finalize work does).

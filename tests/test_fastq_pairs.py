@@ -119,6 +119,30 @@ def test_gpu_merge_equals_oracle(variant):
 
 
 @pytest.mark.gpu
+def test_gpu_merge_mixed_lengths():
+    """Short and long pairs in one batch: mates around the short-pair limit of k_fq_merge's small-staging instance
+    (504 bases, fastq.hip MG_SHORT - 8; unequal mate lengths, so some pairs have one mate on each side), interleaved
+    with 150-base and 900-base pairs. The long ones go through the second, 2048-byte instance."""
+    import mhm2_proxy_amd as m
+    parts = [c.paired_fastq_text(1500, seed=21),
+             c.paired_fastq_text(300, seed=22, read_len=506, frag_mean=800, frag_sd=120),
+             c.paired_fastq_text(300, seed=23, read_len=900, frag_mean=1500, frag_sd=300),
+             c.paired_fastq_text(300, seed=24, read_len=503, frag_mean=700, frag_sd=100),
+             c.paired_fastq_text(800, seed=25)]
+    t = b"".join(parts)
+    pb, po, pst = O.merge_fastq(t, 33)
+    with m.KmerCounter(21, device=0) as cnt:
+        cnt.add_fastq_pairs(t)
+        gb, go = cnt.fastq_packed()
+        st = cnt.stats()
+    assert len(go) == len(po) and (go == po).all()
+    assert (gb == pb).all()
+    for key in ("pairs", "merged", "ambiguous", "overlap_bases"):
+        assert st["fq_" + key] == pst[key], key
+    assert pst["merged"] > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("k", [21, 63])
 def test_gpu_merged_reads_count_equals_oracle(k):
     """End to end: paired FASTQ -> device merge -> count == the oracle's count of the oracle's merge."""
