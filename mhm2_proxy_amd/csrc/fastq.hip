@@ -437,11 +437,28 @@ struct PairDesc {
   uint32_t L1, L2;
 };
 
+// Pairs whose mates are both at most MG_LONG bases (every short-read run) go through a k_fq_merge instance with
+// MG_SHORT-byte staging: 11 KB of LDS per workgroup instead of 42 KB, so MHMKC_MG_OCC workgroups per CU instead of
+// three hide each other's LDS and shuffle round trips. k_fq_pair_prep lists the other pairs (after the
+// descriptors: a counter, then the pair indices), which a launch of the 2048-byte instance takes.
+#ifndef MHMKC_MG_SHORT
+#define MHMKC_MG_SHORT 512
+#endif
+#ifndef MHMKC_MG_OCC
+#define MHMKC_MG_OCC 6
+#endif
+constexpr int MG_SHORT = MHMKC_MG_SHORT;
+constexpr uint32_t MG_LONG = (uint32_t)MG_SHORT - 8;  // longest mate of a short pair
+__host__ __device__ inline uint32_t *long_pairs(void *desc_buf, uint64_t n_pairs) {  // [counter, 15 pad, list]
+  return (uint32_t *)((char *)desc_buf + (((size_t)n_pairs * sizeof(PairDesc) + 63) & ~(size_t)63));
+}
+
 // One lane per pair: both records' lines and the name checks (:320-321). Many lanes in flight hide the chains
 // of dependent loads that name parsing is; the merge kernel then starts from one descriptor load.
 __global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_prep(const char *text, uint64_t n,
                                                               const unsigned long long *line_end, uint64_t n_pairs,
-                                                              PairDesc *desc, unsigned long long *err) {
+                                                              PairDesc *desc, uint32_t *long_list,
+                                                              unsigned long long *err) {
   const uint64_t p = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x;
   if (p >= n_pairs) return;
   PairDesc d{0, 0, 0, 0, ~0u, 0};
@@ -451,9 +468,15 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_prep(const char *text, u
   if (fq_rec(text, n, line_end, 2 * p, a) && fq_rec(text, n, line_end, 2 * p + 1, b) &&
       fq_norm(text, a.idb, a.idte, pb1, pe1, l1) && fq_norm(text, b.idb, b.idte, pb2, pe2, l2)) {
     bool same = pe1 - pb1 == pe2 - pb2;
-    for (uint64_t i = 0; same && i < pe1 - pb1; i++) {
-      char x = text[pb1 + i], y = text[pb2 + i];
-      same = (x == ' ' ? '_' : x) == (y == ' ' ? '_' : y);
+    // four characters per step (the bytes past a name are the rest of its record): spaces read as '_' on both sides
+    for (uint64_t i = 0; same && i < pe1 - pb1; i += 4) {
+      const uint64_t left = pe1 - pb1 - i;
+      const uint32_t valid = left >= 4 ? ~0u : (1u << (8 * left)) - 1;
+      uint32_t x = load4(text + pb1, (uint32_t)i), y = load4(text + pb2, (uint32_t)i);
+      const uint32_t sx = (zero_bytes(x ^ 0x20202020u) >> 7) * 0xffu, sy = (zero_bytes(y ^ 0x20202020u) >> 7) * 0xffu;
+      x = (x & ~sx) | (0x5f5f5f5fu & sx);
+      y = (y & ~sy) | (0x5f5f5f5fu & sy);
+      same = ((x ^ y) & valid) == 0;
     }
     if (!same) {
       fq_fail(err, 2 * p + 1, FQ_E_PAIR_NAME);
@@ -461,6 +484,7 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_prep(const char *text, u
       fq_fail(err, 2 * p + 1, FQ_E_PAIR_NUM);
     } else {
       d = PairDesc{a.sb, a.qb, b.sb, b.qb, a.L, b.L};
+      if (a.L > MG_LONG || b.L > MG_LONG) long_list[16 + atomicAdd(long_list, 1u)] = (uint32_t)p;
     }
   }
   desc[p] = d;
@@ -487,16 +511,6 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // order and the qualities of pairs with an N go to the scratch for k_fq_merge_pack.
 constexpr int MG_WAVES = 4;
 constexpr int MG_MAXL = 2048;  // > FQ_MAX_LINE + 4 (unaligned 4-byte reads past a line stay inside)
-// Pairs whose mates are both at most MG_SHORT - 8 bases (every short-read run) go through an instance with
-// MG_SHORT-byte staging: 11 KB of LDS per workgroup instead of 42 KB, so MHMKC_MG_OCC workgroups per CU instead of
-// three hide each other's LDS and shuffle round trips; a second launch of the 2048-byte instance takes the others.
-#ifndef MHMKC_MG_SHORT
-#define MHMKC_MG_SHORT 512
-#endif
-#ifndef MHMKC_MG_OCC
-#define MHMKC_MG_OCC 6
-#endif
-constexpr int MG_SHORT = MHMKC_MG_SHORT;
 
 __device__ __forceinline__ uint32_t lds_u32(const char *p) {  // 4 bytes from any LDS byte address
   const uintptr_t a = (uintptr_t)p;
@@ -557,14 +571,13 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// MAXL < MG_MAXL: the pairs with a mate longer than MAXL - 8 are left to the MG_MAXL instance, which (with
-// long_only) takes only those.
+// MAXL < MG_MAXL: the pairs with a mate longer than MG_LONG are left to the MG_MAXL instance, which (given
+// long_list) takes only the listed pairs.
 template <int MAXL>
 __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) void k_fq_merge(
     const char *text, const PairDesc *desc, uint64_t n_pairs, const unsigned long long *rec_offs, int qual_offset,
     char *scratch, uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
-    unsigned long long *stats, bool long_only) {
-  constexpr uint32_t LONG = (uint32_t)MG_SHORT - 8;  // longest mate of a short pair
+    unsigned long long *stats, const uint32_t *long_list) {
   __shared__ __align__(16) char lds[MG_WAVES][4][MAXL + 16];
   // the bases again as 4-bit codes, 16 per word (A C G T N = 0..4, any other mate-1 character 15: it equals
   // no mate-2 base), for the fast filter's 16-base compares
@@ -582,17 +595,18 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   uint64_t merged = 0, ambiguous = 0, ov_bases = 0;
   const uint64_t n_waves = (uint64_t)gridDim.x * MG_WAVES;
   if (blockIdx.x == 0 && threadIdx.x == 0) out_len[2 * n_pairs] = 0;  // the scan's last element
-  for (uint64_t p = (uint64_t)blockIdx.x * MG_WAVES + w; p < n_pairs; p += n_waves) {
+  const uint64_t n_items = long_list ? long_list[0] : n_pairs;
+  for (uint64_t it = (uint64_t)blockIdx.x * MG_WAVES + w; it < n_items; it += n_waves) {
+    const uint64_t p = long_list ? long_list[16 + it] : it;
     const PairDesc d = desc[p];
-    const bool is_long = d.L1 != ~0u && (d.L1 > LONG || d.L2 > LONG);
-    if (long_only && !is_long) continue;
+    const bool is_long = d.L1 != ~0u && (d.L1 > MG_LONG || d.L2 > MG_LONG);
+    if (MAXL < MG_MAXL && is_long) continue;  // (listed for the MG_MAXL instance, which initialises its outputs)
     if (lane == 0) {
       pair_info[p] = 0;
       out_len[2 * p] = 0;
       out_len[2 * p + 1] = 0;
     }
     if (d.L1 == ~0u) continue;  // (its error is reported)
-    if (MAXL < MG_MAXL && is_long) continue;  // (the MG_MAXL instance's)
     const int L1 = (int)d.L1, L2 = (int)d.L2;
     const char *s1 = text + d.s1, *tq1 = text + d.q1, *s2 = text + d.s2, *tq2 = text + d.q2;
     // staging, four bytes per lane and step (one load round trip for reads up to 256 bases); a step may read
@@ -803,16 +817,41 @@ __global__ __launch_bounds__(64 * MG_WAVES) void k_fq_merge_pack(const char *tex
                                                                   uint8_t *out, unsigned long long *err) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int max_match_qual = 41 + qual_offset;
-  for (uint64_t p = (uint64_t)blockIdx.x * MG_WAVES + w; p < n_pairs; p += (uint64_t)gridDim.x * MG_WAVES) {
-    const PairDesc d = desc[p];
+  const uint64_t stride = (uint64_t)gridDim.x * MG_WAVES;
+  // The next pair's descriptor, verdict and offsets are loaded while this pair is packed: the text loads of a
+  // pair are then its only global round trip before the stores.
+  uint64_t p = (uint64_t)blockIdx.x * MG_WAVES + w;
+  PairDesc dn{0, 0, 0, 0, ~0u, 0};
+  uint32_t infon = 0;
+  unsigned long long ro0n = 0, ro1n = 0, oo0n = 0, oo1n = 0;
+  if (p < n_pairs) {
+    dn = desc[p];
+    infon = pair_info[p];
+    ro0n = rec_offs[2 * p];
+    ro1n = rec_offs[2 * p + 1];
+    oo0n = out_offs[2 * p];
+    oo1n = out_offs[2 * p + 1];
+  }
+  for (; p < n_pairs; p += stride) {
+    const PairDesc d = dn;
+    const uint32_t info = infon;
+    const unsigned long long ro0 = ro0n, ro1 = ro1n, oo0 = oo0n, oo1 = oo1n;
+    const uint64_t pn = p + stride;
+    if (pn < n_pairs) {
+      dn = desc[pn];
+      infon = pair_info[pn];
+      ro0n = rec_offs[2 * pn];
+      ro1n = rec_offs[2 * pn + 1];
+      oo0n = out_offs[2 * pn];
+      oo1n = out_offs[2 * pn + 1];
+    }
     if (d.L1 == ~0u) continue;
-    const uint32_t info = pair_info[p];
     const int ov = (int)(info & ~MP_HASN) - 1;  // -1: not merged
     const bool hasN = (info & MP_HASN) != 0;
     const int L1 = (int)d.L1, L2 = (int)d.L2;
     const char *s1 = text + d.s1, *tq1 = text + d.q1, *s2 = text + d.s2, *tq2 = text + d.q2;
-    const char *cq1 = scratch + rec_offs[2 * p], *crq2 = scratch + rec_offs[2 * p + 1];
-    uint8_t *dst0 = out + out_offs[2 * p], *dst1 = out + out_offs[2 * p + 1];
+    const char *cq1 = scratch + ro0, *crq2 = scratch + ro1;
+    uint8_t *dst0 = out + oo0, *dst1 = out + oo1;
     const int Lo0 = ov >= 0 ? L1 + L2 - ov : L1, st = ov >= 0 ? L1 - ov : L1;
     bool bad = false;
     for (int x0 = 4 * lane; x0 < Lo0; x0 += 256) {
@@ -912,28 +951,31 @@ hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long l
   return hipGetLastError();
 }
 
-size_t fq_pair_desc_bytes(uint64_t n_pairs) { return (size_t)n_pairs * sizeof(PairDesc) + 64; }
+size_t fq_pair_desc_bytes(uint64_t n_pairs) {  // the descriptors, then the long-pair counter and list
+  return (((size_t)n_pairs * sizeof(PairDesc) + 63) & ~(size_t)63) + 64 + (size_t)n_pairs * 4 + 64;
+}
 
 hipError_t launch_fq_merge(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
                            const unsigned long long *rec_offs, int qual_offset, char *scratch, void *desc_buf,
                            uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
                            unsigned long long *stats, hipStream_t s) {
   PairDesc *desc = (PairDesc *)desc_buf;
+  uint32_t *long_list = long_pairs(desc_buf, n_pairs);
+  hipError_t e = hipMemsetAsync(long_list, 0, 4, s);
+  if (e != hipSuccess) return e;
   if (n_pairs) {
     k_fq_pair_prep<<<dim3((unsigned)((n_pairs + FQ_THREADS - 1) / FQ_THREADS)), dim3(FQ_THREADS), 0, s>>>(
-        text, n, line_end, n_pairs, desc, err);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+        text, n, line_end, n_pairs, desc, long_list, err);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // grid-stride over the pairs, one wave each; enough waves to fill the chip several times over
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n_pairs + MG_WAVES - 1) / MG_WAVES, 16384));
   k_fq_merge<MG_SHORT><<<dim3((unsigned)blocks), dim3(64 * MG_WAVES), 0, s>>>(
-      text, desc, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats, false);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || MG_SHORT >= MG_MAXL) return e;
-  // the long pairs (a pass over the descriptors when there are none)
-  k_fq_merge<MG_MAXL><<<dim3((unsigned)std::min<uint64_t>(blocks, 2048)), dim3(64 * MG_WAVES), 0, s>>>(
-      text, desc, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats, true);
+      text, desc, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats, nullptr);
+  if ((e = hipGetLastError()) != hipSuccess || MG_SHORT >= MG_MAXL) return e;
+  // the listed long pairs (the waves of an empty list exit at once)
+  k_fq_merge<MG_MAXL><<<dim3((unsigned)std::min<uint64_t>(blocks, 1024)), dim3(64 * MG_WAVES), 0, s>>>(
+      text, desc, n_pairs, rec_offs, qual_offset, scratch, pair_info, out_len, err, stats, long_list);
   return hipGetLastError();
 }
 
