@@ -447,6 +447,9 @@ struct PairDesc {
 #ifndef MHMKC_MG_OCC
 #define MHMKC_MG_OCC 6
 #endif
+#ifndef MHMKC_MG_OPAQUE
+#define MHMKC_MG_OPAQUE 1
+#endif
 constexpr int MG_SHORT = MHMKC_MG_SHORT;
 constexpr uint32_t MG_LONG = (uint32_t)MG_SHORT - 8;  // longest mate of a short pair
 __host__ __device__ inline uint32_t *long_pairs(void *desc_buf, uint64_t n_pairs) {  // [counter, 15 pad, list]
@@ -565,6 +568,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
   }
   return v;
 }
+// The lane index, recomputed where it is called: the compiler cannot hoist the lane-derived LDS addresses of a
+// loop body built from it out of the loop (in k_fq_merge's pair loop they took a dozen VGPRs for the whole
+// kernel and pushed it into spills at 80 VGPRs).
+__device__ __forceinline__ int opaque_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -597,6 +608,9 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   if (blockIdx.x == 0 && threadIdx.x == 0) out_len[2 * n_pairs] = 0;  // the scan's last element
   const uint64_t n_items = long_list ? long_list[0] : n_pairs;
   for (uint64_t it = (uint64_t)blockIdx.x * MG_WAVES + w; it < n_items; it += n_waves) {
+#if MHMKC_MG_OPAQUE
+    const int lane = opaque_lane();
+#endif
     const uint64_t p = long_list ? long_list[16 + it] : it;
     const PairDesc d = desc[p];
     const bool is_long = d.L1 != ~0u && (d.L1 > MG_LONG || d.L2 > MG_LONG);

@@ -2230,6 +2230,15 @@ __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, c
 }
 
 
+#ifndef MHMKC_COPAQUE
+#define MHMKC_COPAQUE 0
+#endif
+__device__ __forceinline__ int count_opaque_tid() {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+  return t;
+}
+
 template <int NL, bool PACKED, bool CMP>
 __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // A capped fine bucket overflowed in k_part_scatter (same stream, earlier launch): its cursor, which is
@@ -2274,8 +2283,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
 
+#if MHMKC_COPAQUE  // (A/B) the thread index recomputed at every use: nothing derived from it is hoisted out of the
+                   // bucket loop to live in registers across it
+#define tid (count_opaque_tid())
+#define lane (count_opaque_tid() & 63)
+#define wid (count_opaque_tid() >> 6)
+#else
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
+#endif
   const uint64_t low_mask = (1ull << (EXT_BITS + p.hbits)) - 1;
 
   constexpr int R = count_rpt<NL>();
@@ -3042,6 +3058,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     atomicMax(&p.stats[STAT_MAXBUCKET], my_maxb);
   }
 }
+#if MHMKC_COPAQUE
+#undef tid
+#undef lane
+#undef wid
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // launchers
