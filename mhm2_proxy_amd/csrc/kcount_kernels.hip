@@ -2230,13 +2230,24 @@ __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, c
 }
 
 
-#ifndef MHMKC_COPAQUE
-#define MHMKC_COPAQUE 0
+// k_count's thread index. For NL >= MHMKC_COPAQUE_NL it is recomputed through an opaque move at every use, so that
+// nothing derived from it is hoisted out of the bucket loop to live in registers across it: at NL = 4 that took
+// 9 spilled VGPRs to none (127 -> 124) and the count at k = 99 11.79 -> 11.05 ms; at NL = 1-3 it measured 1-3 %
+// slower (the recomputed addresses cost more than the registers they free).
+#ifndef MHMKC_COPAQUE_NL
+#define MHMKC_COPAQUE_NL 4
 #endif
 __device__ __forceinline__ int count_opaque_tid() {
   int t;
   asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
   return t;
+}
+template <int NL>
+__device__ __forceinline__ int count_tid() {
+  if constexpr (NL >= MHMKC_COPAQUE_NL)
+    return count_opaque_tid();
+  else
+    return (int)threadIdx.x;
 }
 
 template <int NL, bool PACKED, bool CMP>
@@ -2283,15 +2294,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
 
-#if MHMKC_COPAQUE  // (A/B) the thread index recomputed at every use: nothing derived from it is hoisted out of the
-                   // bucket loop to live in registers across it
-#define tid (count_opaque_tid())
-#define lane (count_opaque_tid() & 63)
-#define wid (count_opaque_tid() >> 6)
-#else
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-#endif
+#define tid (count_tid<NL>())  // (see count_tid; #undef after the kernel)
+#define lane (count_tid<NL>() & 63)
+#define wid (count_tid<NL>() >> 6)
   const uint64_t low_mask = (1ull << (EXT_BITS + p.hbits)) - 1;
 
   constexpr int R = count_rpt<NL>();
@@ -3058,11 +3063,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     atomicMax(&p.stats[STAT_MAXBUCKET], my_maxb);
   }
 }
-#if MHMKC_COPAQUE
 #undef tid
 #undef lane
 #undef wid
-#endif
 
 // ------------------------------------------------------------------------------------------------
 // launchers
