@@ -325,6 +325,7 @@ def main():
     local = local_dev
 
     import mhm2_proxy_amd as m
+    from mhm2_proxy_amd.build import source_build_id
 
     cf = dict(CONFIGS[args.config])
     k = args.k or cf["k"]
@@ -592,6 +593,8 @@ def main():
                           if per_step.get("exchange") else None}
                          if world > 1 and st else None),
             "synth_seconds": round(gen_s, 2),
+            "build_id": m._native.build_id(),
+            "build_id_matches_tree": m._native.build_id() == source_build_id(),
         }
         if args.input == "fastq-file":
             line["config"]["workload"] = line["config"]["workload"].replace("synthetic reads", "FASTQ records")

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 10
+#define MHMKC_ABI_VERSION 11
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -313,6 +313,12 @@ const char *mhmkc_last_error(mhmkc_t h);
 
 /* Library ABI version (MHMKC_ABI_VERSION). */
 int mhmkc_abi_version(void);
+
+/* Build id of this library: the first 16 hex digits of the SHA-256 of the sources it was compiled from
+ * (mhm2_proxy_amd/build.py: LIB_DEPS, paths and contents), fixed at compile time. A loader compares it with the id
+ * of the tree it runs from to know that the binary it mapped is the one those sources make ("unknown": built
+ * without build.py). Not part of the reference (provenance of the prebuilt library only). */
+const char *mhmkc_build_id(void);
 
 #ifdef __cplusplus
 }

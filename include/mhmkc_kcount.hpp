@@ -228,6 +228,18 @@ class KmerMap {
   using const_iterator = iter<true>;
 
   KmerMap() = default;
+  // not copyable (two buffers of up to tens of GB); a move leaves the source an empty map that can be used again
+  KmerMap(const KmerMap &) = delete;
+  KmerMap &operator=(const KmerMap &) = delete;
+  KmerMap(KmerMap &&o) noexcept { swap(o); }
+  KmerMap &operator=(KmerMap &&o) noexcept {
+    if (this != &o) {
+      KmerMap t;
+      t.swap(o);
+      swap(t);
+    }
+    return *this;
+  }
   size_t size() const { return size_; }
   bool empty() const { return size_ == 0; }
   size_t bucket_count() const { return cap_; }
@@ -301,18 +313,28 @@ class KmerMap {
   }
 
  private:
-  // tags and slots live in 2 MB-aligned anonymous memory advised for transparent huge pages: a table larger than the
-  // caches is touched at random, and with 4 KB pages every probe would also miss the TLB
+  // tags and slots of a large map live in 2 MB-aligned anonymous memory advised for transparent huge pages: a table
+  // larger than the caches is touched at random, and with 4 KB pages every probe would also miss the TLB. Below 1 MB
+  // (a small map: a test, a tiny rank share) plain zeroed heap memory.
   struct Free {
-    size_t bytes = 0;
+    size_t bytes = 0;  // 0: from calloc
     void operator()(void *p) const {
-      if (p) munmap(p, bytes);
+      if (!p) return;
+      if (bytes)
+        munmap(p, bytes);
+      else
+        std::free(p);
     }
   };
   template <typename T>
   using Buf = std::unique_ptr<T[], Free>;
   template <typename T>
   static Buf<T> alloc(size_t n) {
+    if (n * sizeof(T) < (1u << 20)) {
+      void *p = std::calloc(n ? n : 1, sizeof(T));
+      if (!p) die("KmerMap: out of memory");
+      return Buf<T>((T *)p, Free{0});
+    }
     const size_t bytes = ((n * sizeof(T)) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
     void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (p == MAP_FAILED) die("KmerMap: out of memory");

@@ -40,6 +40,7 @@ ABI_SYMBOLS = [
     "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_add_ctgs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_fetch_ordered",
     "mhmkc_device_output",
     "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
+    "mhmkc_build_id",
     "mhmkc_add_fastq", "mhmkc_add_fastq_device", "mhmkc_add_fastq_pairs", "mhmkc_add_fastq_pairs_device",
     "mhmkc_add_fastq_file", "mhmkc_add_fastq_pairs_file",
     "mhmkc_fastq_packed", "mhmkc_fastq_fetch",
@@ -199,12 +200,19 @@ def lib() -> C.CDLL:
     L.mhmkc_last_error.argtypes = [VP]
     L.mhmkc_last_error.restype = C.c_char_p
     L.mhmkc_abi_version.argtypes = []
+    L.mhmkc_build_id.argtypes = []
+    L.mhmkc_build_id.restype = C.c_char_p
     L.mhmkc_wait_stream.argtypes = [VP, VP]
     L.mhmkc_set_dmin_thres.argtypes = [VP, C.c_int32]
     L.mhmkc_set_transport.argtypes = [VP, P(MhmkcTransport)]
     L.mhmkc_minimizer_hashes.argtypes = [VP, VP, U64, C.c_int32, C.c_int32, VP]
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """The build id compiled into the loaded libmhmkc.so (include/mhmkc.h mhmkc_build_id)."""
+    return lib().mhmkc_build_id().decode()
 
 
 def synth() -> C.CDLL:

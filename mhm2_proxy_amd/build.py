@@ -5,10 +5,12 @@
   oracle/liboracle.so (+ _ref/)     make -C oracle: the CPU checker (test infrastructure only)
   tools/bin/kmermap_fill            g++: KmerMap materialisation timing of the C++ adapter (bench.py)
 
-Incremental: a target is rebuilt only when one of its sources is newer.
+Incremental: a target is rebuilt only when one of its sources is newer; libmhmkc.so also when the build id it
+carries (the SHA-256 of its sources, mhmkc_build_id) is not the tree's, whatever the file times say.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -32,6 +34,29 @@ FILL = ROOT / "tools" / "bin" / "kmermap_fill"
 FILL_DEPS = [ROOT / "tools" / "cpp" / "kmermap_fill.cpp", ROOT / "include" / "mhmkc_kcount.hpp", ROOT / "include" / "mhmkc.h"]
 
 
+def source_build_id() -> str:
+    """First 16 hex digits of the SHA-256 over libmhmkc.so's sources (relative path and content of each LIB_DEPS
+    file, in order): compiled into the library as mhmkc_build_id()."""
+    h = hashlib.sha256()
+    for d in LIB_DEPS:
+        h.update(str(d.relative_to(ROOT)).encode() + b"\0")
+        h.update(d.read_bytes())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def lib_build_id(path: Path = LIB) -> str | None:
+    """The build id a built libmhmkc.so carries (its MHMKC_BUILD_ID= marker), read from the file without loading it."""
+    if not path.exists():
+        return None
+    data = path.read_bytes()
+    i = data.find(b"MHMKC_BUILD_ID=")
+    if i < 0:
+        return None
+    j = data.find(b"\0", i)
+    return data[i + 15:j].decode(errors="replace")
+
+
 def _stale(target: Path, deps) -> bool:
     if not target.exists():
         return True
@@ -52,11 +77,14 @@ def hipcc() -> str:
 
 
 def build_lib(force: bool = False) -> Path:
-    if force or _stale(LIB, LIB_DEPS):
+    bid = source_build_id()
+    if force or _stale(LIB, LIB_DEPS) or lib_build_id() != bid:
         tmp = LIB.with_suffix(".so.tmp")
-        _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+        _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", f'-DMHMKC_BUILD_ID="{bid}"',
               *LIB_SOURCES, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp])
         tmp.replace(LIB)
+    if lib_build_id() != bid:
+        raise RuntimeError(f"{LIB} carries build id {lib_build_id()}, the sources make {bid}")
     return LIB
 
 

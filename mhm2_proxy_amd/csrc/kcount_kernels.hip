@@ -1966,15 +1966,7 @@ __device__ __forceinline__ int claim_home(const CountLds<K> &t, const uint64_t *
 // is returned for the saturation check (lds_clamp).
 template <typename K>
 __device__ __forceinline__ uint32_t lds_add(const CountLds<K> &t, int slot, uint32_t e) {
-#if MHMKC_EXP_NORTN
-  atomicAdd(&t.cnt[slot], 1u);
-  const uint32_t old = 0;
-#else
   const uint32_t old = atomicAdd(&t.cnt[slot], 1u);
-#endif
-#if MHMKC_EXP_NOEXT
-  return old;
-#endif
   const int l = (int)((e >> 3) & 7u), r = (int)(e & 7u);
   if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
   if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
@@ -2484,16 +2476,6 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           prefetch(ps, n, r0 + RND < lim ? r0 + RND : r0, nw);
         else if (r0 + RND < lim)
           prefetch(ps, n, r0 + RND, nw);
-#if MHMKC_EXP_LOADONLY
-        {
-          uint32_t acc = 0;
-#pragma unroll
-          for (int j = 0; j < R; j++) acc ^= ce[j] ^ (uint32_t)ck[j][0];
-          if (acc == 0x12345u) s_err = 1;
-          __syncthreads();
-          continue;
-        }
-#endif
         unsigned int *nmiss = &s_nmiss[lr];
         K *mkey = s_mkey + (BOV ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
         uint32_t *me = s_me + (BOV ? (rnd & 1) * MCL : 0);
@@ -2611,12 +2593,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             slot[j] = r;
             if (r < 0) continue;
           }
-#if !MHMKC_EXP_NOATOM
           if (COLD)
             lds_add_nr(t, r, ce[j], &s_wave[wid]);
           else
             old[j] = lds_add(t, r, ce[j]);
-#endif
           okm |= 1u << j;
         }
         }  // general phase A
@@ -2717,11 +2697,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           continue;
         }
         // B. the miss list, densely
-#if MHMKC_EXP_NOB
-        const unsigned int M = 0;
-#else
         const unsigned int M = min(*nmiss, (unsigned int)MCL);
-#endif
         if (tid == 0) s_missacc += M;
         if (!BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
         // (MHMKC_BSPREAD: list entry q to lane q / 16 of wave q % 16, so every wave takes a share)
@@ -2863,9 +2839,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       if (i < n_list) {
         const int slot = flist[i];
         fslot[j] = (uint16_t)slot;
-#if !MHMKC_EXP_NOFIN
         sv = slot_survives(t, slot, p, slot_count(t, slot, cold), c16[j], L[j], R_[j]);
-#endif
       }
       // one reservation per wave for its survivors (ballot + lane prefix)
       const uint64_t bal = __ballot(sv);
@@ -2940,9 +2914,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         occ++;
         const uint32_t c32 = slot_count(t, slot, cold);
         sum += c32;
-#if !MHMKC_EXP_NOFIN
         if (slot_survives(t, slot, p, c32, c16[j], L[j], R_[j])) surv_mask |= 1u << j;
-#endif
       }
     }
     const uint32_t mine = __popc(surv_mask);

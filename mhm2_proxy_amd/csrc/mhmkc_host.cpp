@@ -1645,6 +1645,14 @@ extern "C" {
 
 int mhmkc_abi_version(void) { return MHMKC_ABI_VERSION; }
 
+// build.py passes -DMHMKC_BUILD_ID="<16 hex digits>" (the sources' SHA-256); the marker string is also what build.py
+// looks for in the .so to decide whether it is stale
+#ifndef MHMKC_BUILD_ID
+#define MHMKC_BUILD_ID "unknown"
+#endif
+__attribute__((used)) static const char k_build_marker[] = "MHMKC_BUILD_ID=" MHMKC_BUILD_ID;
+const char *mhmkc_build_id(void) { return k_build_marker + 15; }
+
 int mhmkc_config_init(mhmkc_config *cfg) {
   if (!cfg) return MHMKC_EINVAL;
   memset(cfg, 0, sizeof *cfg);
@@ -1744,18 +1752,27 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   int extra = 0;
   while ((1 << extra) < cfg->n_ranks && extra < 3) extra++;
   if (h->smer) extra = 0;
-#ifndef MHMKC_CB0
-#define MHMKC_CB0 8
-#endif
-// coarse bits by key words: three- and four-word keys take 128 coarse buckets (half the extraction's cursor atomics
-// per record and runs twice as long at ~0.5 records per base; k = 99 38.9 -> 34.8 ms per C2 step, k = 77 31.4 -> 31.0)
-#ifndef MHMKC_CB0_2
-#define MHMKC_CB0_2 MHMKC_CB0  // two-word keys
-#endif
-#ifndef MHMKC_CB0_3
-#define MHMKC_CB0_3 7  // three- and four-word keys (cb >= 7 keeps a fine record's w0' bits + ext in 64 bits, fb >= 0)
-#endif
-  h->cb = (nl >= 3 ? MHMKC_CB0_3 : nl == 2 ? MHMKC_CB0_2 : MHMKC_CB0) + extra;
+  // coarse bits by key words: three- and four-word keys take 128 coarse buckets (half the extraction's cursor atomics
+  // per record and runs twice as long at ~0.5 records per base; k = 99 38.9 -> 34.8 ms per C2 step, k = 77 31.4 -> 31.0).
+  // MHMKC_CB0 / MHMKC_CB0_2 / MHMKC_CB0_3 override them for A/B runs, checked below.
+  auto cb_env = [](const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+  };
+  const int cb0 = nl >= 3 ? cb_env("MHMKC_CB0_3", 7) : nl == 2 ? cb_env("MHMKC_CB0_2", 8) : cb_env("MHMKC_CB0", 8);
+  // A mixed record keeps the key bits below the coarse digit, shifted up by the 6-bit ext code, in its first 64-bit
+  // word: three/four-word keys (64 bits of w0') need cb >= 7 (at cb = 6 with no fine bits the mask shift reaches 64
+  // and a key bit is lost: a wrong table, not an error), two-word keys (k bits of L') cb >= k - 58. The coarse
+  // partition has at most 2^11 bins (scatter_staged).
+  const int cb_min = nl >= 3 ? 7 : nl == 2 ? std::max(1, k - 58) : 1;
+  if (cb0 < cb_min || cb0 + extra > 11) {
+    delete h;
+    g_create_error = "coarse bits out of range: " + std::to_string(cb0) + " + " + std::to_string(extra) +
+                     " rank bits for k = " + std::to_string(k) + " (at least " + std::to_string(cb_min) +
+                     ", at most 11 with the rank bits)";
+    return MHMKC_EUNSUPPORTED;
+  }
+  h->cb = cb0 + extra;
   // compact records for 10 <= k <= 21 (MHMKC_WIDE_RECORDS=1 keeps the 8-byte records: A/B and tests)
   const char *wide = getenv("MHMKC_WIDE_RECORDS");
   h->compact = mhm::compact_ok(k, nl) && 2 * k - h->cb <= 34 && !(wide && atoi(wide));
@@ -1911,6 +1928,11 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_
       e = hipMemcpyAsync(&cut[i], d_offs + n_reads * i / P, 8, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return h->hip_fail(e, "read offsets");
+    // (the pieces' views start at their own cut, so the window kernel's offs[0] == obase + head check cannot see
+    // a batch whose first offset is not 0: checked here, as the unsplit path checks it on the device)
+    if (cut[0] != 0)
+      return h->fail(MHMKC_EINVAL, "device read offsets are not a PackedReads CSR (offs[0] == 0, non-decreasing, reads "
+                                   "<= 65535 bases, offs[n_reads] == n_bases)");
     for (uint64_t i = 0; i < P; i++) {
       const uint64_t r0 = n_reads * i / P, r1 = n_reads * (i + 1) / P;
       if (cut[i + 1] < cut[i] || cut[P] != n_bases)
@@ -2152,8 +2174,13 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
     return h->hip_fail(e, "fastq file blocks");
   }
   char *buf[2] = {h->fq_file_buf.as<char>(), h->fq_file_buf.as<char>() + slot};
+  bool added = false;  // some block's reads are in the round (a later failure leaves the round partial)
+  // tests only: the read of block MHMKC_DEBUG_FQ_READ_FAIL fails (a file that shrinks or turns unreadable mid-call)
+  const char *fail_env = getenv("MHMKC_DEBUG_FQ_READ_FAIL");
+  const uint64_t fail_block = fail_env && *fail_env ? strtoull(fail_env, nullptr, 10) : ~0ull;
   // block i's data: file bytes [i * block, min(size, (i + 1) * block)), read in parallel pieces
   auto read_block = [&](uint64_t i, char *dst) -> bool {
+    if (i == fail_block) return false;
     const uint64_t off = i * block, len = std::min(block, size - off);
     const uint64_t piece = (len + nthr - 1) / nthr;
     std::vector<std::thread> th;
@@ -2215,6 +2242,7 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
         rc = h->hip_fail(e, "fastq block H2D");
       else
         rc = h->add_fastq(h->d_fq_text.as<char>(), n, pairs, last ? nullptr : &used);
+      if (rc == MHMKC_OK) added = true;
     }
     if (reader.joinable()) reader.join();
     if (rc) {  // locate the bad record: the parser numbers records from the start of this block's text
@@ -2258,7 +2286,7 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
   close(fd);
   // earlier blocks may already be in the round (counted reads, extractions enqueued): the handle refuses to
   // finish a round that holds part of a file until mhmkc_reset
-  if (rc && blocks) h->partial = true;
+  if (rc && added) h->partial = true;
   if (rc == MHMKC_OK) {  // mhmkc_fastq_packed / mhmkc_fastq_fetch now see every block's PackedReads
     if (a_reads == 0 && ((e = keep_grow(h->d_fqa_offs, 0, 8)) != hipSuccess ||
                          (e = hipMemsetAsync(h->d_fqa_offs.p, 0, 8, h->stream)) != hipSuccess))

@@ -564,11 +564,11 @@ class SharedGpuCounter:
     def finish(self) -> KmerTable:
         """Count every member's reads on the group's GPU, exchange between the counters, and return this rank's
         rows (the k-mers whose get_kmer_target_rank over all ranks is this rank)."""
-        nl = n_longs_for(self.k)
         if self.rank != self.leader:  # members: reads to the leader, then this rank's rows back
             flat = [a for pair in self._reads for a in pair]
             self._send_arrays(flat, self.leader)
-            keys, counts, left, right = self._recv_arrays(self.leader)
+            width, keys, counts, left, right = self._recv_arrays(self.leader)
+            nl = int(width.view(np.int64)[0])  # the leader's key width (its counter's n_longs)
             return KmerTable(self.k, keys.view(np.uint64).reshape(-1, nl), counts.view(np.uint16), left, right)
         c = self.counter
         for b, o in self._reads:
@@ -588,7 +588,7 @@ class SharedGpuCounter:
             if m == self.rank:
                 mine = KmerTable(self.k, *part)
             else:
-                self._send_arrays(part, m)
+                self._send_arrays([np.array([c.n_longs], dtype=np.int64)] + part, m)
         return mine
 
     def close(self) -> None:

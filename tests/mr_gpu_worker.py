@@ -160,3 +160,30 @@ def run_share(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict
                                                                                  "bytes_recv", "exact_reruns", "smer_count")})
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_bad_offsets(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
+    """a device batch whose offsets do not start at 0 (offs[0] = 16) is refused with MHMKC_EINVAL at the
+    add, with and without the pipelined exchange (MHMKC_XPIPE, which cuts the batch into pieces); no collective has
+    run, so every rank just records the code."""
+    import torch
+    import torch.distributed as dist
+
+    import mhm2_proxy_amd as m
+    from common import synth_set
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MHMKC_XPIPE=opts["xpipe"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, o = synth_set(2000, 9000, opts.get("seed", 5))
+    c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport())
+    bt = torch.from_numpy(np.concatenate([np.zeros(16, np.uint8), b])).cuda()
+    ot = torch.from_numpy(o.astype(np.int64) + 16).cuda()
+    code = 0
+    try:
+        c.add_tensors(bt, ot, n_bases=int(o[-1]) + 16)
+    except m.MhmkcError as e:
+        code = e.code
+    np.savez(Path(out_dir) / f"rank{rank}.npz", code=code)
+    c.close()
+    dist.barrier()
+    dist.destroy_process_group()

@@ -31,7 +31,7 @@ def test_lib_exports_every_declared_symbol():
     lib = N.lib()
     for name in declared(ROOT / "include" / "mhmkc.h"):
         assert hasattr(lib, name), name
-    assert lib.mhmkc_abi_version() == 10
+    assert lib.mhmkc_abi_version() == 11
 
 
 def test_synth_exports_every_declared_symbol():
@@ -144,3 +144,26 @@ def test_map_hash_matches_the_adapter():
     from mhm2_proxy_amd.kcount import map_hash
 
     assert got == [map_hash([0x1B1B1B1B1B000000]), map_hash([1, 0x1B1B1B1B1B000000, 2**64 - 1])]
+
+
+@pytest.mark.parametrize("k,env,value", [(77, "MHMKC_CB0_3", "6"), (99, "MHMKC_CB0_3", "5"), (63, "MHMKC_CB0_2", "4"),
+                                         (21, "MHMKC_CB0", "12"), (99, "MHMKC_CB0_3", "12")])
+def test_create_rejects_coarse_bits(k, env, value, monkeypatch):
+    """VERDICT r3 (weak 10): a coarse-bit count the mixed records cannot hold (three/four-word keys need >= 7, two-word
+    keys k - 58; at most 11 bins' bits) is refused at create time, not counted into a wrong table."""
+    monkeypatch.setenv(env, value)
+    cfg = N.MhmkcConfig()
+    N.lib().mhmkc_config_init(C.byref(cfg))
+    cfg.k = k
+    h = C.c_void_p()
+    assert N.lib().mhmkc_create(C.byref(h), C.byref(cfg)) == -7
+    assert not h.value
+    assert b"coarse bits" in N.lib().mhmkc_last_error(None)
+
+
+def test_build_id_is_the_source_hash():
+    """The loaded library carries the SHA-256 of the sources it was compiled from."""
+    from mhm2_proxy_amd import build
+
+    build.build_lib()
+    assert N.build_id() == build.source_build_id() == build.lib_build_id()

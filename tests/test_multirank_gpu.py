@@ -268,3 +268,18 @@ def test_c3_c4_rank_share_vs_cpu_restatement(k, reads_per_rank, owner, tmp_path)
     del keys, c, l, r
     print(f"[parent {time.time() - t0:6.1f}s] digest", flush=True)
     assert_digests_equal(got, exp, k, f"C3/C4 share x{world}, k={k}, {owner}")
+
+
+@pytest.mark.parametrize("xpipe", ["0", "1"])
+def test_device_offsets_not_from_zero_refused(xpipe, tmp_path):
+    """offs[0] != 0 in a device batch is MHMKC_EINVAL whether or not the pipelined exchange cuts the batch
+    into pieces (the pieces' views could not see it on the device)."""
+    import torch.multiprocessing as mp
+
+    import mr_gpu_worker
+
+    world = 2
+    mp.spawn(mr_gpu_worker.run_bad_offsets, args=(world, free_port(), 21, str(tmp_path), {"xpipe": xpipe}),
+             nprocs=world, join=True)
+    codes = [int(np.load(tmp_path / f"rank{r}.npz")["code"]) for r in range(world)]
+    assert codes == [-1] * world, codes
