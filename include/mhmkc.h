@@ -124,6 +124,11 @@ typedef struct {
   uint64_t xchg_rounds;    /* pipelined record exchange: rounds (one per slab of the rank with the most slabs) */
   double ms_xchg;          /* ... device time of the rounds' transfers (exchange stream events, summed) */
   double ms_xchg_exposed;  /* ... of it after the last extraction ended (what the overlap did not hide) */
+  uint64_t finish_passes;  /* finish: parts of the owned hash range counted one after the other (memory: MHMKC_PASSES,
+                              or as many as free device memory asks for) */
+  uint64_t out_reruns;     /* finish passes redone because the output (sized from the distinct-key sketch) was full */
+  uint64_t device_bytes;   /* device memory held by this process's handles after the finish */
+  uint64_t device_bytes_peak; /* ... the most it held at any time */
 } mhmkc_stats;
 
 enum {

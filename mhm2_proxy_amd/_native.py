@@ -110,6 +110,10 @@ class MhmkcStats(C.Structure):
         ("xchg_rounds", C.c_uint64),
         ("ms_xchg", C.c_double),
         ("ms_xchg_exposed", C.c_double),
+        ("finish_passes", C.c_uint64),
+        ("out_reruns", C.c_uint64),
+        ("device_bytes", C.c_uint64),
+        ("device_bytes_peak", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

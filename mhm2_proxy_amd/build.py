@@ -79,9 +79,18 @@ def hipcc() -> str:
 def build_lib(force: bool = False) -> Path:
     bid = source_build_id()
     if force or _stale(LIB, LIB_DEPS) or lib_build_id() != bid:
+        # one hipcc per source, in parallel (the kernels file dominates), then one link
+        from concurrent.futures import ThreadPoolExecutor
+
+        obj_dir = ROOT / "build" / "obj"
+        obj_dir.mkdir(parents=True, exist_ok=True)
+        objs = [obj_dir / (src.name + ".o") for src in LIB_SOURCES]
+        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f'-DMHMKC_BUILD_ID="{bid}"']
+        with ThreadPoolExecutor(max_workers=len(LIB_SOURCES)) as ex:
+            list(ex.map(lambda so: _run([hipcc(), *flags, "-c", so[0], "-o", so[1]]), zip(LIB_SOURCES, objs)))
         tmp = LIB.with_suffix(".so.tmp")
-        _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", f'-DMHMKC_BUILD_ID="{bid}"',
-              *LIB_SOURCES, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", tmp])
+        _run([hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-L/opt/rocm/lib", "-lrccl",
+              "-Wl,-rpath,/opt/rocm/lib", "-o", tmp])
         tmp.replace(LIB)
     if lib_build_id() != bid:
         raise RuntimeError(f"{LIB} carries build id {lib_build_id()}, the sources make {bid}")

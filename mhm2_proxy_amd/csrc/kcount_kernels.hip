@@ -1354,6 +1354,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_smer_extract(ExtractParams 
       r = nr_;
     }
     window_record<NL, PACKED, CMP>(key, (l << 3) | r, valid, p, rk[j], inf[j]);
+    if (p.bin_hi && ((inf[j] & 0xffffu) < p.bin_lo || (inf[j] & 0xffffu) >= p.bin_hi)) inf[j] = 0u;  // other pass
 #pragma unroll
     for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[j][w]));
     asm volatile("" : "+v"(inf[j]));
@@ -2108,8 +2109,8 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
       }
       return lo;
     };
-    s_range[0] = lower(b);
-    s_range[1] = lower(b + 1);
+    s_range[0] = lower(p.ctg_base + b);
+    s_range[1] = lower(p.ctg_base + b + 1);
   }
   __syncthreads();
   const uint64_t q0 = s_range[0], q1 = s_range[1];
@@ -2188,6 +2189,12 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
       atomicAdd(&p.stats[STAT_COUNTSUM], (unsigned long long)c);
       if (c >= 2 && !(L == 'X' && R == 'X')) {
         const unsigned long long o = atomicAdd(p.out_cursor, 1ull);
+        atomicAdd(&p.stats[STAT_NOUT], 1ull);
+        if (o >= p.out_cap) {  // the output is full: flag the launch (the host grows it and redoes the pass)
+          atomicOr(p.err, 16u);
+          p.ctg_done[q] = 1;
+          continue;
+        }
         uint64_t *ok = p.out_keys + o * (uint64_t)p.nlo;
 #pragma unroll
         for (int w = 0; w < NL; w++) ok[w] = key[w];
@@ -2195,7 +2202,6 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
         p.out_counts[o] = (uint16_t)c;
         p.out_left[o] = L;
         p.out_right[o] = R;
-        atomicAdd(&p.stats[STAT_NOUT], 1ull);
       } else {
         atomicAdd(&p.stats[STAT_PURGED], 1ull);
       }
@@ -2857,12 +2863,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     __syncthreads();
     if (tid == 0) {
       const uint32_t acc = s_fin[1];
-      s_gbase = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      unsigned long long gb = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      if (acc && gb + acc > p.out_cap) {  // the output is full: write nothing, flag the launch (the cursor still
+        atomicOr(p.err, 16u);             // counts: the host grows the output to it and redoes the pass)
+        gb = ~0ull;
+      }
+      s_gbase = gb;
       my_out += acc;
       s_fin[0] = 0;
       s_fin[1] = 0;
     }
     __syncthreads();
+    if (s_gbase == ~0ull) surv_mask = 0;
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
       if ((surv_mask >> j) & 1u) {
@@ -2933,10 +2945,16 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         s_wave[w] = acc;
         acc += c;
       }
-      s_gbase = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      unsigned long long gb = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      if (acc && gb + acc > p.out_cap) {
+        atomicOr(p.err, 16u);
+        gb = ~0ull;
+      }
+      s_gbase = gb;
       my_out += acc;
     }
     __syncthreads();
+    if (s_gbase == ~0ull) surv_mask = 0;
     unsigned long long g = s_gbase + s_wave[wid] + (incl - mine);
 #pragma unroll
     for (int j = 0; j < SPT; j++) {

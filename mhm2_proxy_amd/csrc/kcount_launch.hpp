@@ -46,6 +46,8 @@ struct ExtractParams {
   unsigned int *ovf;                // bit 1: a capped bin of this slab overflowed (per slab)
   const uint32_t *tile_starts;      // per tile: its read-start bitmap (k_tile_starts, kGroups words), or nullptr:
                                     // load_tile builds it from the offsets
+  uint32_t bin_lo, bin_hi;          // k_smer_extract: only records of coarse bins [bin_lo, bin_hi) are kept (a finish
+                                    // pass over part of the hash range); 0, n_bins = all
 };
 
 constexpr int SMER_SLICES = 64;  // counter slices per destination (spread the workgroups' atomics)
@@ -149,14 +151,18 @@ struct CountParams {
   char *out_left;
   char *out_right;
   unsigned long long *out_cursor;
+  unsigned long long out_cap;         // output rows allocated: a reservation past it sets err bit 4 (16) and writes
+                                      // nothing (the cursor still counts, so the host learns the size and redoes the pass)
   unsigned long long *stats;          // [STAT_*]
-  const unsigned int *err;            // k_part_scatter's flag word: bit 1 set = a capped fine bucket overflowed,
+  unsigned int *err;                  // k_part_scatter's flag word: bit 1 set = a capped fine bucket overflowed,
                                       // its cursor ran past the bucket, so the launch is void (returns at once)
   // contig pass (kcount_ctg.hip): folded contig k-mers sorted by bucket; 0 entries = no contig pass
   uint64_t ctg_n;
   const uint64_t *ctg_keys[4];        // [NL][ctg_n] canonical key words
   const uint32_t *ctg_state;          // count (16 bits) | left code << 16 | right code << 19
   const uint32_t *ctg_bucket;         // local fine bucket of each entry (sorted ascending)
+  uint32_t ctg_base;                  // local fine bucket of this launch's bucket 0 (a finish pass over part of the
+                                      // owned range: its first coarse bucket << fine_bits)
   uint8_t *ctg_done;                  // [ctg_n] applied (zeroed before the launch)
 };
 

@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -34,6 +35,9 @@ namespace {
 
 thread_local std::string g_create_error;
 
+// device bytes held by this process's handles (live, and the most at any time): mhmkc_stats.device_bytes[_peak]
+std::atomic<uint64_t> g_dev_live{0}, g_dev_peak{0};
+
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
@@ -47,10 +51,17 @@ struct DevBuf {
       return e;
     }
     cap = want;
+    const uint64_t live = g_dev_live.fetch_add(want) + want;
+    uint64_t pk = g_dev_peak.load();
+    while (live > pk && !g_dev_peak.compare_exchange_weak(pk, live)) {
+    }
     return hipSuccess;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipFree(p);
+      g_dev_live.fetch_sub(cap);
+    }
     p = nullptr;
     cap = 0;
   }
@@ -111,6 +122,7 @@ struct Slab {
   // supermer exchange: a read slab's supermers per destination (words and supermers, their exact spans), or
   // (recv) the records of the supermers this rank received
   bool recv = false;
+  uint32_t bin_lo = 0, bin_hi = 0;  // recv slab of a finish pass: only coarse bins [bin_lo, bin_hi) (bin_hi 0: all)
   uint64_t *codes = nullptr, *desc = nullptr;
   uint32_t *good = nullptr;
   std::vector<uint64_t> sw, ss, swb, ssb;  // [G] words, supermers per destination and their first word / supermer
@@ -207,8 +219,12 @@ struct mhmkc {
   bool smer = false;
   DevBuf d_owners, d_rcodes, d_rgood, d_rdesc, d_rnwin, d_rwpre, d_rtiles, d_rtmp;
   mhm::SmerSource rsrc{};
+  uint64_t smer_nwin = 0, smer_seen = 0;  // received windows; records extracted from them by the finish passes so far
+  uint32_t smer_tiles = 0;
+  Slab *smer_slab = nullptr;  // the received supermers' records of the current finish pass
   int smer_build(Slab *sl);
   int smer_exchange(std::vector<Source> &srcs);
+  int smer_records(uint32_t lo, uint32_t hi, std::vector<Source> &srcs);
   PinBuf x_send, x_recv;  // host-staged exchange
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
@@ -307,6 +323,7 @@ struct mhmkc {
     if (n_slabs == slabs.size()) slabs.push_back(new Slab());
     Slab *sl = slabs[n_slabs++];
     sl->recv = false;
+    sl->bin_lo = sl->bin_hi = 0;
     return sl;
   }
   Arena *new_arena() {
@@ -336,6 +353,22 @@ struct mhmkc {
     return MHMKC_OK;
   }
 
+  // Move a plane set so that record index `sh` lands on its first entry (a capped slab that holds only the segments
+  // from sh on: the kernels keep indexing segment i at i * cap)
+  void shift_planes(mhm::PlaneSet &ps, uint64_t sh) const {
+    if (!sh) return;
+    if (compact) {
+      ps.w[0] = (uint64_t *)((uint32_t *)ps.w[0] - sh);
+    } else if (mixed2 && MHMKC_M2AOS) {
+      ps.w[0] -= 2 * sh;
+      if (ps.w[1]) ps.w[1] -= sh;
+    } else {
+      for (int w = 0; w < 4; w++)
+        if (ps.w[w]) ps.w[w] -= sh;
+    }
+    if (ps.ext) ps.ext -= sh;
+  }
+
   int add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known);
   int extract(Slab *sl, bool exact);
   int resolve_slabs();
@@ -347,6 +380,8 @@ struct mhmkc {
                   std::vector<uint16_t> &gd);
   int handoff();
   int finish(uint64_t *n_out_ret);
+  int finish_passes(uint64_t owned) const;
+  hipError_t grow_keep(DevBuf &b, size_t used, size_t need);
   int qcut_pending = 20;  // quality cutoff of the batch being added (add_seqs encodes quality as case)
 };
 
@@ -409,6 +444,11 @@ int mhmkc::extract(Slab *sl, bool exact) {
   p.cursor = dcur;
   p.err = d_err.as<unsigned int>();
   p.ovf = (unsigned int *)(dcur + nseg);
+  const bool filt = sl->bin_hi != 0;  // (received supermers of a finish pass: its coarse bins only)
+  const uint32_t blo = filt ? sl->bin_lo : 0, bhi = filt ? sl->bin_hi : nb;
+  p.bin_lo = filt ? blo : 0;
+  p.bin_hi = filt ? bhi : 0;
+  uint64_t shift = 0;
   if (!sl->recv) {  // (the received supermers' tile index is made once by smer_exchange)
     prof_begin(MHMKC_STAGE_TILEIDX);
     e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
@@ -446,13 +486,17 @@ int mhmkc::extract(Slab *sl, bool exact) {
     sl->bases[nseg] = tot;
     p.bin_cap = 0;
   } else {
+    // every segment gets the expected share of the windows (+4 % + 1024); a filtered slab allocates only the
+    // segments of its bins and shifts its planes so that segment i still starts at record i * cap
     const uint64_t expect = sl->wins / nseg;
     const uint64_t cap = align_up(expect + expect / 25 + 1024, 64);
-    for (uint32_t i = 0; i <= nseg; i++) sl->bases[i] = (uint64_t)i * cap;
+    for (uint32_t i = 0; i <= nseg; i++) sl->bases[i] = (uint64_t)std::min(std::max(i, blo * NSUB), bhi * NSUB) * cap;
     p.bin_cap = cap;
+    shift = (uint64_t)blo * NSUB * cap;
   }
   int rc;
-  if ((rc = set_planes(sl->buf, sl->bases[nseg], sl->planes))) return rc;
+  if ((rc = set_planes(sl->buf, sl->bases[nseg] - shift, sl->planes))) return rc;
+  shift_planes(sl->planes, shift);
   // device cursors are sub-major (cursor[s * nb + b]): the 64 lanes of one atomic instruction then hit 64
   // consecutive words, which the memory-side atomic unit serves as whole lines
   uint64_t *hc = sl->pin.as<uint64_t>();
@@ -542,7 +586,7 @@ int mhmkc::resolve_one(Slab *sl, bool &redo) {
     sl->counts[i] = hc[(size_t)(i % NSUB) * nb + i / NSUB] - sl->bases[i];
     tot += sl->counts[i];
   }
-  if (tot != sl->wins) return fail(MHMKC_EHIP, "internal: slab holds %llu records, expected %llu",
+  if (!sl->bin_hi && tot != sl->wins) return fail(MHMKC_EHIP, "internal: slab holds %llu records, expected %llu",
                                    (unsigned long long)tot, (unsigned long long)sl->wins);
   sl->n = tot;
   sl->pending = false;
@@ -1083,25 +1127,42 @@ int mhmkc::smer_exchange(std::vector<Source> &srcs) {
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "supermer tiles");
   rsrc = mhm::SmerSource{rcodes, rgood, rdesc, (const uint64_t *)wpre, d_rtiles.as<uint64_t>(), St, n_win, Wt + 2};
-  // 4. the received windows' records, as one more slab (capped layout; an overflow reruns it exactly)
-  const size_t n_read_slabs = n_slabs;
-  if (n_win) {
-    Slab *rs = new_slab();
-    rs->recv = true;
-    rs->rv = mhm::ReadsView{};
-    rs->wins = n_win;
-    rs->tiles = (uint32_t)tiles64;
-    rs->qcut = cfg.qual_cutoff;
-    rs->n = 0;
-    if ((rc = extract(rs, getenv("MHMKC_DEBUG_EXACT") != nullptr))) return rc;
-    if ((rc = resolve_slabs())) return rc;
-    Source src;
-    src.planes = rs->planes;
-    src.start.assign(rs->bases.begin(), rs->bases.begin() + (size_t)nb * NSUB);
-    src.count = rs->counts;
-    srcs.push_back(std::move(src));
+  // 4. the received windows' records are extracted per finish pass (smer_records), one more slab
+  smer_nwin = n_win;
+  smer_tiles = (uint32_t)tiles64;
+  (void)srcs;
+  return MHMKC_OK;
+}
+
+// The records of the received supermers whose coarse bucket is in [lo, hi) (a finish pass; all of them when the pass
+// covers the whole range), as the recv slab (capped layout; an overflow reruns it exactly); appended to srcs.
+int mhmkc::smer_records(uint32_t lo, uint32_t hi, std::vector<Source> &srcs) {
+  if (!smer_nwin) return MHMKC_OK;
+  int rc;
+  if (!smer_slab) smer_slab = new Slab();
+  Slab *rs = smer_slab;
+  rs->recv = true;
+  rs->rv = mhm::ReadsView{};
+  rs->wins = smer_nwin;
+  rs->tiles = smer_tiles;
+  rs->qcut = cfg.qual_cutoff;
+  rs->n = 0;
+  rs->bin_lo = lo;
+  rs->bin_hi = (lo == 0 && hi == nb) ? 0 : hi;
+  if ((rc = extract(rs, getenv("MHMKC_DEBUG_EXACT") != nullptr))) return rc;
+  for (int pass = 0; rs->pending; pass++) {
+    bool redo = false;
+    if ((rc = resolve_one(rs, redo))) return rc;
+    if (redo && pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
   }
-  (void)n_read_slabs;
+  uint64_t tot = 0;
+  for (uint64_t c : rs->counts) tot += c;
+  smer_seen += tot;
+  Source src;
+  src.planes = rs->planes;
+  src.start.assign(rs->bases.begin(), rs->bases.begin() + (size_t)nb * NSUB);
+  src.count = rs->counts;
+  srcs.push_back(std::move(src));
   return MHMKC_OK;
 }
 
@@ -1306,6 +1367,43 @@ int mhmkc::handoff() {
 
 // Fine buckets are capped at 1.25x their expected size (+256): a single scatter pass, no histogram. If a
 // bucket overflows, the count kernel returns at once and the pass is redone with part_hist + scan.
+//
+// Finish passes (memory): the owned coarse range is counted in P contiguous parts, each fine-partitioned into the
+// same buffer, counted, and its survivors appended to the output. One pass holds 1/P of the fine records (and, with
+// the supermer exchange, of the received windows' records, extracted per pass from the received supermers), so a
+// shard larger than free device memory (or several ranks sharing one GPU) still counts. P: MHMKC_PASSES, else the
+// smallest power of two whose pass fits 80 % of the free device memory. The output is sized from the distinct-key
+// sketch (half the estimated distinct keys + 1M rows: the survivors, count >= 2, are a fraction of them); a pass
+// that fills it stops writing, and is redone after the output has grown to the rows its cursor counted.
+int mhmkc::finish_passes(uint64_t owned) const {
+  const uint32_t no = n_owned();
+  if (const char *env = getenv("MHMKC_PASSES")) return std::max(1, std::min<int>(atoi(env), (int)std::max(1u, no)));
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 1;
+  double need = (double)owned * (double)(compact ? 4 : rec_bytes()) * 1.3;  // capped fine records
+  if (smer) need += (double)owned * (double)rec_bytes() * 1.1;              // the received windows' coarse records
+  const double have = 0.8 * (double)fr + (double)d_r2.cap + (smer_slab ? (double)smer_slab->buf.cap : 0.0);
+  int P = 1;
+  while (P < (int)no && need / P > have) P *= 2;
+  return std::min<int>(P, (int)std::max(1u, no));
+}
+
+// A device buffer grown to `need` bytes with its first `used` bytes kept (the output of earlier passes).
+hipError_t mhmkc::grow_keep(DevBuf &b, size_t used, size_t need) {
+  if (need <= b.cap && b.p) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return e;
+  DevBuf nb_;
+  if ((e = nb_.ensure(need)) != hipSuccess) return e;
+  if (used && b.p && (e = hipMemcpy(nb_.p, b.p, std::min(used, b.cap), hipMemcpyDeviceToDevice)) != hipSuccess) {
+    nb_.release();
+    return e;
+  }
+  b.release();
+  b = nb_;
+  return hipSuccess;
+}
+
 int mhmkc::finish(uint64_t *n_out_ret) {
   if (partial) return fail(MHMKC_ESTATE, "a failed mhmkc_add_fastq_file left part of the file in this round; call mhmkc_reset");
   int rc = begin_round();
@@ -1365,274 +1463,325 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       srcs.push_back(std::move(src));
     }
   }
-  std::vector<uint64_t> per_coarse(no, 0);
-  uint64_t owned = 0;
+  uint64_t owned = smer ? smer_nwin : 0;  // (the received windows' records are extracted per pass)
   for (auto &s : srcs)
-    for (uint32_t i = 0; i < no * NSUB; i++) {
-      per_coarse[i / NSUB] += s.count[i];
-      owned += s.count[i];
-    }
+    for (uint32_t i = 0; i < no * NSUB; i++) owned += s.count[i];
   st.owned_records = owned;
   st.coarse_record_bytes = rec_bytes();
   st.fine_record_bytes = compact ? 4 : rec_bytes();
-  for (uint32_t c = 0; c < no; c++)  // k_count indexes a bucket with 32 bits
-    if (per_coarse[c] >= 0xffffffffull)
-      return fail(MHMKC_EUNSUPPORTED, "more than 2^32 records in one hash bucket (split the input into batches of ranks)");
+  smer_seen = 0;
+  const int passes = finish_passes(owned);
+  st.finish_passes = (uint64_t)passes;
 
-  // run table: one entry per non-empty (source, segment) span; the device expands it into chunks
   const int T = mhm::chunk_records(nl);  // records per partition chunk
-  std::vector<mhm::SRun> runs;
-  std::vector<mhm::PlaneSet> ps;
-  uint64_t n_chunks = 0, n_c0 = 0;  // n_c0: chunks of the first owned coarse bucket (they come first)
-  uint64_t xcd_start[9] = {0};
-  for (size_t s = 0; s < srcs.size(); s++) ps.push_back(srcs[s].planes);
-  // ordered by XCD class (coarse % 8), then coarse bucket, segment, source (see xcd_chunk)
-  for (uint32_t x = 0; x < 8; x++) {
-    xcd_start[x] = n_chunks;
-    for (uint32_t c = x; c < no; c += 8) {
-      for (uint32_t q = 0; q < NSUB; q++)
-        for (size_t s = 0; s < srcs.size(); s++) {
-          const uint32_t i = c * NSUB + q;
-          const uint64_t cnt = srcs[s].count[i];
-          if (!cnt) continue;
-          runs.push_back({srcs[s].start[i], cnt, (uint32_t)s, c, (uint32_t)n_chunks, 0});
-          n_chunks += (cnt + T - 1) / T;
-        }
-      if (c == 0) n_c0 = n_chunks;
-    }
-  }
-  xcd_start[8] = n_chunks;
-  if (n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
-  uint64_t xcd_max = 0;
-  for (int x = 0; x < 8; x++) xcd_max = std::max(xcd_max, xcd_start[x + 1] - xcd_start[x]);
-  if ((e = grow(d_chunks, std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun) + 4 * (n_chunks + 1) + 256)) !=
-      hipSuccess)
-    return hip_fail(e, "chunk table");
-  mhm::SRun *d_runs = d_chunks.as<mhm::SRun>();
-  uint32_t *d_chunk_run = (uint32_t *)(d_chunks.as<char>() + align_up(runs.size() * sizeof(mhm::SRun), 256));
-  if ((e = grow(d_srcs, std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 16 * (size_t)no)) != hipSuccess)
-    return hip_fail(e, "source table");
-  unsigned long long *d_cfit = (unsigned long long *)(d_srcs.as<char>() + align_up(ps.size() * sizeof(mhm::PlaneSet), 16));
-  // the tables are small: synchronous copies (their host vectors go out of scope)
-  if (!runs.empty()) {
-    if ((e = hipMemcpyAsync(d_runs, runs.data(), runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, stream)) !=
-        hipSuccess)
-      return hip_fail(e, "run table H2D");
-    if ((e = mhm::launch_chunk_runs(d_runs, (uint32_t)runs.size(), d_chunk_run, T, stream)) != hipSuccess)
-      return hip_fail(e, "chunk index");
-  }
-  if (!ps.empty() && (e = hipMemcpyAsync(d_srcs.p, ps.data(), ps.size() * sizeof(mhm::PlaneSet),
-                                         hipMemcpyHostToDevice, stream)) != hipSuccess)
-    return hip_fail(e, "source H2D");
-
-  // fine bits: at most FINE_LOAD x the LDS table slots of distinct keys per fine bucket,
-  // with the distinct keys of the first owned coarse bucket estimated by a HyperLogLog sketch (the ratio
-  // of distinct keys to records grows with k and the error rate, so the record count alone misjudges it)
   const uint32_t cap_slots = (uint32_t)mhm::count_cap(nl, compact);
-  fb = 4;
+  bool exact_env = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
+  uint64_t out_cap = 0, out_used = 0;  // output rows allocated / written by the earlier passes
+  unsigned long long acc_stats[mhm::STAT_ALLOC] = {0};
   double est_fine = 0;  // estimated distinct keys per fine bucket (0: no estimate)
-  if (n_c0) {
-    mhm::PartitionParams sp{};
-    sp.runs = d_runs;
-    sp.chunk_run = d_chunk_run;
-    sp.n_runs = (uint32_t)runs.size();
-    sp.n_chunks = (uint32_t)n_chunks;
-    sp.srcs = d_srcs.as<mhm::PlaneSet>();
-    sp.k = k;
-    sp.coarse_bits = cb;
-    sp.hbits = hbits;
-    sp.compact = mixed();
-    std::vector<uint32_t> reg(mhm::SKETCH_M + 1);
-    prof_begin(MHMKC_STAGE_OTHER);
-    if ((e = grow(d_hll, 4 * mhm::SKETCH_M + 64)) != hipSuccess ||
-        (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_M + 4, stream)) != hipSuccess ||
-        (e = mhm::launch_sketch(sp, (uint32_t)n_c0, d_hll.as<unsigned int>(), nl, packed, stream)) != hipSuccess)
-      return hip_fail(e, "distinct sketch");
-    prof_end();
-    if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * mhm::SKETCH_M + 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(stream)) != hipSuccess)
-      return hip_fail(e, "sketch D2H");
-    // extension adds of the sampled coarse bucket, scaled to all owned records (the LDS op mix, stats only)
-    if (per_coarse[0]) st.lds_ext_adds = (uint64_t)((double)reg[mhm::SKETCH_M] * (double)owned / (double)per_coarse[0]);
-    reg.resize(mhm::SKETCH_M);
-    const double est = hll_estimate(reg);
-    st.distinct_estimate = (uint64_t)(est * no);
-    while (fb < 11 && est / (double)(1u << fb) > FINE_LOAD * cap_slots) fb++;
-    est_fine = est;
-  } else {  // no records in the first coarse bucket: ~4 records per slot
-    const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
-    while (fb < 11 && (avg_coarse >> fb) > (uint64_t)cap_slots * 4) fb++;
-  }
-  if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
-  fb = std::max(fb, min_fine_bits());
-  nf = 1u << fb;
-  est_fine /= nf;
-  const uint32_t n_fine = no * nf;
-  st.fine_buckets = n_fine;
-  if ((rc = prepare_ctgs())) return rc;
-
-  // capped fine layout
-  std::vector<uint64_t> cfit(2 * (size_t)no);  // [coarse_base | coarse_fcap]
-  uint64_t r2_size = 0;
-  for (uint32_t c = 0; c < no; c++) {
-    const uint64_t ex = per_coarse[c] >> fb;
-    const uint64_t fcap = align_up(ex + ex / 4 + 256, 16);
-    cfit[c] = r2_size;
-    cfit[no + c] = fcap;
-    r2_size += fcap << fb;
-  }
-  if (no && (e = hipMemcpyAsync(d_cfit, cfit.data(), 16 * (size_t)no, hipMemcpyHostToDevice, stream)) != hipSuccess)
-    return hip_fail(e, "layout H2D");
-  if ((e = grow(d_fine_hist, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
-  if ((e = grow(d_fine_base, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
-  if ((e = grow(d_fine_cursor, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine cursor");
-  const uint64_t out_cap = owned / 2 + ctg_n + 1;
-  if ((e = grow(d_out_keys, out_cap * 8 * nlo)) != hipSuccess) return hip_fail(e, "output keys");
-  if ((e = grow(d_out_counts, out_cap * 2)) != hipSuccess) return hip_fail(e, "output counts");
-  if ((e = grow(d_out_left, out_cap)) != hipSuccess) return hip_fail(e, "output left");
-  if ((e = grow(d_out_right, out_cap)) != hipSuccess) return hip_fail(e, "output right");
-  if ((e = grow(d_out_cursor, 8)) != hipSuccess) return hip_fail(e, "output cursor");
-
-  mhm::PartitionParams pp{};
-  pp.runs = d_runs;
-  pp.chunk_run = d_chunk_run;
-  pp.n_runs = (uint32_t)runs.size();
-  pp.n_chunks = (uint32_t)n_chunks;
-  for (int x = 0; x < 9; x++) pp.xcd_start[x] = (uint32_t)xcd_start[x];
-  pp.grid = (uint32_t)(8 * xcd_max);
-  pp.srcs = d_srcs.as<mhm::PlaneSet>();
-  pp.k = k;
-  pp.coarse_bits = cb;
-  pp.fine_bits = fb;
-  pp.hbits = hbits;
-  pp.compact = mixed();
-  pp.fine_hist = d_fine_hist.as<unsigned long long>();
-  pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
-  pp.err = d_err.as<unsigned int>();
-
-  mhm::CountParams cp{};
-  cp.bucket_base = d_fine_base.as<unsigned long long>();
-  cp.bucket_end = d_fine_cursor.as<unsigned long long>();
-  cp.hbits = hbits;
-  cp.compact = mixed();
-  cp.coarse_bits = cb;
-  cp.fine_bits = fb;
-  cp.bucket0 = own_lo << fb;
-  cp.n_buckets = n_fine;
-  cp.grid = (uint32_t)std::max(0, n_cu * mhm::C_SPLIT);  // persistent workgroups filling every CU's LDS
-  cp.k = k;
-  cp.cap = mhm::count_cap(nl, compact);
-  // The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
-  // LDS table (C2: 0.44). The table k_count clears and finalizes per bucket is cut to CAP_LOAD of the estimate
-  // (multiples of 64 slots): both passes cost per slot, not per key.
-  if (est_fine > 0 && CAP_LOAD > 0) {
-    const double want = est_fine / CAP_LOAD;
-    const uint32_t fit = (uint32_t)std::min<double>(cp.cap, std::max(1024.0, std::ceil(want / 64.0) * 64.0));
-    cp.cap = std::min(cp.cap, (int)fit);
-  }
-  st.table_slots = (uint64_t)cp.cap;
-  if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
-  cp.dmin_thres = dmin;
-  cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
-  cp.nlo = nlo;
-  cp.out_keys = d_out_keys.as<uint64_t>();
-  cp.out_counts = d_out_counts.as<uint16_t>();
-  cp.out_left = d_out_left.as<char>();
-  cp.out_right = d_out_right.as<char>();
-  cp.out_cursor = d_out_cursor.as<unsigned long long>();
-  cp.stats = d_stats.as<unsigned long long>();
-  cp.err = d_err.as<unsigned int>();
-  cp.ctg_n = ctg_n;
-  for (int w = 0; w < 4; w++) cp.ctg_keys[w] = w < nl ? d_ctg_keys[w].as<uint64_t>() : nullptr;
-  cp.ctg_state = d_ctg_state.as<uint32_t>();
-  cp.ctg_bucket = d_ctg_bucket.as<uint32_t>();
-  cp.ctg_done = d_ctg_done.as<uint8_t>();
-
-  bool exact = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
-  unsigned long long stats[mhm::STAT_ALLOC];
   unsigned int errf = 0;
-  for (int attempt = 0; attempt < 2; attempt++) {
-    mhm::PlaneSet r2{};
-    if (exact) {  // (k_scan rounds every bucket up to a multiple of 4 records)
-      if ((rc = set_planes(d_r2, owned + 3 * (uint64_t)n_fine + 4, r2, true))) return rc;
-    } else {
-      if ((rc = set_planes(d_r2, r2_size, r2, true))) return rc;
+  st.fine_buckets = 0;
+  for (int pass = 0; pass < passes; pass++) {
+    const uint32_t c0 = (uint32_t)((uint64_t)no * pass / passes), c1 = (uint32_t)((uint64_t)no * (pass + 1) / passes);
+    const uint32_t np_ = c1 - c0;  // coarse buckets of this pass
+    if (!np_) continue;
+    const size_t n_srcs0 = srcs.size();
+    if (smer && (rc = smer_records(own_lo + c0, own_lo + c1, srcs))) return rc;
+    std::vector<uint64_t> per_coarse(np_, 0);
+    uint64_t owned_p = 0;
+    for (auto &s : srcs)
+      for (uint32_t i = c0 * NSUB; i < c1 * NSUB; i++) {
+        per_coarse[i / NSUB - c0] += s.count[i];
+        owned_p += s.count[i];
+      }
+    for (uint32_t c = 0; c < np_; c++)  // k_count indexes a bucket with 32 bits
+      if (per_coarse[c] >= 0xffffffffull)
+        return fail(MHMKC_EUNSUPPORTED, "more than 2^32 records in one hash bucket (split the input into batches of ranks)");
+
+    // run table: one entry per non-empty (source, segment) span of the pass's coarse buckets; the device expands it
+    // into chunks, ordered by XCD class (coarse % 8), then coarse bucket, segment, source (see xcd_chunk)
+    std::vector<mhm::SRun> runs;
+    std::vector<mhm::PlaneSet> ps;
+    uint64_t n_chunks = 0, n_c0 = 0;  // n_c0: chunks of the pass's first coarse bucket (they come first)
+    uint64_t xcd_start[9] = {0};
+    for (size_t s = 0; s < srcs.size(); s++) ps.push_back(srcs[s].planes);
+    for (uint32_t x = 0; x < 8; x++) {
+      xcd_start[x] = n_chunks;
+      for (uint32_t c = c0 + ((x + 8 - c0 % 8) % 8); c < c1; c += 8) {
+        for (uint32_t q = 0; q < NSUB; q++)
+          for (size_t s = 0; s < srcs.size(); s++) {
+            const uint32_t i = c * NSUB + q;
+            const uint64_t cnt = srcs[s].count[i];
+            if (!cnt) continue;
+            runs.push_back({srcs[s].start[i], cnt, (uint32_t)s, c - c0, (uint32_t)n_chunks, 0});
+            n_chunks += (cnt + T - 1) / T;
+          }
+        if (c == c0) n_c0 = n_chunks;
+      }
     }
-    prof_begin(MHMKC_STAGE_OTHER);
-    e = hipMemsetAsync(d_out_cursor.p, 0, 8, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_ALLOC, stream);
-    if (e == hipSuccess && ctg_n) e = hipMemsetAsync(d_ctg_done.p, 0, ctg_n, stream);
-    if (e == hipSuccess && exact) e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
-    if (e == hipSuccess && !exact)
-      e = mhm::launch_init_fine(d_cfit, d_cfit + no, no, fb, d_fine_base.as<unsigned long long>(),
-                                d_fine_cursor.as<unsigned long long>(), stream);
-    prof_end();
-    if (e != hipSuccess) return hip_fail(e, "fine layout");
-    if (exact) {
-      pp.coarse_base = nullptr;
-      pp.coarse_fcap = nullptr;
-      prof_begin(MHMKC_STAGE_SHIST);
-      e = mhm::launch_part_hist(pp, nl, packed, stream);
-      prof_end();
-      if (e != hipSuccess) return hip_fail(e, "part_hist");
+    xcd_start[8] = n_chunks;
+    if (n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
+    uint64_t xcd_max = 0;
+    for (int x = 0; x < 8; x++) xcd_max = std::max(xcd_max, xcd_start[x + 1] - xcd_start[x]);
+    if ((e = grow(d_chunks, std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun) + 4 * (n_chunks + 1) + 256)) !=
+        hipSuccess)
+      return hip_fail(e, "chunk table");
+    mhm::SRun *d_runs = d_chunks.as<mhm::SRun>();
+    uint32_t *d_chunk_run = (uint32_t *)(d_chunks.as<char>() + align_up(runs.size() * sizeof(mhm::SRun), 256));
+    if ((e = grow(d_srcs, std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 16 * (size_t)np_)) != hipSuccess)
+      return hip_fail(e, "source table");
+    unsigned long long *d_cfit = (unsigned long long *)(d_srcs.as<char>() + align_up(ps.size() * sizeof(mhm::PlaneSet), 16));
+    // the tables are small: their copies are waited for below (the host vectors go out of scope)
+    if (!runs.empty()) {
+      if ((e = hipMemcpyAsync(d_runs, runs.data(), runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, stream)) !=
+          hipSuccess)
+        return hip_fail(e, "run table H2D");
+      if ((e = mhm::launch_chunk_runs(d_runs, (uint32_t)runs.size(), d_chunk_run, T, stream)) != hipSuccess)
+        return hip_fail(e, "chunk index");
+    }
+    if (!ps.empty() && (e = hipMemcpyAsync(d_srcs.p, ps.data(), ps.size() * sizeof(mhm::PlaneSet),
+                                           hipMemcpyHostToDevice, stream)) != hipSuccess)
+      return hip_fail(e, "source H2D");
+
+    if (pass == 0) {
+      // fine bits: at most FINE_LOAD x the LDS table slots of distinct keys per fine bucket, with
+      // the distinct keys of the first owned coarse bucket estimated by a HyperLogLog sketch (the ratio of distinct
+      // keys to records grows with k and the error rate, so the record count alone misjudges it); the same fine bits
+      // for every pass (the contig pass buckets its k-mers with them once)
+      fb = 4;
+      double est = 0;
+      if (n_c0) {
+        mhm::PartitionParams sp{};
+        sp.runs = d_runs;
+        sp.chunk_run = d_chunk_run;
+        sp.n_runs = (uint32_t)runs.size();
+        sp.n_chunks = (uint32_t)n_chunks;
+        sp.srcs = d_srcs.as<mhm::PlaneSet>();
+        sp.k = k;
+        sp.coarse_bits = cb;
+        sp.hbits = hbits;
+        sp.compact = mixed();
+        std::vector<uint32_t> reg(mhm::SKETCH_M + 1);
+        prof_begin(MHMKC_STAGE_OTHER);
+        if ((e = grow(d_hll, 4 * mhm::SKETCH_M + 64)) != hipSuccess ||
+            (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_M + 4, stream)) != hipSuccess ||
+            (e = mhm::launch_sketch(sp, (uint32_t)n_c0, d_hll.as<unsigned int>(), nl, packed, stream)) != hipSuccess)
+          return hip_fail(e, "distinct sketch");
+        prof_end();
+        if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * mhm::SKETCH_M + 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream)) != hipSuccess)
+          return hip_fail(e, "sketch D2H");
+        // extension adds of the sampled coarse bucket, scaled to all owned records (the LDS op mix, stats only)
+        if (per_coarse[0]) st.lds_ext_adds = (uint64_t)((double)reg[mhm::SKETCH_M] * (double)owned / (double)per_coarse[0]);
+        reg.resize(mhm::SKETCH_M);
+        est = hll_estimate(reg);
+        st.distinct_estimate = (uint64_t)(est * no);
+        while (fb < 11 && est / (double)(1u << fb) > FINE_LOAD * cap_slots) fb++;
+        est_fine = est;
+      } else {  // no records in the first coarse bucket: ~4 records per slot
+        const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
+        while (fb < 11 && (avg_coarse >> fb) > (uint64_t)cap_slots * 4) fb++;
+      }
+      if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
+      fb = std::max(fb, min_fine_bits());
+      nf = 1u << fb;
+      est_fine /= nf;
+      if ((rc = prepare_ctgs())) return rc;
+      // the output: survivors have count >= 2, so at most owned / 2 read k-mers (+ the contig k-mers); the sketch
+      // bounds them by the distinct keys, of which half is a generous guess (C2: 52M survivors of 207M distinct)
+      out_cap = owned / 2;
+      if (est > 0) out_cap = std::min<uint64_t>(out_cap, (uint64_t)(0.5 * est * no) + (1u << 20));
+      if (const char *env = getenv("MHMKC_DEBUG_OUT_CAP")) out_cap = strtoull(env, nullptr, 10);  // tests only
+      out_cap += ctg_n + 1;
+      if ((e = grow(d_out_keys, out_cap * 8 * nlo)) != hipSuccess || (e = grow(d_out_counts, out_cap * 2)) != hipSuccess ||
+          (e = grow(d_out_left, out_cap)) != hipSuccess || (e = grow(d_out_right, out_cap)) != hipSuccess ||
+          (e = grow(d_out_cursor, 8)) != hipSuccess)
+        return hip_fail(e, "output");
+    }
+    const uint32_t n_fine = np_ * nf;
+    st.fine_buckets += n_fine;
+
+    // capped fine layout of the pass
+    std::vector<uint64_t> cfit(2 * (size_t)np_);  // [coarse_base | coarse_fcap]
+    uint64_t r2_size = 0;
+    for (uint32_t c = 0; c < np_; c++) {
+      const uint64_t ex = per_coarse[c] >> fb;
+      const uint64_t fcap = align_up(ex + ex / 4 + 256, 16);
+      cfit[c] = r2_size;
+      cfit[np_ + c] = fcap;
+      r2_size += fcap << fb;
+    }
+    if ((e = hipMemcpyAsync(d_cfit, cfit.data(), 16 * (size_t)np_, hipMemcpyHostToDevice, stream)) != hipSuccess)
+      return hip_fail(e, "layout H2D");
+    if ((e = grow(d_fine_hist, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
+    if ((e = grow(d_fine_base, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
+    if ((e = grow(d_fine_cursor, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine cursor");
+
+    mhm::PartitionParams pp{};
+    pp.runs = d_runs;
+    pp.chunk_run = d_chunk_run;
+    pp.n_runs = (uint32_t)runs.size();
+    pp.n_chunks = (uint32_t)n_chunks;
+    for (int x = 0; x < 9; x++) pp.xcd_start[x] = (uint32_t)xcd_start[x];
+    pp.grid = (uint32_t)(8 * xcd_max);
+    pp.srcs = d_srcs.as<mhm::PlaneSet>();
+    pp.k = k;
+    pp.coarse_bits = cb;
+    pp.fine_bits = fb;
+    pp.hbits = hbits;
+    pp.compact = mixed();
+    pp.fine_hist = d_fine_hist.as<unsigned long long>();
+    pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
+    pp.err = d_err.as<unsigned int>();
+
+    mhm::CountParams cp{};
+    cp.bucket_base = d_fine_base.as<unsigned long long>();
+    cp.bucket_end = d_fine_cursor.as<unsigned long long>();
+    cp.hbits = hbits;
+    cp.compact = mixed();
+    cp.coarse_bits = cb;
+    cp.fine_bits = fb;
+    cp.bucket0 = (own_lo + c0) << fb;
+    cp.n_buckets = n_fine;
+    cp.grid = (uint32_t)std::max(0, n_cu * mhm::C_SPLIT);  // persistent workgroups filling every CU's LDS
+    cp.k = k;
+    cp.cap = mhm::count_cap(nl, compact);
+    // The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
+    // LDS table (C2: 0.44). The table k_count clears and finalizes per bucket is cut to CAP_LOAD of the estimate
+    // (multiples of 64 slots): both passes cost per slot, not per key.
+    if (est_fine > 0 && CAP_LOAD > 0) {
+      const double want = est_fine / CAP_LOAD;
+      const uint32_t fit = (uint32_t)std::min<double>(cp.cap, std::max(1024.0, std::ceil(want / 64.0) * 64.0));
+      cp.cap = std::min(cp.cap, (int)fit);
+    }
+    st.table_slots = (uint64_t)cp.cap;
+    if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
+    cp.dmin_thres = dmin;
+    cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
+    cp.nlo = nlo;
+    cp.out_cursor = d_out_cursor.as<unsigned long long>();
+    cp.stats = d_stats.as<unsigned long long>();
+    cp.err = d_err.as<unsigned int>();
+    cp.ctg_n = ctg_n;
+    for (int w = 0; w < 4; w++) cp.ctg_keys[w] = w < nl ? d_ctg_keys[w].as<uint64_t>() : nullptr;
+    cp.ctg_state = d_ctg_state.as<uint32_t>();
+    cp.ctg_bucket = d_ctg_bucket.as<uint32_t>();
+    cp.ctg_done = d_ctg_done.as<uint8_t>();
+    cp.ctg_base = c0 << fb;
+
+    bool exact = exact_env;
+    unsigned long long stats[mhm::STAT_ALLOC], cursor_end = 0;
+    for (int attempt = 0;; attempt++) {
+      if (attempt >= 4) return fail(MHMKC_EHIP, "internal: finish pass %d did not settle", pass);
+      mhm::PlaneSet r2{};
+      if (exact) {  // (k_scan rounds every bucket up to a multiple of 4 records)
+        if ((rc = set_planes(d_r2, owned_p + 3 * (uint64_t)n_fine + 4, r2, true))) return rc;
+      } else {
+        if ((rc = set_planes(d_r2, r2_size, r2, true))) return rc;
+      }
+      cp.out_keys = d_out_keys.as<uint64_t>();
+      cp.out_counts = d_out_counts.as<uint16_t>();
+      cp.out_left = d_out_left.as<char>();
+      cp.out_right = d_out_right.as<char>();
+      cp.out_cap = out_cap;
+      const unsigned long long cur0 = out_used;
       prof_begin(MHMKC_STAGE_OTHER);
-      e = mhm::launch_scan(d_fine_hist.as<unsigned long long>(), d_fine_base.as<unsigned long long>(),
-                           d_fine_cursor.as<unsigned long long>(), n_fine, stream);
+      e = hipMemcpyAsync(d_out_cursor.p, &cur0, 8, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_ALLOC, stream);
+      if (e == hipSuccess && ctg_n) e = hipMemsetAsync(d_ctg_done.p, 0, ctg_n, stream);  // (earlier passes' are done)
+      if (e == hipSuccess && exact) e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
+      if (e == hipSuccess && !exact)
+        e = mhm::launch_init_fine(d_cfit, d_cfit + np_, np_, fb, d_fine_base.as<unsigned long long>(),
+                                  d_fine_cursor.as<unsigned long long>(), stream);
       prof_end();
-      if (e != hipSuccess) return hip_fail(e, "scan");
-    } else {
-      pp.coarse_base = d_cfit;
-      pp.coarse_fcap = d_cfit + no;
+      if (e != hipSuccess) return hip_fail(e, "fine layout");
+      if (exact) {
+        pp.coarse_base = nullptr;
+        pp.coarse_fcap = nullptr;
+        prof_begin(MHMKC_STAGE_SHIST);
+        e = mhm::launch_part_hist(pp, nl, packed, stream);
+        prof_end();
+        if (e != hipSuccess) return hip_fail(e, "part_hist");
+        prof_begin(MHMKC_STAGE_OTHER);
+        e = mhm::launch_scan(d_fine_hist.as<unsigned long long>(), d_fine_base.as<unsigned long long>(),
+                             d_fine_cursor.as<unsigned long long>(), n_fine, stream);
+        prof_end();
+        if (e != hipSuccess) return hip_fail(e, "scan");
+      } else {
+        pp.coarse_base = d_cfit;
+        pp.coarse_fcap = d_cfit + np_;
+      }
+      pp.out = r2;
+      prof_begin(MHMKC_STAGE_SSCAT);
+      e = mhm::launch_part_scatter(pp, nl, packed, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "part_scatter");
+      cp.recs = r2;
+      prof_begin(MHMKC_STAGE_COUNT);
+      e = mhm::launch_count(cp, nl, packed, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "count");
+      (void)hipEventRecord(ev_end, stream);
+      if ((e = hipMemcpyAsync(stats, d_stats.p, sizeof stats, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(&cursor_end, d_out_cursor.p, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipStreamSynchronize(stream)) != hipSuccess)
+        return hip_fail(e, "finish");
+      if (!(errf & (2u | 16u))) break;
+      if (errf & 2u) {  // a capped fine bucket overflowed (skewed input): the pass again with exact bucket sizes
+        exact = true;
+        st.exact_reruns++;
+      } else if (errf & 16u) {  // the output is full: grow it to the rows the cursor counted, keep the earlier passes'
+        const uint64_t need = cursor_end + cursor_end / 16 + 1024;
+        if ((e = grow_keep(d_out_keys, out_used * 8 * nlo, need * 8 * nlo)) != hipSuccess ||
+            (e = grow_keep(d_out_counts, out_used * 2, need * 2)) != hipSuccess ||
+            (e = grow_keep(d_out_left, out_used, need)) != hipSuccess ||
+            (e = grow_keep(d_out_right, out_used, need)) != hipSuccess)
+          return hip_fail(e, "output growth");
+        out_cap = need;
+        st.out_reruns++;
+      }
+      errf &= ~(2u | 16u);
+      if ((e = hipMemcpy(d_err.p, &errf, 4, hipMemcpyHostToDevice)) != hipSuccess) return hip_fail(e, "flag reset");
     }
-    pp.out = r2;
-    prof_begin(MHMKC_STAGE_SSCAT);
-    e = mhm::launch_part_scatter(pp, nl, packed, stream);
-    prof_end();
-    if (e != hipSuccess) return hip_fail(e, "part_scatter");
-    cp.recs = r2;
-    prof_begin(MHMKC_STAGE_COUNT);
-    e = mhm::launch_count(cp, nl, packed, stream);
-    prof_end();
-    if (e != hipSuccess) return hip_fail(e, "count");
-    (void)hipEventRecord(ev_end, stream);
-    if ((e = hipMemcpyAsync(stats, d_stats.p, sizeof stats, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-      return hip_fail(e, "stats D2H");
-    if ((e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-      return hip_fail(e, "error flag D2H");
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(e, "finish");
-    if (!(errf & 2u)) break;
-    errf &= ~2u;
-    if ((e = hipMemcpy(d_err.p, &errf, 4, hipMemcpyHostToDevice)) != hipSuccess) return hip_fail(e, "flag reset");
-    exact = true;
-    st.exact_reruns++;
+    if (stats[mhm::STAT_N - 1]) return fail(MHMKC_EHIP, "internal: LDS probe bound exceeded");
+    for (int i = 0; i < mhm::STAT_ALLOC; i++)
+      acc_stats[i] = i == mhm::STAT_MAXBUCKET ? std::max(acc_stats[i], stats[i]) : acc_stats[i] + stats[i];
+    out_used = cursor_end;
+    srcs.resize(n_srcs0);  // (the pass's received-supermer records)
   }
+  if (smer && smer_seen != smer_nwin)
+    return fail(MHMKC_EHIP, "internal: the finish passes extracted %llu of %llu received windows",
+                (unsigned long long)smer_seen, (unsigned long long)smer_nwin);
   float ms = 0;
   if (hipEventElapsedTime(&ms, ev_begin, ev_end) == hipSuccess) st.ms_total = ms;
   finished = true;
   if (errf & 1u) return fail(MHMKC_EBADCHAR, "input byte with a base code > 4 (not A,C,G,T,N)");
   if (errf & 8u) return fail(MHMKC_EHIP, "internal: supermer spans inconsistent");
-  if (stats[mhm::STAT_N - 1]) return fail(MHMKC_EHIP, "internal: LDS probe bound exceeded");
   if (getenv("MHMKC_PRINT_STAMPS")) {  // k_count phase cycles of an MHMKC_STAMP build (diagnostics)
     const char *names[6] = {"clear", "loadwait", "insert", "barrier", "overflow", "finalize"};
     double tot = 0;
-    for (int i = 0; i < 6; i++) tot += (double)stats[8 + i];
+    for (int i = 0; i < 6; i++) tot += (double)acc_stats[8 + i];
     fprintf(stderr, "k_count stamps:");
-    for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f%%", names[i], tot > 0 ? 100.0 * stats[8 + i] / tot : 0.0);
+    for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f%%", names[i], tot > 0 ? 100.0 * acc_stats[8 + i] / tot : 0.0);
     fprintf(stderr, " (total %.3g wave-cycles)\n", tot);
   }
-  st.distinct = stats[mhm::STAT_DISTINCT];
-  st.n_out = stats[mhm::STAT_NOUT];
-  st.purged = stats[mhm::STAT_PURGED];
-  st.count_sum = stats[mhm::STAT_COUNTSUM];
-  st.overflow_sweeps = stats[mhm::STAT_SWEEPS];
-  st.max_bucket = stats[mhm::STAT_MAXBUCKET];
-  st.lds_misses = stats[mhm::STAT_MISSES];
+  st.distinct = acc_stats[mhm::STAT_DISTINCT];
+  st.n_out = acc_stats[mhm::STAT_NOUT];
+  st.purged = acc_stats[mhm::STAT_PURGED];
+  st.count_sum = acc_stats[mhm::STAT_COUNTSUM];
+  st.overflow_sweeps = acc_stats[mhm::STAT_SWEEPS];
+  st.max_bucket = acc_stats[mhm::STAT_MAXBUCKET];
+  st.lds_misses = acc_stats[mhm::STAT_MISSES];
   st.dropped = 0;
   n_out = st.n_out;
-  if (n_out > out_cap) return fail(MHMKC_EHIP, "internal: output overflow");
+  if (n_out != out_used) return fail(MHMKC_EHIP, "internal: output rows %llu, cursor %llu", (unsigned long long)n_out,
+                                     (unsigned long long)out_used);
   if (cfg.output_owner == MHMKC_OWNER_MINIMIZER && G() > 1 && !smer) {  // (supermers already went to that owner)
     if ((rc = handoff())) return rc;
   }
+  st.device_bytes = g_dev_live.load();
+  st.device_bytes_peak = g_dev_peak.load();
   prof_collect();
   if (n_out_ret) *n_out_ret = n_out;
   return MHMKC_OK;
@@ -1863,6 +2012,7 @@ void mhmkc_destroy(mhmkc_t h) {
   if (h->ev_xdone) (void)hipEventDestroy(h->ev_xdone);
   if (h->ev_xext) (void)hipEventDestroy(h->ev_xext);
   if (h->xstream) (void)hipStreamDestroy(h->xstream);
+  if (h->smer_slab) h->slabs.push_back(h->smer_slab);
   for (Slab *s : h->slabs) {
     if (s->ev) (void)hipEventDestroy(s->ev);
     s->buf.release();

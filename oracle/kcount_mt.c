@@ -83,11 +83,21 @@ static int bin_push(mt_bin *b, const uint64_t *key, int nl, uint8_t e) {
   return 1;
 }
 
+/* Key range of a canonical k-mer for a table built one part at a time (orc_kcount_mt_range): a one-multiply mix of
+ * the first and last key words, cheap next to mt_hash, so that a pass over all windows spends the hash and the
+ * binning only on the windows of its range. Any function of the key partitions the table; this one is the checker's
+ * own (not the product's owner function). */
+static inline uint32_t mt_range(const uint64_t *key, int nl, uint32_t n_ranges) {
+  const uint64_t x = (key[0] * 0x9E3779B97F4A7C15ULL ^ key[nl - 1]) * 0xD6E8FEB86659FD93ULL;
+  return (uint32_t)(((x >> 32) * (uint64_t)n_ranges) >> 32);
+}
+
 typedef struct {
   /* input */
   const uint8_t *bytes;
   const uint64_t *offs;
   uint64_t r0, r1;
+  uint32_t range, n_ranges; /* keep only the k-mers with mt_range == range */
   int k, nl, qcut, dmin;
   double dyn_mult; /* 1.0 - DYN_MIN_DEPTH, in double as the reference computes it */
   int nthreads;
@@ -166,6 +176,7 @@ static void *mt_extract(void *arg) {
           break;
         }
       const uint64_t *key = use_rc ? rc : fw;
+      if (w->n_ranges > 1 && mt_range(key, nl, w->n_ranges) != w->range) continue;
       if (use_rc) { /* complement and swap (comp_nucleotide, src/utils.cpp:121-143) */
         const int nl_ = rr < 4 ? 3 - rr : 4, nr_ = l < 4 ? 3 - l : 4;
         l = nl_;
@@ -329,9 +340,12 @@ typedef struct {
   uint64_t occurrences, purged, reads;
 } mt_table;
 
-/* Returns NULL on bad input (a base code > 4: the reference DIEs) or allocation failure. */
-mt_table *orc_kcount_mt(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int k, int n_longs,
-                        int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads) {
+/* The part `range` of n_ranges of the table (the k-mers with mt_range(key) == range): a table too large for host
+ * memory at once (C3: 1.28e10 occurrences) is built and compared one part at a time. Returns NULL on bad input (a
+ * base code > 4: the reference DIEs) or allocation failure. */
+mt_table *orc_kcount_mt_range(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int k, int n_longs,
+                              int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads, int range,
+                              int n_ranges) {
   const int nl = k / 32 + 1;
   if (k < 1 || k > 127 || k % 32 == 0 || n_longs < nl || n_longs > 8) return NULL;
   if (threads < 1) threads = 1;
@@ -350,6 +364,8 @@ mt_table *orc_kcount_mt(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     w[t].dmin = dmin_thres;
     w[t].dyn_mult = 1.0 - dyn_min_depth;
     w[t].nthreads = threads;
+    w[t].range = (uint32_t)range;
+    w[t].n_ranges = n_ranges < 1 ? 1u : (uint32_t)n_ranges;
     w[t].bins = (mt_bin *)calloc(MT_PARTS, sizeof(mt_bin));
     if (!w[t].bins) return NULL;
   }
@@ -424,4 +440,27 @@ mt_table *orc_kcount_mt(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   free(w);
   free(tid);
   return out;
+}
+
+/* The whole table (one range). */
+mt_table *orc_kcount_mt(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int k, int n_longs,
+                        int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads) {
+  return orc_kcount_mt_range(bytes, offs, n_reads, k, n_longs, qual_cutoff, dmin_thres, dyn_min_depth, threads, 0, 1);
+}
+
+/* mt_range of n keys (stride words per row, the first nl used) into out[n]: the part of each row of a GPU table. */
+void orc_mt_ranges(const uint64_t *keys, uint64_t n, int stride, int nl, int n_ranges, uint8_t *out) {
+  for (uint64_t i = 0; i < n; i++) out[i] = (uint8_t)mt_range(keys + i * (uint64_t)stride, nl, (uint32_t)n_ranges);
+}
+
+/* A 64-bit fingerprint of every row (key words, count, left, right) into out[n]: sorted, two tables' fingerprint
+ * lists are compared element by element (equal tables give equal lists; a differing row changes its fingerprint). */
+void orc_row_fingerprints(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n,
+                          int stride, int nl, uint64_t *out) {
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t h = 0x243F6A8885A308D3ULL;
+    for (int w = 0; w < nl; w++) h = mt_fmix(h ^ keys[i * (uint64_t)stride + w]) + 0x9E3779B97F4A7C15ULL;
+    h = mt_fmix(h ^ ((uint64_t)counts[i] | (uint64_t)(uint8_t)left[i] << 16 | (uint64_t)(uint8_t)right[i] << 24));
+    out[i] = h;
+  }
 }

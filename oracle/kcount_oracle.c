@@ -252,6 +252,11 @@ int orc_kmer_target_rank(const uint64_t *longs, int k, int n_longs, int rank_n) 
   return (int)(orc_minimizer_hash_fast(longs, k, n_longs, orc_minimizer_len(k)) % (uint64_t)rank_n);
 }
 
+/* orc_kmer_target_rank of n keys (stride words per row) into out[n]. */
+void orc_kmer_target_ranks(const uint64_t *keys, uint64_t n, int stride, int k, int n_longs, int rank_n, uint8_t *out) {
+  for (uint64_t i = 0; i < n; i++) out[i] = (uint8_t)orc_kmer_target_rank(keys + i * (uint64_t)stride, k, n_longs, rank_n);
+}
+
 /* ---------------------------------------------------------------------------------------------
  * ExtCounts / KmerExtsCounts (src/kcount/kcount_cpu.cpp:115-200) */
 

@@ -187,3 +187,60 @@ def run_bad_offsets(rank: int, world: int, port: int, k: int, out_dir: str, opts
     c.close()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
+    """One rank of C3 / C4 as configured: reads [rank * R, (rank + 1) * R) of the config's 1e8-read
+    set (genome opts["genome"], seed opts["seed"]) counted with opts["owner"], exchanged over the host transport, the
+    owned range counted in opts["passes"] finish passes. The rank's rows leave as (key-range part, row fingerprint)
+    pairs for the parent's part-by-part comparison with the CPU restatement; with the minimizer owner every row is
+    first checked to be on its get_kmer_target_rank."""
+    import time
+
+    import torch.distributed as dist
+
+    import mhm2_proxy_amd as m
+    import oracle_lib as O
+
+    t0 = time.time()
+
+    def say(what):
+        print(f"[rank {rank} {time.time() - t0:6.1f}s] {what}", flush=True)
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MHMKC_XPIPE=opts.get("xpipe", "1"),
+                      MHMKC_PASSES=str(opts.get("passes", 4)))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R = opts["reads_per_rank"]
+    g = m.synth_genome(opts["genome"], opts["seed"])
+    b, o = m.synth_reads(g, R, 150, opts["seed"], first_read=rank * R, threads=2)
+    del g
+    say(f"{R} reads")
+    owner = m.MHMKC_OWNER_MINIMIZER if opts.get("owner") == "minimizer" else m.MHMKC_OWNER_HASH
+    c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner)
+    dist.barrier()
+    t1 = time.time()
+    c.add_packed_reads(b, o)
+    del b, o
+    c.finish()
+    t_count = time.time() - t1
+    st = c.stats()
+    say(f"counted in {t_count:.1f} s: {st['n_out']} rows, {st['finish_passes']} passes, device "
+        f"{st['device_bytes'] / 2**30:.1f} GiB (peak {st['device_bytes_peak'] / 2**30:.1f} GiB), sent "
+        f"{st['bytes_sent'] / 2**30:.2f} GiB")
+    t = c.fetch()
+    c.close()
+    if owner == m.MHMKC_OWNER_MINIMIZER:
+        off = np.flatnonzero(O.target_ranks(t.keys, k, world) != rank)
+        assert off.size == 0, f"rank {rank}: {off.size} rows not on their target rank"
+    parts = O.mt_ranges(t.keys, k, opts["n_parts"])
+    fps = O.row_fingerprints(t.keys, t.counts, t.left, t.right, k)
+    del t
+    np.save(Path(out_dir) / f"rank{rank}_parts.npy", parts)
+    np.save(Path(out_dir) / f"rank{rank}_fps.npy", fps)
+    say(f"{fps.size} row fingerprints saved")
+    np.savez(Path(out_dir) / f"rank{rank}_stats.npz", seconds=t_count,
+             **{key: st[key] for key in ("occurrences", "owned_records", "bytes_sent", "bytes_recv", "exact_reruns",
+                                         "smer_count", "n_out", "distinct", "finish_passes", "out_reruns",
+                                         "device_bytes", "device_bytes_peak", "xchg_rounds", "ms_xchg")})
+    dist.barrier()
+    dist.destroy_process_group()

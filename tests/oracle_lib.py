@@ -48,6 +48,14 @@ def oracle() -> C.CDLL:
         L.orc_kcount.restype = VP
         L.orc_kcount_mt.argtypes = [VP, VP, U64, I, I, I, I, C.c_double, I]
         L.orc_kcount_mt.restype = VP
+        L.orc_kcount_mt_range.argtypes = [VP, VP, U64, I, I, I, I, C.c_double, I, I, I]
+        L.orc_kcount_mt_range.restype = VP
+        L.orc_mt_ranges.argtypes = [VP, U64, I, I, I, VP]
+        L.orc_mt_ranges.restype = None
+        L.orc_row_fingerprints.argtypes = [VP, VP, VP, VP, U64, I, I, VP]
+        L.orc_row_fingerprints.restype = None
+        L.orc_kmer_target_ranks.argtypes = [VP, U64, I, I, I, I, VP]
+        L.orc_kmer_target_ranks.restype = None
         L.orc_kcount_ctgs.argtypes = [VP, VP, U64, VP, VP, VP, U64, I, I, I, I, C.c_double]
         L.orc_kcount_ctgs.restype = VP
         L.orc_extract.argtypes = [VP, VP, U64, I, I, I, VP, VP, U64]
@@ -129,6 +137,48 @@ def kcount_mt(packed_bytes, offsets, k, n_longs=None, qual_cutoff=20, dmin_thres
     ptr = oracle().orc_kcount_mt(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, dmin_thres,
                                  dyn_min_depth, threads)
     return OracleTable(ptr, nl, k)
+
+
+def kcount_mt_range(packed_bytes, offsets, k, part, n_parts, threads=8, qual_cutoff=20, dmin_thres=2,
+                    dyn_min_depth=0.9) -> OracleTable:
+    """Part `part` of n_parts of the multi-threaded restatement's table (the k-mers whose mt_range is `part`,
+    oracle/kcount_mt.c): a table too large for host memory is built and checked one part at a time."""
+    nl = k // 32 + 1
+    b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ptr = oracle().orc_kcount_mt_range(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, dmin_thres,
+                                       dyn_min_depth, threads, part, n_parts)
+    return OracleTable(ptr, nl, k)
+
+
+def mt_ranges(keys, k, n_parts):
+    """The kcount_mt_range part of every row of an (n, n_longs) key array."""
+    kk = np.ascontiguousarray(keys, dtype=np.uint64)
+    out = np.empty(kk.shape[0], dtype=np.uint8)
+    oracle().orc_mt_ranges(kk.ctypes.data, kk.shape[0], kk.shape[1] if kk.ndim == 2 else 1, k // 32 + 1, n_parts,
+                           out.ctypes.data)
+    return out
+
+
+def row_fingerprints(keys, counts, left, right, k):
+    """A 64-bit fingerprint of every (key, count, left, right) row (oracle/kcount_mt.c orc_row_fingerprints)."""
+    kk = np.ascontiguousarray(keys, dtype=np.uint64)
+    c = np.ascontiguousarray(counts, dtype=np.uint16)
+    lft = np.ascontiguousarray(left).view(np.uint8)
+    rgt = np.ascontiguousarray(right).view(np.uint8)
+    out = np.empty(kk.shape[0], dtype=np.uint64)
+    oracle().orc_row_fingerprints(kk.ctypes.data, c.ctypes.data, lft.ctypes.data, rgt.ctypes.data, kk.shape[0],
+                                  kk.shape[1] if kk.ndim == 2 else 1, k // 32 + 1, out.ctypes.data)
+    return out
+
+
+def target_ranks(keys, k, rank_n):
+    """KmerDHT::get_kmer_target_rank of every row (oracle restatement, src/kcount/kmer_dht.cpp:193-196)."""
+    kk = np.ascontiguousarray(keys, dtype=np.uint64)
+    out = np.empty(kk.shape[0], dtype=np.uint8)
+    oracle().orc_kmer_target_ranks(kk.ctypes.data, kk.shape[0], kk.shape[1] if kk.ndim == 2 else 1, k, k // 32 + 1,
+                                   rank_n, out.ctypes.data)
+    return out
 
 
 def kcount_ctgs(packed_bytes, offsets, ctg_seqs, ctg_depths, k, n_longs=None, qual_cutoff=20, dmin_thres=2,

@@ -555,3 +555,41 @@ def test_fetch_ordered(k, nl):
     assert_tables_equal(ordered, plain, "ordered fetch")
     top = np.array([m.kcount.map_hash(row) >> 32 for row in ordered.keys.tolist()], dtype=np.uint64)
     assert len(top) > 1000 and (np.diff(top.astype(np.int64)) >= 0).all()
+
+
+@pytest.mark.parametrize("k,passes", [(21, "3"), (33, "2"), (63, "5"), (99, "4"), (77, "256"), (19, "7")])
+def test_finish_passes_vs_oracle(k, passes, monkeypatch):
+    """The owned hash range counted in several finish passes (MHMKC_PASSES: each pass fine-partitions and counts its
+    coarse buckets into the same buffer and appends its survivors to the output): the table is the one-pass table."""
+    monkeypatch.setenv("MHMKC_PASSES", passes)
+    b, o = synth_set(2500, 12000, 600 + k)
+    got, st = hip_table(b, o, k, batches=2)
+    assert st["finish_passes"] == min(int(passes), 128 if k > 64 else 256)
+    assert_tables_equal(got, oracle_table(b, o, k), f"{passes} passes, k={k}")
+    check_stats(st)
+
+
+@pytest.mark.parametrize("k,passes", [(21, "4"), (63, "3"), (99, "2")])
+def test_finish_passes_with_contigs(k, passes, monkeypatch):
+    """Contig k-mers are folded once and applied in the pass that counts their bucket (CountParams.ctg_base)."""
+    monkeypatch.setenv("MHMKC_PASSES", passes)
+    b, o, seqs, depths = ctg_set(seed=610 + k)
+    got, st = ctg_table(b, o, seqs, depths, k)
+    assert st["ctg_kmers"] > 0 and st["finish_passes"] == int(passes)
+    assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, k), f"contigs over {passes} passes, k={k}")
+
+
+@pytest.mark.parametrize("k,passes,exact", [(21, "1", False), (21, "3", False), (63, "2", True), (99, "1", False)])
+def test_output_overflow_redoes_the_pass(k, passes, exact, monkeypatch):
+    """An output sized too small (MHMKC_DEBUG_OUT_CAP rows) fills: the pass writes nothing past it, the output grows to
+    the rows its cursor counted (the earlier passes' rows kept) and the pass is redone; the table is unchanged."""
+    monkeypatch.setenv("MHMKC_PASSES", passes)
+    monkeypatch.setenv("MHMKC_DEBUG_OUT_CAP", "100")
+    if exact:
+        monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+    b, o = synth_set(2500, 12000, 620 + k)
+    got, st = hip_table(b, o, k)
+    assert st["out_reruns"] >= 1
+    assert_tables_equal(got, oracle_table(b, o, k), f"output overflow, {passes} passes, k={k}")
+    check_stats(st)
+    assert st["device_bytes_peak"] >= st["device_bytes"] > 0

@@ -82,7 +82,10 @@ def test_minimizer_owner_handoff(k, world, seed, tmp_path):
 
 
 @pytest.mark.parametrize("k,world,env", [(63, 2, {"MHMKC_SMER": "0"}), (99, 2, {"MHMKC_SMER": "0"}),
-                                         (63, 3, {"MHMKC_DEBUG_EXACT": "1"}), (33, 2, {"MHMKC_CHUNK_BYTES": "3000"})])
+                                         (63, 3, {"MHMKC_DEBUG_EXACT": "1"}), (33, 2, {"MHMKC_CHUNK_BYTES": "3000"}),
+                                         (63, 3, {"MHMKC_PASSES": "3"}), (99, 2, {"MHMKC_PASSES": "5"}),
+                                         (55, 2, {"MHMKC_PASSES": "4", "MHMKC_DEBUG_EXACT": "1"}),
+                                         (63, 2, {"MHMKC_PASSES": "2", "MHMKC_DEBUG_OUT_CAP": "50"})])
 def test_supermer_exchange_variants(k, world, env, tmp_path):
     """MHMKC_OWNER_MINIMIZER at k >= 33 ships supermers; MHMKC_SMER=0 keeps the record exchange +
     hand-off; the exact (histogram) layout of the received records; many H2D chunks = many supermer slabs."""
@@ -102,6 +105,7 @@ def test_supermer_exchange_variants(k, world, env, tmp_path):
 
 @pytest.mark.parametrize("k,world,opts", [
     (21, 2, {}), (33, 3, {}), (63, 2, {}), (99, 2, {}), (21, 3, {"minimizer": True}),
+    (21, 3, {"env": {"MHMKC_PASSES": "3"}}), (21, 2, {"minimizer": True, "env": {"MHMKC_PASSES": "2"}}),
     (21, 2, {"env_by_rank": {0: {"MHMKC_CHUNK_BYTES": "2000"}}}),   # rank 0: ~20 slabs, rank 1: a few
     (63, 3, {"idle_rank": 0}),                                          # a rank with no slab at all
     (21, 2, {"env": {"MHMKC_DEBUG_EXACT": "1"}}),
@@ -283,3 +287,52 @@ def test_device_offsets_not_from_zero_refused(xpipe, tmp_path):
              nprocs=world, join=True)
     codes = [int(np.load(tmp_path / f"rank{r}.npz")["code"]) for r in range(world)]
     assert codes == [-1] * world, codes
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(1150)
+@pytest.mark.parametrize("cfg", ["C3", "C4"])
+def test_c3_c4_eight_ranks_vs_cpu_restatement(cfg, tmp_path):
+    """C3 (1e8 x 150 bp, G = 500 Mbp, seed 3, k = 21, hash-range owner) and C4 (the same reads at
+    k = 63 with MHMKC_OWNER_MINIMIZER: the supermer exchange) as configured, as 8 ranks of 12.5M reads sharing the one
+    GPU over the host transport, each counting its owned range in 4 finish passes. The union of the 8 tables is
+    compared with the multi-threaded CPU restatement (oracle/kcount_mt.c) row by row, one key-range part at a time
+    (kcount_mt_range: the 1e8-read table does not fit host memory at once): in each part the sorted lists of 64-bit
+    row fingerprints (key words, count, left, right) must be equal. C4 also checks every row's target rank."""
+    import torch.multiprocessing as mp
+
+    import mr_gpu_worker
+
+    world, n_parts = 8, 8
+    k, owner = (21, "hash") if cfg == "C3" else (63, "minimizer")
+    opts = {"reads_per_rank": 12_500_000, "genome": 500_000_000, "seed": 3, "owner": owner, "passes": 4,
+            "n_parts": n_parts}
+    t0 = time.time()
+    mp.spawn(mr_gpu_worker.run_share_full, args=(world, free_port(), k, str(tmp_path), opts), nprocs=world, join=True)
+    stats = [dict(np.load(tmp_path / f"rank{r}_stats.npz")) for r in range(world)]
+    assert sum(int(s["owned_records"]) for s in stats) == sum(int(s["occurrences"]) for s in stats) == \
+        100_000_000 * (150 - k - 1)
+    assert sum(int(s["bytes_sent"]) for s in stats) == sum(int(s["bytes_recv"]) for s in stats) > 0
+    assert all(int(s["finish_passes"]) == 4 for s in stats)
+    print(f"[parent {time.time() - t0:6.1f}s] {cfg}: 8 ranks counted; per rank: "
+          + ", ".join(f"{float(s['seconds']):.1f} s / {int(s['device_bytes_peak']) / 2**30:.1f} GiB peak" for s in stats),
+          flush=True)
+    parts = np.concatenate([np.load(tmp_path / f"rank{r}_parts.npy") for r in range(world)])
+    fps = np.concatenate([np.load(tmp_path / f"rank{r}_fps.npy") for r in range(world)])
+    assert fps.size == sum(int(s["n_out"]) for s in stats)
+    g = m.synth_genome(500_000_000, 3)
+    b, o = m.synth_reads(g, world * 12_500_000, 150, 3, threads=16)
+    del g
+    print(f"[parent {time.time() - t0:6.1f}s] {o.size - 1} reads regenerated", flush=True)
+    rows = 0
+    for p in range(n_parts):
+        t = O.kcount_mt_range(b, o, k, p, n_parts, threads=16)
+        exp = np.sort(O.row_fingerprints(*t.fetch(), k))
+        del t
+        got = np.sort(fps[parts == p])
+        rows += exp.size
+        print(f"[parent {time.time() - t0:6.1f}s] part {p}: {exp.size} rows (CPU) vs {got.size} (GPU)", flush=True)
+        assert got.size == exp.size, f"{cfg} part {p}: {got.size} GPU rows vs {exp.size}"
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, f"{cfg} part {p}: {bad.size} rows differ"
+    assert rows == fps.size

@@ -240,3 +240,34 @@ def test_mt_restatement_reproduces_golden(name):
     t = O.kcount_mt(b, o, k, threads=4)
     keys, c, l, r = t.fetch()
     assert_tables_equal(m.KmerTable(k, keys, c, l, r), read_table_file(GOLDEN / name, k), name)
+
+
+@pytest.mark.parametrize("k,parts", [(21, 8), (63, 5), (99, 3)])
+def test_mt_range_parts_union_is_the_table(k, parts):
+    """kcount_mt built one key range at a time (the C3/C4 8-rank check builds a 1e8-read table that way): the parts
+    are disjoint, every row is in the part mt_ranges names, and their union is the whole table; row fingerprints of
+    equal tables are equal multisets and a changed row changes its fingerprint."""
+    b, o = synth_set(3000, 20000, 700 + k)
+    whole = O.kcount_mt(b, o, k, threads=4).fetch()
+    fw = np.sort(O.row_fingerprints(*whole, k))
+    got = []
+    for p in range(parts):
+        t = O.kcount_mt_range(b, o, k, p, parts, threads=4).fetch()
+        assert (O.mt_ranges(t[0], k, parts) == p).all()
+        got.append(O.row_fingerprints(*t, k))
+    assert np.array_equal(np.sort(np.concatenate(got)), fw)
+    keys, c, lft, rgt = whole
+    assert (O.mt_ranges(keys, k, parts) < parts).all()
+    c2 = c.copy()
+    c2[0] ^= 1
+    assert not np.array_equal(np.sort(O.row_fingerprints(keys, c2, lft, rgt, k)), fw)
+
+
+@pytest.mark.parametrize("k,world", [(21, 8), (63, 8), (77, 3)])
+def test_batch_target_ranks(k, world):
+    b, o = synth_set(400, 5000, 720 + k)
+    keys = O.kcount(b, o, k).fetch()[0]
+    L = O.oracle()
+    exp = [L.orc_kmer_target_rank(np.ascontiguousarray(keys[i]).ctypes.data, k, keys.shape[1], world)
+           for i in range(len(keys))]
+    assert O.target_ranks(keys, k, world).tolist() == exp
