@@ -76,22 +76,34 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: libmhmkc.so cannot be built")
 
 
+def _compile_lib(out: Path, bid: str, extra=(), tag: str = "main") -> None:
+    """One hipcc per source, in parallel (the kernels file dominates), then one link."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    obj_dir = ROOT / "build" / f"obj_{tag}"
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    objs = [obj_dir / (src.name + ".o") for src in LIB_SOURCES]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f'-DMHMKC_BUILD_ID="{bid}"', *extra]
+    with ThreadPoolExecutor(max_workers=len(LIB_SOURCES)) as ex:
+        list(ex.map(lambda so: _run([hipcc(), *flags, "-c", so[0], "-o", so[1]]), zip(LIB_SOURCES, objs)))
+    tmp = out.with_suffix(".so.tmp")
+    _run([hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-L/opt/rocm/lib", "-lrccl",
+          "-Wl,-rpath,/opt/rocm/lib", "-o", tmp])
+    tmp.replace(out)
+
+
+def build_variant(name: str, defines) -> Path:
+    """exp/libmhmkc_<name>.so with extra -D flags (performance A/B runs; MHMKC_LIB selects it)."""
+    out = ROOT / "exp" / f"libmhmkc_{name}.so"
+    out.parent.mkdir(exist_ok=True)
+    _compile_lib(out, source_build_id(), list(defines), tag=name)
+    return out
+
+
 def build_lib(force: bool = False) -> Path:
     bid = source_build_id()
     if force or _stale(LIB, LIB_DEPS) or lib_build_id() != bid:
-        # one hipcc per source, in parallel (the kernels file dominates), then one link
-        from concurrent.futures import ThreadPoolExecutor
-
-        obj_dir = ROOT / "build" / "obj"
-        obj_dir.mkdir(parents=True, exist_ok=True)
-        objs = [obj_dir / (src.name + ".o") for src in LIB_SOURCES]
-        flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f'-DMHMKC_BUILD_ID="{bid}"']
-        with ThreadPoolExecutor(max_workers=len(LIB_SOURCES)) as ex:
-            list(ex.map(lambda so: _run([hipcc(), *flags, "-c", so[0], "-o", so[1]]), zip(LIB_SOURCES, objs)))
-        tmp = LIB.with_suffix(".so.tmp")
-        _run([hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-L/opt/rocm/lib", "-lrccl",
-              "-Wl,-rpath,/opt/rocm/lib", "-o", tmp])
-        tmp.replace(LIB)
+        _compile_lib(LIB, bid)
     if lib_build_id() != bid:
         raise RuntimeError(f"{LIB} carries build id {lib_build_id()}, the sources make {bid}")
     return LIB
@@ -131,4 +143,7 @@ def build_all(force: bool = False) -> None:
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":  # python -m mhm2_proxy_amd.build --variant NAME -DX=V ...
+        print(build_variant(sys.argv[2], sys.argv[3:]))
+    else:
+        build_all(force="--force" in sys.argv)

@@ -2357,9 +2357,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       nx[j] = PACKED ? 0u : (uint32_t)src.ext[idx];
     }
   };
-  auto bucket = [&](uint32_t bb, PlaneSet &src, uint32_t &cnt) {
-    const uint64_t base = p.bucket_base[bb];
-    cnt = (uint32_t)(p.bucket_end[bb] - base);  // < 2^32 records per bucket (host check)
+  // a bucket's records from its extent [base, end) (< 2^32 records per bucket: host check)
+  auto bucket_at = [&](uint64_t base, uint64_t end, PlaneSet &src, uint32_t &cnt) {
+    cnt = (uint32_t)(end - base);
     src = p.recs;
     if (RK::C32) {
       src.w[0] = (uint64_t *)((uint32_t *)src.w[0] + base);
@@ -2371,6 +2371,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     }
     if (!PACKED) src.ext += base;
   };
+  auto bucket = [&](uint32_t bb, PlaneSet &src, uint32_t &cnt) { bucket_at(p.bucket_base[bb], p.bucket_end[bb], src, cnt); };
 
   // Position of a record deferred to the next sweep. With per-wave queues a wave defers only records it loaded
   // itself, so its d-th deferral goes to its own d-th record position of the sweep (wave-owned positions in round
@@ -2406,6 +2407,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   uint32_t nb_next = 0;
   PlaneSet ps_next;
   const uint32_t b_next = b + gridDim.x;
+  // the next bucket's extent, loaded now so that its first records can be fetched at this bucket's finalize without
+  // a dependent round trip there (unconditional: without a next bucket it re-reads this bucket's, never used)
+  const uint32_t b_ext = b_next < p.n_buckets ? b_next : b;
+  const uint64_t nx_base = p.bucket_base[b_ext], nx_end = p.bucket_end[b_ext];
   while (true) {  // sweeps of bucket b
     STAMP(t_sw0);
     {  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
@@ -2746,8 +2751,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       rounds(std::true_type{});
     else
       rounds(std::false_type{});
+    STAMP(t_b0);
     __syncthreads();
     STAMP(t_f0);
+    STAMP_ADD(3, t_f0 - t_b0);  // (the sweep's end barrier: the waves' imbalance; cold sweeps have no round barrier)
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
     if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
@@ -2757,11 +2764,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       // its own first round), it re-reads this bucket's first records, never used (cnt >= 1 keeps the read at
       // or next to the bucket's base, inside the records' allocation)
       const bool nxt = last_sweep && b_next < p.n_buckets;
-      if (nxt) bucket(b_next, ps_next, nb_next);
+      if (nxt) bucket_at(nx_base, nx_end, ps_next, nb_next);
       const bool use_next = nxt && nb_next;
       prefetch(use_next ? ps_next : ps, use_next ? nb_next : (n ? n : 1u), 0, NONE);
     } else if (last_sweep && b_next < p.n_buckets) {
-      bucket(b_next, ps_next, nb_next);
+      bucket_at(nx_base, nx_end, ps_next, nb_next);
       if (nb_next) prefetch(ps_next, nb_next, 0, NONE);
     }
 

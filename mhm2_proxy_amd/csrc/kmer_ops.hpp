@@ -436,8 +436,9 @@ MHM_HD char ext_choice(uint32_t a, uint32_t c, uint32_t g, uint32_t t, int thr) 
   }
   if ((int)top < thr) return 'X';
   if ((int)second >= thr) return 'F';
-  const char bases[4] = {'A', 'C', 'G', 'T'};
-  return bases[arg];
+  // 'A' 'C' 'G' 'T' = 0x41 0x43 0x47 0x54, one byte each of a constant (a char array here was compiled into a
+  // global-memory table: two dependent loads per decided k-mer in k_count's finalize)
+  return (char)((0x54474341u >> (8 * arg)) & 0xffu);
 }
 
 MHM_HD int dyn_threshold(uint32_t count16, double dyn_mult, int dmin_thres) {
