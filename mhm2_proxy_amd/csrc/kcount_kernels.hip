@@ -1754,6 +1754,11 @@ constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
 #ifndef MHMKC_WDEF
 #define MHMKC_WDEF 1
 #endif
+// Dynamic record slots in cold sweeps (with a spill area, CountParams.spill); 0 = every wave its static share
+#ifndef MHMKC_DYN
+#define MHMKC_DYN 1
+#endif
+constexpr bool kDynSweeps = MHMKC_DYN != 0;
 
 // Two-pass finalize (list the slots with count >= 2, then decide them densely); 0 = one pass over all slots.
 #ifndef MHMKC_FIN2
@@ -2263,7 +2268,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   t.keys = (K *)smem;
   t.cnt = (uint32_t *)(t.keys + NL * t.cap);
   t.ext = t.cnt + t.cap;
-  // scalars live after the table in the same dynamic region (count_lds_bytes adds 192 bytes)
+  // scalars live after the table in the same dynamic region (count_table_bytes adds 256 bytes)
   unsigned long long *s_u64 = (unsigned long long *)(t.ext + 4 * t.cap);
   unsigned long long &s_gbase = s_u64[0];
   unsigned long long *s_red = s_u64 + 1;  // [3]
@@ -2272,6 +2277,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
   unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
   unsigned int *s_wdef = (unsigned int *)(s_u64 + 16);  // [16] per-wave deferred records of the sweep (WQ)
+  unsigned int &s_next = *(unsigned int *)(s_u64 + 24);   // dynamic sweeps: the next record slot to hand out
   // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
   constexpr int MC = miss_cap(NL, RK::C32);
   // B_OVERLAP: phase B of round r overlaps phase A of round r + 1, so the miss list is double-buffered
@@ -2326,10 +2332,33 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   static_assert(!RK::C32 || R == 4, "compact rounds take one 16-byte load of 4 records per lane");
   // nwv: NONE for a dense sweep of cnt records, else this wave's records of a re-sweep (wave-owned positions,
   // see defer_pos; lanes past them read the bucket's first record or quad)
-  auto prefetch = [&](const PlaneSet &src, uint32_t cnt, uint32_t first, uint32_t nwv) {
+  // A record source: the fine records (p.recs) or this workgroup's spill area (p.spill), from record `off` on. Kept
+  // as (offset, which) and turned into plane pointers where used: full plane sets for the bucket, the next bucket and
+  // the spill area held across the sweep loop spilled registers at three and four key words.
+  struct Src {
+    uint64_t off;
+    uint32_t spl;
+  };
+  auto planes_of = [&](const Src &sr) -> PlaneSet {
+    PlaneSet q = sr.spl ? p.spill : p.recs;
+    const uint64_t o = sr.off;
+    if (RK::C32) {
+      q.w[0] = (uint64_t *)((uint32_t *)q.w[0] + o);
+    } else if (RK::M2 && kM2Aos) {
+      q.w[0] += 2 * o;
+    } else {
+#pragma unroll
+      for (int w = 0; w < NL; w++) q.w[w] += o;
+    }
+    if (!PACKED) q.ext += o;
+    return q;
+  };
+  // (vt: the thread slot whose records to load, tid except in dynamic sweeps)
+  auto prefetch = [&](const Src &sr, uint32_t cnt, uint32_t first, uint32_t nwv, uint32_t vt) {
+    const PlaneSet src = planes_of(sr);
     const uint32_t dbase = first / RND * (uint32_t)(64 * R);
     if constexpr (RK::C32) {
-      const uint32_t q = first + 4u * (uint32_t)tid, qmax = (cnt - 1) & ~3u;
+      const uint32_t q = first + 4u * vt, qmax = (cnt - 1) & ~3u;
       const uint32_t qq = nwv == NONE ? (q < qmax ? q : qmax) : (dbase + 4u * (uint32_t)lane < nwv ? q : 0u);
       const u32x4 v = gload4((const uint32_t *)src.w[0] + qq);
       nk[0][0] = v.x;
@@ -2342,7 +2371,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     }
 #pragma unroll
     for (int j = 0; j < R; j++) {
-      const uint32_t i = first + (uint32_t)tid + (uint32_t)j * C_THREADS;
+      const uint32_t i = first + vt + (uint32_t)j * C_THREADS;
       const uint32_t idx = nwv == NONE ? (i < cnt ? i : cnt - 1) : (dbase + (uint32_t)(64 * j + lane) < nwv ? i : 0u);
       if (RK::C32) {
         nk[j][0] = ((const uint32_t *)src.w[0])[idx];
@@ -2358,20 +2387,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     }
   };
   // a bucket's records from its extent [base, end) (< 2^32 records per bucket: host check)
-  auto bucket_at = [&](uint64_t base, uint64_t end, PlaneSet &src, uint32_t &cnt) {
+  auto bucket_at = [&](uint64_t base, uint64_t end, Src &src, uint32_t &cnt) {
     cnt = (uint32_t)(end - base);
-    src = p.recs;
-    if (RK::C32) {
-      src.w[0] = (uint64_t *)((uint32_t *)src.w[0] + base);
-    } else if (RK::M2 && kM2Aos) {
-      src.w[0] += 2 * base;
-    } else {
-#pragma unroll
-      for (int w = 0; w < NL; w++) src.w[w] += base;
-    }
-    if (!PACKED) src.ext += base;
+    src = Src{base, 0u};
   };
-  auto bucket = [&](uint32_t bb, PlaneSet &src, uint32_t &cnt) { bucket_at(p.bucket_base[bb], p.bucket_end[bb], src, cnt); };
+  auto bucket = [&](uint32_t bb, Src &src, uint32_t &cnt) { bucket_at(p.bucket_base[bb], p.bucket_end[bb], src, cnt); };
 
   // Position of a record deferred to the next sweep. With per-wave queues a wave defers only records it loaded
   // itself, so its d-th deferral goes to its own d-th record position of the sweep (wave-owned positions in round
@@ -2394,18 +2414,29 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     s_missacc = 0;
     s_u64[3] = 0;  // finalize's counters (MHMKC_FIN2)
   }
+  // this workgroup's spill area (dynamic sweeps: their deferred records; the sweep after reads them from there)
+  const Src spill{(uint64_t)blockIdx.x * SPILL_RECORDS, 1u};
+  const bool has_spill = p.spill.w[0] != nullptr;
   uint32_t b = blockIdx.x;
-  PlaneSet ps;
+  Src ps;
   uint32_t n;
   bucket(b, ps, n);
-  if (n) prefetch(ps, n, 0, NONE);
+  if (n) prefetch(ps, n, 0, NONE, (uint32_t)tid);
   while (true) {  // buckets
   my_maxb = my_maxb > n ? my_maxb : n;
   bool first_sweep = true;
   // records of this wave in a re-sweep (NONE: the first sweep, dense over [0, n)) and the sweep's round bound
   uint32_t nw = NONE, lim = n;
+  // Dynamic sweeps (cold, with a spill area): the rounds' record slots of 64 lanes (a round's wave slot: lane l of
+  // slot s of round r takes what thread 64 s + l would) are handed to the waves in order as they ask, so a wave that
+  // runs ahead takes more of them and the waves reach the sweep's barrier together (statically, each wave's share
+  // of a cold sweep ran without barriers and the waves drifted apart: the barrier held 17-25 % of k_count's wave
+  // cycles, MHMKC_STAMP). Their deferred records go densely to the other of (bucket region, spill area), which the
+  // next sweep (dynamic too: fewer records) reads.
+  bool dyn_sweep = false;
+  Src pd = spill;  // where a dynamic sweep defers to
   uint32_t nb_next = 0;
-  PlaneSet ps_next;
+  Src ps_next;
   const uint32_t b_next = b + gridDim.x;
   // the next bucket's extent, loaded now so that its first records can be fetched at this bucket's finalize without
   // a dependent round trip there (unconditional: without a next bucket it re-reads this bucket's, never used)
@@ -2429,6 +2460,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       s_err = 0;
     }
     if (tid < C_THREADS / 64) s_wdef[tid] = 0;
+    if (tid == 0) s_next = 2 * (C_THREADS / 64);  // (slots s and 16 + s are wave s's own: already prefetched / next)
     __syncthreads();
     STAMP(t_sw1);
     STAMP_ADD(0, t_sw1 - t_sw0);
@@ -2440,21 +2472,31 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     //   B. after a barrier the miss list is worked off densely, one record per lane (probing, CAS insert,
     //      counting), so the ~20 % of records that need the slow path no longer hold every wave of the
     //      workgroup in a divergent loop.
-    if (!first_sweep && n) prefetch(ps, n, 0, nw);  // a re-sweep reads the deferred records
+    if (!first_sweep && n) prefetch(ps, n, 0, nw, (uint32_t)tid);  // a re-sweep reads the deferred records
     first_sweep = false;
     // a sweep of fewer than 0xC000 records cannot bring a counter to the clamp level: its rounds count
     // with non-returning adds and carry no clamp check (COLD instantiation of the round loop)
-    auto rounds = [&](auto cold_tag) {
+    auto rounds = [&](auto cold_tag, auto dyn_tag) {
       constexpr bool COLD = decltype(cold_tag)::value;
+      constexpr bool DYN = decltype(dyn_tag)::value;  // dynamic slots (cold sweeps only)
+      constexpr uint32_t NWV = C_THREADS / 64;
       int rnd = 0, lr = 0;           // lr = rnd % 3: the round's miss counter
       uint32_t wq_n = 0;             // WQ: entries in this wave's miss queue (wave-uniform)
-      for (uint32_t r0 = 0; r0 < lim; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
+      // DYN: this wave's slot (round cc / NWV, wave slot cc % NWV) and its next one; wave s starts with slots s and
+      // NWV + s, every later one comes from s_next (asked for one slot ahead, so the answer is never waited for)
+      uint32_t cc = (uint32_t)wid, cn = (uint32_t)wid + NWV;
+      auto slot_first = [&](uint32_t c) { return c / NWV * RND + c % NWV * (RK::C32 ? 256u : 64u); };
+      for (uint32_t r0 = 0; DYN ? slot_first(cc) < n : r0 < lim; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
         STAMP(t_r0);
         uint64_t ck[R][NL];
         uint32_t ce[R];
+        uint32_t ca = 0;  // DYN: the slot after cn (lane 0 asks now, the answer is read at the end of the round)
+        if (DYN && lane == 0) ca = atomicAdd(&s_next, 1u);
+        const uint32_t cr0 = DYN ? cc / NWV * RND : r0;                              // the slot's round
+        const uint32_t vt = DYN ? cc % NWV * 64u + (uint32_t)lane : (uint32_t)tid;  // its thread slot
         // record j of this lane is valid iff j * vstep < vrem: the records left from this lane's first one (a dense
         // sweep: [r0, n) in thread order; a re-sweep: this wave's own nw positions), saturated at 0
-        const uint32_t vfirst = nw == NONE ? r0 + (RK::C32 ? 4u * (uint32_t)tid : (uint32_t)tid)
+        const uint32_t vfirst = nw == NONE ? cr0 + (RK::C32 ? 4u * vt : vt)
                                            : (uint32_t)rnd * (uint32_t)(64 * R) + (RK::C32 ? 4u * (uint32_t)lane : (uint32_t)lane);
         const uint32_t vend = nw == NONE ? n : nw;
         const uint32_t vrem = (vend > vfirst ? vend : vfirst) - vfirst;
@@ -2483,10 +2525,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #ifndef MHMKC_PF_UNCOND
 #define MHMKC_PF_UNCOND 1
 #endif
-        if (MHMKC_PF_UNCOND)
-          prefetch(ps, n, r0 + RND < lim ? r0 + RND : r0, nw);
+        if (DYN)  // (unconditional too: past the records it re-reads the last quad / record)
+          prefetch(ps, n, cn / NWV * RND, NONE, cn % NWV * 64u + (uint32_t)lane);
+        else if (MHMKC_PF_UNCOND)
+          prefetch(ps, n, r0 + RND < lim ? r0 + RND : r0, nw, (uint32_t)tid);
         else if (r0 + RND < lim)
-          prefetch(ps, n, r0 + RND, nw);
+          prefetch(ps, n, r0 + RND, nw, (uint32_t)tid);
         unsigned int *nmiss = &s_nmiss[lr];
         K *mkey = s_mkey + (BOV ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
         uint32_t *me = s_me + (BOV ? (rnd & 1) * MCL : 0);
@@ -2662,7 +2706,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
           for (int j = 0; j < R; j++) {
             if ((defer >> j) & 1u) {
-              store_record<NL, PACKED, CMP>(ps, defer_pos(), ck[j], ce[j]);
+              if (DYN)
+                store_record<NL, PACKED, CMP>(planes_of(pd), atomicAdd(&s_ovf, 1u), ck[j], ce[j]);
+              else
+                store_record<NL, PACKED, CMP>(planes_of(ps), defer_pos(), ck[j], ce[j]);
             }
           }
         }
@@ -2672,7 +2719,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           // the next barrier with the misses of all the others. The sweep's rounds run while r0 < lim (lim = n
           // in a first sweep; in a re-sweep lim >= n covers the largest wave share of deferred records), so the
           // queue is drained in the round the loop ends with.
-          const bool last_round = r0 + RND >= lim;
+          const bool last_round = DYN ? slot_first(cn) >= n : r0 + RND >= lim;
           while (wq_n >= (uint32_t)WQ_THR || (last_round && wq_n > 0)) {
             const uint32_t take = wq_n < 64u ? wq_n : 64u;
             const uint32_t qb = wq_n - take;
@@ -2693,13 +2740,20 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
                 else if (lds_add(t, r, e) >= HOT)
                   lds_clamp(t, r, e);
               } else if (r == -1) {
-                store_record<NL, PACKED, CMP>(ps, defer_pos(), key, e);
+                if (DYN)
+                  store_record<NL, PACKED, CMP>(planes_of(pd), atomicAdd(&s_ovf, 1u), key, e);
+                else
+                  store_record<NL, PACKED, CMP>(planes_of(ps), defer_pos(), key, e);
               } else {
                 s_err = 1;
               }
             }
             if (lane == 0) atomicAdd(&s_missacc, (unsigned long long)take);
             wq_n = qb;
+          }
+          if (DYN) {
+            cc = cn;
+            cn = __builtin_amdgcn_readfirstlane(ca);
           }
 #if MHMKC_STAMP
           const uint64_t t_r4w = __builtin_amdgcn_s_memtime();
@@ -2729,7 +2783,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             else if (lds_add(t, r, e) >= HOT)
               lds_clamp(t, r, e);
           } else if (r == -1) {
-            store_record<NL, PACKED, CMP>(ps, defer_pos(), key, e);
+            store_record<NL, PACKED, CMP>(planes_of(ps), defer_pos(), key, e);
           } else {
             s_err = 1;
           }
@@ -2746,11 +2800,26 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       }
     };
     // (s_wave holds the dummy words of the cold adds until finalize overwrites it after a barrier)
-    const bool cold = n < 0xC000u;
-    if (cold)
-      rounds(std::true_type{});
-    else
-      rounds(std::false_type{});
+    // dynamic: a cold first sweep, or a sweep after a dynamic one (fewer records: cold too). A cold sweep after a hot
+    // (static) one, whose deferred records sit in wave-owned positions, or one without a spill area runs the hot
+    // instantiation (only two instantiations of the round loop: a third spilled registers at every key width).
+    // `cold` is the table's counter encoding (lds_add_nr / slot_count) of the instantiation that ran.
+    // (one- and two-word keys only: with three and four key words the dynamic instantiation spilled 20-40 VGPRs
+    // and made k_count 10-22 % slower, against 2 % faster at k = 21 and 63)
+    constexpr bool DYNS = kDynSweeps && WQ && WDEF && NL <= 2;
+    dyn_sweep = DYNS && has_spill && n < 0xC000u && (dyn_sweep || nw == NONE);
+    const bool cold = DYNS ? dyn_sweep : n < 0xC000u;
+    if constexpr (DYNS) {
+      if (dyn_sweep)
+        rounds(std::true_type{}, std::true_type{});
+      else
+        rounds(std::false_type{}, std::false_type{});
+    } else {
+      if (cold)
+        rounds(std::true_type{}, std::false_type{});
+      else
+        rounds(std::false_type{}, std::false_type{});
+    }
     STAMP(t_b0);
     __syncthreads();
     STAMP(t_f0);
@@ -2766,10 +2835,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       const bool nxt = last_sweep && b_next < p.n_buckets;
       if (nxt) bucket_at(nx_base, nx_end, ps_next, nb_next);
       const bool use_next = nxt && nb_next;
-      prefetch(use_next ? ps_next : ps, use_next ? nb_next : (n ? n : 1u), 0, NONE);
+      prefetch(use_next ? ps_next : ps, use_next ? nb_next : (n ? n : 1u), 0, NONE, (uint32_t)tid);
     } else if (last_sweep && b_next < p.n_buckets) {
       bucket_at(nx_base, nx_end, ps_next, nb_next);
-      if (nb_next) prefetch(ps_next, nb_next, 0, NONE);
+      if (nb_next) prefetch(ps_next, nb_next, 0, NONE, (uint32_t)tid);
     }
 
 #if MHMKC_FIN2
@@ -3011,7 +3080,12 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     if (last_sweep) break;
     n = s_ovf;
     lim = n;
-    if (WDEF) {  // each wave re-reads its own deferred records; the rounds cover the largest share
+    if (dyn_sweep) {  // the deferred records, dense in pd, are the next sweep's; the region it read takes its deferrals
+      const Src t_ = ps;
+      ps = pd;
+      pd = t_;
+      nw = NONE;
+    } else if (WDEF) {  // each wave re-reads its own deferred records; the rounds cover the largest share
       nw = s_wdef[wid];
       uint32_t mx = 0;
 #pragma unroll
@@ -3027,6 +3101,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   b = b_next;  // the finalize above ended with a barrier: the table may be cleared for the next bucket
   ps = ps_next;
   n = nb_next;
+  pd = spill;
+  dyn_sweep = false;
   }  // buckets
 
 #if MHMKC_STAMP

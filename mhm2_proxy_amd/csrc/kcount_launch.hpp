@@ -163,6 +163,8 @@ struct CountParams {
   const uint32_t *ctg_bucket;         // local fine bucket of each entry (sorted ascending)
   uint32_t ctg_base;                  // local fine bucket of this launch's bucket 0 (a finish pass over part of the
                                       // owned range: its first coarse bucket << fine_bits)
+  PlaneSet spill;                     // deferred records of cold sweeps: SPILL_RECORDS per workgroup (fine record
+                                      // layout; planes of grid * SPILL_RECORDS entries); w[0] == nullptr: none
   uint8_t *ctg_done;                  // [ctg_n] applied (zeroed before the launch)
 };
 
@@ -209,7 +211,10 @@ enum {
   STAT_MISSES = 6,    // records worked off in phase B (not in their home group)
   STAT_N = 8,         // stats[STAT_N - 1]: internal error flag
 };
-constexpr int STAT_ALLOC = 16;  // stats[8..13]: k_count phase stamps in MHMKC_STAMP builds
+constexpr int STAT_ALLOC = 16;
+// k_count's cold sweeps (< 0xC000 records) hand their waves the rounds' record slots dynamically; their deferred
+// records go to a per-workgroup spill area of this many records (and from there back to the bucket's own region)
+constexpr uint32_t SPILL_RECORDS = 0xC000;  // stats[8..13]: k_count phase stamps in MHMKC_STAMP builds
 
 // threads of the extract / partition workgroups (each thread takes tile / E_THREADS windows or records)
 #ifndef MHMKC_ETHREADS
@@ -325,7 +330,7 @@ __host__ __device__ constexpr int count_cap(int nl, bool cmp = false) {
   return ((cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? MHMKC_CAP2 : nl == 3 ? MHMKC_CAP3 : MHMKC_CAP4) / C_SPLIT) & ~3;
 }
 __host__ __device__ constexpr size_t count_table_bytes(int nl, bool cmp = false) {
-  return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 192;
+  return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 256;  // + k_count's scalars
 }
 __host__ __device__ constexpr int miss_cap(int nl, bool cmp = false) {
   return (int)(((C_LDS - count_table_bytes(nl, cmp)) / (count_key_bytes(cmp) * nl + 4)) & ~(size_t)63);
@@ -419,7 +424,7 @@ struct OutRows {
 // KmerDHT minimizer length for k (src/kcount/kmer_dht.cpp:114-116)
 inline int minimizer_len_for(int k) { return k * 2 / 3 + 1 < 15 ? 15 : (k * 2 / 3 + 1 > 27 ? 27 : k * 2 / 3 + 1); }
 // mhmkc_fetch_ordered: the output rows in the order of the top 32 bits of mhmkc_map_hash (kcount_owner.hip)
-size_t map_order_scratch_bytes(uint64_t n);
+size_t map_order_scratch_bytes(uint64_t n, int nlo);
 hipError_t launch_map_order(const OutRows &in, uint64_t n, int nlo, void *scratch, size_t scratch_bytes, const OutRows &out,
                             hipStream_t s);
 // minimizer_hash_fast of n keys (nlo words each, the first k/32+1 used)

@@ -94,10 +94,76 @@ __global__ __launch_bounds__(O_THREADS) void k_gather_rows(OutRows in, const uin
   }
 }
 
+// mhmkc_fetch_ordered for keys of up to four words: every row packed into one record (key words, then count | left << 16
+// | right << 24), sorted with its hash key, then unpacked: all streaming. (A sort of row indices followed by a gather
+// from the four output planes fetched >= 21x the rows' bytes: four narrow random reads per row.)
+template <int NLO>
+struct PackedRow {
+  uint64_t key[NLO];
+  uint32_t meta, pad;
+};
+
+template <int NLO>
+__global__ __launch_bounds__(O_THREADS) void k_pack_rows(OutRows in, uint64_t n, uint32_t *hkey, PackedRow<NLO> *rows) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    PackedRow<NLO> r;
+#pragma unroll
+    for (int w = 0; w < NLO; w++) r.key[w] = in.keys[i * NLO + w];
+    r.meta = (uint32_t)in.counts[i] | (uint32_t)(uint8_t)in.left[i] << 16 | (uint32_t)(uint8_t)in.right[i] << 24;
+    r.pad = 0;
+    hkey[i] = (uint32_t)(mhmkc_map_hash(r.key, NLO) >> 32);
+    rows[i] = r;
+  }
+}
+
+template <int NLO>
+__global__ __launch_bounds__(O_THREADS) void k_unpack_rows(const PackedRow<NLO> *rows, uint64_t n, OutRows out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const PackedRow<NLO> r = rows[i];
+#pragma unroll
+    for (int w = 0; w < NLO; w++) out.keys[i * NLO + w] = r.key[w];
+    out.counts[i] = (uint16_t)r.meta;
+    out.left[i] = (char)(r.meta >> 16);
+    out.right[i] = (char)(r.meta >> 24);
+  }
+}
+
+template <int NLO>
+size_t packed_order_bytes(uint64_t n) {
+  size_t t = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, t, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                  (const PackedRow<NLO> *)nullptr, (PackedRow<NLO> *)nullptr, (size_t)n);
+  const size_t a = (n + 63) / 64 * 64;
+  return 2 * a * 4 + 2 * a * sizeof(PackedRow<NLO>) + t + 512;
+}
+
+template <int NLO>
+hipError_t packed_order(const OutRows &in, uint64_t n, void *scratch, size_t scratch_bytes, const OutRows &out,
+                        hipStream_t s) {
+  const size_t a = (n + 63) / 64 * 64;
+  uint32_t *hk = (uint32_t *)scratch, *hk2 = hk + a;
+  PackedRow<NLO> *rw = (PackedRow<NLO> *)(hk2 + a), *rw2 = rw + a;
+  void *tmp = rw2 + a;
+  size_t tb = scratch_bytes - (2 * a * 4 + 2 * a * sizeof(PackedRow<NLO>));
+  k_pack_rows<NLO><<<grid_for(n), O_THREADS, 0, s>>>(in, n, hk, rw);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if ((e = rocprim::radix_sort_pairs(tmp, tb, hk, hk2, rw, rw2, (size_t)n, 0, 32, s)) != hipSuccess) return e;
+  k_unpack_rows<NLO><<<grid_for(n), O_THREADS, 0, s>>>(rw2, n, out);
+  return hipGetLastError();
+}
+
 }  // namespace
 
-size_t map_order_scratch_bytes(uint64_t n) {
-  size_t t = 0;
+size_t map_order_scratch_bytes(uint64_t n, int nlo) {
+  switch (nlo) {
+    case 1: return packed_order_bytes<1>(n);
+    case 2: return packed_order_bytes<2>(n);
+    case 3: return packed_order_bytes<3>(n);
+    case 4: return packed_order_bytes<4>(n);
+    default: break;
+  }
+  size_t t = 0;  // wider output keys (n_longs 5..8): sort row indices, then gather
   (void)rocprim::radix_sort_pairs(nullptr, t, (const uint32_t *)nullptr, (uint32_t *)nullptr, (const uint32_t *)nullptr,
                                   (uint32_t *)nullptr, (size_t)n);
   return 4 * ((n + 63) / 64 * 64) * 4 + t + 256;
@@ -106,7 +172,14 @@ size_t map_order_scratch_bytes(uint64_t n) {
 hipError_t launch_map_order(const OutRows &in, uint64_t n, int nlo, void *scratch, size_t scratch_bytes, const OutRows &out,
                             hipStream_t s) {
   if (!n) return hipSuccess;
-  if (n >= 0xffffffffull || scratch_bytes < map_order_scratch_bytes(n)) return hipErrorInvalidValue;
+  if (n >= 0xffffffffull || scratch_bytes < map_order_scratch_bytes(n, nlo)) return hipErrorInvalidValue;
+  switch (nlo) {
+    case 1: return packed_order<1>(in, n, scratch, scratch_bytes, out, s);
+    case 2: return packed_order<2>(in, n, scratch, scratch_bytes, out, s);
+    case 3: return packed_order<3>(in, n, scratch, scratch_bytes, out, s);
+    case 4: return packed_order<4>(in, n, scratch, scratch_bytes, out, s);
+    default: break;
+  }
   const size_t a = (n + 63) / 64 * 64;
   uint32_t *hk = (uint32_t *)scratch, *hk2 = hk + a, *ix = hk2 + a, *ix2 = ix + a;
   void *tmp = ix2 + a;

@@ -214,6 +214,7 @@ struct mhmkc {
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
   DevBuf d_hll, d_dest, d_ohist, d_out2_keys, d_out2_counts, d_out2_left, d_out2_right, d_mh;
   DevBuf d_ord;  // mhmkc_fetch_ordered: sort keys, row indices, radix-sort scratch
+  DevBuf d_spill;  // k_count: the deferred records of cold sweeps, mhm::SPILL_RECORDS per persistent workgroup
   // supermer exchange (smer): owner bytes of a slab's tiles; the received supermers (codes, good bits, descriptors),
   // their window counts / prefix, per-tile first supermer, scan scratch
   bool smer = false;
@@ -368,6 +369,12 @@ struct mhmkc {
     }
     if (ps.ext) ps.ext -= sh;
   }
+
+  // Device -> host copy of `bytes` into caller (pageable) memory through two pinned staging buffers: chunk i's DMA
+  // runs while chunk i - 1 is copied out of the other buffer by host threads (a plain copy into pageable memory
+  // moved the C2 table at ~17 GB/s).
+  PinBuf d2h_stage[2];
+  hipError_t d2h(void *dst, const void *src, size_t bytes);
 
   int add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known);
   int extract(Slab *sl, bool exact);
@@ -1668,6 +1675,9 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     cp.ctg_bucket = d_ctg_bucket.as<uint32_t>();
     cp.ctg_done = d_ctg_done.as<uint8_t>();
     cp.ctg_base = c0 << fb;
+    if (cp.grid) {  // (MHMKC_DYN builds: dynamic cold sweeps defer into it)
+      if ((rc = set_planes(d_spill, (uint64_t)cp.grid * mhm::SPILL_RECORDS, cp.spill, true))) return rc;
+    }
 
     bool exact = exact_env;
     unsigned long long stats[mhm::STAT_ALLOC], cursor_end = 0;
@@ -1785,6 +1795,50 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   prof_collect();
   if (n_out_ret) *n_out_ret = n_out;
   return MHMKC_OK;
+}
+
+hipError_t mhmkc::d2h(void *dst, const void *src, size_t bytes) {
+  constexpr size_t CH = 32ull << 20;
+  hipError_t e;
+  hipPointerAttribute_t pa{};
+  const bool pinned = hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // (pageable memory is "not a HIP pointer": not an error to keep)
+  if (bytes < 2 * CH || pinned) {  // pinned caller memory: one DMA straight into it
+    if ((e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
+    return hipStreamSynchronize(stream);
+  }
+  if ((e = d2h_stage[0].ensure(CH)) != hipSuccess || (e = d2h_stage[1].ensure(CH)) != hipSuccess) return e;
+  hipEvent_t ev[2] = {take_event(), take_event()};
+  const size_t n_ch = (bytes + CH - 1) / CH;
+  auto drain = [&](size_t c) {  // host copy of chunk c out of its staging buffer, four threads
+    const size_t off = c * CH, len = std::min(CH, bytes - off);
+    const char *sp = d2h_stage[c & 1].as<char>();
+    char *dp = (char *)dst + off;
+    std::thread th[3];
+    const size_t q = (len / 4 + 63) & ~(size_t)63;
+    for (int t = 0; t < 3; t++) {
+      const size_t a = std::min(len, (t + 1) * q), b = std::min(len, (t + 2) * q);
+      th[t] = std::thread([=] { if (b > a) memcpy(dp + a, sp + a, b - a); });
+    }
+    memcpy(dp, sp, std::min(len, q));
+    for (auto &x : th) x.join();
+  };
+  e = hipSuccess;
+  for (size_t c = 0; c < n_ch && e == hipSuccess; c++) {
+    const size_t off = c * CH, len = std::min(CH, bytes - off);
+    if (c >= 2 && (e = hipEventSynchronize(ev[c & 1])) != hipSuccess) break;  // (its buffer was drained below)
+    if ((e = hipMemcpyAsync(d2h_stage[c & 1].p, (const char *)src + off, len, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipEventRecord(ev[c & 1], stream)) != hipSuccess)
+      break;
+    if (c >= 1) {
+      if ((e = hipEventSynchronize(ev[(c - 1) & 1])) != hipSuccess) break;
+      drain(c - 1);
+    }
+  }
+  if (e == hipSuccess && (e = hipEventSynchronize(ev[(n_ch - 1) & 1])) == hipSuccess) drain(n_ch - 1);
+  ev_pool.push_back(ev[0]);
+  ev_pool.push_back(ev[1]);
+  return e;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2030,6 +2084,7 @@ void mhmkc_destroy(mhmkc_t h) {
                     &h->d_out_keys, &h->d_out_counts, &h->d_out_left,   &h->d_out_right,  &h->d_out_cursor,
                     &h->d_recv,     &h->d_xg,         &h->d_hll,        &h->d_dest,       &h->d_ohist,
                     &h->d_out2_keys, &h->d_out2_counts, &h->d_out2_left, &h->d_out2_right, &h->d_mh, &h->d_ord,
+                    &h->d_spill,
                     &h->d_owners, &h->d_rcodes, &h->d_rgood, &h->d_rdesc, &h->d_rnwin, &h->d_rwpre, &h->d_rtiles,
                     &h->d_rtmp,
                     &h->d_fqa_bytes, &h->d_fqa_offs,
@@ -2042,6 +2097,8 @@ void mhmkc_destroy(mhmkc_t h) {
   for (DevBuf *b : cbufs) b->release();
   h->x_send.release();
   h->x_recv.release();
+  h->d2h_stage[0].release();
+  h->d2h_stage[1].release();
   h->fq_file_buf.release();
   for (auto &p : h->prof) {
     h->ev_pool.push_back(p.a);
@@ -2598,10 +2655,10 @@ int mhmkc_fetch(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *r
   if (!h->finished) return h->fail(MHMKC_ESTATE, "fetch before finish");
   const uint64_t n = h->n_out;
   hipError_t e = hipSuccess;
-  if (n && keys) e = hipMemcpyAsync(keys, h->d_out_keys.p, n * 8 * h->nlo, hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess && n && counts) e = hipMemcpyAsync(counts, h->d_out_counts.p, n * 2, hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess && n && left) e = hipMemcpyAsync(left, h->d_out_left.p, n, hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess && n && right) e = hipMemcpyAsync(right, h->d_out_right.p, n, hipMemcpyDeviceToHost, h->stream);
+  if (n && keys) e = h->d2h(keys, h->d_out_keys.p, n * 8 * h->nlo);
+  if (e == hipSuccess && n && counts) e = h->d2h(counts, h->d_out_counts.p, n * 2);
+  if (e == hipSuccess && n && left) e = h->d2h(left, h->d_out_left.p, n);
+  if (e == hipSuccess && n && right) e = h->d2h(right, h->d_out_right.p, n);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   if (e != hipSuccess) return h->hip_fail(e, "fetch");
   return MHMKC_OK;
@@ -2614,23 +2671,30 @@ int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left,
   if (!n) return MHMKC_OK;
   if (n >= 0xffffffffull) return h->fail(MHMKC_EUNSUPPORTED, "mhmkc_fetch_ordered: at most 2^32-1 rows");
   const int nlo = h->nlo;
-  const size_t sb = mhm::map_order_scratch_bytes(n);
+  const size_t sb = mhm::map_order_scratch_bytes(n, nlo);
+  const size_t ob = align_up(n * 8 * nlo + 64, 256) + align_up(n * 2 + 64, 256) + 2 * align_up(n + 64, 256);
   hipError_t e;
-  // the second output set holds the ordered rows (it is only used inside finish, by the owner hand-off)
-  if ((e = h->grow(h->d_ord, sb)) != hipSuccess || (e = h->grow(h->d_out2_keys, n * 8 * nlo + 64)) != hipSuccess ||
-      (e = h->grow(h->d_out2_counts, n * 2 + 64)) != hipSuccess || (e = h->grow(h->d_out2_left, n + 64)) != hipSuccess ||
-      (e = h->grow(h->d_out2_right, n + 64)) != hipSuccess)
-    return h->hip_fail(e, "fetch_ordered buffers");
+  // scratch and the ordered rows: the fine-record buffer of the finish (idle once the table is out, and larger
+  // than both at every k: >= 4 B per counted occurrence against < 6 B per output row + the sort's 40-72 B), else
+  // the handle's own buffers (a first hipMalloc of the sort's ~2 GB at C2 cost more than the sort)
+  char *base = nullptr;
+  if (h->d_r2.p && h->d_r2.cap >= sb + ob) {
+    base = h->d_r2.as<char>();
+  } else {
+    if ((e = h->grow(h->d_ord, sb + ob)) != hipSuccess) return h->hip_fail(e, "fetch_ordered buffers");
+    base = h->d_ord.as<char>();
+  }
+  char *ok = base + sb, *oc = ok + align_up(n * 8 * nlo + 64, 256), *ol = oc + align_up(n * 2 + 64, 256),
+       *orr = ol + align_up(n + 64, 256);
   mhm::OutRows in{h->d_out_keys.as<uint64_t>(), h->d_out_counts.as<uint16_t>(), h->d_out_left.as<char>(),
                   h->d_out_right.as<char>()};
-  mhm::OutRows out{h->d_out2_keys.as<uint64_t>(), h->d_out2_counts.as<uint16_t>(), h->d_out2_left.as<char>(),
-                   h->d_out2_right.as<char>()};
-  if ((e = mhm::launch_map_order(in, n, nlo, h->d_ord.p, h->d_ord.cap, out, h->stream)) != hipSuccess)
+  mhm::OutRows out{(uint64_t *)ok, (uint16_t *)oc, ol, orr};
+  if ((e = mhm::launch_map_order(in, n, nlo, base, sb, out, h->stream)) != hipSuccess)
     return h->hip_fail(e, "fetch_ordered sort");
-  if (keys) e = hipMemcpyAsync(keys, out.keys, n * 8 * nlo, hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess && counts) e = hipMemcpyAsync(counts, out.counts, n * 2, hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess && left) e = hipMemcpyAsync(left, out.left, n, hipMemcpyDeviceToHost, h->stream);
-  if (e == hipSuccess && right) e = hipMemcpyAsync(right, out.right, n, hipMemcpyDeviceToHost, h->stream);
+  if (keys) e = h->d2h(keys, out.keys, n * 8 * nlo);
+  if (e == hipSuccess && counts) e = h->d2h(counts, out.counts, n * 2);
+  if (e == hipSuccess && left) e = h->d2h(left, out.left, n);
+  if (e == hipSuccess && right) e = h->d2h(right, out.right, n);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fetch_ordered");
 }

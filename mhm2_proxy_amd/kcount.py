@@ -413,16 +413,24 @@ class KmerCounter:
         self.n_out = int(n.value)
         return self.n_out
 
-    def fetch(self, ordered: bool = False) -> KmerTable:
+    def fetch(self, ordered: bool = False, out: KmerTable | None = None) -> KmerTable:
         """The finished table on the host (mhmkc_fetch). ordered=True: rows in the order of the top 32 bits of
-        map_hash(key) (mhmkc_fetch_ordered, a device sort), the slot order of the C++ adapter's KmerMap."""
+        map_hash(key) (mhmkc_fetch_ordered, a device sort), the slot order of the C++ adapter's KmerMap.
+        out: a table whose arrays are filled (at least n_out rows; e.g. pinned host memory, which the copies reach
+        directly) instead of new ones."""
         if self.n_out is None:
             raise RuntimeError("fetch before finish")
         n = self.n_out
-        keys = np.empty((n, self.n_longs), dtype=np.uint64)
-        counts = np.empty(n, dtype=np.uint16)
-        left = np.empty(n, dtype=np.uint8)
-        right = np.empty(n, dtype=np.uint8)
+        if out is not None:
+            if (len(out) < n or out.keys.shape[1] != self.n_longs or out.keys.dtype != np.uint64
+                    or not all(a.flags.c_contiguous for a in (out.keys, out.counts, out.left, out.right))):
+                raise ValueError("out: contiguous arrays of at least n_out rows with n_longs key words")
+            keys, counts, left, right = out.keys[:n], out.counts[:n], out.left[:n], out.right[:n]
+        else:
+            keys = np.empty((n, self.n_longs), dtype=np.uint64)
+            counts = np.empty(n, dtype=np.uint16)
+            left = np.empty(n, dtype=np.uint8)
+            right = np.empty(n, dtype=np.uint8)
         fn = N.lib().mhmkc_fetch_ordered if ordered else N.lib().mhmkc_fetch
         self._check(fn(self._h, keys.ctypes.data, counts.ctypes.data, left.ctypes.data, right.ctypes.data))
         return KmerTable(self.k, keys, counts, left, right)

@@ -542,7 +542,7 @@ def test_valid_window_walk_long_and_ragged_reads(k, monkeypatch):
     assert_tables_equal(got2, exp, f"long/ragged reads in 5000-byte chunks, k={k}")
 
 
-@pytest.mark.parametrize("k,nl", [(21, 0), (63, 0), (21, 2), (99, 0)])
+@pytest.mark.parametrize("k,nl", [(21, 0), (63, 0), (21, 2), (99, 0), (77, 0), (21, 6)])
 def test_fetch_ordered(k, nl):
     """mhmkc_fetch_ordered: the same rows as mhmkc_fetch, ordered by the top 32 bits of mhmkc_map_hash (the slot
     order of the C++ adapter's KmerMap)."""
@@ -593,3 +593,27 @@ def test_output_overflow_redoes_the_pass(k, passes, exact, monkeypatch):
     assert_tables_equal(got, oracle_table(b, o, k), f"output overflow, {passes} passes, k={k}")
     check_stats(st)
     assert st["device_bytes_peak"] >= st["device_bytes"] > 0
+
+
+@pytest.mark.parametrize("k,pinned", [(21, False), (63, True)])
+def test_fetch_into_existing_buffers(k, pinned):
+    """fetch(out=...) fills the caller's arrays (larger than the table; pinned host memory is reached by one DMA,
+    pageable memory through the staging buffers): the rows equal a plain fetch's, ordered or not."""
+    torch = pytest.importorskip("torch")
+    b, o = synth_set(2000, 10000, 95 + k)
+    with m.KmerCounter(k) as c:
+        c.add_packed_reads(b, o)
+        n = c.finish()
+        plain = c.fetch()
+        nl, rows = c.n_longs, n + 100
+        if pinned:
+            arrs = [torch.empty(s, dtype=t, pin_memory=True).numpy() for s, t in
+                    (((rows, nl), torch.int64), (rows, torch.int16), (rows, torch.uint8), (rows, torch.uint8))]
+            out = m.KmerTable(k, arrs[0].view(np.uint64), arrs[1].view(np.uint16), arrs[2], arrs[3])
+        else:
+            out = m.KmerTable(k, np.zeros((rows, nl), np.uint64), np.zeros(rows, np.uint16), np.zeros(rows, np.uint8),
+                              np.zeros(rows, np.uint8))
+        for ordered in (False, True):
+            got = c.fetch(ordered=ordered, out=out)
+            assert len(got) == n
+            assert_tables_equal(got, plain, f"fetch into existing buffers, ordered={ordered}")
