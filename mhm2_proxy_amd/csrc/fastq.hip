@@ -232,12 +232,13 @@ __device__ __forceinline__ int base_code(unsigned char c) {
 // text is read whole: allocations are at least 4-byte granular.
 constexpr int FQ_GROUP = 16;
 __device__ __forceinline__ uint32_t load4(const char *text, uint32_t a) {
-  const uintptr_t p = (uintptr_t)(text + a);  // aligned in the address space, not relative to text
-  const uint32_t *w = (const uint32_t *)(p & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(p & 3u);
-  const uint32_t v0 = w[0];
-  if (sh == 0) return v0;
-  return __builtin_amdgcn_alignbyte(w[1], v0, sh);  // v_alignbyte_b32: ({w1, v0} >> 8 * sh)
+  // aligned in the address space, not relative to text; the dword pointer is derived from text (not rebuilt
+  // from an integer) so that the compiler keeps global loads instead of flat ones
+  const char *p = text + a;
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+  const uint32_t *w = (const uint32_t *)(p - sh);
+  // the second dword only when the four bytes straddle one, without a branch (the address is selected)
+  return __builtin_amdgcn_alignbyte(*(sh ? w + 1 : w), w[0], sh);  // v_alignbyte_b32: ({w1, w0} >> 8 * sh)
 }
 // exact per-byte zero test: bit 7 of each byte of the result is set iff that byte of x is 0
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
@@ -416,17 +417,6 @@ __device__ bool fq_norm(const char *s, uint64_t b, uint64_t e, uint64_t &pb, uin
   return true;
 }
 
-// revcomp's complement (utils.cpp: IUPAC -> N), 0 for a character it DIEs on
-__device__ __forceinline__ char fq_comp(char c) {
-  switch (c) {
-    case 'A': return 'T';
-    case 'C': return 'G';
-    case 'G': return 'C';
-    case 'T': return 'A';
-  }
-  return base_code((unsigned char)c) == 4 ? 'N' : 0;
-}
-
 // per pair: (overlap + 1) of the merge (0: not merged) | has-N << 31
 constexpr uint32_t MP_HASN = 1u << 31;
 
@@ -513,44 +503,62 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // quality read at an N is always the one just set. It does change the output, so it is applied in LDS in scan
 // order and the qualities of pairs with an N go to the scratch for k_fq_merge_pack.
 constexpr int MG_WAVES = 4;
+// Diagnostic phase stamps of k_fq_merge (MHMKC_MGSTAMP builds only): wave cycles of staging, fast filter,
+// offset scans and the verdict tail, then the number of scans and of filter rounds, into stats[4..9]
+#ifndef MHMKC_MGSTAMP
+#define MHMKC_MGSTAMP 0
+#endif
+#if MHMKC_MGSTAMP
+#define MG_STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define MG_ADD(i, v) mg_acc[i] += (v)
+#else
+#define MG_STAMP(var)
+#define MG_ADD(i, v)
+#endif
 constexpr int MG_MAXL = 2048;  // > FQ_MAX_LINE + 4 (unaligned 4-byte reads past a line stay inside)
 
-__device__ __forceinline__ uint32_t lds_u32(const char *p) {  // 4 bytes from any LDS byte address
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3u);
-  return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+// Byte classification by v_perm_b32 lookups: the low three bits of A C T N G (1 3 4 6 7) are distinct, so
+// one 8-entry byte table indexed by them gives a candidate answer and a second gives the character that index
+// stands for; a byte is A/C/G/T/N exactly when it equals that character. No per-byte branches: the switch-like
+// compare chains these replace compiled to divergent branch trees, and k_fq_merge was bound by SALU issue.
+__device__ __forceinline__ uint32_t perm8(uint64_t table, uint32_t sel) {
+  return __builtin_amdgcn_perm((uint32_t)(table >> 32), (uint32_t)table, sel);
 }
-// 0xff in every byte of w equal to v, 0 elsewhere
-__device__ __forceinline__ uint32_t byte_eq_mask(uint32_t w, uint32_t v) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) m |= (((w >> (8 * i)) & 0xffu) == v) ? 0xffu << (8 * i) : 0u;
-  return m;
+constexpr uint64_t byte_table(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3, uint32_t v4, uint32_t v5, uint32_t v6,
+                              uint32_t v7) {
+  return (uint64_t)v0 | (uint64_t)v1 << 8 | (uint64_t)v2 << 16 | (uint64_t)v3 << 24 | (uint64_t)v4 << 32 |
+         (uint64_t)v5 << 40 | (uint64_t)v6 << 48 | (uint64_t)v7 << 56;
 }
+// index (low 3 bits):          0     1    2     3    4    5     6    7
+constexpr uint64_t T_CHAR = byte_table(0x01, 'A', 0x01, 'C', 'T', 0x01, 'N', 'G');  // 0x01: matches no byte there
+constexpr uint64_t T_NIB = byte_table(15, 0, 15, 1, 3, 15, 4, 2);
+constexpr uint64_t T_COMP = byte_table(0, 'T', 0, 'G', 'A', 0, 'N', 'C');
+// 0x01 in every byte of w that is one of A C G T N, 0 elsewhere
+__device__ __forceinline__ uint32_t acgtn_bytes(uint32_t w, uint32_t sel) {
+  return zero_bytes(w ^ perm8(T_CHAR, sel)) >> 7;
+}
+// bit 7 of every byte of w equal to v (v replicated), 0 elsewhere
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t v4) { return zero_bytes(w ^ v4); }
 // 4-bit codes of the four characters of w: A C G T N -> 0..4, anything else 15 (16 bits)
 __device__ __forceinline__ uint32_t nib4(uint32_t w) {
-  uint32_t out = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t c = (w >> (8 * i)) & 0xffu;
-    const uint32_t v = c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : c == 'N' ? 4u : 15u;
-    out |= v << (4 * i);
-  }
-  return out;
+  const uint32_t sel = w & 0x07070707u;
+  const uint32_t v = perm8(T_NIB, sel) | ((acgtn_bytes(w, sel) ^ 0x01010101u) * 15u);
+  const uint32_t t = v | (v >> 4);  // byte 0: codes 0 and 1, byte 2: codes 2 and 3
+  return (t & 0xffu) | ((t >> 8) & 0xff00u);
 }
 // fq_comp of every byte of w (A<->T, C<->G, N and IUPAC -> N, anything else 0)
 __device__ __forceinline__ uint32_t comp4(uint32_t w) {
-  constexpr uint32_t NI = (1u << ('N' - 'A')) | (1u << ('U' - 'A')) | (1u << ('R' - 'A')) | (1u << ('Y' - 'A')) |
-                          (1u << ('K' - 'A')) | (1u << ('M' - 'A')) | (1u << ('S' - 'A')) | (1u << ('W' - 'A')) |
-                          (1u << ('B' - 'A')) | (1u << ('D' - 'A')) | (1u << ('H' - 'A')) | (1u << ('V' - 'A'));
-  uint32_t out = 0;
+  const uint32_t sel = w & 0x07070707u, ok = acgtn_bytes(w, sel);
+  uint32_t out = perm8(T_COMP, sel) & (ok * 0xffu);
+  if (ok != 0x01010101u) {  // another character: IUPAC codes complement to N (utils.cpp revcomp), the rest to 0
+    constexpr uint32_t NI = (1u << ('N' - 'A')) | (1u << ('U' - 'A')) | (1u << ('R' - 'A')) | (1u << ('Y' - 'A')) |
+                            (1u << ('K' - 'A')) | (1u << ('M' - 'A')) | (1u << ('S' - 'A')) | (1u << ('W' - 'A')) |
+                            (1u << ('B' - 'A')) | (1u << ('D' - 'A')) | (1u << ('H' - 'A')) | (1u << ('V' - 'A'));
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t c = (w >> (8 * i)) & 0xffu, k = c - 'A';
-    const uint32_t r = (c == 'A' || c == 'T') ? 149u - c : (c == 'C' || c == 'G') ? 138u - c
-                       : (k < 26u && ((NI >> k) & 1u)) ? (uint32_t)'N' : 0u;
-    out |= r << (8 * i);
+    for (int i = 0; i < 4; i++) {
+      const uint32_t k = ((w >> (8 * i)) & 0xffu) - 'A';
+      if (!((ok >> (8 * i)) & 1u) && k < 26u && ((NI >> k) & 1u)) out |= (uint32_t)'N' << (8 * i);
+    }
   }
   return out;
 }
@@ -560,13 +568,32 @@ __device__ __forceinline__ int nz_bytes(uint32_t x) {  // bytes of x that are no
   x |= x >> 1;
   return __popc(x & 0x01010101u);
 }
+// inclusive prefix sum over the wave: DPP row shifts within the 16-lane rows, then the GFX9 row broadcasts
+// (row_bcast:15, row_bcast:31) across them; six VALU moves instead of six ds_bpermute round trips
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(v, d, 64);
-    if (lane >= d) v += y;
-  }
+  const int rl = lane & 15;
+  uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  if (rl >= 1) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  if (rl >= 2) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  if (rl >= 4) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  if (rl >= 8) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+  if (lane & 16) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+  if (lane >= 32) v += t;
   return v;
+}
+// lane l's value (l uniform): v_readlane into a scalar register, no LDS round trip as __shfl's ds_bpermute
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ double lane_f64(double v, int l) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long lo = lane_u32((uint32_t)b, l), hi = lane_u32((uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)((hi << 32) | lo));
 }
 // The lane index, recomputed where it is called: the compiler cannot hoist the lane-derived LDS addresses of a
 // loop body built from it out of the loop (in k_fq_merge's pair loop they took a dozen VGPRs for the whole
@@ -604,6 +631,9 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   const int16_t MIN_OVERLAP = 12, EXTRA_TEST_OVERLAP = 2, MAX_MISMATCHES = 3, EXTRA_PER_1000 = 150;
   const double MAX_PERROR = 0.025;
   uint64_t merged = 0, ambiguous = 0, ov_bases = 0;
+#if MHMKC_MGSTAMP
+  uint64_t mg_acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
   const uint64_t n_waves = (uint64_t)gridDim.x * MG_WAVES;
   if (blockIdx.x == 0 && threadIdx.x == 0) out_len[2 * n_pairs] = 0;  // the scan's last element
   const uint64_t n_items = long_list ? long_list[0] : n_pairs;
@@ -611,6 +641,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
 #if MHMKC_MG_OPAQUE
     const int lane = opaque_lane();
 #endif
+    MG_STAMP(t_p0);
     const uint64_t p = long_list ? long_list[16 + it] : it;
     const PairDesc d = desc[p];
     const bool is_long = d.L1 != ~0u && (d.L1 > MG_LONG || d.L2 > MG_LONG);
@@ -632,7 +663,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       *(uint32_t *)(Q1 + x0) = q;
       ((uint16_t *)S1n)[x0 >> 2] = nib4(c);
       const int nb = min(4, L1 - x0);
-      hasN |= (byte_eq_mask(c, 'N') & (0xffffffffu >> (32 - 8 * nb))) != 0;
+      hasN |= (eq_bytes(c, 0x4e4e4e4eu) & (0xffffffffu >> (32 - 8 * nb))) != 0;
     }
     for (int j0 = 4 * lane; j0 < L2; j0 += 256) {  // RC[j] = comp(s2[L2 - 1 - j]), RQ[j] = tq2[L2 - 1 - j]
       const int a0 = L2 - 4 - j0;  // s2 bytes a0 .. a0 + 3 are RC[j0 + 3] .. RC[j0]
@@ -642,8 +673,8 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       ((uint16_t *)RCn)[j0 >> 2] = nib4(c);
       const int nb = min(4, L2 - j0);
       const uint32_t valid = 0xffffffffu >> (32 - 8 * nb);
-      bad2 |= (byte_eq_mask(c, 0) & valid) != 0;
-      hasN |= (byte_eq_mask(c, 'N') & valid) != 0;
+      bad2 |= (zero_bytes(c) & valid) != 0;
+      hasN |= (eq_bytes(c, 0x4e4e4e4eu) & valid) != 0;
     }
     wave_sync_lds();
     if (lane < 4) {  // the fast filter's 4-byte reads past the lines see fixed bytes
@@ -655,6 +686,8 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       if (lane == 0) fq_fail(err, 2 * p + 1, FQ_E_CHAR2);
       continue;
     }
+    MG_STAMP(t_p1);
+    MG_ADD(0, t_p1 - t_p0);
     hasN = __ballot(hasN) != 0;
     const int16_t len = (int16_t)(L2 < L1 ? L2 : L1);
     const int16_t start_i = (len == (int16_t)L1) ? 0 : (int16_t)(L1 - len);
@@ -663,6 +696,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
     bool abort_merge = false, qbad = false, stop = false;
     for (int r0 = 0; r0 < n_off && !stop; r0 += 64) {
       // 1. fast filter of offsets r0 .. r0 + 63
+      MG_STAMP(t_f0);
       const int i = r0 + lane;
       bool pass = false;
       if (i < n_off) {
@@ -683,6 +717,11 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
         pass = mm <= emax;
       }
       uint64_t kept = __ballot(pass);
+#if MHMKC_MGSTAMP
+      const uint64_t t_f1 = __builtin_amdgcn_s_memtime();
+      MG_ADD(1, t_f1 - t_f0);
+      MG_ADD(5, 1);
+#endif
       // 2. + 3. the kept offsets in order
       while (kept && !stop) {
         const int io = r0 + __ffsll((long long)kept) - 1;
@@ -703,9 +742,11 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
           const uint8_t qa = ps == 'N' ? 0 : (uint8_t)(Q1[base + j] - qual_offset);
           const uint8_t qb = rs == 'N' ? 0 : (uint8_t)(RQ[j] - qual_offset);
           const bool bq = mis && (qa >= 81 || qb >= 81);
-          const uint32_t M = cM + wave_incl_scan(mis ? 1u + (uint32_t)nmis : 0u, lane);
-          const uint32_t NC = cN + wave_incl_scan(both ? 2u : (uint32_t)nmis, lane);
-          const uint32_t B = cB + wave_incl_scan(both ? 1u : 0u, lane);
+          // one scan of the three increments packed in 10-bit fields (a chunk adds at most 128 to each)
+          const uint32_t S = wave_incl_scan((mis ? 1u + (uint32_t)nmis : 0u) | ((both ? 2u : (uint32_t)nmis) << 10) |
+                                                (both ? 1u << 20 : 0u),
+                                            lane);
+          const uint32_t M = cM + (S & 0x3ffu), NC = cN + ((S >> 10) & 0x3ffu), B = cB + (S >> 20);
           // the reference's checks at j, in its order: a second both-N (in the match branch), a bad quality (in
           // the mismatch branch), then more than 3 N, then too many mismatches
           const int e = !in ? 0 : (both && B >= 2) ? 2 : bq ? 3 : NC > 3 ? 2 : (int)M > err_max ? 1 : 0;
@@ -725,8 +766,8 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
           while (mm) {
             const int l = __ffsll((long long)mm) - 1;
             mm &= mm - 1;
-            if ((nm >> l) & 1ull) perror += __shfl(t1, l, 64);
-            perror += __shfl(t2, l, 64);
+            if ((nm >> l) & 1ull) perror += lane_f64(t1, l);
+            perror += lane_f64(t2, l);
           }
           // the scan's quality effects (an N's quality := the offset), in LDS for the output
           if (nmis && j <= c0 + f) {
@@ -737,12 +778,12 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
           }
           if (f < 64) {
             jb = c0 + f;
-            ev = __shfl(e, f, 64);
-            cM = __shfl(M, f, 64);
+            ev = (int)lane_u32((uint32_t)e, f);
+            cM = lane_u32(M, f);
           } else {
-            cM = __shfl(M, 63, 64);
-            cN = __shfl(NC, 63, 64);
-            cB = __shfl(B, 63, 64);
+            cM = lane_u32(M, 63);
+            cN = lane_u32(NC, 63);
+            cB = lane_u32(B, 63);
           }
         }
         wave_sync_lds();
@@ -777,7 +818,11 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
           }
         }
         if (abort_merge) stop = true;  // the next offset's "if (abort_merge) break"
+        MG_ADD(4, 1);
       }
+#if MHMKC_MGSTAMP
+      MG_ADD(2, __builtin_amdgcn_s_memtime() - t_f1);
+#endif
     }
     if (qbad) {
       if (lane == 0) fq_fail(err, 2 * p + 1, FQ_E_QUAL);
@@ -804,7 +849,14 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       for (int j = lane; j < L2; j += 64) crq2[j] = RQ[j];
     }
     wave_sync_lds();  // the next pair overwrites the wave's LDS
+#if MHMKC_MGSTAMP
+    MG_ADD(3, __builtin_amdgcn_s_memtime() - t_p1);
+#endif
   }
+#if MHMKC_MGSTAMP
+  if (lane == 0)
+    for (int i = 0; i < 6; i++) atomicAdd(&stats[4 + i], (unsigned long long)mg_acc[i]);
+#endif
   if (lane == 0 && (merged | ambiguous)) {
     atomicAdd(&stats[1], (unsigned long long)merged);
     atomicAdd(&stats[2], (unsigned long long)ambiguous);

@@ -2239,7 +2239,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs, uint64_t *consu
     R_out = 2 * P;
     if ((e = grow(d_fq_recoffs, (R + 1) * 8)) != hipSuccess ||
         (e = grow(d_fq_scratch, std::max<uint64_t>(n_bases, 1) + 64)) != hipSuccess ||
-        (e = grow(d_fq_pairinfo, (P + 1) * 4)) != hipSuccess || (e = grow(d_fq_stats, 64)) != hipSuccess ||
+        (e = grow(d_fq_pairinfo, (P + 1) * 4)) != hipSuccess || (e = grow(d_fq_stats, 128)) != hipSuccess ||
         (e = grow(d_fq_desc, mhm::fq_pair_desc_bytes(P))) != hipSuccess ||
         (e = grow(d_fq_len, (2 * P + 1) * 8)) != hipSuccess)
       return hip_fail(e, "fastq pairs");
@@ -2252,7 +2252,7 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs, uint64_t *consu
     unsigned long long *len2 = d_fq_len.as<unsigned long long>();
     prof_begin(MHMKC_STAGE_OTHER);
     e = hipMemcpyAsync(roffs, offs, (R + 1) * 8, hipMemcpyDeviceToDevice, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(fst, 0, 32, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(fst, 0, 128, stream);
     if (e == hipSuccess)
       e = mhm::launch_fq_merge(d_text, n, lend, P, roffs, cfg.qual_offset, d_fq_scratch.as<char>(), d_fq_desc.p,
                                d_fq_pairinfo.as<uint32_t>(), len2, err_d, fst, stream);
@@ -2264,6 +2264,15 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs, uint64_t *consu
         (e = hipMemcpyAsync(hs, fst, 32, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipStreamSynchronize(stream)) != hipSuccess)
       return hip_fail(e, "fastq merge D2H");
+    if (getenv("MHMKC_PRINT_STAMPS")) {  // k_fq_merge phase cycles of an MHMKC_MGSTAMP build (diagnostics)
+      unsigned long long ms[6] = {0, 0, 0, 0, 0, 0};
+      if (hipMemcpy(ms, fst + 4, sizeof ms, hipMemcpyDeviceToHost) == hipSuccess && (ms[0] | ms[1] | ms[2] | ms[3])) {
+        const double t = (double)(ms[0] + ms[3]), tail = (double)ms[3] - (double)ms[1] - (double)ms[2];
+        fprintf(stderr, "k_fq_merge stamps: stage %.1f%% filter %.1f%% scans %.1f%% tail %.1f%% (%.0f cycles/pair); "
+                "%.2f scans and %.2f filter rounds per pair\n", 100 * ms[0] / t, 100 * ms[1] / t, 100 * ms[2] / t,
+                100 * tail / t, t / std::max<double>(1, P), ms[4] / std::max<double>(1, P), ms[5] / std::max<double>(1, P));
+      }
+    }
     st.fq_pairs = P;
     st.fq_merged = hs[1];
     st.fq_ambiguous = hs[2];
