@@ -568,23 +568,9 @@ __device__ __forceinline__ int nz_bytes(uint32_t x) {  // bytes of x that are no
   x |= x >> 1;
   return __popc(x & 0x01010101u);
 }
-// inclusive prefix sum over the wave: DPP row shifts within the 16-lane rows, then the GFX9 row broadcasts
-// (row_bcast:15, row_bcast:31) across them; six VALU moves instead of six ds_bpermute round trips
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-  const int rl = lane & 15;
-  uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  if (rl >= 1) v += t;
-  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  if (rl >= 2) v += t;
-  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  if (rl >= 4) v += t;
-  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  if (rl >= 8) v += t;
-  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x142, 0xf, 0xf, false);  // row_bcast:15
-  if (lane & 16) v += t;
-  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x143, 0xf, 0xf, false);  // row_bcast:31
-  if (lane >= 32) v += t;
-  return v;
+// the lanes below this one whose bit is set in m (v_mbcnt_lo / v_mbcnt_hi)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 // lane l's value (l uniform): v_readlane into a scalar register, no LDS round trip as __shfl's ds_bpermute
 __device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) {
@@ -742,11 +728,11 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
           const uint8_t qa = ps == 'N' ? 0 : (uint8_t)(Q1[base + j] - qual_offset);
           const uint8_t qb = rs == 'N' ? 0 : (uint8_t)(RQ[j] - qual_offset);
           const bool bq = mis && (qa >= 81 || qb >= 81);
-          // one scan of the three increments packed in 10-bit fields (a chunk adds at most 128 to each)
-          const uint32_t S = wave_incl_scan((mis ? 1u + (uint32_t)nmis : 0u) | ((both ? 2u : (uint32_t)nmis) << 10) |
-                                                (both ? 1u << 20 : 0u),
-                                            lane);
-          const uint32_t M = cM + (S & 0x3ffu), NC = cN + ((S >> 10) & 0x3ffu), B = cB + (S >> 20);
+          // the running counts up to j from ballots: mismatches (+1 more at an N), N bases (2 at a both-N),
+          // both-N positions; v_mbcnt counts a mask's lanes below this one
+          const uint64_t bmis = __ballot(mis), bnm = __ballot(nmis), bboth = __ballot(both);
+          const uint32_t im = lanes_below(bmis) + mis, in_ = lanes_below(bnm) + nmis, ib = lanes_below(bboth) + both;
+          const uint32_t M = cM + im + in_, NC = cN + 2 * ib + in_, B = cB + ib;
           // the reference's checks at j, in its order: a second both-N (in the match branch), a bad quality (in
           // the mismatch branch), then more than 3 N, then too many mismatches
           const int e = !in ? 0 : (both && B >= 2) ? 2 : bq ? 3 : NC > 3 ? 2 : (int)M > err_max ? 1 : 0;
@@ -762,7 +748,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
             t2 = dq <= 2 ? 0.5 : q2p[dq];
           }
           uint64_t mm = __ballot(mis && !bq) & upto;
-          const uint64_t nm = __ballot(nmis);
+          const uint64_t nm = bnm;
           while (mm) {
             const int l = __ffsll((long long)mm) - 1;
             mm &= mm - 1;
@@ -781,9 +767,10 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
             ev = (int)lane_u32((uint32_t)e, f);
             cM = lane_u32(M, f);
           } else {
-            cM = lane_u32(M, 63);
-            cN = lane_u32(NC, 63);
-            cB = lane_u32(B, 63);
+            const uint32_t pm = (uint32_t)__popcll(bmis), pn = (uint32_t)__popcll(bnm), pb = (uint32_t)__popcll(bboth);
+            cM += pm + pn;
+            cN += 2 * pb + pn;
+            cB += pb;
           }
         }
         wave_sync_lds();
@@ -864,18 +851,32 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   }
 }
 
-// PackedRead byte of base c with quality character q (packed_reads.cpp:87-105); false for a fatal character
-__device__ __forceinline__ uint8_t fq_byte(char c, char q, int qual_offset, bool &bad) {
-  const int code = base_code((unsigned char)c);
-  bad |= code < 0;
-  int v = (int)(signed char)q - qual_offset;
-  v = v > 31 ? 31 : v;
-  return (uint8_t)((code & 7) | (uint8_t)((unsigned char)v << 3));
+// Writes a wave's 256 packed bytes of one record (lane t: record bytes base + 4t .. + 3, packed in w) as ALIGNED
+// dwords, like k_fq_pack: the output dword of lane t holds record bytes [base + 4t - s, base + 4t + 4 - s), s the
+// record's misalignment, i.e. the high s bytes of the next lower lane's word (wave_shr:1 DPP; lane 0 takes the
+// previous step's lane 63, carry) and the low 4 - s of its own. Only the record's first and last dwords, which it
+// shares with its neighbours, are written bytewise. Every lane of the wave must call it (the DPP move).
+__device__ __forceinline__ void put_run(uint8_t *dst, int L, int base, int lane, uint32_t w, uint32_t &carry) {
+  const int s = (int)((uintptr_t)dst & 3u);
+  const uint32_t wm = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)w, 0x138, 0xf, 0xf, false);
+  carry = (uint32_t)__builtin_amdgcn_readlane((int)w, 63);
+  const uint32_t ow = s ? __builtin_amdgcn_alignbyte(w, wm, 4 - s) : w;
+  const int x0 = base + 4 * lane - s;  // record byte of the output dword's first byte
+  uint8_t *const o = dst + x0;          // aligned
+  if (x0 >= 0 && x0 + 4 <= L) {
+    *(uint32_t *)o = ow;
+  } else if (x0 < L && x0 + 4 > 0) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (x0 + j >= 0 && x0 + j < L) o[j] = (uint8_t)(ow >> (8 * j));
+  }
 }
 
 // One wave per pair (grid-stride), four output bytes per lane and step: the pair's output reads from its
 // descriptor in one round of loads. Merged read (x < L1 - ov: mate 1; the overlap: the higher-quality base,
 // :449-469; then the rest of mate 2 reverse-complemented, :472-473) + the dummy "N", or both mates as read.
+// The merge rules run per byte as selects, the four bytes are packed by pack4 (k_fq_pack's SWAR path) and
+// stored as aligned dwords (put_run).
 __global__ __launch_bounds__(64 * MG_WAVES) void k_fq_merge_pack(const char *text, const PairDesc *desc, uint64_t n_pairs,
                                                                   const unsigned long long *rec_offs,
                                                                   const char *scratch, const uint32_t *pair_info,
@@ -920,63 +921,62 @@ __global__ __launch_bounds__(64 * MG_WAVES) void k_fq_merge_pack(const char *tex
     uint8_t *dst0 = out + oo0, *dst1 = out + oo1;
     const int Lo0 = ov >= 0 ? L1 + L2 - ov : L1, st = ov >= 0 ? L1 - ov : L1;
     bool bad = false;
-    for (int x0 = 4 * lane; x0 < Lo0; x0 += 256) {
-      const uint32_t cs = x0 < L1 ? load4(s1 + x0, 0u) : 0u;
-      const uint32_t cq = x0 < L1 ? load4((hasN ? cq1 : tq1) + x0, 0u) : 0u;
-      uint32_t rc = 0, rq = 0;
-      const int jj = x0 - st;  // RC index of output byte x0
-      if (ov >= 0 && jj > -4) {
-        rc = comp4(__builtin_bswap32(load4(s2 + (L2 - 4 - jj), 0u)));
-        // (the scratch copy is in RC order; before its start, shift instead of reading before the buffer)
-        rq = hasN ? (jj >= 0 ? load4(crq2 + jj, 0u) : load4(crq2, 0u) << (8 * -jj))
-                  : __builtin_bswap32(load4(tq2 + (L2 - 4 - jj), 0u));
-      }
-      uint32_t ob = 0;
-      const int nb = min(4, Lo0 - x0);
+    uint32_t carry = 0;
+    const int s0 = (int)((uintptr_t)dst0 & 3u);
+    for (int base = 0; base - s0 < Lo0; base += 256) {
+      const int x0 = base + 4 * lane;
+      uint32_t w = 0;
+      if (x0 < Lo0) {
+        uint32_t cs = 0, cq = 0, rc = 0, rq = 0;
+        if (x0 < L1) {
+          cs = load4(s1 + x0, 0u);
+          cq = load4((hasN ? cq1 : tq1) + x0, 0u);
+        }
+        const int jj = x0 - st;  // RC index of output byte x0
+        if (ov >= 0 && jj > -4) {
+          rc = comp4(__builtin_bswap32(load4(s2 + (L2 - 4 - jj), 0u)));
+          // (the scratch copy is in RC order; before its start, shift instead of reading before the buffer)
+          rq = hasN ? (jj >= 0 ? load4(crq2 + jj, 0u) : load4(crq2, 0u) << (8 * -jj))
+                    : __builtin_bswap32(load4(tq2 + (L2 - 4 - jj), 0u));
+        }
+        uint32_t oc = cs, oq = cq;
+        if (ov >= 0 && x0 + 3 >= st) {
+          oc = 0;
+          oq = 0;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int x = x0 + i;
-        char c = (char)(cs >> (8 * i)), q = (char)(cq >> (8 * i));
-        const char r = (char)(rc >> (8 * i)), rqq = (char)(rq >> (8 * i));
-        if (ov >= 0 && x >= st) {
-          if (x < L1) {  // :449-469
-            if (c == r) {
-              const uint16_t nq = (uint16_t)(q + rqq - qual_offset);
-              q = (char)(nq > max_match_qual ? max_match_qual : nq);
-            } else {
-              uint8_t nq;
-              if (q < rqq) {
-                nq = (uint8_t)(rqq - q + qual_offset);
-                c = r;
-              } else {
-                nq = (uint8_t)(q - rqq + qual_offset);
-              }
-              q = (char)(nq > 2 + qual_offset ? nq : 2 + qual_offset);
-            }
-          } else {
-            c = r;
-            q = rqq;
+          for (int i = 0; i < 4; i++) {
+            const int x = x0 + i;
+            const char c = (char)(cs >> (8 * i)), q = (char)(cq >> (8 * i));
+            const char r = (char)(rc >> (8 * i)), rqq = (char)(rq >> (8 * i));
+            // :449-469 in the overlap (both bases), :472-473 after it (mate 2's)
+            const uint16_t nq1 = (uint16_t)(q + rqq - qual_offset);
+            const char qeq = (char)(nq1 > max_match_qual ? max_match_qual : nq1);
+            const bool lt = q < rqq;
+            const uint8_t nq2 = (uint8_t)(lt ? rqq - q + qual_offset : q - rqq + qual_offset);
+            const char qne = (char)(nq2 > 2 + qual_offset ? nq2 : 2 + qual_offset);
+            const bool inB = x >= st && x < L1, inC = x >= L1;
+            const char co = inB ? (c == r ? c : (lt ? r : c)) : inC ? r : c;
+            const char qo = inB ? (c == r ? qeq : qne) : inC ? rqq : q;
+            oc |= (uint32_t)(uint8_t)co << (8 * i);
+            oq |= (uint32_t)(uint8_t)qo << (8 * i);
           }
         }
-        bool bb = false;
-        const uint8_t v = fq_byte(c, q, qual_offset, bb);
-        bad |= bb && i < nb;
-        ob |= (uint32_t)v << (8 * i);
+        w = pack4(oc, oq, min(4, Lo0 - x0), qual_offset, bad);
       }
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-        if (i < nb) dst0[x0 + i] = (uint8_t)(ob >> (8 * i));
+      put_run(dst0, Lo0, base, lane, w, carry);
     }
     if (ov >= 0) {
       if (lane == 0) dst1[0] = 4;  // the dummy mate "N" with quality qual_offset
     } else {
-      for (int x0 = 4 * lane; x0 < L2; x0 += 256) {  // mate 2 as read (its bases passed the revcomp check)
-        const uint32_t cs = load4(s2 + x0, 0u), cq = load4(tq2 + x0, 0u);
-        const int nb = min(4, L2 - x0);
+      // mate 2 as read (its bases passed the revcomp check)
+      const int s1o = (int)((uintptr_t)dst1 & 3u);
+      carry = 0;
+      for (int base = 0; base - s1o < L2; base += 256) {
+        const int x0 = base + 4 * lane;
+        uint32_t w = 0;
         bool bb = false;
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-          if (i < nb) dst1[x0 + i] = fq_byte((char)(cs >> (8 * i)), (char)(cq >> (8 * i)), qual_offset, bb);
+        if (x0 < L2) w = pack4(load4(s2 + x0, 0u), load4(tq2 + x0, 0u), min(4, L2 - x0), qual_offset, bb);
+        put_run(dst1, L2, base, lane, w, carry);
       }
     }
     if (__ballot(bad) && lane == 0) fq_fail(err, 2 * p + 1, FQ_E_CHAR1);  // mate 1's (or the merged) PackedRead
