@@ -531,7 +531,8 @@ constexpr uint64_t byte_table(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3
 }
 // index (low 3 bits):          0     1    2     3    4    5     6    7
 constexpr uint64_t T_CHAR = byte_table(0x01, 'A', 0x01, 'C', 'T', 0x01, 'N', 'G');  // 0x01: matches no byte there
-constexpr uint64_t T_NIB = byte_table(15, 0, 15, 1, 3, 15, 4, 2);
+constexpr uint64_t T_CODE2 = byte_table(0, 0, 0, 1, 3, 0, 0, 2);
+constexpr uint64_t T_FLAG = byte_table(0, 0, 0, 0, 0, 0, 1, 0);
 constexpr uint64_t T_COMP = byte_table(0, 'T', 0, 'G', 'A', 0, 'N', 'C');
 // 0x01 in every byte of w that is one of A C G T N, 0 elsewhere
 __device__ __forceinline__ uint32_t acgtn_bytes(uint32_t w, uint32_t sel) {
@@ -539,12 +540,17 @@ __device__ __forceinline__ uint32_t acgtn_bytes(uint32_t w, uint32_t sel) {
 }
 // bit 7 of every byte of w equal to v (v replicated), 0 elsewhere
 __device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t v4) { return zero_bytes(w ^ v4); }
-// 4-bit codes of the four characters of w: A C G T N -> 0..4, anything else 15 (16 bits)
-__device__ __forceinline__ uint32_t nib4(uint32_t w) {
-  const uint32_t sel = w & 0x07070707u;
-  const uint32_t v = perm8(T_NIB, sel) | ((acgtn_bytes(w, sel) ^ 0x01010101u) * 15u);
-  const uint32_t t = v | (v >> 4);  // byte 0: codes 0 and 1, byte 2: codes 2 and 3
-  return (t & 0xffu) | ((t >> 8) & 0xff00u);
+// The fast filter's view of four characters: 2-bit codes (A C G T = 0..3, N and the rest 0) and 2-bit flags
+// (N 1, a character other than A C G T N 2, else 0), one byte each, first character in the low bits. Two
+// characters are equal exactly when both their codes and their flags are.
+__device__ __forceinline__ uint32_t pack2x4(uint32_t v) {  // four 2-bit values, one per byte, into one byte
+  const uint32_t t = v | (v >> 6);
+  return (t & 0xfu) | ((t >> 12) & 0xf0u);
+}
+__device__ __forceinline__ void codes_flags4(uint32_t w, uint32_t &code, uint32_t &flag) {
+  const uint32_t sel = w & 0x07070707u, ok = acgtn_bytes(w, sel);
+  code = pack2x4(perm8(T_CODE2, sel) & (ok * 0xffu));
+  flag = pack2x4((perm8(T_FLAG, sel) & (ok * 0xffu)) | ((ok ^ 0x01010101u) * 2u));
 }
 // fq_comp of every byte of w (A<->T, C<->G, N and IUPAC -> N, anything else 0)
 __device__ __forceinline__ uint32_t comp4(uint32_t w) {
@@ -603,9 +609,9 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
     char *scratch, uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
     unsigned long long *stats, const uint32_t *long_list) {
   __shared__ __align__(16) char lds[MG_WAVES][4][MAXL + 16];
-  // the bases again as 4-bit codes, 16 per word (A C G T N = 0..4, any other mate-1 character 15: it equals
-  // no mate-2 base), for the fast filter's 16-base compares
-  __shared__ __align__(16) uint64_t nib[MG_WAVES][2][MAXL / 16 + 4];
+  // the bases again as 2-bit codes and 2-bit flags (codes_flags4), 32 per word, for the fast filter's 32-base
+  // compares: [wave][S1 codes, S1 flags, RC codes, RC flags][word]
+  __shared__ __align__(16) uint64_t cf[MG_WAVES][4][MAXL / 32 + 4];
   // Q2Perror in LDS: a mismatch's table reads are divergent, and from constant memory each was a memory round
   // trip on the scan's critical path
   __shared__ double q2p[81];
@@ -613,7 +619,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   char *S1 = lds[w][0], *RC = lds[w][1], *Q1 = lds[w][2], *RQ = lds[w][3];
-  uint64_t *S1n = nib[w][0], *RCn = nib[w][1];
+  uint64_t *S1c = cf[w][0], *S1f = cf[w][1], *RCc = cf[w][2], *RCf = cf[w][3];
   const int16_t MIN_OVERLAP = 12, EXTRA_TEST_OVERLAP = 2, MAX_MISMATCHES = 3, EXTRA_PER_1000 = 150;
   const double MAX_PERROR = 0.025;
   uint64_t merged = 0, ambiguous = 0, ov_bases = 0;
@@ -647,7 +653,10 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       const uint32_t c = load4(s1, (uint32_t)x0), q = load4(tq1, (uint32_t)x0);
       *(uint32_t *)(S1 + x0) = c;
       *(uint32_t *)(Q1 + x0) = q;
-      ((uint16_t *)S1n)[x0 >> 2] = nib4(c);
+      uint32_t cc, ff;
+      codes_flags4(c, cc, ff);
+      ((uint8_t *)S1c)[x0 >> 2] = (uint8_t)cc;
+      ((uint8_t *)S1f)[x0 >> 2] = (uint8_t)ff;
       const int nb = min(4, L1 - x0);
       hasN |= (eq_bytes(c, 0x4e4e4e4eu) & (0xffffffffu >> (32 - 8 * nb))) != 0;
     }
@@ -656,16 +665,14 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       const uint32_t c = comp4(__builtin_bswap32(load4(s2 + a0, 0u))), q = __builtin_bswap32(load4(tq2 + a0, 0u));
       *(uint32_t *)(RC + j0) = c;
       *(uint32_t *)(RQ + j0) = q;
-      ((uint16_t *)RCn)[j0 >> 2] = nib4(c);
+      uint32_t cc, ff;
+      codes_flags4(c, cc, ff);
+      ((uint8_t *)RCc)[j0 >> 2] = (uint8_t)cc;
+      ((uint8_t *)RCf)[j0 >> 2] = (uint8_t)ff;
       const int nb = min(4, L2 - j0);
       const uint32_t valid = 0xffffffffu >> (32 - 8 * nb);
       bad2 |= (zero_bytes(c) & valid) != 0;
       hasN |= (eq_bytes(c, 0x4e4e4e4eu) & valid) != 0;
-    }
-    wave_sync_lds();
-    if (lane < 4) {  // the fast filter's 4-byte reads past the lines see fixed bytes
-      S1[L1 + lane] = 0;
-      RC[L2 + lane] = 1;
     }
     wave_sync_lds();
     if (__ballot(bad2)) {
@@ -688,16 +695,18 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       if (i < n_off) {
         const int ov = len - i;
         const int emax = (MAX_MISMATCHES + (EXTRA_PER_1000 * ov / 1000)) * 4 / 3 + 1;
-        // 16 bases per step: mate 1 from base start_i + i on (a funnel of two code words) against mate 2's
-        const int b0 = 4 * (start_i + i), k0 = b0 >> 6, sh = b0 & 63;
+        // 32 bases per step: mate 1 from base start_i + i on (funnels of two code and two flag words) against
+        // mate 2's; a base differs when its code or its flag does
+        const int b0 = 2 * (start_i + i), k0 = b0 >> 6, sh = b0 & 63;
         int mm = 0;
-        for (int j = 0; j < ov && mm <= emax; j += 16) {
-          const int k = k0 + (j >> 4);
-          const uint64_t a = (S1n[k] >> sh) | ((S1n[k + 1] << 1) << (63 - sh));
-          uint64_t x = a ^ RCn[j >> 4];
-          x = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111111111111111ull;
+        for (int j = 0; j < ov && mm <= emax; j += 32) {
+          const int k = k0 + (j >> 5);
+          const uint64_t ca = (S1c[k] >> sh) | ((S1c[k + 1] << 1) << (63 - sh));
+          const uint64_t fa = (S1f[k] >> sh) | ((S1f[k + 1] << 1) << (63 - sh));
+          uint64_t x = (ca ^ RCc[j >> 5]) | (fa ^ RCf[j >> 5]);
+          x = (x | (x >> 1)) & 0x5555555555555555ull;
           const int left = ov - j;  // bases of this step inside the overlap
-          if (left < 16) x &= (1ull << (4 * left)) - 1;
+          if (left < 32) x &= (1ull << (2 * left)) - 1;
           mm += __popcll(x);
         }
         pass = mm <= emax;
