@@ -731,11 +731,44 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
         for (int c0 = 0; c0 < overlap && jb < 0; c0 += 64) {
           const int j = c0 + lane;
           const bool in = j < overlap;
+          if (!hasN) {  // (uniform) a pair without N: no both-N or N-mismatch terms, no quality effects
+            const char ps = in ? S1[base + j] : 'A', rs = in ? RC[j] : 'A';
+            const bool eq = in && ps == rs, mis = in && ps != rs;
+            const uint8_t qa = in ? (uint8_t)(Q1[base + j] - qual_offset) : 0;
+            const uint8_t qb = in ? (uint8_t)(RQ[j] - qual_offset) : 0;
+            const bool bq = mis && (qa >= 81 || qb >= 81);
+            const uint64_t bmis = __ballot(mis);
+            const uint32_t M = cM + lanes_below(bmis) + mis;
+            const int e = !in ? 0 : bq ? 3 : (int)M > err_max ? 1 : 0;
+            const uint64_t evm = __ballot(e != 0);
+            const int f = evm ? __ffsll((long long)evm) - 1 : 64;
+            const uint64_t upto = f < 64 ? (f == 63 ? ~0ull : ((2ull << f) - 1)) : ~0ull;  // lanes <= f
+            matches += (uint32_t)__popcll(__ballot(eq) & upto);
+            double t2 = 0.0;
+            if (mis && !bq) {
+              const uint8_t dq = qa > qb ? qa - qb : qb - qa;
+              t2 = dq <= 2 ? 0.5 : q2p[dq];
+            }
+            uint64_t mm = __ballot(mis && !bq) & upto;
+            while (mm) {
+              const int l = __ffsll((long long)mm) - 1;
+              mm &= mm - 1;
+              perror += lane_f64(t2, l);
+            }
+            if (f < 64) {
+              jb = c0 + f;
+              ev = (int)lane_u32((uint32_t)e, f);
+              cM = lane_u32(M, f);
+            } else {
+              cM += (uint32_t)__popcll(bmis);
+            }
+            continue;
+          }
           const char ps = in ? S1[base + j] : 'A', rs = in ? RC[j] : 'A';
           const bool eq = in && ps == rs, both = eq && ps == 'N', mis = in && ps != rs;
           const bool nmis = mis && (ps == 'N' || rs == 'N');
-          const uint8_t qa = ps == 'N' ? 0 : (uint8_t)(Q1[base + j] - qual_offset);
-          const uint8_t qb = rs == 'N' ? 0 : (uint8_t)(RQ[j] - qual_offset);
+          const uint8_t qa = (ps == 'N' || !in) ? 0 : (uint8_t)(Q1[base + j] - qual_offset);
+          const uint8_t qb = (rs == 'N' || !in) ? 0 : (uint8_t)(RQ[j] - qual_offset);
           const bool bq = mis && (qa >= 81 || qb >= 81);
           // the running counts up to j from ballots: mismatches (+1 more at an N), N bases (2 at a both-N),
           // both-N positions; v_mbcnt counts a mask's lanes below this one
