@@ -50,11 +50,29 @@ __device__ __forceinline__ uint32_t nl_mask(const char *text, uint64_t pos, uint
   return m;
 }
 
+// Inclusive prefix sum over the wave: DPP row shifts within the 16-lane rows, then the GFX9 row broadcasts
+// (row_bcast:15, row_bcast:31) across them; six VALU moves instead of six ds_bpermute round trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+  const int rl = lane & 15;
+  uint32_t t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  if (rl >= 1) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  if (rl >= 2) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  if (rl >= 4) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  if (rl >= 8) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+  if (lane & 16) v += t;
+  t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+  if (lane >= 32) v += t;
+  return v;
+}
+
 __global__ __launch_bounds__(FQ_THREADS) void k_fq_count(const char *text, uint64_t n, unsigned long long *chunk) {
   __shared__ uint32_t s_w[FQ_THREADS / 64];
   const uint64_t pos = (uint64_t)blockIdx.x * FQ_CHUNK + (uint64_t)threadIdx.x * FQ_BYTES;
-  uint32_t c = __popc(nl_mask(text, pos, n));
-  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(__popc(nl_mask(text, pos, n)), threadIdx.x & 63), 63);
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -102,18 +120,15 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_lines(const char *text, uint6
   uint32_t v[4];
   uint32_t m = load16(text, pos, n, v);
   const uint32_t c = __popc(m);
-  uint32_t incl = c;
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
+  const uint32_t incl = wave_incl_scan(c, lane);
   if (lane == 63) s_w[wid] = incl;
   __syncthreads();
   uint64_t o = chunk_base[blockIdx.x] + (incl - c);
   for (int w = 0; w < wid; w++) o += s_w[w];
   // the neighbouring lanes' edge bytes (the byte before this lane's 16 and the byte after them), so that
   // only the wave's edge lanes go to memory for them
-  const uint32_t prev_w = __shfl_up(v[3], 1, 64), next_w = __shfl_down(v[0], 1, 64);
+  const uint32_t prev_w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[3], 0x138, 0xf, 0xf, false);  // wave_shr:1
+  const uint32_t next_w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[0], 0x130, 0xf, 0xf, false);  // wave_shl:1
   while (m) {
     const int b = __ffs(m) - 1;
     m &= m - 1;
@@ -483,11 +498,6 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_prep(const char *text, u
   desc[p] = d;
 }
 
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
 
 // One wave per pair (grid-stride). The pair is staged in the wave's LDS: mate 1's bases and qualities, mate
 // 2 reverse-complemented (RC) with its reversed qualities (RQ). Then
