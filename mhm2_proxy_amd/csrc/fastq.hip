@@ -450,7 +450,7 @@ struct PairDesc {
 #define MHMKC_MG_SHORT 512
 #endif
 #ifndef MHMKC_MG_OCC
-#define MHMKC_MG_OCC 6
+#define MHMKC_MG_OCC 8
 #endif
 #ifndef MHMKC_MG_OPAQUE
 #define MHMKC_MG_OPAQUE 1
@@ -627,7 +627,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   __shared__ double q2p[81];
   for (int t = threadIdx.x; t < 81; t += blockDim.x) q2p[t] = Q2P_TAB[t];
   __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (w scalar: scalar pair loads)
   char *S1 = lds[w][0], *RC = lds[w][1], *Q1 = lds[w][2], *RQ = lds[w][3];
   uint64_t *S1c = cf[w][0], *S1f = cf[w][1], *RCc = cf[w][2], *RCf = cf[w][3];
   const int16_t MIN_OVERLAP = 12, EXTRA_TEST_OVERLAP = 2, MAX_MISMATCHES = 3, EXTRA_PER_1000 = 150;
@@ -934,7 +934,9 @@ __global__ __launch_bounds__(64 * MG_WAVES) void k_fq_merge_pack(const char *tex
                                                                   const char *scratch, const uint32_t *pair_info,
                                                                   const unsigned long long *out_offs, int qual_offset,
                                                                   uint8_t *out, unsigned long long *err) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // the wave index as a scalar: the pair index, its descriptor, verdict and offsets then live in scalar registers
+  // (scalar loads), not in 25 VGPRs of every lane
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int max_match_qual = 41 + qual_offset;
   const uint64_t stride = (uint64_t)gridDim.x * MG_WAVES;
   // The next pair's descriptor, verdict and offsets are loaded while this pair is packed: the text loads of a
