@@ -2245,6 +2245,9 @@ __device__ __forceinline__ int count_opaque_tid() {
   asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
   return t;
 }
+#ifndef MHMKC_SWID
+#define MHMKC_SWID 1
+#endif
 template <int NL>
 __device__ __forceinline__ int count_tid() {
   if constexpr (NL >= MHMKC_COPAQUE_NL)
@@ -2293,14 +2296,19 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #else
   constexpr int WQ_THR = MW / 2 < 64 ? MW / 2 : 64;
 #endif
-  const uint32_t wq_base = (uint32_t)(threadIdx.x >> 6) * (uint32_t)MW;
+  const uint32_t wq_base = (uint32_t)(MHMKC_SWID ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6)) * (uint32_t)MW;
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
 
 #define tid (count_tid<NL>())  // (see count_tid; #undef after the kernel)
 #define lane (count_tid<NL>() & 63)
+#if MHMKC_SWID  // the wave index as a scalar (readfirstlane): per-wave queue / deferral / scan-slot addresses in SGPRs
+// (A/B: k = 21 count 4.83 -> 4.78 ms, k = 63 9.05 -> 8.95, k = 99 11.08 -> 11.03)
+#define wid (__builtin_amdgcn_readfirstlane(count_tid<NL>() >> 6))
+#else
 #define wid (count_tid<NL>() >> 6)
+#endif
   const uint64_t low_mask = (1ull << (EXT_BITS + p.hbits)) - 1;
 
   constexpr int R = count_rpt<NL>();
