@@ -259,20 +259,45 @@ __device__ __forceinline__ uint32_t load4(const char *text, uint32_t a) {
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
   return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
 }
+// Byte classification by v_perm_b32 lookups: the low three bits of A C T N G (1 3 4 6 7) are distinct, so
+// one 8-entry byte table indexed by them gives a candidate answer and a second gives the character that index
+// stands for; a byte is A/C/G/T/N exactly when it equals that character. No per-byte branches: the switch-like
+// compare chains these replace compiled to divergent branch trees, and k_fq_merge was bound by SALU issue.
+__device__ __forceinline__ uint32_t perm8(uint64_t table, uint32_t sel) {
+  return __builtin_amdgcn_perm((uint32_t)(table >> 32), (uint32_t)table, sel);
+}
+constexpr uint64_t byte_table(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3, uint32_t v4, uint32_t v5, uint32_t v6,
+                              uint32_t v7) {
+  return (uint64_t)v0 | (uint64_t)v1 << 8 | (uint64_t)v2 << 16 | (uint64_t)v3 << 24 | (uint64_t)v4 << 32 |
+         (uint64_t)v5 << 40 | (uint64_t)v6 << 48 | (uint64_t)v7 << 56;
+}
+// index (low 3 bits):          0     1    2     3    4    5     6    7
+constexpr uint64_t T_CHAR = byte_table(0x01, 'A', 0x01, 'C', 'T', 0x01, 'N', 'G');  // 0x01: matches no byte there
+constexpr uint64_t T_CODE5 = byte_table(0, 0, 0, 1, 3, 0, 4, 2);  // PackedRead base codes: A 0, C 1, G 2, T 3, N 4
+constexpr uint64_t T_CODE2 = byte_table(0, 0, 0, 1, 3, 0, 0, 2);
+constexpr uint64_t T_FLAG = byte_table(0, 0, 0, 0, 0, 0, 1, 0);
+constexpr uint64_t T_COMP = byte_table(0, 'T', 0, 'G', 'A', 0, 'N', 'C');
+// 0x01 in every byte of w that is one of A C G T N, 0 elsewhere
+__device__ __forceinline__ uint32_t acgtn_bytes(uint32_t w, uint32_t sel) {
+  return zero_bytes(w ^ perm8(T_CHAR, sel)) >> 7;
+}
+// bit 7 of every byte of w equal to v (v replicated), 0 elsewhere
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t v4) { return zero_bytes(w ^ v4); }
 __device__ __forceinline__ uint32_t pack4(uint32_t vs, uint32_t vq, int n_valid, int qual_offset, bool &bad) {
-  // SWAR fast path: four A/C/G/T bases with qualities in [qual_offset, 0x7f]
-  const uint32_t acgt = zero_bytes(vs ^ 0x41414141u) | zero_bytes(vs ^ 0x43434343u) | zero_bytes(vs ^ 0x47474747u) |
-                        zero_bytes(vs ^ 0x54545454u);
+  // SWAR fast path: A/C/G/T/N bases (codes by table, as nib and comp) with qualities in [qual_offset, 0x7f]; bytes
+  // past n_valid count as 'A' with quality qual_offset and come out 0, so a record's last word takes it too
   const uint32_t qo = (uint32_t)qual_offset * 0x01010101u;
-  const bool q_ok = (vq & 0x80808080u) == 0 && (((vq | 0x80808080u) - qo) & 0x80808080u) == 0x80808080u;
-  if (n_valid >= 4 && acgt == 0x80808080u && q_ok) {
-    uint32_t code = (vs >> 1) & 0x03030303u;  // A 0, C 1, G 3, T 2
-    code ^= (code >> 1) & 0x01010101u;        // G 2, T 3
-    uint32_t x = vq - qo;                     // q - offset per byte, no borrows
-    uint32_t over = x & 0x60606060u;          // q - offset >= 32 (< 0x80): bit 5 or 6
+  const uint32_t vm = n_valid >= 4 ? ~0u : (1u << (8 * n_valid)) - 1u;  // the valid bytes (n_valid >= 1)
+  const uint32_t s = (vs & vm) | (0x41414141u & ~vm), q = (vq & vm) | (qo & ~vm);
+  const uint32_t sel = s & 0x07070707u;
+  const bool q_ok = (q & 0x80808080u) == 0 && (((q | 0x80808080u) - qo) & 0x80808080u) == 0x80808080u;
+  if (acgtn_bytes(s, sel) == 0x01010101u && q_ok) {
+    const uint32_t code = perm8(T_CODE5, sel);  // A 0, C 1, G 2, T 3, N 4
+    uint32_t x = q - qo;                        // q - offset per byte, no borrows
+    uint32_t over = x & 0x60606060u;            // q - offset >= 32 (< 0x80): bit 5 or 6
     over = ((over | (over >> 1)) >> 5) & 0x01010101u;
     x = (x & ~(over * 0xffu)) | (over * 31u);  // min(q - offset, 31)
-    return code | (x << 3);
+    return (code | (x << 3)) & vm;
   }
   uint32_t w = 0;
 #pragma unroll
@@ -527,29 +552,6 @@ constexpr int MG_WAVES = 4;
 #endif
 constexpr int MG_MAXL = 2048;  // > FQ_MAX_LINE + 4 (unaligned 4-byte reads past a line stay inside)
 
-// Byte classification by v_perm_b32 lookups: the low three bits of A C T N G (1 3 4 6 7) are distinct, so
-// one 8-entry byte table indexed by them gives a candidate answer and a second gives the character that index
-// stands for; a byte is A/C/G/T/N exactly when it equals that character. No per-byte branches: the switch-like
-// compare chains these replace compiled to divergent branch trees, and k_fq_merge was bound by SALU issue.
-__device__ __forceinline__ uint32_t perm8(uint64_t table, uint32_t sel) {
-  return __builtin_amdgcn_perm((uint32_t)(table >> 32), (uint32_t)table, sel);
-}
-constexpr uint64_t byte_table(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3, uint32_t v4, uint32_t v5, uint32_t v6,
-                              uint32_t v7) {
-  return (uint64_t)v0 | (uint64_t)v1 << 8 | (uint64_t)v2 << 16 | (uint64_t)v3 << 24 | (uint64_t)v4 << 32 |
-         (uint64_t)v5 << 40 | (uint64_t)v6 << 48 | (uint64_t)v7 << 56;
-}
-// index (low 3 bits):          0     1    2     3    4    5     6    7
-constexpr uint64_t T_CHAR = byte_table(0x01, 'A', 0x01, 'C', 'T', 0x01, 'N', 'G');  // 0x01: matches no byte there
-constexpr uint64_t T_CODE2 = byte_table(0, 0, 0, 1, 3, 0, 0, 2);
-constexpr uint64_t T_FLAG = byte_table(0, 0, 0, 0, 0, 0, 1, 0);
-constexpr uint64_t T_COMP = byte_table(0, 'T', 0, 'G', 'A', 0, 'N', 'C');
-// 0x01 in every byte of w that is one of A C G T N, 0 elsewhere
-__device__ __forceinline__ uint32_t acgtn_bytes(uint32_t w, uint32_t sel) {
-  return zero_bytes(w ^ perm8(T_CHAR, sel)) >> 7;
-}
-// bit 7 of every byte of w equal to v (v replicated), 0 elsewhere
-__device__ __forceinline__ uint32_t eq_bytes(uint32_t w, uint32_t v4) { return zero_bytes(w ^ v4); }
 // The fast filter's view of four characters: 2-bit codes (A C G T = 0..3, N and the rest 0) and 2-bit flags
 // (N 1, a character other than A C G T N 2, else 0), one byte each, first character in the low bits. Two
 // characters are equal exactly when both their codes and their flags are.
