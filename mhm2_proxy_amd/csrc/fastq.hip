@@ -431,9 +431,15 @@ __device__ bool fq_norm(const char *s, uint64_t b, uint64_t e, uint64_t &pb, uin
       return true;
     }
     uint64_t tab = len, sp = len;
-    for (uint64_t i = 0; i < len && tab == len; i++) {
-      if (h[i] == '\t') tab = i;
-      if (h[i] == ' ' && sp == len) sp = i;
+    for (uint64_t i0 = 0; i0 < len && tab == len; i0 += 16) {  // 16 independent loads per step, as name_ok
+      char v[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) v[j] = i0 + j < len ? h[i0 + j] : 'x';
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        if (v[j] == '\t' && tab == len) tab = i0 + j;
+        if (v[j] == ' ' && sp == len) sp = i0 + j;
+      }
     }
     const uint64_t ep = tab < len ? tab : sp;
     if (ep == len) {  // no comment: unchanged
@@ -981,44 +987,38 @@ __global__ __launch_bounds__(64 * MG_WAVES) void k_fq_merge_pack(const char *tex
     const int s0 = (int)((uintptr_t)dst0 & 3u);
     for (int base = 0; base - s0 < Lo0; base += 256) {
       const int x0 = base + 4 * lane;
-      uint32_t w = 0;
-      if (x0 < Lo0) {
-        uint32_t cs = 0, cq = 0, rc = 0, rq = 0;
-        if (x0 < L1) {
-          cs = load4(s1 + x0, 0u);
-          cq = load4((hasN ? cq1 : tq1) + x0, 0u);
-        }
-        const int jj = x0 - st;  // RC index of output byte x0
-        if (ov >= 0 && jj > -4) {
-          rc = comp4(__builtin_bswap32(load4(s2 + (L2 - 4 - jj), 0u)));
-          // (the scratch copy is in RC order; before its start, shift instead of reading before the buffer)
-          rq = hasN ? (jj >= 0 ? load4(crq2 + jj, 0u) : load4(crq2, 0u) << (8 * -jj))
-                    : __builtin_bswap32(load4(tq2 + (L2 - 4 - jj), 0u));
-        }
-        uint32_t oc = cs, oq = cq;
-        if (ov >= 0 && x0 + 3 >= st) {
-          oc = 0;
-          oq = 0;
+      // branch-free: every lane loads (addresses clamped into the lines) and computes, selects pick the result
+      const int xs = min(x0, L1 - 1);
+      const uint32_t cs0 = load4(s1 + xs, 0u), cq0 = load4((hasN ? cq1 : tq1) + xs, 0u);
+      const uint32_t cs = x0 < L1 ? cs0 : 0u, cq = x0 < L1 ? cq0 : 0u;
+      const int jj = min(max(x0 - st, -3), L2 - 1);  // RC index of output byte x0 (clamped)
+      const uint32_t rc = comp4(__builtin_bswap32(load4(s2 + (L2 - 4 - jj), 0u)));
+      // (the scratch copy is in RC order; before its start, shift instead of reading before the buffer)
+      const uint32_t rq = hasN ? (jj >= 0 ? load4(crq2 + jj, 0u) : load4(crq2, 0u) << (8 * -jj))
+                               : __builtin_bswap32(load4(tq2 + (L2 - 4 - jj), 0u));
+      uint32_t mc = 0, mq = 0;
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int x = x0 + i;
-            const char c = (char)(cs >> (8 * i)), q = (char)(cq >> (8 * i));
-            const char r = (char)(rc >> (8 * i)), rqq = (char)(rq >> (8 * i));
-            // :449-469 in the overlap (both bases), :472-473 after it (mate 2's)
-            const uint16_t nq1 = (uint16_t)(q + rqq - qual_offset);
-            const char qeq = (char)(nq1 > max_match_qual ? max_match_qual : nq1);
-            const bool lt = q < rqq;
-            const uint8_t nq2 = (uint8_t)(lt ? rqq - q + qual_offset : q - rqq + qual_offset);
-            const char qne = (char)(nq2 > 2 + qual_offset ? nq2 : 2 + qual_offset);
-            const bool inB = x >= st && x < L1, inC = x >= L1;
-            const char co = inB ? (c == r ? c : (lt ? r : c)) : inC ? r : c;
-            const char qo = inB ? (c == r ? qeq : qne) : inC ? rqq : q;
-            oc |= (uint32_t)(uint8_t)co << (8 * i);
-            oq |= (uint32_t)(uint8_t)qo << (8 * i);
-          }
-        }
-        w = pack4(oc, oq, min(4, Lo0 - x0), qual_offset, bad);
+      for (int i = 0; i < 4; i++) {
+        const int x = x0 + i;
+        const char c = (char)(cs >> (8 * i)), q = (char)(cq >> (8 * i));
+        const char r = (char)(rc >> (8 * i)), rqq = (char)(rq >> (8 * i));
+        // :449-469 in the overlap (both bases), :472-473 after it (mate 2's)
+        const uint16_t nq1 = (uint16_t)(q + rqq - qual_offset);
+        const char qeq = (char)(nq1 > max_match_qual ? max_match_qual : nq1);
+        const bool lt = q < rqq;
+        const uint8_t nq2 = (uint8_t)(lt ? rqq - q + qual_offset : q - rqq + qual_offset);
+        const char qne = (char)(nq2 > 2 + qual_offset ? nq2 : 2 + qual_offset);
+        const bool inB = x >= st && x < L1, inC = x >= L1;
+        const char co = inB ? (c == r ? c : (lt ? r : c)) : inC ? r : c;
+        const char qo = inB ? (c == r ? qeq : qne) : inC ? rqq : q;
+        mc |= (uint32_t)(uint8_t)co << (8 * i);
+        mq |= (uint32_t)(uint8_t)qo << (8 * i);
       }
+      const bool mrg = ov >= 0 && x0 + 3 >= st;
+      bool bw = false;
+      const uint32_t pw = pack4(mrg ? mc : cs, mrg ? mq : cq, max(1, min(4, Lo0 - x0)), qual_offset, bw);
+      const uint32_t w = x0 < Lo0 ? pw : 0u;
+      bad |= bw && x0 < Lo0;
       put_run(dst0, Lo0, base, lane, w, carry);
     }
     if (ov >= 0) {
