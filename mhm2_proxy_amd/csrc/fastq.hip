@@ -709,26 +709,26 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       // 1. fast filter of offsets r0 .. r0 + 63
       MG_STAMP(t_f0);
       const int i = r0 + lane;
-      bool pass = false;
-      if (i < n_off) {
-        const int ov = len - i;
-        const int emax = (MAX_MISMATCHES + (EXTRA_PER_1000 * ov / 1000)) * 4 / 3 + 1;
-        // 32 bases per step: mate 1 from base start_i + i on (funnels of two code and two flag words) against
-        // mate 2's; a base differs when its code or its flag does
-        const int b0 = 2 * (start_i + i), k0 = b0 >> 6, sh = b0 & 63;
-        int mm = 0;
-        for (int j = 0; j < ov && mm <= emax; j += 32) {
-          const int k = k0 + (j >> 5);
-          const uint64_t ca = (S1c[k] >> sh) | ((S1c[k + 1] << 1) << (63 - sh));
-          const uint64_t fa = (S1f[k] >> sh) | ((S1f[k + 1] << 1) << (63 - sh));
-          uint64_t x = (ca ^ RCc[j >> 5]) | (fa ^ RCf[j >> 5]);
-          x = (x | (x >> 1)) & 0x5555555555555555ull;
-          const int left = ov - j;  // bases of this step inside the overlap
-          if (left < 32) x &= (1ull << (2 * left)) - 1;
-          mm += __popcll(x);
-        }
-        pass = mm <= emax;
+      // every lane runs the same steps (a uniform exit on a ballot, no per-lane loop masks): a lane past the
+      // offsets or already over its limit keeps adding masked or surplus counts, which change no verdict
+      const bool live = i < n_off;
+      const int ov = live ? len - i : 0;
+      const int emax = (MAX_MISMATCHES + (EXTRA_PER_1000 * ov / 1000)) * 4 / 3 + 1;
+      // 32 bases per step: mate 1 from base start_i + i on (funnels of two code and two flag words) against
+      // mate 2's; a base differs when its code or its flag does
+      const int b0 = 2 * (start_i + (live ? i : 0)), k0 = b0 >> 6, sh = b0 & 63;
+      int mm = 0;
+      for (int j = 0; __ballot(j < ov && mm <= emax) != 0; j += 32) {
+        const int k = k0 + (j >> 5);
+        const uint64_t ca = (S1c[k] >> sh) | ((S1c[k + 1] << 1) << (63 - sh));
+        const uint64_t fa = (S1f[k] >> sh) | ((S1f[k + 1] << 1) << (63 - sh));
+        uint64_t x = (ca ^ RCc[j >> 5]) | (fa ^ RCf[j >> 5]);
+        x = (x | (x >> 1)) & 0x5555555555555555ull;
+        const int left = ov - j;  // bases of this step inside the overlap
+        x &= left >= 32 ? ~0ull : left > 0 ? (1ull << (2 * left)) - 1 : 0ull;
+        mm += __popcll(x);
       }
+      const bool pass = live && mm <= emax;
       uint64_t kept = __ballot(pass);
 #if MHMKC_MGSTAMP
       const uint64_t t_f1 = __builtin_amdgcn_s_memtime();
