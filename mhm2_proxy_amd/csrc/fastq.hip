@@ -667,30 +667,34 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
     // staging, four bytes per lane and step (one load round trip for reads up to 256 bases); a step may read
     // up to three bytes before or after a line, which are text (the id line before it, the newline after it)
     bool bad2 = false, hasN = false;
-    for (int x0 = 4 * lane; x0 < L1; x0 += 256) {
-      const uint32_t c = load4(s1, (uint32_t)x0), q = load4(tq1, (uint32_t)x0);
-      *(uint32_t *)(S1 + x0) = c;
-      *(uint32_t *)(Q1 + x0) = q;
-      uint32_t cc, ff;
+    // both mates in one uniform loop: every lane loads (addresses clamped into the lines) and classifies, only the
+    // stores are masked (per-lane trip counts had the loops' exec masks saved and restored every step)
+    const int LM = L1 > L2 ? L1 : L2;
+    for (int b = 0; b < LM; b += 256) {
+      const int x0 = b + 4 * lane;
+      const int xs = min(x0, L1 - 1), js = min(x0, L2 - 1);
+      const uint32_t c = load4(s1, (uint32_t)xs), q = load4(tq1, (uint32_t)xs);
+      const int a0 = L2 - 4 - js;  // s2 bytes a0 .. a0 + 3 are RC[js + 3] .. RC[js]
+      const uint32_t rc = comp4(__builtin_bswap32(load4(s2 + a0, 0u))), rq = __builtin_bswap32(load4(tq2 + a0, 0u));
+      uint32_t cc, ff, rcc, rff;
       codes_flags4(c, cc, ff);
-      ((uint8_t *)S1c)[x0 >> 2] = (uint8_t)cc;
-      ((uint8_t *)S1f)[x0 >> 2] = (uint8_t)ff;
-      const int nb = min(4, L1 - x0);
-      hasN |= (eq_bytes(c, 0x4e4e4e4eu) & (0xffffffffu >> (32 - 8 * nb))) != 0;
-    }
-    for (int j0 = 4 * lane; j0 < L2; j0 += 256) {  // RC[j] = comp(s2[L2 - 1 - j]), RQ[j] = tq2[L2 - 1 - j]
-      const int a0 = L2 - 4 - j0;  // s2 bytes a0 .. a0 + 3 are RC[j0 + 3] .. RC[j0]
-      const uint32_t c = comp4(__builtin_bswap32(load4(s2 + a0, 0u))), q = __builtin_bswap32(load4(tq2 + a0, 0u));
-      *(uint32_t *)(RC + j0) = c;
-      *(uint32_t *)(RQ + j0) = q;
-      uint32_t cc, ff;
-      codes_flags4(c, cc, ff);
-      ((uint8_t *)RCc)[j0 >> 2] = (uint8_t)cc;
-      ((uint8_t *)RCf)[j0 >> 2] = (uint8_t)ff;
-      const int nb = min(4, L2 - j0);
-      const uint32_t valid = 0xffffffffu >> (32 - 8 * nb);
-      bad2 |= (zero_bytes(c) & valid) != 0;
-      hasN |= (eq_bytes(c, 0x4e4e4e4eu) & valid) != 0;
+      codes_flags4(rc, rcc, rff);
+      if (x0 < L1) {
+        *(uint32_t *)(S1 + x0) = c;
+        *(uint32_t *)(Q1 + x0) = q;
+        ((uint8_t *)S1c)[x0 >> 2] = (uint8_t)cc;
+        ((uint8_t *)S1f)[x0 >> 2] = (uint8_t)ff;
+      }
+      if (x0 < L2) {  // RC[j] = comp(s2[L2 - 1 - j]), RQ[j] = tq2[L2 - 1 - j]
+        *(uint32_t *)(RC + x0) = rc;
+        *(uint32_t *)(RQ + x0) = rq;
+        ((uint8_t *)RCc)[x0 >> 2] = (uint8_t)rcc;
+        ((uint8_t *)RCf)[x0 >> 2] = (uint8_t)rff;
+      }
+      const uint32_t v1 = x0 >= L1 ? 0u : L1 - x0 >= 4 ? ~0u : (1u << (8 * (L1 - x0))) - 1u;
+      const uint32_t v2 = x0 >= L2 ? 0u : L2 - x0 >= 4 ? ~0u : (1u << (8 * (L2 - x0))) - 1u;
+      bad2 |= (zero_bytes(rc) & v2) != 0;
+      hasN |= ((eq_bytes(c, 0x4e4e4e4eu) & v1) | (eq_bytes(rc, 0x4e4e4e4eu) & v2)) != 0;
     }
     wave_sync_lds();
     if (__ballot(bad2)) {
