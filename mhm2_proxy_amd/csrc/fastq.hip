@@ -647,13 +647,26 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   const uint64_t n_waves = (uint64_t)gridDim.x * MG_WAVES;
   if (blockIdx.x == 0 && threadIdx.x == 0) out_len[2 * n_pairs] = 0;  // the scan's last element
   const uint64_t n_items = long_list ? long_list[0] : n_pairs;
-  for (uint64_t it = (uint64_t)blockIdx.x * MG_WAVES + w; it < n_items; it += n_waves) {
+  // The next pair's index and descriptor are loaded (scalar loads) while this pair is worked: a pair starts with
+  // its text loads, not with a descriptor round trip before them.
+  const uint64_t it0 = (uint64_t)blockIdx.x * MG_WAVES + w;
+  uint64_t pn = 0;
+  PairDesc dn{0, 0, 0, 0, ~0u, 0};
+  if (it0 < n_items) {
+    pn = long_list ? long_list[16 + it0] : it0;
+    dn = desc[pn];
+  }
+  for (uint64_t it = it0; it < n_items; it += n_waves) {
 #if MHMKC_MG_OPAQUE
     const int lane = opaque_lane();
 #endif
     MG_STAMP(t_p0);
-    const uint64_t p = long_list ? long_list[16 + it] : it;
-    const PairDesc d = desc[p];
+    const uint64_t p = pn;
+    const PairDesc d = dn;
+    if (it + n_waves < n_items) {
+      pn = long_list ? long_list[16 + it + n_waves] : it + n_waves;
+      dn = desc[pn];
+    }
     const bool is_long = d.L1 != ~0u && (d.L1 > MG_LONG || d.L2 > MG_LONG);
     if (MAXL < MG_MAXL && is_long) continue;  // (listed for the MG_MAXL instance, which initialises its outputs)
     if (lane == 0) {
