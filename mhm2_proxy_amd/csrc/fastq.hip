@@ -392,31 +392,11 @@ __constant__ double Q2P_TAB[81] = {
     2.512e-07, 1.995e-07, 1.585e-07, 1.259e-07, 1e-07,     7.943e-08, 6.310e-08, 5.012e-08, 3.981e-08, 3.1622e-08, 2.512e-08,
     1.995e-08, 1.585e-08, 1.259e-08, 1e-08};
 
-// The lines of record r: id [b, te), sequence [sb, sb + L), quality [qb, qb + L); false when its lines are
-// not a valid record (k_fq_records reports that record)
+// A record's lines: id [idb, idte), sequence [sb, sb + L), quality [qb, qb + L) (fq_record_check)
 struct FqRec {
   uint64_t idb, idte, sb, qb;
   uint32_t L;
 };
-__device__ bool fq_rec(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t r, FqRec &o) {
-  uint64_t lw[5], lb[4], le[4], te[4];
-#pragma unroll
-  for (int i = 0; i < 5; i++) lw[i] = (4 * r + i) ? line_end[4 * r + i - 1] : 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    lb[i] = (4 * r + i) ? (lw[i] & FQ_LE_MASK) + 1 : 0;
-    le[i] = lw[i + 1] & FQ_LE_MASK;
-    te[i] = le[i] == n ? rtrim_end(text, lb[i], le[i]) : le[i] - ((lw[i + 1] >> FQ_LE_BITS) & 0xffffu);
-    if (le[i] - lb[i] > FQ_MAX_LINE) return false;
-  }
-  if (te[1] - lb[1] != te[3] - lb[3] || te[0] == lb[0]) return false;
-  o.idb = lb[0];
-  o.idte = te[0];
-  o.sb = lb[1];
-  o.qb = lb[3];
-  o.L = (uint32_t)(te[1] - lb[1]);
-  return true;
-}
 
 // get_fq_name + replace_spaces (fastq.cpp:73-122, :544): the normalized name of the trimmed id line [b, e) as
 // prefix [pb, pe) (the name without its last two characters) and the last character
@@ -466,7 +446,7 @@ __device__ bool fq_norm(const char *s, uint64_t b, uint64_t e, uint64_t &pb, uin
 // per pair: (overlap + 1) of the merge (0: not merged) | has-N << 31
 constexpr uint32_t MP_HASN = 1u << 31;
 
-// Where a pair's lines are (k_fq_pair_prep); L1 = ~0: the pair is not merged (a record or name error, which
+// Where a pair's lines are (k_fq_pair_records); L1 = ~0: the pair is not merged (a record or name error, which
 // is reported)
 struct PairDesc {
   uint64_t s1, q1, s2, q2;
@@ -475,7 +455,7 @@ struct PairDesc {
 
 // Pairs whose mates are both at most MG_LONG bases (every short-read run) go through a k_fq_merge instance with
 // MG_SHORT-byte staging: 11 KB of LDS per workgroup instead of 42 KB, so MHMKC_MG_OCC workgroups per CU instead of
-// three hide each other's LDS and shuffle round trips. k_fq_pair_prep lists the other pairs (after the
+// three hide each other's LDS and shuffle round trips. k_fq_pair_records lists the other pairs (after the
 // descriptors: a counter, then the pair indices), which a launch of the 2048-byte instance takes.
 #ifndef MHMKC_MG_SHORT
 #define MHMKC_MG_SHORT 512
@@ -492,22 +472,80 @@ __host__ __device__ inline uint32_t *long_pairs(void *desc_buf, uint64_t n_pairs
   return (uint32_t *)((char *)desc_buf + (((size_t)n_pairs * sizeof(PairDesc) + 63) & ~(size_t)63));
 }
 
-// One lane per pair: both records' lines and the name checks (:320-321). Many lanes in flight hide the chains
-// of dependent loads that name parsing is; the merge kernel then starts from one descriptor load.
-__global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_prep(const char *text, uint64_t n,
-                                                              const unsigned long long *line_end, uint64_t n_pairs,
-                                                              PairDesc *desc, uint32_t *long_list,
-                                                              unsigned long long *err) {
-  const uint64_t p = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x;
-  if (p >= n_pairs) return;
-  PairDesc d{0, 0, 0, 0, ~0u, 0};
+// Paired input: the records' checks (as k_fq_records) and the pairs' descriptors in one pass, one lane per pair
+// (until round 4 a separate k_fq_pair_prep re-read every id line and line-end word). Each record gets
+// k_fq_records' checks, length and errors (the id line's get_fq_name verdict is fq_norm's, which also gives the
+// name to compare); then the pair's names (replace_spaces: spaces read as '_', four characters per load) and
+// pair numbers are checked (:320-321) and its descriptor written. A trailing unpaired record (odd count) is
+// checked as a record only.
+__device__ bool fq_record_check(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t r,
+                                unsigned long long *len, unsigned long long *err, FqRec &o, uint64_t &pb, uint64_t &pe,
+                                char &last) {
+  uint64_t lw[5], lb[4], le[4], te[4];
+#pragma unroll
+  for (int i = 0; i < 5; i++) lw[i] = (4 * r + i) ? line_end[4 * r + i - 1] : 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    lb[i] = (4 * r + i) ? (lw[i] & FQ_LE_MASK) + 1 : 0;
+    le[i] = lw[i + 1] & FQ_LE_MASK;
+    te[i] = le[i] == n ? rtrim_end(text, lb[i], le[i]) : le[i] - ((lw[i + 1] >> FQ_LE_BITS) & 0xffffu);
+  }
+  len[r] = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    if (le[i] - lb[i] > FQ_MAX_LINE) {
+      fq_fail(err, r, FQ_E_LONG);
+      return false;
+    }
+  const unsigned char c_id = r ? (unsigned char)(lw[0] >> 56) : (n ? (unsigned char)text[0] : 0);
+  const unsigned char c_plus = (unsigned char)(lw[2] >> 56);
+  if (te[0] == lb[0] || c_id != '@') {
+    fq_fail(err, r, FQ_E_ID);
+    return false;
+  }
+  if (le[2] == lb[2] || c_plus != '+') {
+    fq_fail(err, r, FQ_E_PLUS);
+    return false;
+  }
+  if (!fq_norm(text, lb[0], te[0], pb, pe, last)) {
+    fq_fail(err, r, FQ_E_NAME);
+    return false;
+  }
+  const uint64_t L = te[1] - lb[1];
+  if (L != te[3] - lb[3]) {
+    fq_fail(err, r, FQ_E_LEN);
+    return false;
+  }
+  len[r] = L;
+  o.idb = lb[0];
+  o.idte = te[0];
+  o.sb = lb[1];
+  o.qb = lb[3];
+  o.L = (uint32_t)L;
+  return true;
+}
+__global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_records(const char *text, uint64_t n,
+                                                                 const unsigned long long *line_end, uint64_t n_rec,
+                                                                 unsigned long long *len, unsigned long long *err,
+                                                                 PairDesc *desc, uint32_t *long_list) {
+  const uint64_t p = (uint64_t)blockIdx.x * FQ_THREADS + threadIdx.x, r0 = 2 * p;
+  if (r0 > n_rec) return;
+  if (r0 == n_rec) {  // the scan's last element: offs[n_rec] = total
+    len[n_rec] = 0;
+    return;
+  }
   FqRec a, b;
-  uint64_t pb1, pe1, pb2, pe2;
-  char l1, l2;
-  if (fq_rec(text, n, line_end, 2 * p, a) && fq_rec(text, n, line_end, 2 * p + 1, b) &&
-      fq_norm(text, a.idb, a.idte, pb1, pe1, l1) && fq_norm(text, b.idb, b.idte, pb2, pe2, l2)) {
+  uint64_t pb1 = 0, pe1 = 0, pb2 = 0, pe2 = 0;
+  char l1 = 0, l2 = 0;
+  const bool ok1 = fq_record_check(text, n, line_end, r0, len, err, a, pb1, pe1, l1);
+  if (r0 + 1 == n_rec) {  // an unpaired last record; the scan's last element
+    len[n_rec] = 0;
+    return;
+  }
+  const bool ok2 = fq_record_check(text, n, line_end, r0 + 1, len, err, b, pb2, pe2, l2);
+  PairDesc d{0, 0, 0, 0, ~0u, 0};
+  if (ok1 && ok2) {
     bool same = pe1 - pb1 == pe2 - pb2;
-    // four characters per step (the bytes past a name are the rest of its record): spaces read as '_' on both sides
     for (uint64_t i = 0; same && i < pe1 - pb1; i += 4) {
       const uint64_t left = pe1 - pb1 - i;
       const uint32_t valid = left >= 4 ? ~0u : (1u << (8 * left)) - 1;
@@ -528,7 +566,6 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_prep(const char *text, u
   }
   desc[p] = d;
 }
-
 
 // One wave per pair (grid-stride). The pair is staged in the wave's LDS: mate 1's bases and qualities, mate
 // 2 reverse-complemented (RC) with its reversed qualities (RQ). Then
@@ -1094,19 +1131,25 @@ size_t fq_pair_desc_bytes(uint64_t n_pairs) {  // the descriptors, then the long
   return (((size_t)n_pairs * sizeof(PairDesc) + 63) & ~(size_t)63) + 64 + (size_t)n_pairs * 4 + 64;
 }
 
+hipError_t launch_fq_pair_records(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_rec,
+                                  unsigned long long *len, unsigned long long *err, void *desc_buf, hipStream_t s) {
+  const uint64_t n_pairs = n_rec / 2;
+  hipError_t e = hipMemsetAsync(long_pairs(desc_buf, n_pairs), 0, 4, s);
+  if (e != hipSuccess) return e;
+  const uint64_t nt = n_rec / 2 + 1;
+  k_fq_pair_records<<<dim3((unsigned)((nt + FQ_THREADS - 1) / FQ_THREADS)), dim3(FQ_THREADS), 0, s>>>(
+      text, n, line_end, n_rec, len, err, (PairDesc *)desc_buf, long_pairs(desc_buf, n_pairs));
+  return hipGetLastError();
+}
+
 hipError_t launch_fq_merge(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_pairs,
                            const unsigned long long *rec_offs, int qual_offset, char *scratch, void *desc_buf,
                            uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
                            unsigned long long *stats, hipStream_t s) {
+  // (the descriptors and the long-pair list come from launch_fq_pair_records)
   PairDesc *desc = (PairDesc *)desc_buf;
   uint32_t *long_list = long_pairs(desc_buf, n_pairs);
-  hipError_t e = hipMemsetAsync(long_list, 0, 4, s);
-  if (e != hipSuccess) return e;
-  if (n_pairs) {
-    k_fq_pair_prep<<<dim3((unsigned)((n_pairs + FQ_THREADS - 1) / FQ_THREADS)), dim3(FQ_THREADS), 0, s>>>(
-        text, n, line_end, n_pairs, desc, long_list, err);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
+  hipError_t e = hipSuccess;
   // grid-stride over the pairs, one wave each; enough waves to fill the chip several times over
   const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((n_pairs + MG_WAVES - 1) / MG_WAVES, 16384));
   k_fq_merge<MG_SHORT><<<dim3((unsigned)blocks), dim3(64 * MG_WAVES), 0, s>>>(

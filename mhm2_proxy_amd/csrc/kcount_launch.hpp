@@ -395,6 +395,9 @@ hipError_t launch_fq_lines(const char *text, uint64_t n, const unsigned long lon
                            unsigned long long *line_end, hipStream_t s);
 // per record: sequence length (len[n_rec] = 0 for the scan) and format checks (err: atomicMin of
 // record << 4 | FQ_E_*)
+// paired input: k_fq_records' checks and the pair descriptors in one pass (launch_fq_merge reads the descriptors)
+hipError_t launch_fq_pair_records(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_rec,
+                                  unsigned long long *len, unsigned long long *err, void *desc_buf, hipStream_t s);
 hipError_t launch_fq_records(const char *text, uint64_t n, const unsigned long long *line_end, uint64_t n_rec,
                              unsigned long long *len, unsigned long long *err, hipStream_t s);
 // pair p = records 2p, 2p+1: verdict in pair_info, output read lengths (merged + 1, or L1, L2) in out_len

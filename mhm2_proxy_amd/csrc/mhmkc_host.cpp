@@ -2219,7 +2219,12 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs, uint64_t *consu
   if (e == hipSuccess && !consumed && last != '\n')
     e = hipMemcpyAsync(lend + lines - 1, &n_end, 8, hipMemcpyHostToDevice, stream);
   if (e == hipSuccess) e = hipMemsetAsync(err_d, 0xff, 8, stream);
-  if (e == hipSuccess) e = mhm::launch_fq_records(d_text, n, lend, R, len, err_d, stream);
+  if (e == hipSuccess && pairs) {  // the records' checks and the pairs' descriptors in one pass
+    if ((e = grow(d_fq_desc, mhm::fq_pair_desc_bytes(R / 2))) == hipSuccess)
+      e = mhm::launch_fq_pair_records(d_text, n, lend, R, len, err_d, d_fq_desc.p, stream);
+  } else if (e == hipSuccess) {
+    e = mhm::launch_fq_records(d_text, n, lend, R, len, err_d, stream);
+  }
   if (e == hipSuccess) e = mhm::fq_scan(d_fq_tmp.p, tmp_bytes, len, offs, R + 1, stream);
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "fastq records");
