@@ -2638,6 +2638,10 @@ int mhmkc_set_transport(mhmkc_t h, const mhmkc_transport *t) {
   if (h->comm) return h->fail(MHMKC_EINVAL, "the handle already has an RCCL communicator (comm_id)");
   h->xp = *t;
   h->has_xp = true;
+  // A host-staged transport moves a few GB/s, so the last exchange round (the one no extraction overlaps) is
+  // what a step waits for: cut the batch finer (2 ranks, C2: 252 -> 57 ms exposed for 4 % more bytes, DESIGN.md
+  // §3.5e). RCCL over xGMI keeps 4 pieces, where the pieces' slack bytes cost more than their overlap gains.
+  if (!getenv("MHMKC_XPIECES")) h->xpieces = 16;
   return MHMKC_OK;
 }
 
