@@ -343,12 +343,14 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pack(const char *text, const 
   // (hoisting the loads of 4 runs ahead of their use measured slower: 3.38 vs 3.09 ms at C2)
   for (int base = 0; 4 * base - 3 < wave_L; base += FQ_GROUP) {
     const int d = base + gl, i = 4 * d;
-    uint32_t vs = 0x41414141u, vq = 0;
-    if (i < L) {
-      vs = load4(sp, (uint32_t)i);
-      vq = load4(qp, (uint32_t)i);
-    }
-    const uint32_t w = pack4(vs, vq, min(4, L - i), qual_offset, bad);
+    // every lane loads (clamped into the record; an idle group's L = 0 reads the text's first dword) and packs;
+    // lanes past the record keep 0 and raise no error
+    const int ic = min(i, max(L - 1, 0));
+    const uint32_t vs = load4(sp, (uint32_t)ic), vq = load4(qp, (uint32_t)ic);
+    bool bw = false;
+    const uint32_t pw = pack4(vs, vq, max(1, min(4, L - i)), qual_offset, bw);
+    const uint32_t w = i < L ? pw : 0u;
+    bad |= bw && i < L;
     // W_{d-1}: row_shr:1 within the 16-lane row; lane 0 of the row keeps 'old' = carry
     const uint32_t wm = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)w, 0x111, 0xf, 0xf, false);
     carry = (uint32_t)__shfl((int)w, last_of_group, 64);
