@@ -1692,12 +1692,18 @@ __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, uns
 #ifndef MHMKC_CRPT
 #define MHMKC_CRPT 4
 #endif
-template <int NL>
+// two-word keys: one record per lane per round (round 4, with the dynamic slots of cold sweeps: fewer records in
+// flight lose fewer claims to each other, phase-B records at k = 63 100M -> 71M; count k = 63 8.92 -> 8.81 ms,
+// k = 33 8.56 -> 8.19 ms)
 #ifndef MHMKC_CRPT2
-#define MHMKC_CRPT2 2
+#define MHMKC_CRPT2 1
 #endif
+#ifndef MHMKC_CRPT3
+#define MHMKC_CRPT3 1  // three- and four-word keys (was 2: count k = 77 10.49 -> 10.25 ms, k = 99 11.02 -> 10.06 ms)
+#endif
+template <int NL>
 constexpr int count_rpt() {
-  return NL == 1 ? MHMKC_CRPT : NL == 2 ? MHMKC_CRPT2 : 2;
+  return NL == 1 ? MHMKC_CRPT : NL == 2 ? MHMKC_CRPT2 : MHMKC_CRPT3;
 }
 
 // LDS slot hash of k_count. All keys of a fine bucket share their top MurmurHash3 bits, so the slot
