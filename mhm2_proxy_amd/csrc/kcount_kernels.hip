@@ -1797,7 +1797,8 @@ constexpr int C_PROBE = MHMKC_CPROBE;
 #define MHMKC_GS_C 4  // compact (32-bit) keys
 #endif
 #ifndef MHMKC_GS_M2
-#define MHMKC_GS_M2 2  // mixed two-word keys (the last word, 64-bit, is the one read): k = 63 count 9.32 -> 9.09 ms
+#define MHMKC_GS_M2 4  // mixed two-word keys: 2 (one ds_read_b128 of the last words) measured 9.32 -> 9.09 ms at k = 63
+                       // in round 3; with one record per lane per round and full-slice queues 4 is faster (8.18 -> 7.99)
 #endif
 #ifndef MHMKC_GS_MX
 #define MHMKC_GS_MX 4  // mixed three- and four-word keys
@@ -2300,7 +2301,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #ifdef MHMKC_WQ_DIV  // (A/B: work the queue off at MW / MHMKC_WQ_DIV entries)
   constexpr int WQ_THR = MW / MHMKC_WQ_DIV < 64 ? MW / MHMKC_WQ_DIV : 64;
 #else
-  constexpr int WQ_THR = MW / 2 < 64 ? MW / 2 : 64;
+  // (round 4, with one record per lane per round: a two-word key's queue is worked off when its slice is full, not
+  // half full: k = 63 count 8.27 -> 8.00 ms; three-word keys measured 10.28 -> 11.48 ms that way, four-word the same)
+  constexpr int WQ_THR = NL == 2 ? (MW < 64 ? MW : 64) : (MW / 2 < 64 ? MW / 2 : 64);
 #endif
   const uint32_t wq_base = (uint32_t)(MHMKC_SWID ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6)) * (uint32_t)MW;
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
