@@ -383,7 +383,7 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pack(const char *text, const 
 // output keeps; pairs with an N therefore scan copies of their quality lines in a scratch laid out like the
 // packed records (mate 1's qualities, mate 2's reversed), the others read the text in place.
 
-// Q2Perror (merge_reads.cpp:57-65), 81 entries
+// Q2Perror (merge_reads.cpp:73-81), 81 entries
 __constant__ double Q2P_TAB[81] = {
     1.0,       0.7943,    0.6309,    0.5012,    0.3981,    0.3162,    0.2512,    0.1995,    0.1585,    0.1259,     0.1,
     0.07943,   0.06310,   0.05012,   0.03981,   0.03162,   0.02512,   0.01995,   0.01585,   0.01259,   0.01,       0.007943,

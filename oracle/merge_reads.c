@@ -23,7 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-/* Q2Perror of merge_reads.cpp:57-65: 10^(-q/10) as the reference tabulates it (81 entries, q = 0..80) */
+/* Q2Perror of merge_reads.cpp:73-81: 10^(-q/10) as the reference tabulates it (81 entries, q = 0..80) */
 static const double Q2P[81] = {
     1.0,       0.7943,    0.6309,    0.5012,    0.3981,    0.3162,    0.2512,    0.1995,    0.1585,    0.1259,     0.1,
     0.07943,   0.06310,   0.05012,   0.03981,   0.03162,   0.02512,   0.01995,   0.01585,   0.01259,   0.01,       0.007943,
