@@ -395,6 +395,39 @@ __device__ __forceinline__ void walk_c32(const uint64_t *fwd, const uint32_t *go
   }
 }
 
+// walk_c32 with each window's record in two u32 registers instead of a u64 and an info word: lo = the record's low
+// 32 bits, hi = valid << 31 | (the record's bits 32..39) << 11 | bin (bits 19..30 stay free for the window's rank
+// in its bin, scatter_staged_c40). 48 -> 32 VGPRs of records per thread, so the kernel fits 96 VGPRs (five
+// workgroups per CU) without spilling.
+template <int W>
+__device__ __forceinline__ void walk_c32_lh(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
+                                            uint32_t tile, uint64_t n_bases, uint32_t head, int k, int cb,
+                                            uint32_t (&lo)[W], uint32_t (&hi)[W]) {
+  WalkSpan<1> sp(fwd, good, start, tile, n_bases, head, k);
+  const int B = 2 * k, a = B >> 1, b = B - a, rb = B - cb;
+  const uint64_t mB = (1ull << B) - 1, rmask = (1ull << rb) - 1;
+  uint64_t fw = WalkSpan<1>::codes64(fwd, sp.lp0) >> (64 - B);
+  uint64_t rc = rev2(~fw) >> (64 - B);
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    uint32_t cr, e_f, e_r;
+    const bool valid = sp.step(i, k, cr, e_f, e_r);
+    const bool use_rc = rc < fw;
+    const uint64_t x = use_rc ? rc : fw;
+    const uint32_t e = use_rc ? e_r : e_f;
+    uint32_t R = (uint32_t)x & ((1u << a) - 1), L = (uint32_t)(x >> a);
+    cmix_lr(L, R, a, b);
+    const uint64_t y = ((uint64_t)L << a) | R;
+    const uint64_t r = ((y & rmask) << EXT_BITS) | e;
+    lo[i] = (uint32_t)r;
+    hi[i] = valid ? (1u << 31) | (((uint32_t)(r >> 32) & 0xffu) << 11) | (uint32_t)(y >> rb) : 0u;
+    asm volatile("" : "+v"(lo[i]), "+v"(hi[i]));
+    sp.cl = (uint32_t)(fw >> (B - 2));
+    fw = ((fw << 2) | cr) & mB;
+    rc = (rc >> 2) | ((uint64_t)(cr ^ 3u) << (B - 2));
+  }
+}
+
 // Mixed two-word walk (33 <= k <= 63, §3.7b): the 2k-bit key kept as its two k-bit halves (L = the top k bits,
 // R = the low k bits), the form m2_mix_lr takes, rolled and compared as halves; record w[0] = (L' below the coarse
 // digit) << 6 | ext, w[1] = R', bin = the coarse digit (L''s top cb bits).
@@ -636,8 +669,14 @@ constexpr size_t WSUM_BYTES = ((1024 / 64 + 1) * 4 + 15) & ~(size_t)15;  // bloc
 // lanes store consecutive addresses of one bin (runs of ~T/nb records instead of one line per lane).
 // LDS: counters [lcnt | goff | lstart | wsum] then the stage area [NL][T] u64 | sbin[T] u16 | sext[T] u8,
 // which may alias the tile (the first barrier below is after every thread's walk).
+// The bins' run starts (lstart) reuse the rank counters (lcnt): each thread reads its bins' counts, then
+// overwrites the same entries (MHMKC_LSALIAS=0: a plane of their own). At k = 21 this keeps an extraction
+// workgroup's LDS (counters + the staged tile) under 32 KiB, five per CU.
+#ifndef MHMKC_LSALIAS
+#define MHMKC_LSALIAS 1
+#endif
 __host__ __device__ constexpr size_t staged_cnt_bytes(uint32_t nb) {
-  return scatter_lds_bytes(nb) + (((size_t)nb * 4 + 15) & ~(size_t)15) + WSUM_BYTES;
+  return scatter_lds_bytes(nb) + (MHMKC_LSALIAS ? 0 : (((size_t)nb * 4 + 15) & ~(size_t)15)) + WSUM_BYTES;
 }
 // Compact records are staged at their stored width: u32 (+ the high byte for SF_C40).
 __host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packed, int sf = SF_WORDS) {
@@ -654,7 +693,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   constexpr int T = W * NT;
   uint32_t *lcnt = (uint32_t *)smem;
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
-  uint32_t *lstart = (uint32_t *)(smem + scatter_lds_bytes(nb));
+  uint32_t *lstart = MHMKC_LSALIAS ? lcnt : (uint32_t *)(smem + scatter_lds_bytes(nb));
   uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - WSUM_BYTES);
   constexpr bool C32 = SF == SF_C40 || SF == SF_C32;  // compact: low 32 bits in stage32, the high byte (SF_C40) in sext
   uint64_t *stage = (uint64_t *)area;
@@ -735,6 +774,76 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
         for (int w = 0; w < NL; w++) v[w] = stage[w * T + pos];
       }
       store_out<NL, PACKED, SF>(out, dst, v, PACKED ? 0u : sext[pos]);
+    }
+  }
+}
+
+// scatter_staged for compact 40-bit records held as lo / hi words (walk_c32_lh): the window's rank in its bin
+// goes into hi's free bits 19..30 instead of a register of its own (bins <= 2048, T <= 4096).
+template <int W, int NT>
+__device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (&hi)[W], uint32_t nb,
+                                                   unsigned char *smem, unsigned char *area,
+                                                   unsigned long long *cursor, const PlaneSet &out,
+                                                   const BinLimit lim, unsigned int *err) {
+  constexpr int T = W * NT;
+  static_assert(T <= 4096 && 8 * NT <= 2048, "rank in 12 bits, bin in 11");
+  uint32_t *lcnt = (uint32_t *)smem;
+  unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
+  uint32_t *lstart = MHMKC_LSALIAS ? lcnt : (uint32_t *)(smem + scatter_lds_bytes(nb));
+  uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - WSUM_BYTES);
+  uint32_t *stage32 = (uint32_t *)area;
+  uint16_t *sbin = (uint16_t *)(stage32 + T);
+  uint8_t *sext = (uint8_t *)(sbin + T);
+#pragma unroll
+  for (int j = 0; j < W; j++)
+    if (hi[j] >> 31) hi[j] |= atomicAdd(&lcnt[hi[j] & 0x7ffu], 1u) << 19;
+  __syncthreads();
+  unsigned long long off[8];
+  uint32_t cnt[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t b = threadIdx.x + i * NT;
+    off[i] = 0;
+    cnt[i] = 0;
+    if (b < nb) {
+      const uint32_t c = lcnt[b];
+      cnt[i] = c;
+      if (c) off[i] = atomicAdd(&cursor[b], (unsigned long long)c);
+      lstart[b] = c;
+    }
+  }
+  __syncthreads();
+  const uint32_t total = block_excl_scan<NT>(lstart, (int)nb, wsum);
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    if (hi[j] >> 31) {
+      const uint32_t d = hi[j] & 0x7ffu;
+      const uint32_t pos = lstart[d] + ((hi[j] >> 19) & 0xfffu);
+      stage32[pos] = lo[j];
+      sext[pos] = (uint8_t)(hi[j] >> 11);
+      sbin[pos] = (uint16_t)d;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t b = threadIdx.x + i * NT;
+    if (b < nb) {
+      const bool over = lim.cap && cnt[i] && off[i] + cnt[i] > lim.end(b);
+      if (over) atomicOr(err, 2u);
+      goff[b] = over ? ~0ull : off[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    const uint32_t pos = threadIdx.x + j * NT;
+    if (pos < total) {
+      const uint32_t d = sbin[pos];
+      const unsigned long long go = goff[d];
+      if (go == ~0ull) continue;
+      const unsigned long long dst = go + (pos - lstart[d]);
+      ((uint32_t *)out.w[0])[dst] = stage32[pos];
+      out.ext[dst] = sext[pos];
     }
   }
 }
@@ -917,8 +1026,25 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
 // ------------------------------------------------------------------------------------------------
 // extract: scatter into coarse buckets
 
+// Compact records of the extraction as two u32 registers per window (walk_c32_lh + scatter_staged_c40)
+#ifndef MHMKC_C40REG
+#define MHMKC_C40REG 1
+#endif
+constexpr bool kC40Reg = MHMKC_C40REG != 0;
+// Minimum waves per SIMD asked of the compiler for the extraction (caps its VGPRs; 1: no cap)
+#ifndef MHMKC_EWAVES1
+#define MHMKC_EWAVES1 1
+#endif
+#ifndef MHMKC_EWAVES2
+#define MHMKC_EWAVES2 1
+#endif
+template <int NL>
+constexpr int kEWaves() {
+  return NL == 1 ? MHMKC_EWAVES1 : NL == 2 ? MHMKC_EWAVES2 : 1;
+}
+
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractParams p) {
+__global__ __launch_bounds__(kEThreads<NL>()) __attribute__((amdgpu_waves_per_eu(kEWaves<NL>()))) void k_extract_scatter(ExtractParams p) {
   constexpr int ET = kEThreads<NL>(), T = kTile<NL>(), W = T / ET;
   const int kk = p.k;
   extern __shared__ __align__(16) unsigned char smem0[];
@@ -951,6 +1077,14 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_scatter(ExtractPara
   const int csh = 64 - (2 * kk - p.coarse_bits);  // compact: keep the low 2k - cb bits of the mixed key
   const int m2_csh = kk - p.coarse_bits;            // mixed two-word: L' >> m2_csh = coarse digit
   const uint64_t m2_cmask = (1ull << m2_csh) - 1;
+  if constexpr (RecKind<NL, CMP>::C32 && kMixedWalk && kC40Reg && kEStagedNL<NL>()) {
+    uint32_t lo[W], hi[W];
+    walk_c32_lh<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, lo, hi);
+    const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
+    const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
+    scatter_staged_c40<W, ET>(lo, hi, p.n_bins, smem, area, p.cursor + sub * p.n_bins, p.out, lim, p.ovf);
+    return;
+  }
   uint64_t rk[W][NL];
   uint32_t inf[W];
   if constexpr (RecKind<NL, CMP>::C32 && kMixedWalk) {
