@@ -685,12 +685,16 @@ __host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packe
                         : (size_t)nl * T * 8 + (size_t)T * 2 + (packed ? 0 : (size_t)T);
 }
 
-template <int NL, bool PACKED, int W, int SF, int NT = E_THREADS>
+// CAP < W * NT: the stage area holds CAP records and the records go out in rounds of CAP (bin order), so a
+// workgroup whose windows are mostly not counted (k = 77, 99 on 150-base reads: 48 %, 33 % counted) needs LDS for
+// the records it has, not for one per window.
+template <int NL, bool PACKED, int W, int SF, int NT = E_THREADS, int CAP = W * NT>
 __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
                                                unsigned char *smem, unsigned char *area,
                                                unsigned long long *cursor, uint32_t cstride, const PlaneSet &out,
                                                const BinLimit lim, unsigned int *err) {
-  constexpr int T = W * NT;
+  constexpr int T = CAP;
+  static_assert(CAP <= W * NT && CAP % NT == 0, "stage capacity: whole rows of the workgroup");
   uint32_t *lcnt = (uint32_t *)smem;
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
   uint32_t *lstart = MHMKC_LSALIAS ? lcnt : (uint32_t *)(smem + scatter_lds_bytes(nb));
@@ -723,11 +727,14 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   }
   __syncthreads();
   const uint32_t total = block_excl_scan<NT>(lstart, (int)nb, wsum);
+  for (uint32_t r0 = 0; r0 < total; r0 += CAP) {  // (uniform) one round when CAP = W * NT
+  if (r0) __syncthreads();  // the previous round's copy-out has read the stage area
 #pragma unroll
   for (int j = 0; j < W; j++) {
     if (inf[j] >> 31) {
       const uint32_t d = inf[j] & 0xffffu;
-      const uint32_t pos = lstart[d] + rank[j];
+      const uint32_t pos = lstart[d] + rank[j] - r0;  // (earlier rounds' records wrap to >= CAP)
+      if (CAP < W * NT && pos >= (uint32_t)CAP) continue;
       if (C32) {
         stage32[pos] = (uint32_t)rk[j][0];
         if (SF == SF_C40) sext[pos] = (uint8_t)(rk[j][0] >> 32);
@@ -744,6 +751,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   // A bin that overflows its capped segment flags the pass (the host redoes it with exact sizes) and writes
   // nothing: its run offset becomes ~0, so the copy-out below tests one loaded word per record instead of
   // recomputing the segment end (a 64-bit multiply per record)
+  if (r0 == 0) {
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint32_t b = threadIdx.x + i * NT;
@@ -753,34 +761,36 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       goff[b] = over ? ~0ull : off[i];
     }
   }
+  }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < W; j++) {
-    const uint32_t pos = threadIdx.x + j * NT;
+  for (int j = 0; j < CAP / NT; j++) {
+    const uint32_t sp = threadIdx.x + j * NT, pos = sp + r0;  // stage slot, position in the workgroup's run
     if (pos < total) {
-      const uint32_t d = sbin[pos];
+      const uint32_t d = sbin[sp];
       const unsigned long long go = goff[d];
       if (go == ~0ull) continue;
       const unsigned long long dst = go + (pos - lstart[d]);
       uint64_t v[NL];
       if (C32) {
-        v[0] = (uint64_t)stage32[pos] | (SF == SF_C40 ? (uint64_t)sext[pos] << 32 : 0ull);
+        v[0] = (uint64_t)stage32[sp] | (SF == SF_C40 ? (uint64_t)sext[sp] << 32 : 0ull);
       } else if (SF == SF_AOS2 && kAosStage) {
-        const ulonglong2 q = ((const ulonglong2 *)stage)[pos];
+        const ulonglong2 q = ((const ulonglong2 *)stage)[sp];
         v[0] = q.x;
         v[NL - 1] = q.y;
       } else {
 #pragma unroll
-        for (int w = 0; w < NL; w++) v[w] = stage[w * T + pos];
+        for (int w = 0; w < NL; w++) v[w] = stage[w * T + sp];
       }
-      store_out<NL, PACKED, SF>(out, dst, v, PACKED ? 0u : sext[pos]);
+      store_out<NL, PACKED, SF>(out, dst, v, PACKED ? 0u : sext[sp]);
     }
   }
+  }  // rounds
 }
 
 // scatter_staged for compact 40-bit records held as lo / hi words (walk_c32_lh): the window's rank in its bin
 // goes into hi's free bits 19..30 instead of a register of its own (bins <= 2048, T <= 4096).
-template <int W, int NT>
+template <int W, int NT, bool HB = true>  // HB: the record's top byte goes to the ext plane (false: u32 records)
 __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (&hi)[W], uint32_t nb,
                                                    unsigned char *smem, unsigned char *area,
                                                    unsigned long long *cursor, const PlaneSet &out,
@@ -820,7 +830,7 @@ __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (
       const uint32_t d = hi[j] & 0x7ffu;
       const uint32_t pos = lstart[d] + ((hi[j] >> 19) & 0xfffu);
       stage32[pos] = lo[j];
-      sext[pos] = (uint8_t)(hi[j] >> 11);
+      if (HB) sext[pos] = (uint8_t)(hi[j] >> 11);
       sbin[pos] = (uint16_t)d;
     }
   }
@@ -843,7 +853,7 @@ __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (
       if (go == ~0ull) continue;
       const unsigned long long dst = go + (pos - lstart[d]);
       ((uint32_t *)out.w[0])[dst] = stage32[pos];
-      out.ext[dst] = sext[pos];
+      if (HB) out.ext[dst] = sext[pos];
     }
   }
 }
@@ -1026,11 +1036,38 @@ __device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t t
 // ------------------------------------------------------------------------------------------------
 // extract: scatter into coarse buckets
 
+// ... and of the fine partition (k_part_scatter, compact records)
+#ifndef MHMKC_P32REG
+#define MHMKC_P32REG 1
+#endif
+constexpr bool kP32Reg = MHMKC_P32REG != 0;
 // Compact records of the extraction as two u32 registers per window (walk_c32_lh + scatter_staged_c40)
 #ifndef MHMKC_C40REG
 #define MHMKC_C40REG 1
 #endif
 constexpr bool kC40Reg = MHMKC_C40REG != 0;
+// Records the extraction stages at once (scatter_staged CAP; more go out in further rounds): fewer than the tile's
+// windows for keys of two or more words, whose tiles count 57-77 % (k = 63..33), 48 % (k = 77) and 33 % (k = 99) of
+// their windows on 150-base reads. The LDS saved buys workgroups per CU: two-word 2 -> 3 (extraction k = 63 7.67 ->
+// 6.48 ms, k = 33 7.80 -> 7.14; 3072 keeps two: 7.86, 9.13), three-word 3 -> 5 (k = 77 11.54 -> 9.65 ms); four-word
+// keys are held at two by their VGPRs (13.32 -> 13.29 ms) unless the compiler is asked for six waves (EWAVES4: 80
+// VGPRs, three workgroups of 512 threads, 12.97 ms; the same for three-word keys spills: 13.42 ms)
+#ifndef MHMKC_ECAP2
+#define MHMKC_ECAP2 2560
+#endif
+#ifndef MHMKC_ECAP3
+#define MHMKC_ECAP3 1024
+#endif
+#ifndef MHMKC_ECAP4
+#define MHMKC_ECAP4 1024
+#endif
+template <int NL>
+__host__ __device__ constexpr int kECap() {
+  return NL == 2 ? (MHMKC_ECAP2 < kTile<2>() ? MHMKC_ECAP2 : kTile<2>())
+         : NL == 3 ? (MHMKC_ECAP3 < kTile<3>() ? MHMKC_ECAP3 : kTile<3>())
+         : NL == 4 ? (MHMKC_ECAP4 < kTile<4>() ? MHMKC_ECAP4 : kTile<4>())
+                   : kTile<NL>();
+}
 // Minimum waves per SIMD asked of the compiler for the extraction (caps its VGPRs; 1: no cap)
 #ifndef MHMKC_EWAVES1
 #define MHMKC_EWAVES1 1
@@ -1038,9 +1075,15 @@ constexpr bool kC40Reg = MHMKC_C40REG != 0;
 #ifndef MHMKC_EWAVES2
 #define MHMKC_EWAVES2 1
 #endif
+#ifndef MHMKC_EWAVES3
+#define MHMKC_EWAVES3 1
+#endif
+#ifndef MHMKC_EWAVES4
+#define MHMKC_EWAVES4 6
+#endif
 template <int NL>
 constexpr int kEWaves() {
-  return NL == 1 ? MHMKC_EWAVES1 : NL == 2 ? MHMKC_EWAVES2 : 1;
+  return NL == 1 ? MHMKC_EWAVES1 : NL == 2 ? MHMKC_EWAVES2 : NL == 3 ? MHMKC_EWAVES3 : MHMKC_EWAVES4;
 }
 
 template <int NL, bool PACKED, bool CMP>
@@ -1147,8 +1190,8 @@ __global__ __launch_bounds__(kEThreads<NL>()) __attribute__((amdgpu_waves_per_eu
   const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
   constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
   if (kEStagedNL<NL>())
-    scatter_staged<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1, p.out, lim,
-                                      p.ovf);
+    scatter_staged<NL, PACKED, W, SF, ET, kECap<NL>()>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1,
+                                                       p.out, lim, p.ovf);
   else
     scatter_regs<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
 #ifdef MHMKC_ESTAMP
@@ -1670,6 +1713,36 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParam
   if (!xcd_chunk(p, c)) return;  // no chunk left in this workgroup's XCD class (uniform: before any barrier)
   const SChunk ch = chunk_of<T>(p, c);
   const PlaneSet src = p.srcs[ch.src];
+  if constexpr (RecKind<NL, CMP>::C32 && kPStaged && kP32Reg) {
+    // Compact records as lo / hi registers (the extraction's scatter_staged_c40 with u32 records), loaded from the
+    // chunk's planes through 32-bit offsets from its (uniform) start: 32 VGPRs of records instead of 64, and no
+    // 64-bit address per load
+    const uint32_t *b32 = (const uint32_t *)src.w[0] + ch.start;
+    const uint8_t *b8 = src.ext + ch.start;
+    uint32_t lo[W], hi[W];
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+      const uint32_t i = min((uint32_t)(threadIdx.x + j * NT), ch.count - 1u);
+      lo[j] = gload(b32 + i);
+      hi[j] = gload(b8 + i);
+    }
+    const uint64_t cmask = (1ull << (EXT_BITS + 2 * p.k - p.coarse_bits - p.fine_bits)) - 1;
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+      uint64_t r[1] = {(uint64_t)lo[j] | ((uint64_t)hi[j] << 32)};
+      hi[j] = (threadIdx.x + j * NT < ch.count) ? (1u << 31) | fine_digit<NL, PACKED, CMP>(r, p) : 0u;
+      lo[j] = (uint32_t)(r[0] & cmask);
+    }
+    BinLimit lim{0, 0, 0};
+    if (p.coarse_fcap) {
+      const uint64_t fc = p.coarse_fcap[ch.coarse_local];
+      lim = BinLimit{p.coarse_base[ch.coarse_local], fc, fc};
+    }
+    __syncthreads();
+    scatter_staged_c40<W, NT, false>(lo, hi, nf, smem, smem + staged_cnt_bytes(nf),
+                                     p.fine_cursor + (uint64_t)ch.coarse_local * nf, p.out, lim, p.err);
+    return;
+  }
   uint64_t rk[W][NL];
   uint32_t re[W], inf[W];
   load_chunk<NL, PACKED, CMP, W>(src, ch, rk, re);
@@ -3331,7 +3404,7 @@ template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
   constexpr int T = kTile<NL>();
   const size_t tile_b = tile_lds_bytes<NL>() + (RecKind<NL, CMP>::M2 && kM2Walk ? m2walk_lds_bytes() : 0);
-  const size_t lds = kEStagedNL<NL>() ? staged_cnt_bytes(p.n_bins) + std::max(tile_b, staged_area_bytes(NL, T, PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
+  const size_t lds = kEStagedNL<NL>() ? staged_cnt_bytes(p.n_bins) + std::max(tile_b, staged_area_bytes(NL, kECap<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
                               : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
