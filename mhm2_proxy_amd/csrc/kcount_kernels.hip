@@ -1050,8 +1050,10 @@ constexpr bool kC40Reg = MHMKC_C40REG != 0;
 // windows for keys of two or more words, whose tiles count 57-77 % (k = 63..33), 48 % (k = 77) and 33 % (k = 99) of
 // their windows on 150-base reads. The LDS saved buys workgroups per CU: two-word 2 -> 3 (extraction k = 63 7.67 ->
 // 6.48 ms, k = 33 7.80 -> 7.14; 3072 keeps two: 7.86, 9.13), three-word 3 -> 5 (k = 77 11.54 -> 9.65 ms); four-word
-// keys are held at two by their VGPRs (13.32 -> 13.29 ms) unless the compiler is asked for six waves (EWAVES4: 80
-// VGPRs, three workgroups of 512 threads, 12.97 ms; the same for three-word keys spills: 13.42 ms)
+// keys at 512 threads were held at two by their VGPRs (13.32 -> 13.29 ms; asked for six waves, 80 VGPRs: 12.97 ms);
+// at 256 threads and four waves (EWAVES4: 128 VGPRs) four workgroups fit: 10.04 ms, 9.63 with 768 records staged
+// (five waves, 96 VGPRs, spill: 15.8 ms; six waves for three-word keys spill: 13.42 ms; 1792 records for two-word keys
+// at four waves spill: 12.5 ms)
 #ifndef MHMKC_ECAP2
 #define MHMKC_ECAP2 2560
 #endif
@@ -1059,7 +1061,7 @@ constexpr bool kC40Reg = MHMKC_C40REG != 0;
 #define MHMKC_ECAP3 1024
 #endif
 #ifndef MHMKC_ECAP4
-#define MHMKC_ECAP4 1024
+#define MHMKC_ECAP4 768
 #endif
 template <int NL>
 __host__ __device__ constexpr int kECap() {
@@ -1079,7 +1081,7 @@ __host__ __device__ constexpr int kECap() {
 #define MHMKC_EWAVES3 1
 #endif
 #ifndef MHMKC_EWAVES4
-#define MHMKC_EWAVES4 6
+#define MHMKC_EWAVES4 4
 #endif
 template <int NL>
 constexpr int kEWaves() {

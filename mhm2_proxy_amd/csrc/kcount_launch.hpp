@@ -278,7 +278,8 @@ inline int tile_bases(int nl) {
 #define MHMKC_ETHREADS3 MHMKC_ETHREADS2  // three-word keys
 #endif
 #ifndef MHMKC_ETHREADS4
-#define MHMKC_ETHREADS4 512  // four-word keys: 2048-base tiles over 512 threads (k = 99 extract 13.23 -> 12.83 ms)
+#define MHMKC_ETHREADS4 256  // four-word keys: 2048-base tiles, 8 windows per thread (512 threads: 13.23 -> 12.83 ms before the
+                             // capped stage area; with it 256 threads at 128 VGPRs fit four workgroups: 12.97 -> 10.04 ms)
 #endif
 // records per partition chunk (one E_THREADS workgroup)
 #ifndef MHMKC_PTILE1
