@@ -17,10 +17,11 @@ Workloads (--config):
   C4: configs[3] — C3 at k = 63.
 value = counted k-mer occurrences of all ranks / max-over-ranks time.
 
-Extra JSON fields: roofline (dominant kernel: the LDS time floor of its op mix against its HIP-event time,
-with its HBM figures beside it), cpu_baseline (the multi-threaded CPU restatement on a bounded sample,
-rank 0 at N = 1), stages (per-stage device ms per step), h2d_inclusive (the same step from reads in pinned
-host memory: chunked H2D overlapped with extraction), d2h_fetch (copying the finished table to the host).
+Extra JSON fields: roofline (dominant kernel: algorithmic HBM bytes per launch over its HIP-event time against
+8 TB/s; k_count also carries its LDS-floor model), cpu_baseline (the multi-threaded CPU restatement on a bounded
+sample, rank 0 at N = 1), stages (per-stage device ms per step), h2d_inclusive (BASELINE.md's window: the same step
+from reads in pinned host memory, timed from the first H2D, median of 5 after 3 warm-ups), d2h_fetch (copying the
+finished table to the host), kmermap (the streamed hand-off into the C++ adapter's KmerMap).
 """
 from __future__ import annotations
 
@@ -60,7 +61,8 @@ def parse():
     ap.add_argument("--cpu-sample-reads", type=int, default=10_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16, help="CPU baseline threads (the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--h2d-steps", type=int, default=3, help="steps of the H2D-inclusive leg (0: skip)")
+    ap.add_argument("--h2d-steps", type=int, default=5,
+                    help="timed steps of the H2D-inclusive leg, after 3 warm-ups (BASELINE.md: median of 5; 0: skip)")
     ap.add_argument("--input", choices=("packed", "fastq", "fastq-pairs", "fastq-file"), default="packed",
                     help="packed: PackedRead bytes in HBM (the headline); fastq: FASTQ text in HBM, parsed and "
                          "packed on the device inside every step (mhmkc_add_fastq_device); fastq-pairs: interleaved "
@@ -69,8 +71,8 @@ def parse():
                          "in blocks into pinned memory, each block parsed and counted while the next is read "
                          "(mhmkc_add_fastq_file): the step includes the file read and the H2D")
     ap.add_argument("--no-profile-events", action="store_true")
-    ap.add_argument("--kmermap-sample-rows", type=int, default=-1,
-                    help="rows of the fetched table put into the C++ adapter's KmerMap to time it (-1: all, 0: skip)")
+    ap.add_argument("--no-kmermap", dest="kmermap", action="store_false",
+                    help="skip timing the hand-off into the C++ adapter's KmerMap")
     ap.add_argument("--transport", choices=("rccl", "host", "rccl-same-gpu"), default="rccl",
                     help="exchange between ranks (N > 1): rccl = one rank per GPU, RCCL grouped send/recv over xGMI; "
                          "host = mhmkc_set_transport over a gloo process group (pinned D2H, gloo, H2D), ranks share "
@@ -119,43 +121,36 @@ def lds_floor_seconds(st: dict, k: int) -> tuple:
     return t, b
 
 
-def kmermap_fill_ms(table, k: int, sample_rows: int, ordered: bool):
-    """KmerMap materialisation on the host: the first sample_rows rows of the fetched table go
-    into the C++ adapter's KmerMap<MAX_K> (include/mhmkc_kcount.hpp: open addressing with one-byte tags, the
-    reference's bytell_hash_map family, src/utils.hpp:57-64) through KmerDHT::load_table's fill loop
-    (tools/bin/kmermap_fill, built by build(); one thread, as insert_into_local_hashtable runs per rank), timed in
-    that process; ordered: the rows came from mhmkc_fetch_ordered (the map's slot order). The whole table by
-    default; a sample is extrapolated linearly (a lower bound: a larger map misses the caches more)."""
-    tool = ROOT / "tools" / "bin" / "kmermap_fill"
-    n = min(len(table), sample_rows) if sample_rows >= 0 else len(table)
-    if not sample_rows or not n or not tool.exists():
+def handoff_ms(counter, k: int, threads: int, runs: int = 3):
+    """The hand-off into the C++ adapter's KmerMap, timed in this process on the finished device table (SURVEY.md
+    §8(d)): tools/bin/libmhmkc_handoff.so runs include/mhmkc_kcount.hpp's load_ordered on the counter's handle, which
+    is what HashTableInserter::insert_into_local_hashtable does after mhmkc_finish (the device sort into the map's slot
+    order, chunked D2H on a helper thread, the parallel fill of a fresh map; src/kcount/kcount_cpu.cpp:503-522). The
+    first run includes the device sort; later runs reuse the sorted rows (the sort is ~1.5 ms at C2). Every run fills a
+    fresh map (its page faults included), and a sample of the rows is looked up afterwards (untimed)."""
+    import ctypes as C
+
+    lib_path = ROOT / "tools" / "bin" / "libmhmkc_handoff.so"
+    if not lib_path.exists():
         return None
-    import subprocess
-    import tempfile
-
-    import numpy as np
-
-    d = tempfile.mkdtemp(prefix="mhmkc_fill_", dir="/dev/shm" if Path("/dev/shm").is_dir() else None)
-    try:
-        pre = str(Path(d) / "t")
-        np.ascontiguousarray(table.keys[:n]).tofile(pre + ".keys")
-        np.ascontiguousarray(table.counts[:n]).tofile(pre + ".counts")
-        np.ascontiguousarray(table.left[:n]).view(np.uint8).tofile(pre + ".left")
-        np.ascontiguousarray(table.right[:n]).view(np.uint8).tofile(pre + ".right")
-        r = subprocess.run([str(tool), str(k), str(n), pre], capture_output=True, text=True, timeout=600)
-        if r.returncode != 0:
-            return {"error": (r.stdout + r.stderr).strip()[-300:]}
-        j = json.loads(r.stdout.strip().splitlines()[-1])
-    finally:
-        import shutil
-
-        shutil.rmtree(d, ignore_errors=True)
-    return {"sample_rows": n, "sample_ms": j["ms"], "rows": len(table),
-            "ms_extrapolated": round(j["ms"] * len(table) / n, 1),
-            "ms_per_row_emplace_loop": round(j["ms_emplace_loop"] / n * 1e6, 2),
-            "order": "mhmkc_fetch_ordered (KmerMap slot order)" if ordered else "mhmkc_fetch (unordered)",
-            "kind": "C++ adapter KmerMap<MAX_K> (open addressing, 1-byte tags, huge pages), KmerDHT::load_table's "
-                    "prefetched fill, 1 thread, tools/cpp/kmermap_fill.cpp"}
+    lib = C.CDLL(str(lib_path))
+    lib.mhmkc_handoff_ms.restype = C.c_double
+    lib.mhmkc_handoff_ms.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+    ms, size, bad, parts = [], C.c_uint64(0), C.c_uint64(0), []
+    for _ in range(runs):
+        pa = (C.c_double * 3)()
+        t = lib.mhmkc_handoff_ms(counter._h, k, threads, 0, C.byref(size), C.byref(bad), pa)
+        if t < 0:
+            return {"error": "library error in the hand-off"}
+        ms.append(t)
+        parts.append({n_: round(v, 1) for n_, v in zip(("first_fetch_incl_sort", "fill", "wait_fetch"), pa)})
+    return {"ms": round(sorted(ms)[len(ms) // 2], 1), "statistic": f"median of {runs} runs", "runs_ms": [round(x, 1) for x in ms],
+            "rows": counter.n_out,
+            "map_size": int(size.value), "sample_rows_bad": int(bad.value), "threads": threads, "parts_ms": parts,
+            "kind": "C++ adapter load_ordered (HashTableInserter::insert_into_local_hashtable): device sort by KmerMap "
+                    "slot, 4M-row chunks D2H on a helper thread overlapped with the parallel fill of a fresh "
+                    "KmerMap<MAX_K> (tools/cpp/handoff.cpp)"}
 
 
 def survey_model_bytes(st: dict, k: int, n_reads: int, read_len: int) -> float:
@@ -407,9 +402,12 @@ def main():
     launches = {}
     occ_total = 0
     st = None
+    step_s = []
     for _ in range(args.steps):
+        t_s = time.perf_counter()
         step()
         st = counter.stats()
+        step_s.append(time.perf_counter() - t_s)
         occ_total += st["occurrences"]
         for s_, v in st["ms_kernel"].items():
             stage_ms[s_] = stage_ms.get(s_, 0.0) + v
@@ -440,29 +438,25 @@ def main():
     # measured for this workload only (the config's own sizes)
     pmc = {} if (args.reads_per_gpu or args.reads_total) else pmc.get("configs", {}).get(f"{args.config}/k{k}", {})
     def roofline_of(stage):
-        """The roofline object of one stage's kernel: k_count against its LDS floor (its HBM figures beside it), the
-        streaming kernels against HBM."""
+        """The roofline object of one stage's kernel: algorithmic HBM bytes per launch over the launch's HIP-event
+        time, against the 8 TB/s HBM peak (k_count also carries its LDS-floor model)."""
         ms_launch = stage_ms[stage] / launches[stage]
         alg = algorithmic_bytes(stage, st, k) / max(1, launches[stage] // steps)
         hbm = {"achieved": round(alg / (ms_launch * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                "frac": round(alg / (ms_launch * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "algorithmic_bytes": int(alg)}
         traffic = pmc.get("per_launch_bytes", {}).get(stage)
+        extra = {}
         if stage == "count":
-            # k_count keeps its hash table in LDS and is bound there (DESIGN.md §4): the roofline is its LDS
-            # time floor at the measured random-access LDS rates; achieved / peak are the LDS bytes of its
-            # table operations over the measured time / over that floor
+            # k_count keeps its hash table in LDS (DESIGN.md §4): beside its HBM roofline, the LDS time floor of its
+            # table operations at the measured random-access LDS rates (a model, not a hardware peak)
             t_floor, lds_b = lds_floor_seconds(st, k)
-            return {"bound": "lds", "kernel": "k_count", "achieved": round(lds_b / (ms_launch * 1e-3) / 1e12, 3),
-                    "peak": round(lds_b / t_floor / 1e12, 3), "unit": "TB/s",
-                    "frac": round(t_floor / (ms_launch * 1e-3), 4), "traffic": traffic,
-                    "traffic_source": pmc.get("source"), "avg_launch_ms": round(ms_launch, 4),
-                    "lds_floor_ms": round(t_floor * 1e3, 4),
-                    "lds_ops": {"records": st["owned_records"], "phase_b_records": st["lds_misses"],
-                                "ext_adds": st["lds_ext_adds"]},
-                    "hbm": hbm}
+            extra = {"lds_model": {"floor_ms": round(t_floor * 1e3, 4), "frac": round(t_floor / (ms_launch * 1e-3), 4),
+                                   "lds_TBps": round(lds_b / (ms_launch * 1e-3) / 1e12, 3),
+                                   "ops": {"records": st["owned_records"], "phase_b_records": st["lds_misses"],
+                                           "ext_adds": st["lds_ext_adds"]}}}
         return {"bound": "hbm", "kernel": "k_" + stage, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": hbm["frac"], "traffic": traffic, "traffic_source": pmc.get("source"),
-                "algorithmic_bytes": int(alg), "avg_launch_ms": round(ms_launch, 4)}
+                "algorithmic_bytes": int(alg), "avg_launch_ms": round(ms_launch, 4), **extra}
 
     if dom and launches.get(dom):
         roofline = roofline_of(dom)
@@ -481,6 +475,8 @@ def main():
             ts.append((time.perf_counter() - t1) * 1e3)
         return sorted(ts)[1]
 
+    # the hand-off into the adapter's KmerMap first: its first run includes the device sort into slot order
+    kmermap = handoff_ms(counter, k, threads) if rank == 0 and args.kmermap else None
     n_rows = counter.n_out
     row_b = 8 * counter.n_longs + 4
     table = m.KmerTable(k, np.ones((n_rows, counter.n_longs), np.uint64), np.ones(n_rows, np.uint16),
@@ -502,9 +498,6 @@ def main():
         del ptab, pin
     except RuntimeError:
         pass
-    # the same table in the KmerMap's slot order (device sort), then the adapter's fill
-    counter.fetch(ordered=True, out=table)
-    kmermap = kmermap_fill_ms(table, k, args.kmermap_sample_rows, True) if rank == 0 else None
     del table
 
     # the same step from reads in pinned host memory: chunked H2D on a copy stream, each chunk extracted as
@@ -515,7 +508,7 @@ def main():
         ho = torch.from_numpy(o.view(np.int64)).pin_memory().numpy().view(np.uint64)
         counter.set_profiling(False)
         ts, h2d_ms = [], []
-        for i in range(args.h2d_steps + 1):
+        for i in range(args.h2d_steps + 3):
             if dist:
                 dist.barrier()
             torch.cuda.synchronize()
@@ -529,7 +522,7 @@ def main():
                 tt_ = torch.tensor([dt], dtype=torch.float64, device=cdev)
                 dist.all_reduce(tt_, op=dist.ReduceOp.MAX)
                 dt = float(tt_.item())
-            if i:  # the first is a warm-up (pinned staging, chunk events)
+            if i >= 3:  # three warm-ups (pinned staging, chunk events), BASELINE.md:74
                 ts.append(dt)
                 h2d_ms.append(counter.stats()["ms_h2d"])
         tmed = sorted(ts)[len(ts) // 2]
@@ -538,8 +531,9 @@ def main():
         h2d = {"value": round(occ_total / steps * 1.0 / tmed, 1), "unit": "k-mers/s", "ms_per_step": round(tmed * 1e3, 3),
                "h2d_ms": round(sorted(h2d_ms)[len(h2d_ms) // 2], 3), "h2d_bytes_per_gpu": int(hbytes),
                "h2d_GBps": round(hbytes / (sorted(h2d_ms)[len(h2d_ms) // 2] * 1e-3) / 1e9, 1) if h2d_ms[0] else None,
-               "chunks": int(stt["h2d_chunks"]), "steps": len(ts),
-               "input": "PackedRead bytes + offsets in pinned host memory (torch pin_memory)"}
+               "chunks": int(stt["h2d_chunks"]), "steps": len(ts), "warmup": 3, "statistic": "median",
+               "input": "PackedRead bytes + offsets in pinned host memory (torch pin_memory)",
+               "window": "BASELINE.md:74-75: from the first H2D of the reads to the finished device table"}
         del hb, ho
 
     cpu = None
@@ -556,6 +550,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 3),
+            "ms_per_step_median": round(sorted(step_s)[len(step_s) // 2] * 1e3, 3) if step_s else None,
             "higher_is_better": True,
             "scaling": "weak" if args.config == "C2" else "strong",
             "vs_baseline": None,
@@ -588,8 +583,7 @@ def main():
             "h2d_inclusive": h2d,
             "d2h_fetch": d2h,
             "kmermap": kmermap,
-            "d2h_kmermap_ms": round(d2h["ordered_ms"] + kmermap["ms_extrapolated"], 1)
-            if kmermap and "ms_extrapolated" in kmermap else None,
+            "d2h_kmermap_ms": kmermap["ms"] if kmermap and "ms" in kmermap else None,
             "distinct_per_gpu": st["distinct"] if st else None,
             "n_out_per_gpu": st["n_out"] if st else None,
             "bytes_sent_rank0": st["bytes_sent"] if st else None,

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 11
+#define MHMKC_ABI_VERSION 12
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -278,6 +278,12 @@ static inline uint64_t mhmkc_map_hash(const uint64_t *w, int n_longs) {
  * KmerMap in that order walks its slot array once from front to back instead of touching a random slot per row
  * (insert_into_local_hashtable's loop, src/kcount/kcount_cpu.cpp:503-522). At most 2^32-1 rows. */
 int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right);
+
+/* Rows [row0, row0 + n_rows) of mhmkc_fetch_ordered's order (the device sorts once per finish and keeps the ordered
+ * rows until the next reset): a host that fills its KmerMap chunk by chunk while the next chunk is on the wire (the C++
+ * adapter's insert_into_local_hashtable) never holds the whole table twice. */
+int mhmkc_fetch_ordered_range(mhmkc_t h, uint64_t row0, uint64_t n_rows, uint64_t *keys, uint16_t *counts, char *left,
+                              char *right);
 
 /* Device pointers of the finished table (valid until the next reset/destroy). */
 int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,

@@ -20,15 +20,21 @@
 #include <sys/stat.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <array>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
-#include <algorithm>
+#include <thread>
 #include <type_traits>
 #include <unordered_map>
 #include <utility>
@@ -185,6 +191,63 @@ struct KmerCounts {
 // prefetched, so that filling a table larger than the caches is not one DRAM round trip per row
 // (insert_into_local_hashtable's loop, src/kcount/kcount_cpu.cpp:503-522; a node-allocating std::unordered_map
 // took 136 ns per row at C2).
+// Worker threads of a KmerMap bulk fill (fill_begin .. fill_end): started once, then each chunk's job is handed to them
+// (a chunk is one D2H's worth of rows: spawning threads per chunk cost more than placing the chunk's rows).
+class FillPool {
+ public:
+  explicit FillPool(int n) : n_(n) {
+    for (int t = 1; t < n; t++) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~FillPool() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &x : th_) x.join();
+  }
+  FillPool(const FillPool &) = delete;
+  FillPool &operator=(const FillPool &) = delete;
+  int size() const { return n_; }
+  // f(t) for every t in [0, size()), the caller as thread 0; returns when all are done
+  void run(const std::function<void(int)> &f) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      job_ = &f;
+      left_.store(n_ - 1);
+      gen_++;
+    }
+    cv_.notify_all();
+    f(0);
+    while (left_.load(std::memory_order_acquire)) std::this_thread::yield();
+  }
+
+ private:
+  void loop(int t) {
+    uint64_t seen = 0;
+    while (true) {
+      const std::function<void(int)> *j;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        j = job_;
+      }
+      (*j)(t);
+      left_.fetch_sub(1, std::memory_order_release);
+    }
+  }
+  int n_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  const std::function<void(int)> *job_ = nullptr;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  std::atomic<int> left_{0};
+};
+
 template <int MAX_K>
 class KmerMap {
  public:
@@ -279,12 +342,60 @@ class KmerMap {
   mapped_type &operator[](const key_type &k) { return put(k, mapped_type(), hash_of(k)).first->second; }
 
   // Bulk insert of n finished rows in mhmkc_fetch's layout (keys: N_LONGS words per row). Rows whose key is
-  // already present keep the present entry (as insert does).
-  void fill(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n) {
+  // already present keep the present entry (as insert does). fill = fill_begin + one fill_chunk + fill_end.
+  void fill(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n,
+            int threads = 0) {
+    fill_begin(n, threads);
+    fill_chunk(keys, counts, left, right, n);
+    fill_end();
+  }
+
+  // A bulk insert in chunks, in order (a table streamed from the device chunk by chunk: HashTableInserter's
+  // insert_into_local_hashtable): fill_begin(rows in all chunks), fill_chunk per chunk, fill_end. Into an empty map,
+  // rows in mhmkc_fetch_ordered's order (non-decreasing home slot) are placed by `threads` threads (0: fill_threads())
+  // without probing (chunk_ordered); from the first chunk that is not in that order on, rows go through the one-thread
+  // prefetched loop (chunk_loop).
+  void fill_begin(uint64_t n, int threads = 0) {
     reserve(size_ + n);
-    // three stages per row: A (row i + kAhead2) hashes the key and prefetches its home tags; B (row i + kAhead1) scans the
-    // tags, now cached, for the slot the insert will take (the end of the probe run: at load 3/4 it is several cache
-    // lines past the home slot) and prefetches that slot; C (row i) inserts
+    fs_threads_ = threads > 0 ? threads : fill_threads();
+    fs_ordered_ = size_ == 0 && fs_threads_ > 1 && cap_ <= (1ull << 32);
+    fs_pos_ = -1;
+    fs_prev32_ = 0;
+    fs_any_ = false;
+    fs_wrapped_.clear();
+    fs_pool_.reset();
+    if (fs_threads_ > 1) fs_pool_.reset(new FillPool(fs_threads_));
+    fs_hash_.resize(fs_threads_);
+  }
+  void fill_chunk(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n) {
+    if (!n) return;
+    if (fs_ordered_) {
+      if (chunk_ordered(keys, counts, left, right, n)) return;
+      fs_ordered_ = false;
+      flush_wrapped();  // (the rows of earlier chunks go in first, so that a repeated key keeps its first entry)
+    }
+    chunk_loop(keys, counts, left, right, n);
+  }
+  void fill_end() {
+    flush_wrapped();
+    fs_pool_.reset();
+    fs_hash_.clear();
+    fs_hash_.shrink_to_fit();
+  }
+
+  // Threads of a bulk fill: OMP_NUM_THREADS when set (the rank's CPU share), else the hardware threads, at most 16.
+  static int fill_threads() {
+    if (const char *e = getenv("OMP_NUM_THREADS"))
+      if (atoi(e) > 0) return std::min(64, atoi(e));
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, hw));
+  }
+
+ private:
+  // the one-thread insert loop, three stages per row: A (row i + kAhead2) hashes the key and prefetches its home tags;
+  // B (row i + kAhead1) scans the tags, now cached, for the slot the insert will take (the end of the probe run: at load
+  // 3/4 it is several cache lines past the home slot) and prefetches that slot; C (row i) inserts
+  void chunk_loop(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n) {
     constexpr int kAhead2 = 48, kAhead1 = 16, kRing = 64;
     uint64_t h[kRing];
     const int nl = key_type::N_LONGS;
@@ -312,7 +423,136 @@ class KmerMap {
     }
   }
 
- private:
+  // Parallel placement of rows sorted by home slot (mhmkc_fetch_ordered: the top 32 bits of the hash, which order the
+  // homes for any capacity up to 2^32) into a map that holds only the earlier such rows. Linear probing that inserts in
+  // home order puts row i at
+  //     pos_i = max(home_i, pos_{i-1} + 1)
+  // (the first free slot at or after its home: every slot of [home_i, pos_{i-1}] is taken by earlier rows), so the
+  // positions are a running maximum: over a range of rows with the position c of the row before it,
+  //     pos_last = max(c + n_range, pos_last with no row before it),
+  // and threads over contiguous row ranges need only the ranges' two numbers, combined in order, to place every row
+  // (fs_pos_ carries c from chunk to chunk). Each thread then writes a disjoint slot range (the positions increase).
+  // Rows placed past the last slot wrap to the front, where linear probing continues: those few go through put() at
+  // fill_end. A row whose key equals an earlier row's (the same top-32 hash bits, so within a few rows) keeps the
+  // earlier entry, as insert does. Returns false, with nothing written, when the rows are not in home order.
+  bool chunk_ordered(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right, uint64_t n) {
+    const int nl = key_type::N_LONGS;
+    const int T = (int)std::min<uint64_t>((uint64_t)(fs_pool_ ? fs_pool_->size() : 1), n / 4096 + 1);
+    struct Part {
+      int64_t last = -1;  // pos of the range's last row with nothing before it (-1: no row)
+      uint64_t rows = 0;  // rows that take a slot (not repeats)
+      bool sorted = true;
+      std::vector<uint64_t> wrapped;  // rows placed past the last slot
+    };
+    std::vector<Part> part(T);
+    auto lo_of = [&](int t) { return n * (uint64_t)t / (uint64_t)T; };
+    auto hash32 = [&](uint64_t i) { return hash_words(keys + i * nl) >> 32; };
+    auto same = [&](uint64_t i, uint64_t j) { return std::memcmp(keys + j * nl, keys + i * nl, 8 * (size_t)nl) == 0; };
+    // the chunk's leading rows with the previous chunk's last top bits may repeat a row already in the map: decided
+    // here, before any thread writes
+    std::vector<uint8_t> lead;
+    if (fs_any_)
+      for (uint64_t i = 0; i < n; i++) {
+        const uint64_t hw = hash_words(keys + i * nl);
+        if ((hw >> 32) != fs_prev32_) break;
+        bool d = tag_[locate(key_type(keys + i * nl), hw)] != 0;
+        for (uint64_t j = 0; j < i && !d; j++) d = same(i, j);
+        lead.push_back(d);
+      }
+    // row i repeats an earlier row of the chunk (equal keys have equal hashes: one run of equal top bits)
+    auto repeat = [&](uint64_t i, uint64_t h32) {
+      if (i < lead.size()) return lead[i] != 0;
+      for (uint64_t j = i; j-- > 0;) {
+        if (hash32(j) != h32) return false;
+        if (same(i, j)) return true;
+      }
+      return false;
+    };
+    // (pass 1 keeps each row's hash for pass 2 in its thread's buffer)
+    auto run = [&](int t, bool place, int64_t carry) {
+      Part &p = part[t];
+      const uint64_t a = lo_of(t), b = lo_of(t + 1);
+      std::vector<uint64_t> &hb = fs_hash_[t];
+      if (!place && hb.size() < b - a) hb.resize(b - a);
+      uint64_t prev = a ? hash32(a - 1) : fs_prev32_;
+      int64_t pos = place ? carry : -1;
+      for (uint64_t i = a; i < b; i++) {
+        const uint64_t hw = place ? hb[i - a] : (hb[i - a] = hash_words(keys + i * nl)), h32 = hw >> 32;
+        if (h32 < prev) {
+          p.sorted = false;
+          return;
+        }
+        const bool maybe = i < lead.size() || (i > 0 && h32 == prev);
+        prev = h32;
+        if (maybe && repeat(i, h32)) continue;
+        pos = std::max<int64_t>((int64_t)home(hw), pos + 1);
+        if (!place) {
+          p.rows++;
+          continue;
+        }
+        if ((uint64_t)pos >= cap_) {
+          p.wrapped.push_back(i);
+          continue;
+        }
+        tag_[pos] = tag_of(hw);
+        slot_[pos].first = key_type(keys + i * nl);
+        KmerCounts &kc = slot_[pos].second;
+        kc = KmerCounts();
+        kc.count = counts[i];
+        kc.left = left[i];
+        kc.right = right[i];
+      }
+      if (!place) p.last = pos;
+    };
+    // one thread per range for both passes: the ranges' numbers are combined by thread 0 between them
+    std::vector<int64_t> carry(T + 1, fs_pos_);
+    std::atomic<int> arrived{0};
+    std::atomic<int> go{0};  // 1: carries ready, 2: not in order (no second pass)
+    const std::function<void(int)> worker = [&](int t) {
+      if (t >= T) return;
+      run(t, false, 0);
+      arrived.fetch_add(1);
+      if (t == 0) {
+        while (arrived.load() < T) std::this_thread::yield();
+        bool sorted = true;
+        for (auto &p : part) sorted &= p.sorted;
+        for (int u = 1; u <= T; u++)  // the carry into each range: the position of the last row before it
+          carry[u] = std::max<int64_t>(carry[u - 1] + (int64_t)part[u - 1].rows, part[u - 1].last);
+        go.store(sorted ? 1 : 2);
+      } else {
+        while (!go.load()) std::this_thread::yield();
+      }
+      if (go.load() == 1) run(t, true, carry[t]);
+    };
+    if (fs_pool_) {
+      fs_pool_->run(worker);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 1; t < T; t++) th.emplace_back(worker, t);
+      worker(0);
+      for (auto &x : th) x.join();
+    }
+    if (go.load() != 1) return false;
+    for (auto &p : part) {
+      size_ += p.rows - p.wrapped.size();
+      for (uint64_t i : p.wrapped) {
+        KmerCounts kc;
+        kc.count = counts[i];
+        kc.left = left[i];
+        kc.right = right[i];
+        fs_wrapped_.emplace_back(key_type(keys + i * nl), kc);
+      }
+    }
+    fs_pos_ = carry[T];
+    fs_prev32_ = hash32(n - 1);
+    fs_any_ = true;
+    return true;
+  }
+  void flush_wrapped() {
+    for (auto &kv : fs_wrapped_) put(kv.first, kv.second, hash_of(kv.first));
+    fs_wrapped_.clear();
+  }
+
   // tags and slots of a large map live in 2 MB-aligned anonymous memory advised for transparent huge pages: a table
   // larger than the caches is touched at random, and with 4 KB pages every probe would also miss the TLB. Below 1 MB
   // (a small map: a test, a tiny rank share) plain zeroed heap memory.
@@ -345,6 +585,14 @@ class KmerMap {
   Buf<value_type> slot_;
   size_t cap_ = 0, size_ = 0;
   int shift_ = 64;  // 64 - log2(cap_): the home slot is the top bits of the hash
+  // state of a chunked fill (fill_begin .. fill_end)
+  int fs_threads_ = 1;
+  bool fs_ordered_ = false, fs_any_ = false;
+  int64_t fs_pos_ = -1;     // position of the last row placed in order (-1: none)
+  uint64_t fs_prev32_ = 0;  // the top 32 hash bits of the last row of the previous chunk
+  std::vector<value_type> fs_wrapped_;
+  std::unique_ptr<FillPool> fs_pool_;            // the fill's worker threads
+  std::vector<std::vector<uint64_t>> fs_hash_;  // per fill thread: its rows' hashes (pass 1 -> pass 2)
   // the key words' multiply-xorshift mix (mhmkc_map_hash: the device orders mhmkc_fetch_ordered's rows by its top
   // bits, the home slot here, so that a fill in that order streams through the slot array)
   static uint64_t hash_words(const uint64_t *w) { return mhmkc_map_hash(w, key_type::N_LONGS); }
@@ -466,6 +714,67 @@ struct RankInfo {
   bool table_only = false;  // no counter: the KmerDHT only holds a table given to load_table (no GPU used)
 };
 
+// The finished table of a handle into `map`, streamed in the KmerMap's slot order (mhmkc_fetch_ordered_range):
+// while chunk c is placed by KmerMap::fill_chunk, a helper thread copies chunk c + 1 from the device, so the D2H hides
+// behind the fill and the host never holds the whole table outside the map. Replaces insert_into_local_hashtable's
+// loop over the local table (src/kcount/kcount_cpu.cpp:503-522).
+// where load_ordered's time went (milliseconds; optional)
+struct LoadTimes {
+  double first_fetch = 0, fill = 0, wait_fetch = 0;
+};
+
+template <int MAX_K>
+void load_ordered(mhmkc_t h, KmerMap<MAX_K> &map, uint64_t n, int threads = 0, uint64_t chunk_rows = 4u << 20,
+                  LoadTimes *times = nullptr) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  LoadTimes lt;
+  const int nl = Kmer<MAX_K>::N_LONGS;
+  const uint64_t m = std::min<uint64_t>(std::max<uint64_t>(chunk_rows, 1), std::max<uint64_t>(n, 1));
+  struct Chunk {  // (not zero-filled: the fetch writes every row it is read for)
+    std::unique_ptr<uint64_t[]> keys;
+    std::unique_ptr<uint16_t[]> counts;
+    std::unique_ptr<char[]> left, right;
+  } buf[2];
+  for (auto &b : buf) {
+    b.keys.reset(new uint64_t[m * nl]);
+    b.counts.reset(new uint16_t[m]);
+    b.left.reset(new char[m]);
+    b.right.reset(new char[m]);
+  }
+  auto fetch = [&](uint64_t c) {
+    Chunk &b = buf[c & 1];
+    const uint64_t r0 = c * m;
+    return mhmkc_fetch_ordered_range(h, r0, std::min(m, n - r0), b.keys.get(), b.counts.get(), b.left.get(),
+                                     b.right.get());
+  };
+  map.fill_begin(n, threads);
+  const uint64_t n_ch = (n + m - 1) / m;
+  // (the map's fresh memory is faulted in by the fill threads as they write it: a separate parallel pass to fault it in
+  // while the first chunk was on the wire measured no faster)
+  auto t0 = clk::now();
+  int rc = n_ch ? fetch(0) : MHMKC_OK;
+  lt.first_fetch = ms_since(t0);
+  for (uint64_t c = 0; c < n_ch; c++) {
+    check(rc, h, "mhmkc_fetch_ordered_range");
+    int rc_next = MHMKC_OK;
+    std::thread f;
+    if (c + 1 < n_ch) f = std::thread([&, c] { rc_next = fetch(c + 1); });
+    const Chunk &b = buf[c & 1];
+    auto t1 = clk::now();
+    map.fill_chunk(b.keys.get(), b.counts.get(), b.left.get(), b.right.get(), std::min(m, n - c * m));
+    lt.fill += ms_since(t1);
+    t1 = clk::now();
+    if (f.joinable()) f.join();
+    lt.wait_fetch += ms_since(t1);
+    rc = rc_next;
+  }
+  auto t2 = clk::now();
+  map.fill_end();
+  lt.fill += ms_since(t2);
+  if (times) *times = lt;
+}
+
 template <int MAX_K>
 class HashTableInserter {
   mhmkc_t h_ = nullptr;
@@ -560,12 +869,8 @@ class HashTableInserter {
     check(mhmkc_set_dmin_thres(h_, _dmin_thres), h_, "mhmkc_set_dmin_thres");
     uint64_t n = 0;
     check(mhmkc_finish(h_, &n), h_, "mhmkc_finish");
-    std::vector<uint64_t> keys(n * Kmer<MAX_K>::N_LONGS);
-    std::vector<uint16_t> counts(n);
-    std::vector<char> left(n), right(n);
-    // rows in the map's slot order (a device sort), so that the fill streams through the slot array
-    check(mhmkc_fetch_ordered(h_, keys.data(), counts.data(), left.data(), right.data()), h_, "mhmkc_fetch_ordered");
-    local_kmers.fill(keys.data(), counts.data(), left.data(), right.data(), n);
+    // rows in the map's slot order (a device sort), chunk by chunk, each placed while the next is copied
+    load_ordered(h_, local_kmers, n);
   }
   mhmkc_stats stats() const {
     mhmkc_stats s;

@@ -3,7 +3,8 @@
   mhm2_proxy_amd/libmhmkc.so        hipcc --offload-arch=gfx950: HIP kernels + C ABI (include/mhmkc.h)
   mhm2_proxy_amd/libmhmkc_synth.so  gcc: deterministic synthetic read generator (include/mhmkc_synth.h)
   oracle/liboracle.so (+ _ref/)     make -C oracle: the CPU checker (test infrastructure only)
-  tools/bin/kmermap_fill            g++: KmerMap materialisation timing of the C++ adapter (bench.py)
+  tools/bin/kmermap_fill            g++: KmerMap fill timing of the C++ adapter from table files (tests, bench.py)
+  tools/bin/libmhmkc_handoff.so     g++: the adapter's streamed hand-off (load_ordered) timed in bench.py's process
 
 Incremental: a target is rebuilt only when one of its sources is newer; libmhmkc.so also when the build id it
 carries (the SHA-256 of its sources, mhmkc_build_id) is not the tree's, whatever the file times say.
@@ -32,6 +33,8 @@ LIB_DEPS = LIB_SOURCES + [CSRC / "kcount_launch.hpp", CSRC / "kmer_ops.hpp", ROO
 SYNTH_DEPS = [CSRC / "synth.c", ROOT / "include" / "mhmkc_synth.h"]
 FILL = ROOT / "tools" / "bin" / "kmermap_fill"
 FILL_DEPS = [ROOT / "tools" / "cpp" / "kmermap_fill.cpp", ROOT / "include" / "mhmkc_kcount.hpp", ROOT / "include" / "mhmkc.h"]
+HANDOFF = ROOT / "tools" / "bin" / "libmhmkc_handoff.so"
+HANDOFF_DEPS = [ROOT / "tools" / "cpp" / "handoff.cpp", ROOT / "include" / "mhmkc_kcount.hpp", ROOT / "include" / "mhmkc.h"]
 
 
 def source_build_id() -> str:
@@ -93,10 +96,12 @@ def _compile_lib(out: Path, bid: str, extra=(), tag: str = "main") -> None:
 
 
 def build_variant(name: str, defines) -> Path:
-    """exp/libmhmkc_<name>.so with extra -D flags (performance A/B runs; MHMKC_LIB selects it)."""
+    """exp/libmhmkc_<name>.so with extra -D flags (performance A/B runs; MHMKC_LIB selects it). Its build id is the
+    tree's with the flags' hash appended, so a variant never passes the check that the loaded library is the tree's."""
     out = ROOT / "exp" / f"libmhmkc_{name}.so"
     out.parent.mkdir(exist_ok=True)
-    _compile_lib(out, source_build_id(), list(defines), tag=name)
+    fh = hashlib.sha256("\0".join([ARCH, *defines]).encode()).hexdigest()[:8]
+    _compile_lib(out, f"{source_build_id()}+{fh}", list(defines), tag=name)
     return out
 
 
@@ -129,10 +134,20 @@ def build_fill(force: bool = False) -> Path:
     if force or _stale(FILL, FILL_DEPS + [LIB]):
         FILL.parent.mkdir(parents=True, exist_ok=True)
         tmp = FILL.with_suffix(".tmp")
-        _run(["g++", "-O2", "-std=c++17", "-I", ROOT / "include", FILL_DEPS[0], "-L", PKG, "-lmhmkc", "-lz",
+        _run(["g++", "-O2", "-std=c++17", "-pthread", "-I", ROOT / "include", FILL_DEPS[0], "-L", PKG, "-lmhmkc", "-lz",
               f"-Wl,-rpath,{PKG}", "-Wl,-rpath,$ORIGIN/../../mhm2_proxy_amd", "-o", tmp])
         tmp.replace(FILL)
     return FILL
+
+
+def build_handoff(force: bool = False) -> Path:
+    if force or _stale(HANDOFF, HANDOFF_DEPS + [LIB]):
+        HANDOFF.parent.mkdir(parents=True, exist_ok=True)
+        tmp = HANDOFF.with_suffix(".tmp")
+        _run(["g++", "-O2", "-std=c++17", "-pthread", "-fPIC", "-shared", "-I", ROOT / "include", HANDOFF_DEPS[0], "-L",
+              PKG, "-lmhmkc", "-lz", "-Wl,-rpath,$ORIGIN/../../mhm2_proxy_amd", "-o", tmp])
+        tmp.replace(HANDOFF)
+    return HANDOFF
 
 
 def build_all(force: bool = False) -> None:
@@ -140,6 +155,7 @@ def build_all(force: bool = False) -> None:
     build_synth(force)
     build_oracle(force)
     build_fill(force)
+    build_handoff(force)
 
 
 if __name__ == "__main__":

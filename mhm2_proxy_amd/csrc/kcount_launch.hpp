@@ -429,6 +429,7 @@ struct OutRows {
 inline int minimizer_len_for(int k) { return k * 2 / 3 + 1 < 15 ? 15 : (k * 2 / 3 + 1 > 27 ? 27 : k * 2 / 3 + 1); }
 // mhmkc_fetch_ordered: the output rows in the order of the top 32 bits of mhmkc_map_hash (kcount_owner.hip)
 size_t map_order_scratch_bytes(uint64_t n, int nlo);
+hipError_t preload_owner_kernels();
 hipError_t launch_map_order(const OutRows &in, uint64_t n, int nlo, void *scratch, size_t scratch_bytes, const OutRows &out,
                             hipStream_t s);
 // minimizer_hash_fast of n keys (nlo words each, the first k/32+1 used)

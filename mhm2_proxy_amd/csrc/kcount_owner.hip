@@ -155,6 +155,13 @@ hipError_t packed_order(const OutRows &in, uint64_t n, void *scratch, size_t scr
 
 }  // namespace
 
+// The code object of this file (the hand-off kernels and their rocPRIM sorts) is loaded at its first kernel use; a
+// handle asks for it at create, so that the first ordered fetch of a process does not pay the load (~40 ms).
+hipError_t preload_owner_kernels() {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void *)k_map_hash);
+}
+
 size_t map_order_scratch_bytes(uint64_t n, int nlo) {
   switch (nlo) {
     case 1: return packed_order_bytes<1>(n);

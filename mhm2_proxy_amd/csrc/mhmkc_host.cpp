@@ -21,6 +21,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <mutex>
 #include <thread>
 
 #include <fcntl.h>
@@ -165,6 +166,17 @@ struct Prof {
   hipEvent_t a, b;
 };
 
+// The pinned staging of pageable D2H copies, shared by the process's handles (one at a time): the reference makes a
+// new KmerDHT, so a new handle, per k round, and a first hipHostMalloc of the staging cost a hand-off ~40 ms.
+struct D2HStage {
+  std::mutex mu;
+  PinBuf buf[2];
+};
+D2HStage &d2h_stage() {
+  static D2HStage *s = new D2HStage();  // (never freed: the process's pinned staging)
+  return *s;
+}
+
 // Bytes of one H2D chunk of mhmkc_add_reads (MHMKC_CHUNK_BYTES overrides: tests force many chunks).
 constexpr uint64_t CHUNK_BYTES = 128ull << 20;
 
@@ -214,6 +226,9 @@ struct mhmkc {
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
   DevBuf d_hll, d_dest, d_ohist, d_out2_keys, d_out2_counts, d_out2_left, d_out2_right, d_mh;
   DevBuf d_ord;  // mhmkc_fetch_ordered: sort keys, row indices, radix-sort scratch
+  mhm::OutRows ord{};      // the ordered rows (in d_r2 or d_ord), valid while ord_ready
+  bool ord_ready = false;  // set by order_rows, cleared by finish / reset
+  int order_rows();
   DevBuf d_spill;  // k_count: the deferred records of cold sweeps, mhm::SPILL_RECORDS per persistent workgroup
   // supermer exchange (smer): owner bytes of a slab's tiles; the received supermers (codes, good bits, descriptors),
   // their window counts / prefix, per-tile first supermer, scan scratch
@@ -373,7 +388,6 @@ struct mhmkc {
   // Device -> host copy of `bytes` into caller (pageable) memory through two pinned staging buffers: chunk i's DMA
   // runs while chunk i - 1 is copied out of the other buffer by host threads (a plain copy into pageable memory
   // moved the C2 table at ~17 GB/s).
-  PinBuf d2h_stage[2];
   hipError_t d2h(void *dst, const void *src, size_t bytes);
 
   int add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known);
@@ -1415,6 +1429,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   if (partial) return fail(MHMKC_ESTATE, "a failed mhmkc_add_fastq_file left part of the file in this round; call mhmkc_reset");
   int rc = begin_round();
   if (rc) return rc;
+  ord_ready = false;
   if ((rc = resolve_slabs())) return rc;
   hipError_t e;
   const uint32_t no = n_owned();
@@ -1798,7 +1813,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
 }
 
 hipError_t mhmkc::d2h(void *dst, const void *src, size_t bytes) {
-  constexpr size_t CH = 32ull << 20;
+  constexpr size_t CH = 8ull << 20;
   hipError_t e;
   hipPointerAttribute_t pa{};
   const bool pinned = hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost;
@@ -1807,12 +1822,14 @@ hipError_t mhmkc::d2h(void *dst, const void *src, size_t bytes) {
     if ((e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
     return hipStreamSynchronize(stream);
   }
-  if ((e = d2h_stage[0].ensure(CH)) != hipSuccess || (e = d2h_stage[1].ensure(CH)) != hipSuccess) return e;
+  D2HStage &stg = d2h_stage();
+  std::lock_guard<std::mutex> lock(stg.mu);
+  if ((e = stg.buf[0].ensure(CH)) != hipSuccess || (e = stg.buf[1].ensure(CH)) != hipSuccess) return e;
   hipEvent_t ev[2] = {take_event(), take_event()};
   const size_t n_ch = (bytes + CH - 1) / CH;
   auto drain = [&](size_t c) {  // host copy of chunk c out of its staging buffer, four threads
     const size_t off = c * CH, len = std::min(CH, bytes - off);
-    const char *sp = d2h_stage[c & 1].as<char>();
+    const char *sp = stg.buf[c & 1].as<char>();
     char *dp = (char *)dst + off;
     std::thread th[3];
     const size_t q = (len / 4 + 63) & ~(size_t)63;
@@ -1827,7 +1844,7 @@ hipError_t mhmkc::d2h(void *dst, const void *src, size_t bytes) {
   for (size_t c = 0; c < n_ch && e == hipSuccess; c++) {
     const size_t off = c * CH, len = std::min(CH, bytes - off);
     if (c >= 2 && (e = hipEventSynchronize(ev[c & 1])) != hipSuccess) break;  // (its buffer was drained below)
-    if ((e = hipMemcpyAsync(d2h_stage[c & 1].p, (const char *)src + off, len, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+    if ((e = hipMemcpyAsync(stg.buf[c & 1].p, (const char *)src + off, len, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipEventRecord(ev[c & 1], stream)) != hipSuccess)
       break;
     if (c >= 1) {
@@ -2037,6 +2054,7 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     mhmkc_destroy(h);
     return MHMKC_EHIP;
   }
+  (void)mhm::preload_owner_kernels();  // (the hand-off's code object: loaded here, not in the first fetch)
   if (cfg->n_ranks > 1 && cfg->comm_id) {
     ncclUniqueId id;
     memcpy(&id, cfg->comm_id, sizeof id);
@@ -2097,8 +2115,6 @@ void mhmkc_destroy(mhmkc_t h) {
   for (DevBuf *b : cbufs) b->release();
   h->x_send.release();
   h->x_recv.release();
-  h->d2h_stage[0].release();
-  h->d2h_stage[1].release();
   h->fq_file_buf.release();
   for (auto &p : h->prof) {
     h->ev_pool.push_back(p.a);
@@ -2682,13 +2698,12 @@ int mhmkc_fetch(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *r
   return MHMKC_OK;
 }
 
-int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right) {
-  if (!h) return MHMKC_EINVAL;
-  if (!h->finished) return h->fail(MHMKC_ESTATE, "fetch before finish");
-  const uint64_t n = h->n_out;
-  if (!n) return MHMKC_OK;
-  if (n >= 0xffffffffull) return h->fail(MHMKC_EUNSUPPORTED, "mhmkc_fetch_ordered: at most 2^32-1 rows");
-  const int nlo = h->nlo;
+// The output rows ordered by the top 32 bits of mhmkc_map_hash, on the device (sorted once per finish, then kept for
+// the range fetches).
+int mhmkc::order_rows() {
+  if (ord_ready) return MHMKC_OK;
+  const uint64_t n = n_out;
+  if (n >= 0xffffffffull) return fail(MHMKC_EUNSUPPORTED, "mhmkc_fetch_ordered: at most 2^32-1 rows");
   const size_t sb = mhm::map_order_scratch_bytes(n, nlo);
   const size_t ob = align_up(n * 8 * nlo + 64, 256) + align_up(n * 2 + 64, 256) + 2 * align_up(n + 64, 256);
   hipError_t e;
@@ -2696,23 +2711,42 @@ int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left,
   // than both at every k: >= 4 B per counted occurrence against < 6 B per output row + the sort's 40-72 B), else
   // the handle's own buffers (a first hipMalloc of the sort's ~2 GB at C2 cost more than the sort)
   char *base = nullptr;
-  if (h->d_r2.p && h->d_r2.cap >= sb + ob) {
-    base = h->d_r2.as<char>();
+  if (d_r2.p && d_r2.cap >= sb + ob) {
+    base = d_r2.as<char>();
   } else {
-    if ((e = h->grow(h->d_ord, sb + ob)) != hipSuccess) return h->hip_fail(e, "fetch_ordered buffers");
-    base = h->d_ord.as<char>();
+    if ((e = grow(d_ord, sb + ob)) != hipSuccess) return hip_fail(e, "fetch_ordered buffers");
+    base = d_ord.as<char>();
   }
   char *ok = base + sb, *oc = ok + align_up(n * 8 * nlo + 64, 256), *ol = oc + align_up(n * 2 + 64, 256),
        *orr = ol + align_up(n + 64, 256);
-  mhm::OutRows in{h->d_out_keys.as<uint64_t>(), h->d_out_counts.as<uint16_t>(), h->d_out_left.as<char>(),
-                  h->d_out_right.as<char>()};
-  mhm::OutRows out{(uint64_t *)ok, (uint16_t *)oc, ol, orr};
-  if ((e = mhm::launch_map_order(in, n, nlo, base, sb, out, h->stream)) != hipSuccess)
-    return h->hip_fail(e, "fetch_ordered sort");
-  if (keys) e = h->d2h(keys, out.keys, n * 8 * nlo);
-  if (e == hipSuccess && counts) e = h->d2h(counts, out.counts, n * 2);
-  if (e == hipSuccess && left) e = h->d2h(left, out.left, n);
-  if (e == hipSuccess && right) e = h->d2h(right, out.right, n);
+  mhm::OutRows in{d_out_keys.as<uint64_t>(), d_out_counts.as<uint16_t>(), d_out_left.as<char>(), d_out_right.as<char>()};
+  ord = mhm::OutRows{(uint64_t *)ok, (uint16_t *)oc, ol, orr};
+  if (n && (e = mhm::launch_map_order(in, n, nlo, base, sb, ord, stream)) != hipSuccess)
+    return hip_fail(e, "fetch_ordered sort");
+  ord_ready = true;
+  return MHMKC_OK;
+}
+
+int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left, char *right) {
+  if (!h) return MHMKC_EINVAL;
+  return mhmkc_fetch_ordered_range(h, 0, h->finished ? h->n_out : 0, keys, counts, left, right);
+}
+
+int mhmkc_fetch_ordered_range(mhmkc_t h, uint64_t row0, uint64_t n_rows, uint64_t *keys, uint16_t *counts, char *left,
+                              char *right) {
+  if (!h) return MHMKC_EINVAL;
+  if (!h->finished) return h->fail(MHMKC_ESTATE, "fetch before finish");
+  if (row0 > h->n_out || n_rows > h->n_out - row0) return h->fail(MHMKC_EINVAL, "row range past the table's end");
+  if (!n_rows) return MHMKC_OK;
+  int rc = h->order_rows();
+  if (rc) return rc;
+  const int nlo = h->nlo;
+  const mhm::OutRows &o = h->ord;
+  hipError_t e = hipSuccess;
+  if (keys) e = h->d2h(keys, o.keys + row0 * nlo, n_rows * 8 * nlo);
+  if (e == hipSuccess && counts) e = h->d2h(counts, o.counts + row0, n_rows * 2);
+  if (e == hipSuccess && left) e = h->d2h(left, o.left + row0, n_rows);
+  if (e == hipSuccess && right) e = h->d2h(right, o.right + row0, n_rows);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fetch_ordered");
 }
@@ -2757,6 +2791,7 @@ int mhmkc_reset(mhmkc_t h) {
   h->began = false;
   h->partial = false;
   h->n_out = 0;
+  h->ord_ready = false;
   memset(&h->st, 0, sizeof h->st);
   if ((e = hipMemsetAsync(h->d_err.p, 0, 16, h->stream)) != hipSuccess) return h->hip_fail(e, "reset");
   return MHMKC_OK;

@@ -31,7 +31,7 @@ def test_lib_exports_every_declared_symbol():
     lib = N.lib()
     for name in declared(ROOT / "include" / "mhmkc.h"):
         assert hasattr(lib, name), name
-    assert lib.mhmkc_abi_version() == 11
+    assert lib.mhmkc_abi_version() == 12
 
 
 def test_synth_exports_every_declared_symbol():

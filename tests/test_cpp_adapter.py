@@ -118,3 +118,37 @@ def test_adapter_fastq(k, tmp_path):
     assert "fastq reads 3000" in out.stderr
     pb, po = O.fastq_pack(text)
     assert out.stdout.splitlines() == sorted(oracle_table(pb, po, k).lines())
+
+
+@pytest.mark.parametrize("k,n,chunks,dups", [(21, 400_000, 1, 0), (21, 400_000, 7, 300), (33, 200_000, 3, 50),
+                                             (63, 150_000, 1, 20), (99, 100_000, 5, 10), (21, 3000, 2, 5)])
+def test_kmermap_parallel_fill(k, n, chunks, dups, tmp_path):
+    """KmerMap::fill's threaded placement of rows in mhmkc_fetch_ordered's order (include/mhmkc_kcount.hpp
+    chunk_ordered: positions as a running maximum over thread ranges, rows past the last slot wrapped through put), in
+    one piece and streamed in chunks as load_ordered feeds it, holds every row with its values, exactly like the
+    one-thread insert loop; repeated keys (also across chunk boundaries) keep their first row; unordered rows fall
+    back to the loop."""
+    import numpy as np
+
+    from mhm2_proxy_amd import build as b
+
+    tool = b.build_fill()
+    rng = np.random.default_rng(k + n + chunks)
+    nl = k // 32 + 1
+    keys = rng.integers(0, 2 ** 63, size=(n, nl), dtype=np.uint64)
+    kk = min(k, 32)
+    keys[:, 0] &= np.uint64(((1 << (2 * kk)) - 1) << (64 - 2 * kk))
+    if dups:
+        keys[n - dups:] = keys[rng.integers(0, n - dups, size=dups)]
+    pre = str(tmp_path / "t")
+    keys.tofile(pre + ".keys")
+    rng.integers(0, 65535, size=n, dtype=np.uint16).tofile(pre + ".counts")
+    rng.integers(65, 90, size=n, dtype=np.uint8).tofile(pre + ".left")
+    rng.integers(65, 90, size=n, dtype=np.uint8).tofile(pre + ".right")
+    for extra in (["4", "--sort", "--chunks", str(chunks)], ["4", "--chunks", str(chunks)]):
+        r = subprocess.run([str(tool), str(k), str(n), pre, *extra], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        import json
+
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        assert j["bad"] == 0 and j["size"] == j["size_one_thread"] == len({tuple(x) for x in keys.tolist()})
