@@ -1,0 +1,36 @@
+/* mhmkc_debug.h — the test-only entry point of libmhmkc.so.
+ *
+ * Not part of the product interface (include/mhmkc.h): process-wide switches with which the parity tests force the
+ * rare paths of the counter (exact histogram layouts instead of capped ones, tiny LDS tables, a fixed fine partition,
+ * an output too small for the table, a failing file read, the key-word records the mixed ones are compared with, ...).
+ * A production caller never sets them; the library reads no environment variable for them.
+ */
+#ifndef MHMKC_DEBUG_H
+#define MHMKC_DEBUG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Set one knob (returns MHMKC_OK, or MHMKC_EINVAL for an unknown name). Knobs read at mhmkc_create (wide_records,
+ * smer, cb0, cb0_2, cb0_3) apply to handles created afterwards, the others to the next call that uses them:
+ *   exact         1: exact (histogram) layouts for every slab and finish pass
+ *   cap           k_count's LDS table slots (>= 64; 0: the kernel's own)
+ *   fine_bits     fine bits of the partition (-1: from the distinct-key sketch)
+ *   out_cap       output rows of the first finish pass (-1: from the sketch)
+ *   fq_read_fail  mhmkc_add_fastq_file: the read of this block fails (-1: none)
+ *   wide_records  1: key-word records instead of the compact / mixed ones
+ *   smer          0: MHMKC_OWNER_MINIMIZER at k >= 33 takes the record exchange + hand-off, not supermers
+ *   chunk_bytes   H2D chunk of a host batch (0: 128 MB)
+ *   cb0, cb0_2, cb0_3  coarse bits for one-, two-, three/four-word keys (0: 8, 8, 7) */
+int mhmkc_debug_set(const char *knob, int64_t value);
+/* Every knob back to its default. */
+void mhmkc_debug_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -47,6 +47,8 @@ ABI_SYMBOLS = [
     "mhmkc_wait_stream", "mhmkc_set_dmin_thres", "mhmkc_set_transport", "mhmkc_minimizer_hashes",
 ]
 SYNTH_SYMBOLS = ["mhmkc_synth_config_init", "mhmkc_synth_genome", "mhmkc_synth_reads"]
+# the test-only entry point (include/mhmkc_debug.h)
+DEBUG_SYMBOLS = ["mhmkc_debug_reset", "mhmkc_debug_set"]
 
 
 class MhmkcConfig(C.Structure):
@@ -166,6 +168,17 @@ def _bind_torch_runtime() -> None:
         pass
 
 
+def debug_set(knob: str, value: int) -> None:
+    """A test-only switch of the library (include/mhmkc_debug.h: exact layouts, tiny tables, ...); tests only."""
+    if lib().mhmkc_debug_set(knob.encode(), int(value)) != 0:
+        raise ValueError(f"unknown debug knob {knob!r}")
+
+
+def debug_reset() -> None:
+    if _lib is not None:
+        _lib.mhmkc_debug_reset()
+
+
 def lib() -> C.CDLL:
     """Load libmhmkc.so (raises if it has not been built: no CPU fallback exists)."""
     global _lib
@@ -198,6 +211,9 @@ def lib() -> C.CDLL:
     L.mhmkc_fetch.argtypes = [VP, VP, VP, VP, VP]
     L.mhmkc_fetch_ordered.argtypes = [VP, VP, VP, VP, VP]
     L.mhmkc_fetch_ordered_range.argtypes = [VP, U64, U64, VP, VP, VP, VP]
+    L.mhmkc_debug_set.argtypes = [C.c_char_p, C.c_int64]
+    L.mhmkc_debug_reset.argtypes = []
+    L.mhmkc_debug_reset.restype = None
     L.mhmkc_device_output.argtypes = [VP, P(VP), P(VP), P(VP), P(VP), P(U64)]
     L.mhmkc_get_stats.argtypes = [VP, P(MhmkcStats)]
     L.mhmkc_reset.argtypes = [VP]

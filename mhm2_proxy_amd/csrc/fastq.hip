@@ -456,19 +456,11 @@ struct PairDesc {
 };
 
 // Pairs whose mates are both at most MG_LONG bases (every short-read run) go through a k_fq_merge instance with
-// MG_SHORT-byte staging: 11 KB of LDS per workgroup instead of 42 KB, so MHMKC_MG_OCC workgroups per CU instead of
+// MG_SHORT-byte staging: 11 KB of LDS per workgroup instead of 42 KB, so MG_OCC workgroups per CU instead of
 // three hide each other's LDS and shuffle round trips. k_fq_pair_records lists the other pairs (after the
 // descriptors: a counter, then the pair indices), which a launch of the 2048-byte instance takes.
-#ifndef MHMKC_MG_SHORT
-#define MHMKC_MG_SHORT 512
-#endif
-#ifndef MHMKC_MG_OCC
-#define MHMKC_MG_OCC 8
-#endif
-#ifndef MHMKC_MG_OPAQUE
-#define MHMKC_MG_OPAQUE 1
-#endif
-constexpr int MG_SHORT = MHMKC_MG_SHORT;
+constexpr int MG_SHORT = 512;
+constexpr int MG_OCC = 8;
 constexpr uint32_t MG_LONG = (uint32_t)MG_SHORT - 8;  // longest mate of a short pair
 __host__ __device__ inline uint32_t *long_pairs(void *desc_buf, uint64_t n_pairs) {  // [counter, 15 pad, list]
   return (uint32_t *)((char *)desc_buf + (((size_t)n_pairs * sizeof(PairDesc) + 63) & ~(size_t)63));
@@ -583,18 +575,6 @@ __global__ __launch_bounds__(FQ_THREADS) void k_fq_pair_records(const char *text
 // quality read at an N is always the one just set. It does change the output, so it is applied in LDS in scan
 // order and the qualities of pairs with an N go to the scratch for k_fq_merge_pack.
 constexpr int MG_WAVES = 4;
-// Diagnostic phase stamps of k_fq_merge (MHMKC_MGSTAMP builds only): wave cycles of staging, fast filter,
-// offset scans and the verdict tail, then the number of scans and of filter rounds, into stats[4..9]
-#ifndef MHMKC_MGSTAMP
-#define MHMKC_MGSTAMP 0
-#endif
-#if MHMKC_MGSTAMP
-#define MG_STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
-#define MG_ADD(i, v) mg_acc[i] += (v)
-#else
-#define MG_STAMP(var)
-#define MG_ADD(i, v)
-#endif
 constexpr int MG_MAXL = 2048;  // > FQ_MAX_LINE + 4 (unaligned 4-byte reads past a line stay inside)
 
 // The fast filter's view of four characters: 2-bit codes (A C G T = 0..3, N and the rest 0) and 2-bit flags
@@ -661,7 +641,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 // MAXL < MG_MAXL: the pairs with a mate longer than MG_LONG are left to the MG_MAXL instance, which (given
 // long_list) takes only the listed pairs.
 template <int MAXL>
-__global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) void k_fq_merge(
+__global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MG_OCC : 3) void k_fq_merge(
     const char *text, const PairDesc *desc, uint64_t n_pairs, const unsigned long long *rec_offs, int qual_offset,
     char *scratch, uint32_t *pair_info, unsigned long long *out_len, unsigned long long *err,
     unsigned long long *stats, const uint32_t *long_list) {
@@ -680,9 +660,6 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
   const int16_t MIN_OVERLAP = 12, EXTRA_TEST_OVERLAP = 2, MAX_MISMATCHES = 3, EXTRA_PER_1000 = 150;
   const double MAX_PERROR = 0.025;
   uint64_t merged = 0, ambiguous = 0, ov_bases = 0;
-#if MHMKC_MGSTAMP
-  uint64_t mg_acc[6] = {0, 0, 0, 0, 0, 0};
-#endif
   const uint64_t n_waves = (uint64_t)gridDim.x * MG_WAVES;
   if (blockIdx.x == 0 && threadIdx.x == 0) out_len[2 * n_pairs] = 0;  // the scan's last element
   const uint64_t n_items = long_list ? long_list[0] : n_pairs;
@@ -696,10 +673,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
     dn = desc[pn];
   }
   for (uint64_t it = it0; it < n_items; it += n_waves) {
-#if MHMKC_MG_OPAQUE
     const int lane = opaque_lane();
-#endif
-    MG_STAMP(t_p0);
     const uint64_t p = pn;
     const PairDesc d = dn;
     if (it + n_waves < n_items) {
@@ -753,8 +727,6 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       if (lane == 0) fq_fail(err, 2 * p + 1, FQ_E_CHAR2);
       continue;
     }
-    MG_STAMP(t_p1);
-    MG_ADD(0, t_p1 - t_p0);
     hasN = __ballot(hasN) != 0;
     const int16_t len = (int16_t)(L2 < L1 ? L2 : L1);
     const int16_t start_i = (len == (int16_t)L1) ? 0 : (int16_t)(L1 - len);
@@ -763,7 +735,6 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
     bool abort_merge = false, qbad = false, stop = false;
     for (int r0 = 0; r0 < n_off && !stop; r0 += 64) {
       // 1. fast filter of offsets r0 .. r0 + 63
-      MG_STAMP(t_f0);
       const int i = r0 + lane;
       // every lane runs the same steps (a uniform exit on a ballot, no per-lane loop masks): a lane past the
       // offsets or already over its limit keeps adding masked or surplus counts, which change no verdict
@@ -786,11 +757,6 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       }
       const bool pass = live && mm <= emax;
       uint64_t kept = __ballot(pass);
-#if MHMKC_MGSTAMP
-      const uint64_t t_f1 = __builtin_amdgcn_s_memtime();
-      MG_ADD(1, t_f1 - t_f0);
-      MG_ADD(5, 1);
-#endif
       // 2. + 3. the kept offsets in order
       while (kept && !stop) {
         const int io = r0 + __ffsll((long long)kept) - 1;
@@ -921,11 +887,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
           }
         }
         if (abort_merge) stop = true;  // the next offset's "if (abort_merge) break"
-        MG_ADD(4, 1);
       }
-#if MHMKC_MGSTAMP
-      MG_ADD(2, __builtin_amdgcn_s_memtime() - t_f1);
-#endif
     }
     if (qbad) {
       if (lane == 0) fq_fail(err, 2 * p + 1, FQ_E_QUAL);
@@ -952,14 +914,7 @@ __global__ __launch_bounds__(64 * MG_WAVES, MAXL < MG_MAXL ? MHMKC_MG_OCC : 3) v
       for (int j = lane; j < L2; j += 64) crq2[j] = RQ[j];
     }
     wave_sync_lds();  // the next pair overwrites the wave's LDS
-#if MHMKC_MGSTAMP
-    MG_ADD(3, __builtin_amdgcn_s_memtime() - t_p1);
-#endif
   }
-#if MHMKC_MGSTAMP
-  if (lane == 0)
-    for (int i = 0; i < 6; i++) atomicAdd(&stats[4 + i], (unsigned long long)mg_acc[i]);
-#endif
   if (lane == 0 && (merged | ambiguous)) {
     atomicAdd(&stats[1], (unsigned long long)merged);
     atomicAdd(&stats[2], (unsigned long long)ambiguous);

@@ -24,19 +24,19 @@ namespace mhm {
 
 template <int NL>
 constexpr int kTile() {  // bases per extract tile
-  return NL == 1 ? MHMKC_TILE1 : NL == 2 ? MHMKC_TILE2 : NL == 3 ? MHMKC_TILE3 : MHMKC_TILE4;
+  return TILE_BASES[NL];
 }
 template <int NL>
 constexpr int kEThreads() {  // threads per extract workgroup
-  return NL == 1 ? MHMKC_ETHREADS1 : NL == 2 ? MHMKC_ETHREADS2 : NL == 3 ? MHMKC_ETHREADS3 : MHMKC_ETHREADS4;
+  return E_THREADS_NL[NL];
 }
 template <int NL>
 constexpr int kPTile() {  // records per partition chunk (kPThreads threads)
-  return NL == 1 ? MHMKC_PTILE1 : NL == 2 ? MHMKC_PTILE2 : NL == 3 ? MHMKC_PTILE3 : MHMKC_PTILE4;
+  return P_TILE[NL];
 }
 template <int NL>
 constexpr int kPThreads() {  // threads per partition workgroup
-  return NL == 1 ? MHMKC_PTHREADS1 : NL == 2 ? MHMKC_PTHREADS2 : MHMKC_PTHREADS3;
+  return P_THREADS[NL];
 }
 template <int NL>
 constexpr int kGroups() {
@@ -365,40 +365,10 @@ struct WalkSpan {
 // Compact-record walk (10 <= k <= 21, §3.7): the windows of walk_windows with the key kept right-aligned in its
 // B = 2k bits, the form cmix takes, so no Kmer-layout word is built or shifted into the mix; the record is
 // (y below the coarse digit) << 6 | ext with y = cmix(canonical key), the bin the coarse digit (y's top cb bits).
-// Extraction is VALU-issue bound (§4): this walk issues ~40 % fewer VALU instructions per window.
-template <int W>
-__device__ __forceinline__ void walk_c32(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
-                                         uint32_t tile, uint64_t n_bases, uint32_t head, int k, int cb,
-                                         uint64_t (&rk)[W][1], uint32_t (&inf)[W]) {
-  WalkSpan<1> sp(fwd, good, start, tile, n_bases, head, k);
-  const int B = 2 * k, a = B >> 1, b = B - a, rb = B - cb;
-  const uint64_t mB = (1ull << B) - 1, rmask = (1ull << rb) - 1;
-  uint64_t fw = WalkSpan<1>::codes64(fwd, sp.lp0) >> (64 - B);
-  uint64_t rc = rev2(~fw) >> (64 - B);
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    uint32_t cr, e_f, e_r;
-    const bool valid = sp.step(i, k, cr, e_f, e_r);
-    const bool use_rc = rc < fw;
-    const uint64_t x = use_rc ? rc : fw;
-    const uint32_t e = use_rc ? e_r : e_f;
-    uint32_t R = (uint32_t)x & ((1u << a) - 1), L = (uint32_t)(x >> a);
-    cmix_lr(L, R, a, b);
-    const uint64_t y = ((uint64_t)L << a) | R;
-    rk[i][0] = ((y & rmask) << EXT_BITS) | e;
-    inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(y >> rb) : 0u;
-    asm volatile("" : "+v"(rk[i][0]), "+v"(inf[i]));
-    // roll: base lp leaves (the next window's left neighbour), cr enters
-    sp.cl = (uint32_t)(fw >> (B - 2));
-    fw = ((fw << 2) | cr) & mB;
-    rc = (rc >> 2) | ((uint64_t)(cr ^ 3u) << (B - 2));
-  }
-}
-
-// walk_c32 with each window's record in two u32 registers instead of a u64 and an info word: lo = the record's low
-// 32 bits, hi = valid << 31 | (the record's bits 32..39) << 11 | bin (bits 19..30 stay free for the window's rank
-// in its bin, scatter_staged_c40). 48 -> 32 VGPRs of records per thread, so the kernel fits 96 VGPRs (five
-// workgroups per CU) without spilling.
+// Each window's record is held in two u32 registers instead of a u64 and an info word: lo = the record's low 32
+// bits, hi = valid << 31 | (the record's bits 32..39) << 11 | bin (bits 19..30 stay free for the window's rank in its
+// bin, scatter_staged_c40). 48 -> 32 VGPRs of records per thread, so the kernel fits 96 VGPRs (five workgroups per
+// CU) without spilling.
 template <int W>
 __device__ __forceinline__ void walk_c32_lh(const uint64_t *fwd, const uint32_t *good, const uint32_t *start,
                                             uint32_t tile, uint64_t n_bases, uint32_t head, int k, int cb,
@@ -594,13 +564,9 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_extract_hist(ExtractParams 
 // Global store formats of a scatter: the record words (+ the ext byte plane when not packed), or a
 // compact record (kmer_ops.hpp cmix) split into a u32 plane w[0] + a byte plane ext (coarse buckets,
 // <= 40 bits) or a u32 plane alone (fine buckets, <= 32 bits).
-// SF_AOS2: two-word records as one 16-byte record (the records of mixed two-word keys, MHMKC_M2AOS)
+// SF_AOS2: two-word records as one 16-byte record (the records of mixed two-word keys: a bucket's run of a tile or
+// chunk is one contiguous span, and a record one 16-byte load), staged in LDS as 16-byte records too
 enum { SF_WORDS = 0, SF_C40 = 1, SF_C32 = 2, SF_AOS2 = 3 };
-// ... staged in LDS as 16-byte records too (one ds_write_b128 / ds_read_b128 instead of two 8-byte ones)
-#ifndef MHMKC_AOSSTAGE
-#define MHMKC_AOSSTAGE 1
-#endif
-constexpr bool kAosStage = MHMKC_AOSSTAGE != 0;
 
 template <int NL, bool PACKED, int SF>
 __device__ __forceinline__ void store_out(const PlaneSet &out, uint64_t dst, const uint64_t *v, uint32_t ext) {
@@ -632,52 +598,21 @@ __device__ __forceinline__ void scatter_clear(uint32_t *lcnt, uint32_t nb) {
   for (uint32_t b = threadIdx.x; b < nb; b += NT) lcnt[b] = 0;
 }
 
-// Bin b's cursor is cursor[b * cstride]. In a capped layout a bin that would overflow sets err bit 1
-// and its excess records are not written (the host then redoes the pass with exact bin sizes).
-// Called after lcnt has been cleared and a barrier.
-template <int NL, bool PACKED, int W, int SF, int NT = E_THREADS>
-__device__ __forceinline__ void scatter_regs(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
-                                             unsigned char *smem, unsigned long long *cursor, uint32_t cstride,
-                                             const PlaneSet &out, const BinLimit lim, unsigned int *err) {
-  uint32_t *lcnt = (uint32_t *)smem;
-  unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
-  uint32_t rank[W];
-#pragma unroll
-  for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
-  __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += NT) {
-    const uint32_t c = lcnt[b];
-    const unsigned long long off = c ? atomicAdd(&cursor[(uint64_t)b * cstride], (unsigned long long)c) : 0ull;
-    if (lim.cap && c && off + c > lim.end(b)) atomicOr(err, 2u);
-    goff[b] = off;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < W; j++) {
-    if (inf[j] >> 31) {
-      const uint32_t d = inf[j] & 0xffffu;
-      const unsigned long long dst = goff[d] + rank[j];
-      if (lim.cap && dst >= lim.end(d)) continue;
-      store_out<NL, PACKED, SF>(out, dst, rk[j], (inf[j] >> 16) & 63u);
-    }
-  }
-}
-
 constexpr size_t WSUM_BYTES = ((1024 / 64 + 1) * 4 + 15) & ~(size_t)15;  // block_excl_scan's wave sums (<= 1024 threads)
 
-// Staged variant: the records are first written to LDS in bin order, then copied out so that consecutive
-// lanes store consecutive addresses of one bin (runs of ~T/nb records instead of one line per lane).
-// LDS: counters [lcnt | goff | lstart | wsum] then the stage area [NL][T] u64 | sbin[T] u16 | sext[T] u8,
-// which may alias the tile (the first barrier below is after every thread's walk).
-// The bins' run starts (lstart) reuse the rank counters (lcnt): each thread reads its bins' counts, then
-// overwrites the same entries (MHMKC_LSALIAS=0: a plane of their own). At k = 21 this keeps an extraction
+// The scatter of extraction and partition. Every thread holds its W records (rk, inf = valid<<31 | e<<16 | bin); a
+// returning LDS atomic ranks every record inside its bin, one global atomic per non-empty bin reserves the
+// workgroup's run, the records are written to LDS in bin order, and then copied out so that consecutive lanes store
+// consecutive addresses of one bin (runs of ~T/nb records instead of one line per lane; a register scatter took
+// extraction 8.1 -> 14.3 ms, §4.2). The stores of one bin land in the same segment, which is written by workgroups
+// of one XCD only (E_NSUB segments per coarse bucket, fine buckets per coarse bucket), so partial lines merge in that
+// XCD's L2 before they reach HBM. Bin b's cursor is cursor[b * cstride]; in a capped layout a bin that would
+// overflow sets err bit 1 and its records are not written (the host then redoes the pass with exact bin sizes).
+// LDS: counters [lcnt | goff | wsum] then the stage area [NL][T] u64 | sbin[T] u16 | sext[T] u8, which may alias
+// the tile (the first barrier below is after every thread's walk). The bins' run starts reuse the rank counters
+// (lcnt): each thread reads its bins' counts, then overwrites the same entries. At k = 21 this keeps an extraction
 // workgroup's LDS (counters + the staged tile) under 32 KiB, five per CU.
-#ifndef MHMKC_LSALIAS
-#define MHMKC_LSALIAS 1
-#endif
-__host__ __device__ constexpr size_t staged_cnt_bytes(uint32_t nb) {
-  return scatter_lds_bytes(nb) + (MHMKC_LSALIAS ? 0 : (((size_t)nb * 4 + 15) & ~(size_t)15)) + WSUM_BYTES;
-}
+__host__ __device__ constexpr size_t staged_cnt_bytes(uint32_t nb) { return scatter_lds_bytes(nb) + WSUM_BYTES; }
 // Compact records are staged at their stored width: u32 (+ the high byte for SF_C40).
 __host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packed, int sf = SF_WORDS) {
   return sf == SF_C40   ? (size_t)T * (4 + 1 + 2)
@@ -697,7 +632,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   static_assert(CAP <= W * NT && CAP % NT == 0, "stage capacity: whole rows of the workgroup");
   uint32_t *lcnt = (uint32_t *)smem;
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
-  uint32_t *lstart = MHMKC_LSALIAS ? lcnt : (uint32_t *)(smem + scatter_lds_bytes(nb));
+  uint32_t *lstart = lcnt;
   uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - WSUM_BYTES);
   constexpr bool C32 = SF == SF_C40 || SF == SF_C32;  // compact: low 32 bits in stage32, the high byte (SF_C40) in sext
   uint64_t *stage = (uint64_t *)area;
@@ -738,7 +673,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       if (C32) {
         stage32[pos] = (uint32_t)rk[j][0];
         if (SF == SF_C40) sext[pos] = (uint8_t)(rk[j][0] >> 32);
-      } else if (SF == SF_AOS2 && kAosStage) {  // one 16-byte LDS write per record
+      } else if (SF == SF_AOS2) {  // one 16-byte LDS write per record
         ((ulonglong2 *)stage)[pos] = make_ulonglong2(rk[j][0], rk[j][NL - 1]);
       } else {
 #pragma unroll
@@ -774,7 +709,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
       uint64_t v[NL];
       if (C32) {
         v[0] = (uint64_t)stage32[sp] | (SF == SF_C40 ? (uint64_t)sext[sp] << 32 : 0ull);
-      } else if (SF == SF_AOS2 && kAosStage) {
+      } else if (SF == SF_AOS2) {
         const ulonglong2 q = ((const ulonglong2 *)stage)[sp];
         v[0] = q.x;
         v[NL - 1] = q.y;
@@ -799,7 +734,7 @@ __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (
   static_assert(T <= 4096 && 8 * NT <= 2048, "rank in 12 bits, bin in 11");
   uint32_t *lcnt = (uint32_t *)smem;
   unsigned long long *goff = (unsigned long long *)(smem + scatter_cnt_bytes(nb));
-  uint32_t *lstart = MHMKC_LSALIAS ? lcnt : (uint32_t *)(smem + scatter_lds_bytes(nb));
+  uint32_t *lstart = lcnt;
   uint32_t *wsum = (uint32_t *)(smem + staged_cnt_bytes(nb) - WSUM_BYTES);
   uint32_t *stage32 = (uint32_t *)area;
   uint16_t *sbin = (uint16_t *)(stage32 + T);
@@ -858,234 +793,25 @@ __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (
   }
 }
 
-#ifndef MHMKC_ESTAGE
-#define MHMKC_ESTAGE 1
-#endif
-constexpr bool kEStaged = MHMKC_ESTAGE != 0;
-// three- and four-word keys: a 2048-base tile at k >= 65 makes ~3 records per coarse bin, so staging gains little
-// coalescing and its 48-64 KB of LDS per workgroup cost occupancy (MHMKC_ESTAGE3=0: register scatter for NL >= 3)
-#ifndef MHMKC_ESTAGE3
-#define MHMKC_ESTAGE3 1
-#endif
-template <int NL>
-constexpr bool kEStagedNL() {
-  return NL >= 3 ? (kEStaged && MHMKC_ESTAGE3 != 0) : kEStaged;
-}
-
-#ifndef MHMKC_PSTAGE
-#define MHMKC_PSTAGE 1
-#endif
-constexpr bool kPStaged = MHMKC_PSTAGE != 0;
-// Records of mixed two-word keys as 16-byte records instead of two u64 planes (kcount_launch.hpp MHMKC_M2AOS): a
-// bucket's run of a tile or chunk is one contiguous span (64 B runs became 2 x 32 B ones in the planes), and a
-// record is one 16-byte load.
-constexpr bool kM2Aos = MHMKC_M2AOS != 0;
-
-// ------------------------------------------------------------------------------------------------
-// Mixed two-word extraction over the valid windows only (MHMKC_M2WALK). At k = 63 only 86 of a 150 bp read's
-// positions start a counted window, and the rolling walk above spends the same work on every position. Here
-// the valid windows of the tile (each read's interior windows [s + 1, e - k - 1], kcount_cpu.cpp:316-334) are
-// listed first, and window v of the list goes to thread v % 256, register slot v / 256: each window's
-// forward and reverse-complement words are funnel-loaded from the staged codes and from a reverse-complemented
-// copy of them, so no window depends on its predecessor, and waves whose slots are past the list skip them.
-// Measured at k = 63 on C2 reads: 10.2 ms against 9.6 ms for the rolling walk (the window's LDS reads are a
-// dependent chain the four waves per SIMD do not hide, where rolling keeps everything in registers), so it is
-// off by default; kept for A/B (MHMKC_M2WALK=1) and covered by the parity tests when enabled.
-#ifndef MHMKC_M2WALK
-#define MHMKC_M2WALK 0
-#endif
-constexpr bool kM2Walk = MHMKC_M2WALK != 0 && MHMKC_TILE2 == 2048;  // (its valid-bit scan is one wave over 64 words)
-// Mixed-record walks (walk_c32, walk_m2: the key as the mix takes it); 0 = the generic walk_windows + window_hash.
-#ifndef MHMKC_MIXWALK
-#define MHMKC_MIXWALK 1
-#endif
-constexpr bool kMixedWalk = MHMKC_MIXWALK != 0;
-#ifndef MHMKC_M2BATCH
-#define MHMKC_M2BATCH 2  // valid-window slots per branch-free block
-#endif
-
-// LDS after the staged tile: rc codes [NG] u64 | valid bits [T/32] u32 | their prefix [T/32 + 1] u32 | list [T] u16
-__host__ __device__ constexpr size_t m2walk_lds_bytes() {
-  return align16((size_t)kGroups<2>() * 8) + align16((size_t)(2 * (kTile<2>() / 32) + 1) * 4) + (size_t)kTile<2>() * 2;
-}
-
-// The 32 codes from position q of a staged code array, first in the top bits (branch-free funnel: q & 31 = 0
-// shifts the next word out entirely).
-__device__ __forceinline__ uint64_t funnel_codes(const uint64_t *a, int q) {
-  const int g = q >> 5, sh = (q & 31) * 2;
-  return (a[g] << sh) | ((a[g + 1] >> 1) >> (63 - sh));
-}
-
-template <int W>
-__device__ __forceinline__ void m2_walk_valid(const ExtractParams &p, uint32_t tile, const uint64_t *fwd,
-                                              const uint32_t *good, const uint32_t *start, unsigned char *scratch, uint64_t (&rk)[W][2],
-                                              uint32_t (&inf)[W]
-#ifdef MHMKC_ESTAMP
-                                              , uint64_t &es_list
-#endif
-) {
-  constexpr int T = kTile<2>(), NG = kGroups<2>(), NW = T / 32, P = NG * 32;
-  static_assert(NW == 64 && W * kEThreads<2>() == T && (T / kEThreads<2>()) <= 32 && 32 % (T / kEThreads<2>()) == 0,
-                "one wave scans the valid bits; every position has a slot; a thread's positions in one word");
-  uint64_t *rcw = (uint64_t *)scratch;
-  uint32_t *vb = (uint32_t *)(scratch + align16((size_t)NG * 8));
-  uint32_t *vpre = vb + NW;
-  uint16_t *pos = (uint16_t *)(scratch + align16((size_t)NG * 8) + align16((size_t)(2 * NW + 1) * 4));
-  const int tid = threadIdx.x, k = p.k;
-  for (int g = tid; g < NG; g += kEThreads<2>()) rcw[g] = rev2(~fwd[NG - 1 - g]);  // complement, reversed
-  if (tid < NW) {
-    // Valid-window bits of own positions 32w .. 32w + 31 (staged 32(w+1) + i), MSB first like the staged bit
-    // arrays: window i is valid iff no read start lies at staged positions [q, q + k] (the read-start bits of
-    // load_tile, which include the data end as a start) and it ends before the data does. The start bits
-    // from q on, as a 128-bit string X (position j at bit 127 - j of hi:lo), are dilated towards earlier
-    // positions: Y = OR of X << t for t = 0..k, by doubling to 32 terms, then Y32 | Y32 << (k + 1 - 32).
-    const int w = tid;
-    uint64_t hi = ((uint64_t)start[w + 1] << 32) | start[w + 2], lo = ((uint64_t)start[w + 3] << 32) | start[w + 4];
-#pragma unroll
-    for (int sft = 1; sft < 32; sft <<= 1) {
-      hi |= (hi << sft) | (lo >> (64 - sft));
-      lo |= lo << sft;
-    }
-    const int r = k + 1 - 32;  // in [2, 32]
-    hi |= (hi << r) | (lo >> (64 - r));
-    uint32_t valid = ~(uint32_t)(hi >> 32);
-    const int64_t lim = (int64_t)p.reads.n_bases - k - (int64_t)tile * T - 32 * w;  // window o needs o + k < n
-    valid &= lim >= 32 ? ~0u : lim <= 0 ? 0u : ~(~0u >> (int)lim);
-    vb[w] = valid;
-    const uint32_t c = __popc(valid);
-    uint32_t x = c;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d, 64);
-      if (tid >= d) x += y;
-    }
-    vpre[w] = x - c;
-    if (w == NW - 1) vpre[NW] = x;
-  }
-  __syncthreads();
-  {  // the list: every thread places its 8 positions (one word)
-    const int o0 = tid * (T / kEThreads<2>()), w = o0 >> 5;
-    const uint32_t m = vb[w], base = vpre[w];
-#pragma unroll
-    for (int j = 0; j < T / kEThreads<2>(); j++) {
-      const int i = (o0 + j) & 31;
-      if ((m >> (31 - i)) & 1u) pos[base + __popc(m & ~(~0u >> i))] = (uint16_t)(o0 + j);
-    }
-  }
-  __syncthreads();
-  const uint32_t nv = vpre[NW];
-#ifdef MHMKC_ESTAMP
-  es_list = __builtin_amdgcn_s_memtime();
-#endif
-  const uint64_t m1 = top_mask(k - 32);
-  const int m2_csh = k - p.coarse_bits;
-  const uint64_t m2_cmask = (1ull << m2_csh) - 1;
-  // every list position of the thread up front (v < T always; entries past nv are masked to the tile)
-  int q[W];
-#pragma unroll
-  for (int i = 0; i < W; i++) q[i] = 32 + (int)(pos[tid + i * kEThreads<2>()] & (T - 1));
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    rk[i][0] = 0;
-    rk[i][1] = 0;
-    inf[i] = 0;
-  }
-  // slots in pairs, each pair one branch-free block (the two windows' LDS reads in flight together); a wave
-  // whose pair starts past the list is done
-  constexpr int PB = MHMKC_M2BATCH;
-  static_assert(W % PB == 0, "slot batches");
-#pragma unroll
-  for (int i0 = 0; i0 < W; i0 += PB) {
-    if ((uint32_t)(tid & ~63) + (uint32_t)(i0 * kEThreads<2>()) >= nv) break;
-#pragma unroll
-    for (int i = i0; i < i0 + PB; i++) {
-      const uint32_t v = (uint32_t)tid + (uint32_t)(i * kEThreads<2>());
-      const int qq = q[i];
-      uint64_t fw[2], rc[2];
-      fw[0] = funnel_codes(fwd, qq);
-      fw[1] = funnel_codes(fwd, qq + 32) & m1;
-      const int q0 = P - qq - k;  // the reverse complement starts here in rcw
-      rc[0] = funnel_codes(rcw, q0);
-      rc[1] = funnel_codes(rcw, q0 + 32) & m1;
-      const int ql = qq - 1, qr = qq + k;  // neighbours
-      const uint32_t cl = (uint32_t)(fwd[ql >> 5] >> (62 - 2 * (ql & 31))) & 3u;
-      const uint32_t cr = (uint32_t)(fwd[qr >> 5] >> (62 - 2 * (qr & 31))) & 3u;
-      const uint32_t gl = (good[ql >> 5] >> (31 - (ql & 31))) & 1u, gr = (good[qr >> 5] >> (31 - (qr & 31))) & 1u;
-      int l = gl ? (int)cl : EXT_NONE, r = gr ? (int)cr : EXT_NONE;
-      const bool use_rc = kmer_less<2>(rc, fw);
-      uint64_t key[2];
-      key[0] = use_rc ? rc[0] : fw[0];
-      key[1] = use_rc ? rc[1] : fw[1];
-      const int lr = (r == EXT_NONE) ? EXT_NONE : 3 - r, rr = (l == EXT_NONE) ? EXT_NONE : 3 - l;
-      if (use_rc) {
-        l = lr;
-        r = rr;
-      }
-      const uint32_t e = (uint32_t)((l << 3) | r);
-      uint64_t L, R;
-      m2_mix(key, k, L, R);
-      rk[i][0] = ((L & m2_cmask) << EXT_BITS) | e;
-      rk[i][1] = R;
-      inf[i] = v < nv ? (1u << 31) | (e << 16) | (uint32_t)(L >> m2_csh) : 0u;
-    }
-#pragma unroll
-    for (int i = i0; i < i0 + PB; i++) asm volatile("" : "+v"(rk[i][0]), "+v"(rk[i][1]), "+v"(inf[i]));
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // extract: scatter into coarse buckets
 
-// ... and of the fine partition (k_part_scatter, compact records)
-#ifndef MHMKC_P32REG
-#define MHMKC_P32REG 1
-#endif
-constexpr bool kP32Reg = MHMKC_P32REG != 0;
-// Compact records of the extraction as two u32 registers per window (walk_c32_lh + scatter_staged_c40)
-#ifndef MHMKC_C40REG
-#define MHMKC_C40REG 1
-#endif
-constexpr bool kC40Reg = MHMKC_C40REG != 0;
 // Records the extraction stages at once (scatter_staged CAP; more go out in further rounds): fewer than the tile's
 // windows for keys of two or more words, whose tiles count 57-77 % (k = 63..33), 48 % (k = 77) and 33 % (k = 99) of
 // their windows on 150-base reads. The LDS saved buys workgroups per CU: two-word 2 -> 3 (extraction k = 63 7.67 ->
 // 6.48 ms, k = 33 7.80 -> 7.14; 3072 keeps two: 7.86, 9.13), three-word 3 -> 5 (k = 77 11.54 -> 9.65 ms); four-word
-// keys at 512 threads were held at two by their VGPRs (13.32 -> 13.29 ms; asked for six waves, 80 VGPRs: 12.97 ms);
-// at 256 threads and four waves (EWAVES4: 128 VGPRs) four workgroups fit: 10.04 ms, 9.63 with 768 records staged
+// keys at 256 threads and four waves (kEWaves: 128 VGPRs) fit four workgroups: 10.04 ms, 9.63 with 768 records staged
 // (five waves, 96 VGPRs, spill: 15.8 ms; six waves for three-word keys spill: 13.42 ms; 1792 records for two-word keys
 // at four waves spill: 12.5 ms)
-#ifndef MHMKC_ECAP2
-#define MHMKC_ECAP2 2560
-#endif
-#ifndef MHMKC_ECAP3
-#define MHMKC_ECAP3 1024
-#endif
-#ifndef MHMKC_ECAP4
-#define MHMKC_ECAP4 768
-#endif
+constexpr int E_CAP[5] = {0, 4096, 2560, 1024, 768};
 template <int NL>
 __host__ __device__ constexpr int kECap() {
-  return NL == 2 ? (MHMKC_ECAP2 < kTile<2>() ? MHMKC_ECAP2 : kTile<2>())
-         : NL == 3 ? (MHMKC_ECAP3 < kTile<3>() ? MHMKC_ECAP3 : kTile<3>())
-         : NL == 4 ? (MHMKC_ECAP4 < kTile<4>() ? MHMKC_ECAP4 : kTile<4>())
-                   : kTile<NL>();
+  return E_CAP[NL] < kTile<NL>() ? E_CAP[NL] : kTile<NL>();
 }
 // Minimum waves per SIMD asked of the compiler for the extraction (caps its VGPRs; 1: no cap)
-#ifndef MHMKC_EWAVES1
-#define MHMKC_EWAVES1 1
-#endif
-#ifndef MHMKC_EWAVES2
-#define MHMKC_EWAVES2 1
-#endif
-#ifndef MHMKC_EWAVES3
-#define MHMKC_EWAVES3 1
-#endif
-#ifndef MHMKC_EWAVES4
-#define MHMKC_EWAVES4 4
-#endif
 template <int NL>
 constexpr int kEWaves() {
-  return NL == 1 ? MHMKC_EWAVES1 : NL == 2 ? MHMKC_EWAVES2 : NL == 3 ? MHMKC_EWAVES3 : MHMKC_EWAVES4;
+  return NL == 4 ? 4 : 1;
 }
 
 template <int NL, bool PACKED, bool CMP>
@@ -1095,117 +821,59 @@ __global__ __launch_bounds__(kEThreads<NL>()) __attribute__((amdgpu_waves_per_eu
   extern __shared__ __align__(16) unsigned char smem0[];
   uint64_t *fwd;
   uint32_t *good, *start;
-  unsigned char *smem, *area;
-  if (kEStagedNL<NL>()) {  // counters first, then the tile aliased by the stage area
-    smem = smem0;
-    area = smem0 + staged_cnt_bytes(p.n_bins);
-    carve_tile<NL>(area, fwd, good, start);
-  } else {
-    smem = carve_tile<NL>(smem0, fwd, good, start);
-    area = nullptr;
-  }
-#ifdef MHMKC_ESTAMP
-  const uint64_t es0 = __builtin_amdgcn_s_memtime();
-#endif
+  unsigned char *smem = smem0, *area = smem0 + staged_cnt_bytes(p.n_bins);  // counters, then the tile aliased by
+  carve_tile<NL>(area, fwd, good, start);                                   // the stage area
   scatter_clear<ET>((uint32_t *)smem, p.n_bins);
   const uint32_t tile = blockIdx.x;
   load_tile<NL>(p.reads, tile, p.tile_starts ? 0u : p.tile_first_read[tile], p.qual_cutoff, fwd, good, start, p.err,
                 p.tile_starts);
-#ifdef MHMKC_ESTAMP
-  const uint64_t es1 = __builtin_amdgcn_s_memtime();
-  uint64_t es2 = es1;
-#endif
   const int sh = 64 - p.coarse_bits;
   // stored hash bits, branch-free (hbits == 0: none)
   const int hsh = p.hbits ? 64 - p.hbits : 0;
   const uint64_t hmask = p.hbits ? ~0ull : 0ull;
-  const int csh = 64 - (2 * kk - p.coarse_bits);  // compact: keep the low 2k - cb bits of the mixed key
-  const int m2_csh = kk - p.coarse_bits;            // mixed two-word: L' >> m2_csh = coarse digit
-  const uint64_t m2_cmask = (1ull << m2_csh) - 1;
-  if constexpr (RecKind<NL, CMP>::C32 && kMixedWalk && kC40Reg && kEStagedNL<NL>()) {
+  const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
+  const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
+  if constexpr (RecKind<NL, CMP>::C32) {
     uint32_t lo[W], hi[W];
     walk_c32_lh<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, lo, hi);
-    const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
-    const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
     scatter_staged_c40<W, ET>(lo, hi, p.n_bins, smem, area, p.cursor + sub * p.n_bins, p.out, lim, p.ovf);
     return;
   }
   uint64_t rk[W][NL];
   uint32_t inf[W];
-  if constexpr (RecKind<NL, CMP>::C32 && kMixedWalk) {
-    walk_c32<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, rk, inf);
-  } else if constexpr (RecKind<NL, CMP>::M2 && kMixedWalk && !kM2Walk) {
+  if constexpr (RecKind<NL, CMP>::M2) {
     walk_m2<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, rk, inf);
-  } else if constexpr (RecKind<NL, CMP>::M2 && kM2Walk && kEStagedNL<NL>()) {
-    m2_walk_valid<W>(p, tile, fwd, good, start, area + tile_lds_bytes<NL>(), rk, inf
-#ifdef MHMKC_ESTAMP
-                     , es2
-#endif
-    );
-  } else
-  walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk,
-                   [&](int i, const uint64_t *key, uint32_t e, bool valid) {
-                     if constexpr (RecKind<NL, CMP>::MX) {  // (w0' below the coarse digit) << 6 | ext, r[1..]
-                       uint64_t r[NL];
-                       mx_mix<NL>(key, r);
-                       const int xsh = 64 - p.coarse_bits;
-                       rk[i][0] = ((r[0] & ((1ull << xsh) - 1)) << EXT_BITS) | e;
+  } else {
+    walk_windows<NL>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk,
+                     [&](int i, const uint64_t *key, uint32_t e, bool valid) {
+                       if constexpr (RecKind<NL, CMP>::MX) {  // (w0' below the coarse digit) << 6 | ext, r[1..]
+                         uint64_t r[NL];
+                         mx_mix<NL>(key, r);
+                         const int xsh = 64 - p.coarse_bits;
+                         rk[i][0] = ((r[0] & ((1ull << xsh) - 1)) << EXT_BITS) | e;
 #pragma unroll
-                       for (int w = 1; w < NL; w++) rk[i][w] = r[w];
-                       inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(r[0] >> xsh) : 0u;
+                         for (int w = 1; w < NL; w++) rk[i][w] = r[w];
+                         inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(r[0] >> xsh) : 0u;
+                       } else {  // the key words, the ext code and the stored hash bits packed into the last word
+                         const uint64_t h = part_hash<NL>(key);
 #pragma unroll
-                       for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[i][w]));
-                       asm volatile("" : "+v"(inf[i]));
-                       return;
-                     }
-                     if constexpr (RecKind<NL, CMP>::M2) {  // (L' below the coarse digit) << 6 | ext, R'
-                       uint64_t L, R;
-                       m2_mix(key, kk, L, R);
-                       rk[i][0] = ((L & m2_cmask) << EXT_BITS) | e;
-                       rk[i][1] = R;
-                       inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(L >> m2_csh) : 0u;
+                         for (int w = 0; w < NL; w++) rk[i][w] = key[w];
+                         if (PACKED) {
+                           rk[i][NL - 1] |= e;
+                           rk[i][NL - 1] |= (((h << p.coarse_bits) >> hsh) & hmask) << EXT_BITS;
+                         }
+                         inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(h >> sh) : 0u;
+                       }
+                       // materialise the record now: otherwise its inputs (key, e, h) are sunk into the
+                       // scatter's conditional store and stay live across its barriers (~7 VGPRs/window)
 #pragma unroll
                        for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[i][w]));
                        asm volatile("" : "+v"(inf[i]));
-                       return;
-                     }
-                     const uint64_t h = window_hash<NL, CMP>(key, kk);
-#pragma unroll
-                     for (int w = 0; w < NL; w++) rk[i][w] = key[w];
-                     if (CMP) {
-                       rk[i][0] = (((h << p.coarse_bits) >> csh) << EXT_BITS) | e;
-                     } else if (PACKED) {
-                       rk[i][NL - 1] |= e;
-                       rk[i][NL - 1] |= (((h << p.coarse_bits) >> hsh) & hmask) << EXT_BITS;
-                     }
-                     inf[i] = valid ? (1u << 31) | (e << 16) | (uint32_t)(h >> sh) : 0u;
-                     // materialise the record now: otherwise its inputs (key, e, h) are sunk into the
-                     // scatter's conditional store and stay live across its barriers (~7 VGPRs/window)
-#pragma unroll
-                     for (int w = 0; w < NL; w++) asm volatile("" : "+v"(rk[i][w]));
-                     asm volatile("" : "+v"(inf[i]));
-                   });
-#ifdef MHMKC_ESTAMP
-  const uint64_t es3 = __builtin_amdgcn_s_memtime();
-#endif
-  const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
-  const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
-  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C40 : (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
-  if (kEStagedNL<NL>())
-    scatter_staged<NL, PACKED, W, SF, ET, kECap<NL>()>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1,
-                                                       p.out, lim, p.ovf);
-  else
-    scatter_regs<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
-#ifdef MHMKC_ESTAMP
-  const uint64_t es4 = __builtin_amdgcn_s_memtime();
-  if ((threadIdx.x & 63) == 0) {  // spread over 64 x 4 words (one address per phase would serialise)
-    unsigned long long *h = p.hist + 4 * ((blockIdx.x * 4 + (threadIdx.x >> 6)) & 63);
-    atomicAdd(&h[0], (unsigned long long)(es1 - es0));
-    atomicAdd(&h[1], (unsigned long long)(es2 - es1));
-    atomicAdd(&h[2], (unsigned long long)(es3 - es2));
-    atomicAdd(&h[3], (unsigned long long)(es4 - es3));
+                     });
   }
-#endif
+  constexpr int SF = RecKind<NL, CMP>::M2 ? SF_AOS2 : SF_WORDS;
+  scatter_staged<NL, PACKED, W, SF, ET, kECap<NL>()>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1,
+                                                     p.out, lim, p.ovf);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1552,7 +1220,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) void k_smer_extract(ExtractParams 
     __syncthreads();
     const uint32_t sub = p.bin_cap ? blockIdx.x % E_NSUB : 0;
     const BinLimit lim{(uint64_t)sub * p.bin_cap, (uint64_t)E_NSUB * p.bin_cap, p.bin_cap};
-    constexpr int SF = (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
+    constexpr int SF = RecKind<NL, CMP>::M2 ? SF_AOS2 : SF_WORDS;
     scatter_staged<NL, PACKED, W, SF, ET>(rk, inf, p.n_bins, smem, smem + staged_cnt_bytes(p.n_bins),
                                           p.cursor + sub * p.n_bins, 1, p.out, lim, p.ovf);
   }
@@ -1659,7 +1327,7 @@ __device__ __forceinline__ void load_chunk(const PlaneSet &src, const SChunk &ch
       rx[j] = (uint32_t)gload(src.ext + idx);
       continue;
     }
-    if (RecKind<NL, CMP>::M2 && kM2Aos) {  // one 16-byte record
+    if (RecKind<NL, CMP>::M2) {  // one 16-byte record
       const u32x4 v = gload4((const uint32_t *)src.w[0] + 4 * idx);
       rk[j][0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
       rk[j][NL - 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
@@ -1715,7 +1383,7 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParam
   if (!xcd_chunk(p, c)) return;  // no chunk left in this workgroup's XCD class (uniform: before any barrier)
   const SChunk ch = chunk_of<T>(p, c);
   const PlaneSet src = p.srcs[ch.src];
-  if constexpr (RecKind<NL, CMP>::C32 && kPStaged && kP32Reg) {
+  if constexpr (RecKind<NL, CMP>::C32) {
     // Compact records as lo / hi registers (the extraction's scatter_staged_c40 with u32 records), loaded from the
     // chunk's planes through 32-bit offsets from its (uniform) start: 32 VGPRs of records instead of 64, and no
     // 64-bit address per load
@@ -1766,11 +1434,8 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParam
     lim = BinLimit{p.coarse_base[ch.coarse_local], fc, fc};
   }
   unsigned long long *cur = p.fine_cursor + (uint64_t)ch.coarse_local * nf;
-  constexpr int SF = RecKind<NL, CMP>::C32 ? SF_C32 : (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
-  if (kPStaged)
-    scatter_staged<NL, PACKED, W, SF, NT>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
-  else
-    scatter_regs<NL, PACKED, W, SF, NT>(rk, inf, nf, smem, cur, 1, p.out, lim, p.err);
+  constexpr int SF = RecKind<NL, CMP>::M2 ? SF_AOS2 : SF_WORDS;
+  scatter_staged<NL, PACKED, W, SF, NT>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
 }
 
 // Distinct-key sketch (HyperLogLog, SKETCH_M registers) over the records of one coarse bucket, from which
@@ -1897,22 +1562,13 @@ __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, uns
 // ------------------------------------------------------------------------------------------------
 // count: LDS open-addressing hash table per fine bucket
 
-// Records per thread per round of k_count (register budget: 1024 threads -> <= 128 VGPRs).
-#ifndef MHMKC_CRPT
-#define MHMKC_CRPT 4
-#endif
-// two-word keys: one record per lane per round (round 4, with the dynamic slots of cold sweeps: fewer records in
-// flight lose fewer claims to each other, phase-B records at k = 63 100M -> 71M; count k = 63 8.92 -> 8.81 ms,
-// k = 33 8.56 -> 8.19 ms)
-#ifndef MHMKC_CRPT2
-#define MHMKC_CRPT2 1
-#endif
-#ifndef MHMKC_CRPT3
-#define MHMKC_CRPT3 1  // three- and four-word keys (was 2: count k = 77 10.49 -> 10.25 ms, k = 99 11.02 -> 10.06 ms)
-#endif
+// Records per thread per round of k_count (register budget: 1024 threads -> <= 128 VGPRs): compact keys 4 (one
+// 16-byte load of four records per lane); two-, three- and four-word keys 1 (round 4: fewer records in flight lose
+// fewer claims to each other, phase-B records at k = 63 100M -> 71M; count k = 63 8.92 -> 8.81 ms, k = 33 8.56 ->
+// 8.19 ms, k = 77 10.49 -> 10.25 ms, k = 99 11.02 -> 10.06 ms)
 template <int NL>
 constexpr int count_rpt() {
-  return NL == 1 ? MHMKC_CRPT : NL == 2 ? MHMKC_CRPT2 : MHMKC_CRPT3;
+  return NL == 1 ? 4 : 1;
 }
 
 // LDS slot hash of k_count. All keys of a fine bucket share their top MurmurHash3 bits, so the slot
@@ -1947,75 +1603,18 @@ struct CountLds {
   int cap;         // multiple of 4: slots are probed in groups of 4
 };
 
-#ifndef MHMKC_BOVERLAP
-#define MHMKC_BOVERLAP 1
-#endif
-constexpr bool B_OVERLAP = MHMKC_BOVERLAP != 0;
-// MHMKC_BOV2=0: two-word keys take the whole miss space for one list (960 entries for 2048 records a round).
-// Before phase-A claims the double-buffered half (480) overflowed in the first rounds of a bucket into
-// in-place inserts that held the round barrier (k = 63: 13.2 -> 12.6 ms with one list); with claims a round
-// lists ~330 records and the overlapped double buffer is faster again (11.90 -> 11.64 ms).
-#ifndef MHMKC_BOV2
-#define MHMKC_BOV2 1
-#endif
-#ifndef MHMKC_BSPREAD
-#define MHMKC_BSPREAD 0
-#endif
-#ifndef MHMKC_WAVEQ
-#define MHMKC_WAVEQ 1
-#endif
-// Per-wave deferral positions and no round barrier in cold sweeps (needs MHMKC_WAVEQ; 0 = dense deferral at the
-// front of the bucket behind a barrier every round)
-#ifndef MHMKC_WDEF
-#define MHMKC_WDEF 1
-#endif
-// Dynamic record slots in cold sweeps (with a spill area, CountParams.spill); 0 = every wave its static share
-#ifndef MHMKC_DYN
-#define MHMKC_DYN 1
-#endif
-constexpr bool kDynSweeps = MHMKC_DYN != 0;
-
-// Two-pass finalize (list the slots with count >= 2, then decide them densely); 0 = one pass over all slots.
-#ifndef MHMKC_FIN2
-#define MHMKC_FIN2 1
-#endif
-// Finalize pass 1 on quads of slots from the counters alone (no key-plane read).
-#ifndef MHMKC_FINQ
-#define MHMKC_FINQ 1
-#endif
-
 // Groups a key may probe before its record is deferred to the next sweep of its bucket.
-#ifndef MHMKC_CPROBE
-#define MHMKC_CPROBE 64
-#endif
-constexpr int C_PROBE = MHMKC_CPROBE;
-// First-group reads a lane keeps in flight in k_count.
-// (two-word keys: one at a time, measured 11.39 -> 11.24 ms at k = 63; their group read is two ds_read_b128)
-#ifndef MHMKC_CBATCH2
-#define MHMKC_CBATCH2 1
-#endif
-#ifndef MHMKC_CBATCH
-#define MHMKC_CBATCH 2
-#endif
-
-// Slots per probe group of k_count's table. A lane's home lookup reads one group with one LDS read: 4 slots = one
-// ds_read_b128 of 32-bit keys (two of 64-bit keys), 2 slots = one ds_read_b64 (one ds_read_b128). Random-address
-// ds_read_b64 runs at 3.5x the lane rate of ds_read_b128 on this part (profiles/r01_lds_microbench.txt: its two
-// 32-lane halves over 64 banks against four 16-lane groups), at the price of more home groups that are full.
-#ifndef MHMKC_GS_C
-#define MHMKC_GS_C 4  // compact (32-bit) keys
-#endif
-#ifndef MHMKC_GS_M2
-#define MHMKC_GS_M2 4  // mixed two-word keys: 2 (one ds_read_b128 of the last words) measured 9.32 -> 9.09 ms at k = 63
-                       // in round 3; with one record per lane per round and full-slice queues 4 is faster (8.18 -> 7.99)
-#endif
-#ifndef MHMKC_GS_MX
-#define MHMKC_GS_MX 4  // mixed three- and four-word keys
-#endif
-template <int NL, bool C32, bool M2, bool MX = false>
-constexpr int group_slots() {
-  return C32 ? MHMKC_GS_C : M2 ? MHMKC_GS_M2 : MX ? MHMKC_GS_MX : 4;
+constexpr int C_PROBE = 64;
+// First-group reads a lane keeps in flight in phase A (two-word keys: one at a time, measured 11.39 -> 11.24 ms at
+// k = 63; their group read is two ds_read_b128).
+template <int NL>
+constexpr int count_batch() {
+  return NL == 2 ? 1 : 2;
 }
+// Slots per probe group of k_count's table: a lane's home lookup reads one group, 4 slots = one ds_read_b128 of
+// 32-bit keys (two of 64-bit keys). Two-slot groups (one ds_read_b64 / b128) measured the same for compact keys and
+// slower for two-, three- and four-word keys with one record per lane per round (§3.3, §4.2).
+constexpr int GS_SLOTS = 4;
 
 // The last key words of one group (4 x u64: two ds_read_b128, the group 32-byte aligned; 2 x u64: one)
 template <int GS>
@@ -2051,15 +1650,6 @@ __device__ __forceinline__ bool rest_equal(const CountLds<K> &t, int slot, const
 // Result of looking at one group for key: >= 0 the slot holding it, -1 - i an empty slot i (and the key is
 // not in the group), G_FULL no empty slot and no key, G_BUSY a multi-word key is being written.
 constexpr int G_FULL = -8, G_BUSY = -9;
-#ifndef MHMKC_EXAM2
-#define MHMKC_EXAM2 1
-#endif
-// Compact keys in a cold sweep take a phase A with all claims in flight together (MHMKC_FASTA=0: the general one).
-#ifndef MHMKC_FASTA
-#define MHMKC_FASTA 1
-#endif
-constexpr bool kFastA = MHMKC_FASTA != 0;
-
 template <int NL, int GS, typename K>
 __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_t *key, int g, const K (&v)[GS]) {
   const K kl = (K)key[NL - 1];
@@ -2071,7 +1661,7 @@ __device__ __forceinline__ int examine_group(const CountLds<K> &t, const uint64_
     for (int i = GS - 1; i >= 0; i--) r = v[i] == kl ? GS * g + i : r;  // the key itself takes precedence
     return r;
   }
-  if constexpr (NL >= 2 && MHMKC_EXAM2) {  // the same on the last word, then one read of the other words
+  if constexpr (NL >= 2) {  // the same on the last word, then one read of the other words
     int r = G_FULL;
 #pragma unroll
     for (int i = GS - 1; i >= 0; i--) r = v[i] == (K)KEY_EMPTY ? -1 - i : r;
@@ -2144,22 +1734,12 @@ __device__ int lds_insert(const CountLds<K> &t, const uint64_t *key, int g, int 
   return -2;
 }
 
-// Phase A claim of the home group's first empty slot for a key the group does not hold (MHMKC_CLAIMA): one CAS
+// Phase A claim of the home group's first empty slot for a key the group does not hold: one CAS
 // instead of a trip through the miss list and phase B, for most new keys (a third of all records at k = 63).
 // Returns the slot, or the verdict unchanged when the CAS lost (the record then goes to the miss list).
 // Sound by lds_insert's argument: the home group had an empty slot, so the key is in no later group, and
 // of the lanes that saw this slot empty exactly one claims it; a single-word key that lost to its own key
 // is counted in the winner's slot, any other loser is resolved by phase B.
-#ifndef MHMKC_CLAIMA
-#define MHMKC_CLAIMA 1
-#endif
-constexpr bool kClaimA = MHMKC_CLAIMA != 0;
-// A full home group looks at the next group in phase A before listing the record: measured slower (k = 63
-// count 11.9 -> 12.5 ms, misses only 137M -> 130M: most misses are claim races, not full groups), so off.
-#ifndef MHMKC_PROBE2
-#define MHMKC_PROBE2 0
-#endif
-constexpr bool kProbe2 = MHMKC_PROBE2 != 0;
 template <int NL, int GS, typename K>
 __device__ __forceinline__ int claim_home(const CountLds<K> &t, const uint64_t *key, int g, int r) {
   K *last = t.keys + (NL - 1) * t.cap;
@@ -2200,50 +1780,22 @@ __device__ __forceinline__ uint32_t lds_add(const CountLds<K> &t, int slot, uint
 // derived at the end, count = left A + C + G + T + left-none, where left-none (a neighbour that is not a
 // countable base) is counted in the count word (< 0xC000 there); a right-none add goes to a dummy word of
 // the wave. slot_count() reads it back; ctg_apply stores an explicit count as 0x80000000 | count.
-#ifndef MHMKC_COLD2
-#define MHMKC_COLD2 1
-#endif
-constexpr bool kCold2 = MHMKC_COLD2 != 0;
+// (Three adds, count and both extensions: 8.24 -> 8.32 ms in round 1; branch-free adds of 0 by every lane
+// that has nothing to count: 4.85 -> 5.04 ms in round 3.)
 template <typename K>
 __device__ __forceinline__ void lds_add_nr(const CountLds<K> &t, int slot, uint32_t e, uint32_t *dummy) {
   const uint32_t l = (e >> 3) & 7u, r = e & 7u;
-  if (kCold2) {
-    uint32_t *lw = l < 4u ? &t.ext[(l >> 1) * t.cap + slot] : &t.cnt[slot];
-    atomicAdd(lw, (l & 1u) ? 0x10000u : 1u);
-    uint32_t *rw = r < 4u ? &t.ext[(2 + (r >> 1)) * t.cap + slot] : dummy;
-    atomicAdd(rw, (r & 1u) ? 0x10000u : 1u);
-    return;
-  }
-  atomicAdd(&t.cnt[slot], 1u);
-  if (l < 4) atomicAdd(&t.ext[(l >> 1) * t.cap + slot], (l & 1) ? 0x10000u : 1u);
-  if (r < 4) atomicAdd(&t.ext[(2 + (r >> 1)) * t.cap + slot], (r & 1) ? 0x10000u : 1u);
-}
-
-// lds_add_nr without branches (the compact cold fast path): word offsets and addends from nibble tables indexed by
-// the ext code, so every lane issues its two adds and a lane with nothing to count adds 0. Left: ext plane l >> 1
-// (offset cap * (1 + (l >> 1)) from the count word) adding 1 or 0x10000, or for a left neighbour that is no
-// countable base the count word itself, adding 1; right: ext plane 2 + (r >> 1) (offset cap * (3 + (r >> 1))), or
-// 0 added to the count word (lds_add_nr's dummy word). Needs t.ext == t.cnt + t.cap.
-#ifndef MHMKC_ADDBF
-#define MHMKC_ADDBF 0  // measured slower: count 4.85 -> 5.04 ms at C2 (LDS adds of 0 by every lane that misses)
-#endif
-template <typename K>
-__device__ __forceinline__ void lds_add_nr_bf(const CountLds<K> &t, int slot, uint32_t e, bool ok) {
-  uint32_t *base = t.cnt + slot;
-  const uint32_t sl = (e >> 1) & 0x1Cu, sr = (e << 2) & 0x1Cu;  // 4 * l, 4 * r
-  const uint32_t fl = __builtin_amdgcn_ubfe(0x02211u, sl, 4), fr = __builtin_amdgcn_ubfe(0x04433u, sr, 4);
-  const uint32_t cr = __builtin_amdgcn_ubfe(0x02121u, sr, 4);  // right: 0 none, 1 low half, 2 high half
-  const uint32_t vl = ok ? __umul24((e >> 3) & 1u, 0xFFFFu) + 1u : 0u;
-  const uint32_t vr = ok ? __umul24(cr >> 1, 0xFFFEu) + cr : 0u;
-  atomicAdd(base + __umul24(fl, (uint32_t)t.cap), vl);
-  atomicAdd(base + __umul24(fr, (uint32_t)t.cap), vr);
+  uint32_t *lw = l < 4u ? &t.ext[(l >> 1) * t.cap + slot] : &t.cnt[slot];
+  atomicAdd(lw, (l & 1u) ? 0x10000u : 1u);
+  uint32_t *rw = r < 4u ? &t.ext[(2 + (r >> 1)) * t.cap + slot] : dummy;
+  atomicAdd(rw, (r & 1u) ? 0x10000u : 1u);
 }
 
 // The count of an occupied slot (see lds_add_nr for the cold-sweep encoding).
 template <typename K>
 __device__ __forceinline__ uint32_t slot_count(const CountLds<K> &t, int slot, bool cold) {
   const uint32_t c = t.cnt[slot];
-  if (!kCold2 || !cold) return c;
+  if (!cold) return c;
   if (c >> 31) return c & 0x7fffffffu;
   const uint32_t e0 = t.ext[slot], e1 = t.ext[t.cap + slot];
   return c + (e0 & 0xffffu) + (e0 >> 16) + (e1 & 0xffffu) + (e1 >> 16);
@@ -2335,7 +1887,7 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
   }
   __syncthreads();
   const uint64_t q0 = s_range[0], q1 = s_range[1];
-  constexpr int GS = group_slots<NL, RecKind<NL, CMP>::C32, RecKind<NL, CMP>::M2, RecKind<NL, CMP>::MX>();
+  constexpr int GS = GS_SLOTS;
   const int ng = t.cap / GS;
   const K *last = t.keys + (NL - 1) * t.cap;
   for (uint64_t q = q0 + tid; q < q1; q += C_THREADS) {
@@ -2395,7 +1947,7 @@ __device__ void ctg_apply(const CountLds<K> &t, const CountParams &p, uint32_t b
         uint32_t ew[4] = {0, 0, 0, 0};
         if (l < 4) ew[l >> 1] |= h << ((l & 1u) * 16);
         if (r < 4) ew[2 + (r >> 1)] |= h << ((r & 1u) * 16);
-        t.cnt[slot] = (kCold2 && cold) ? 0x80000000u | c : c;  // an explicit count (slot_count)
+        t.cnt[slot] = cold ? 0x80000000u | c : c;  // an explicit count (slot_count)
 #pragma unroll
         for (int i = 0; i < 4; i++) t.ext[i * t.cap + slot] = ew[i];
       }
@@ -2439,7 +1991,7 @@ __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, c
     ((uint32_t *)ps.w[0])[idx] = (uint32_t)(key[0] | e);
     return;
   }
-  if (RecKind<NL, CMP>::M2 && kM2Aos) {
+  if (RecKind<NL, CMP>::M2) {
     ((ulonglong2 *)ps.w[0])[idx] = make_ulonglong2(key[0] | e, key[NL - 1]);
     return;
   }
@@ -2449,24 +2001,18 @@ __device__ __forceinline__ void store_record(const PlaneSet &ps, uint64_t idx, c
 }
 
 
-// k_count's thread index. For NL >= MHMKC_COPAQUE_NL it is recomputed through an opaque move at every use, so that
-// nothing derived from it is hoisted out of the bucket loop to live in registers across it: at NL = 4 that took
-// 9 spilled VGPRs to none (127 -> 124) and the count at k = 99 11.79 -> 11.05 ms; at NL = 1-3 it measured 1-3 %
-// slower (the recomputed addresses cost more than the registers they free).
-#ifndef MHMKC_COPAQUE_NL
-#define MHMKC_COPAQUE_NL 4
-#endif
+// k_count's thread index. For four-word keys it is recomputed through an opaque move at every use, so that nothing
+// derived from it is hoisted out of the bucket loop to live in registers across it: that took 9 spilled VGPRs to
+// none (127 -> 124) and the count at k = 99 11.79 -> 11.05 ms; at NL = 1-3 it measured 1-3 % slower (the recomputed
+// addresses cost more than the registers they free).
 __device__ __forceinline__ int count_opaque_tid() {
   int t;
   asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
   return t;
 }
-#ifndef MHMKC_SWID
-#define MHMKC_SWID 1
-#endif
 template <int NL>
 __device__ __forceinline__ int count_tid() {
-  if constexpr (NL >= MHMKC_COPAQUE_NL)
+  if constexpr (NL >= 4)
     return count_opaque_tid();
   else
     return (int)threadIdx.x;
@@ -2491,54 +2037,41 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned long long *s_u64 = (unsigned long long *)(t.ext + 4 * t.cap);
   unsigned long long &s_gbase = s_u64[0];
   unsigned long long *s_red = s_u64 + 1;  // [3]
-  unsigned int *s_nmiss = (unsigned int *)(s_u64 + 14);  // [3] miss-list lengths of rounds r % 3
   unsigned int &s_ovf = *(unsigned int *)(s_u64 + 5);
   unsigned int &s_err = *((unsigned int *)(s_u64 + 5) + 1);
   unsigned int *s_wave = (unsigned int *)(s_u64 + 6);  // [16] per-wave survivor counts, then offsets
-  unsigned int *s_wdef = (unsigned int *)(s_u64 + 16);  // [16] per-wave deferred records of the sweep (WQ)
+  unsigned int *s_wdef = (unsigned int *)(s_u64 + 16);  // [16] per-wave deferred records of the sweep
   unsigned int &s_next = *(unsigned int *)(s_u64 + 24);   // dynamic sweeps: the next record slot to hand out
-  // miss list (phase B of a round) after the largest table this NL can have: keys [NL][MC] | ext [MC]
+  // miss space after the largest table this NL can have: keys [NL][MC] | ext [MC], cut into one miss queue per wave
+  // (MW entries; a shared list worked off by the lowest threads held the other waves at the round barrier, §3.3),
+  // worked off by its own wave once it holds WQ_THR entries, and emptied after the sweep's last round
   constexpr int MC = miss_cap(NL, RK::C32);
-  // B_OVERLAP: phase B of round r overlaps phase A of round r + 1, so the miss list is double-buffered
-  constexpr bool BOV = B_OVERLAP && !(NL == 2 && MHMKC_BOV2 == 0);
-  constexpr int MCL = BOV ? (MC / 2) & ~63 : MC;
-  // MHMKC_WAVEQ: a miss queue per wave (MW entries of the miss space) instead of one shared list, worked off by
-  // its own wave after the round barrier once it holds WQ_THR entries, and emptied after the last round
-  constexpr bool WQ = MHMKC_WAVEQ != 0;
-  constexpr bool WDEF = WQ && MHMKC_WDEF != 0;
   constexpr int MW = MC / (C_THREADS / 64);
-#ifdef MHMKC_WQ_DIV  // (A/B: work the queue off at MW / MHMKC_WQ_DIV entries)
-  constexpr int WQ_THR = MW / MHMKC_WQ_DIV < 64 ? MW / MHMKC_WQ_DIV : 64;
-#else
   // (round 4, with one record per lane per round: a two-word key's queue is worked off when its slice is full, not
-  // half full: k = 63 count 8.27 -> 8.00 ms; three-word keys measured 10.28 -> 11.48 ms that way, four-word the same)
+  // half full: k = 63 count 8.27 -> 8.00 ms; three-word keys measured 10.28 -> 11.48 ms that way, four-word the same;
+  // a quarter of the slice: 5.42 -> 5.62 ms at k = 21)
   constexpr int WQ_THR = NL == 2 ? (MW < 64 ? MW : 64) : (MW / 2 < 64 ? MW / 2 : 64);
-#endif
-  const uint32_t wq_base = (uint32_t)(MHMKC_SWID ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : (threadIdx.x >> 6)) * (uint32_t)MW;
+  const uint32_t wq_base = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * (uint32_t)MW;
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
 
 #define tid (count_tid<NL>())  // (see count_tid; #undef after the kernel)
 #define lane (count_tid<NL>() & 63)
-#if MHMKC_SWID  // the wave index as a scalar (readfirstlane): per-wave queue / deferral / scan-slot addresses in SGPRs
-// (A/B: k = 21 count 4.83 -> 4.78 ms, k = 63 9.05 -> 8.95, k = 99 11.08 -> 11.03)
+// the wave index as a scalar (readfirstlane): per-wave queue / deferral / scan-slot addresses in SGPRs
+// (k = 21 count 4.83 -> 4.78 ms, k = 63 9.05 -> 8.95, k = 99 11.08 -> 11.03)
 #define wid (__builtin_amdgcn_readfirstlane(count_tid<NL>() >> 6))
-#else
-#define wid (count_tid<NL>() >> 6)
-#endif
   const uint64_t low_mask = (1ull << (EXT_BITS + p.hbits)) - 1;
 
   constexpr int R = count_rpt<NL>();
   constexpr uint32_t NONE = 0xffffffffu;
   constexpr uint32_t RND = (uint32_t)R * C_THREADS;
   // see ext_clamp: between two barriers a round's records and at most the miss space's queued records are added
-  constexpr uint32_t HOT = 0xC000u - 2u * (RND + (MHMKC_WAVEQ ? (uint32_t)miss_cap(NL, RecKind<NL, CMP>::C32) : 0u));
+  constexpr uint32_t HOT = 0xC000u - 2u * (RND + (uint32_t)miss_cap(NL, RecKind<NL, CMP>::C32));
   static_assert(HOT > 0x8000u, "round too large for the extension-counter clamp");
-  constexpr int CB0 = NL == 2 ? MHMKC_CBATCH2 : MHMKC_CBATCH;
-  constexpr int C_BATCH = CB0 < R ? CB0 : R;
+  constexpr int C_BATCH = count_batch<NL>() < R ? count_batch<NL>() : R;
   static_assert(R % C_BATCH == 0, "batch must divide the records per round");
-  constexpr int GS = group_slots<NL, RK::C32, RK::M2, RK::MX>();  // slots per probe group
+  constexpr int GS = GS_SLOTS;  // slots per probe group
   const int ng = t.cap / GS;
   const K *last = t.keys + (NL - 1) * t.cap;
   // cmp_group: compact keys from their top stored bits; mixed two-word keys from the low 16 bits of R' (the
@@ -2570,7 +2103,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     const uint64_t o = sr.off;
     if (RK::C32) {
       q.w[0] = (uint64_t *)((uint32_t *)q.w[0] + o);
-    } else if (RK::M2 && kM2Aos) {
+    } else if (RK::M2) {
       q.w[0] += 2 * o;
     } else {
 #pragma unroll
@@ -2601,7 +2134,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       const uint32_t idx = nwv == NONE ? (i < cnt ? i : cnt - 1) : (dbase + (uint32_t)(64 * j + lane) < nwv ? i : 0u);
       if (RK::C32) {
         nk[j][0] = ((const uint32_t *)src.w[0])[idx];
-      } else if (RK::M2 && kM2Aos) {  // one 16-byte record
+      } else if (RK::M2) {  // one 16-byte record
         const u32x4 v = gload4((const uint32_t *)src.w[0] + 4 * (uint64_t)idx);
         nk[j][0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
         nk[j][NL - 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
@@ -2623,11 +2156,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // itself, so its d-th deferral goes to its own d-th record position of the sweep (wave-owned positions in round
   // order: lanes 64 apart for one record per lane, 4 consecutive records per lane for compact quads), which it
   // has already consumed: no other wave reads it, and the waves need no barrier between rounds. The next sweep
-  // reads the first s_wdef[w] positions of every wave w. (Shared list: the dense front of the bucket, behind
-  // the round barrier.)
+  // reads the first s_wdef[w] positions of every wave w.
   auto defer_pos = [&]() -> uint32_t {
-    const uint32_t q = atomicAdd(&s_ovf, 1u);
-    if (!WDEF) return q;
+    (void)atomicAdd(&s_ovf, 1u);
     const uint32_t d = atomicAdd(&s_wdef[wid], 1u), rr = d / (uint32_t)(64 * R), rem = d % (uint32_t)(64 * R);
     return rr * RND + (RK::C32 ? (uint32_t)wid * 256u + rem : rem / 64u * C_THREADS + (uint32_t)wid * 64u + rem % 64u);
   };
@@ -2638,7 +2169,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #endif
   if (tid == 0) {  // (the first sweep's clear ends with a barrier)
     s_missacc = 0;
-    s_u64[3] = 0;  // finalize's counters (MHMKC_FIN2)
+    s_u64[3] = 0;  // finalize's counters
   }
   // this workgroup's spill area (dynamic sweeps: their deferred records; the sweep after reads them from there)
   const Src spill{(uint64_t)blockIdx.x * SPILL_RECORDS, 1u};
@@ -2679,9 +2210,6 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       for (int i = tid; i < n_zeros; i += C_THREADS) zeros[i] = make_uint4(0, 0, 0, 0);
     }
     if (tid == 0) {
-      s_nmiss[0] = 0;
-      s_nmiss[1] = 0;
-      s_nmiss[2] = 0;
       s_ovf = 0;
       s_err = 0;
     }
@@ -2693,11 +2221,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 
     // R records per thread per round, the next round prefetched into registers, so that every CU keeps
     // R * 8 KB of record loads in flight. A round has two phases:
-    //   A. every lane looks its records up in their home group; found keys are counted at once, the
-    //      others (new keys, keys displaced by a full group) are appended to a miss list in LDS;
-    //   B. after a barrier the miss list is worked off densely, one record per lane (probing, CAS insert,
-    //      counting), so the ~20 % of records that need the slow path no longer hold every wave of the
-    //      workgroup in a divergent loop.
+    //   A. every lane looks its records up in their home group; found keys are counted at once, a new key with an
+    //      empty slot in its home group claims it, the others (lost claims, keys displaced by a full group) are
+    //      appended to the wave's miss queue in LDS;
+    //   B. the wave works its queue off densely, one record per lane (probing, CAS insert, counting), once it
+    //      holds WQ_THR entries, so the slow path does not hold every wave in a divergent loop.
     if (!first_sweep && n) prefetch(ps, n, 0, nw, (uint32_t)tid);  // a re-sweep reads the deferred records
     first_sweep = false;
     // a sweep of fewer than 0xC000 records cannot bring a counter to the clamp level: its rounds count
@@ -2706,13 +2234,13 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       constexpr bool COLD = decltype(cold_tag)::value;
       constexpr bool DYN = decltype(dyn_tag)::value;  // dynamic slots (cold sweeps only)
       constexpr uint32_t NWV = C_THREADS / 64;
-      int rnd = 0, lr = 0;           // lr = rnd % 3: the round's miss counter
-      uint32_t wq_n = 0;             // WQ: entries in this wave's miss queue (wave-uniform)
+      int rnd = 0;
+      uint32_t wq_n = 0;  // entries in this wave's miss queue (wave-uniform)
       // DYN: this wave's slot (round cc / NWV, wave slot cc % NWV) and its next one; wave s starts with slots s and
       // NWV + s, every later one comes from s_next (asked for one slot ahead, so the answer is never waited for)
       uint32_t cc = (uint32_t)wid, cn = (uint32_t)wid + NWV;
       auto slot_first = [&](uint32_t c) { return c / NWV * RND + c % NWV * (RK::C32 ? 256u : 64u); };
-      for (uint32_t r0 = 0; DYN ? slot_first(cc) < n : r0 < lim; r0 += RND, rnd++, lr = (lr == 2 ? 0 : lr + 1)) {
+      for (uint32_t r0 = 0; DYN ? slot_first(cc) < n : r0 < lim; r0 += RND, rnd++) {
         STAMP(t_r0);
         uint64_t ck[R][NL];
         uint32_t ce[R];
@@ -2748,23 +2276,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         // (unconditional: in the last round it re-reads this round's records, never used. A load under a branch
         // left its registers to a phi whose copies made hipcc wait for the load right there, vmcnt(0), so the next
         // round's records were fetched with the whole HBM latency exposed every round)
-#ifndef MHMKC_PF_UNCOND
-#define MHMKC_PF_UNCOND 1
-#endif
         if (DYN)  // (unconditional too: past the records it re-reads the last quad / record)
           prefetch(ps, n, cn / NWV * RND, NONE, cn % NWV * 64u + (uint32_t)lane);
-        else if (MHMKC_PF_UNCOND)
+        else
           prefetch(ps, n, r0 + RND < lim ? r0 + RND : r0, nw, (uint32_t)tid);
-        else if (r0 + RND < lim)
-          prefetch(ps, n, r0 + RND, nw, (uint32_t)tid);
-        unsigned int *nmiss = &s_nmiss[lr];
-        K *mkey = s_mkey + (BOV ? (rnd & 1) * NL * MCL : 0);  // this round's miss list
-        uint32_t *me = s_me + (BOV ? (rnd & 1) * MCL : 0);
         // A. home-group lookups: the first groups of all R records are read in batches of C_BATCH (the
         //    reads of a batch in flight together), then found records are counted, missed ones listed.
         uint32_t old[R], defer = 0, okm = 0, missm = 0;
         int slot[R], g[R];
-        if constexpr (RK::C32 && COLD && WQ && kFastA) {
+        if constexpr (RK::C32 && COLD) {
           // compact keys in a cold sweep: the R home groups read back to back and examined, every claim CAS
           // issued before the first one is waited for (the general path below waits for each in turn), then the
           // non-returning adds; misses join the wave queue below. Same verdicts as the general path.
@@ -2780,23 +2300,14 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
           for (int j = 0; j < R; j++) {
             res[j] = 0u;
-            if (kClaimA && ce[j] != NONE && slot[j] < 0 && slot[j] > G_FULL)  // slot -1 - r of the home group was empty: claim it
+            if (ce[j] != NONE && slot[j] < 0 && slot[j] > G_FULL)  // slot -1 - r of the home group was empty: claim it
               res[j] = atomicCAS((unsigned int *)&last[GS * g[j] - 1 - slot[j]], 0xffffffffu, (uint32_t)ck[j][0]);
           }
 #pragma unroll
           for (int j = 0; j < R; j++) {
             old[j] = 0;
             int r = slot[j];
-            if (kClaimA && r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = GS * g[j] - 1 - r;
-            if (MHMKC_ADDBF && kCold2) {  // every lane adds (0 when it has nothing to count): no branch per record
-              const bool valid = ce[j] != NONE, ok = valid && r >= 0;
-              lds_add_nr_bf(t, ok ? r : GS * g[j], ce[j], ok);  // (adds of 0 spread over the home groups: one common
-                                                                // dummy address serialised them, count 4.84 -> 5.07 ms)
-              slot[j] = valid ? r : -3;
-              okm |= (uint32_t)ok << j;
-              missm |= (uint32_t)(valid && r < 0) << j;  // a full home group, or a lost claim
-              continue;
-            }
+            if (r < 0 && r > G_FULL && (res[j] == 0xffffffffu || res[j] == (uint32_t)ck[j][0])) r = GS * g[j] - 1 - r;
             if (ce[j] == NONE) {
               slot[j] = -3;
             } else if (r >= 0) {
@@ -2828,7 +2339,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             continue;
           }
           int r = slot[j];
-          if (kClaimA && r < 0 && r > G_FULL) {  // -1 - i: slot i of the home group was empty
+          if (r < 0 && r > G_FULL) {  // -1 - i: slot i of the home group was empty
             const int sl = GS * g[j] + (-1 - r);
             r = claim_home<NL, GS>(t, ck[j], g[j], r);
             if (NL > 1 && r < 0) {  // lost: the winner may have claimed it for this very key (a lane of this
@@ -2838,41 +2349,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             }
             slot[j] = r;
           }
-          if (kProbe2 && r == G_FULL) {  // a full home group: look at the next one before listing the record
-            const int g2 = (g[j] + 1 == ng) ? 0 : g[j] + 1;
-            K v2[GS];
-            read_group<GS>(last, g2, v2);
-            r = examine_group<NL, GS>(t, ck[j], g2, v2);
-            if (kClaimA && r < 0 && r > G_FULL) {
-              const int sl = GS * g2 + (-1 - r);
-              r = claim_home<NL, GS>(t, ck[j], g2, r);
-              if (NL > 1 && r < 0) {
-                const K v = __hip_atomic_load(&last[sl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (v == (K)ck[j][NL - 1] && rest_equal<NL>(t, sl, ck[j])) r = sl;
-              }
-            }
-            if (r < 0) r = G_FULL;  // phase B probes again from the home group
+          if (r < 0) {  // a full home group, or a lost claim: listed below, in wave-uniform code
+            missm |= 1u << j;
             slot[j] = r;
-          }
-          if (r < 0) {
-            if constexpr (WQ) {  // listed below, in wave-uniform code
-              missm |= 1u << j;
-              slot[j] = r;
-              continue;
-            }
-            const unsigned int q = atomicAdd(nmiss, 1u);
-            if (q < (unsigned int)MCL) {  // handed to phase B
-#pragma unroll
-              for (int w = 0; w < NL; w++) mkey[w * MCL + q] = (K)ck[j][w];
-              me[q] = ce[j];
-              slot[j] = -3;
-              continue;
-            }
-            r = lds_insert<NL, GS>(t, ck[j], g[j], r);  // list full (first rounds of a bucket): in place
-            if (r == -1) defer |= 1u << j;
-            if (r == -2) s_err = 1;
-            slot[j] = r;
-            if (r < 0) continue;
+            continue;
           }
           if (COLD)
             lds_add_nr(t, r, ce[j], &s_wave[wid]);
@@ -2881,9 +2361,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           okm |= 1u << j;
         }
         }  // general phase A
-        if constexpr (WQ) {
+        {
           // this wave's misses join its own queue (ballot + prefix: no LDS atomic); a queue without room for
-          // them inserts in place, as a full shared list did
+          // them inserts in place
 #pragma unroll
           for (int j = 0; j < R; j++) {
             const bool mj = (missm >> j) & 1u;
@@ -2919,12 +2399,10 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           if (!COLD && ((okm >> j) & 1u) && old[j] >= HOT) lds_clamp(t, slot[j], ce[j]);
         STAMP(t_r2);
         STAMP_ADD(2, t_r2 - t_r1);
-        // the next round's counter: its last readers (phase B two rounds back) are behind the previous barrier
-        if (!WQ && BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;
-        // The round barrier. A cold sweep with per-wave queues needs none: no clamp bound to keep (§3.4), every wave
-        // works off its own queue, and deferred records go to positions their own wave has consumed (defer_pos),
-        // so the waves drift apart freely until the sweep's barrier (k = 63 count 10.9 -> 9.2 ms).
-        if (!(COLD && WDEF)) __syncthreads();
+        // The round barrier. A cold sweep needs none: no clamp bound to keep (§3.4), every wave works off its own
+        // queue, and deferred records go to positions their own wave has consumed (defer_pos), so the waves drift
+        // apart freely until the sweep's barrier (k = 63 count 10.9 -> 9.2 ms).
+        if (!COLD) __syncthreads();
         STAMP(t_r3);
         STAMP_ADD(3, t_r3 - t_r2);
         // deferred records go back into the bucket for the next sweep, to positions already consumed (defer_pos)
@@ -2939,7 +2417,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
             }
           }
         }
-        if constexpr (WQ) {
+        {
           // B. this wave's queue, 64 entries at a time once it holds WQ_THR (all of it after the sweep's last
           // round): whole-wave batches, and every wave takes its own share of the slow path, so no wave holds
           // the next barrier with the misses of all the others. The sweep's rounds run while r0 < lim (lim = n
@@ -2985,44 +2463,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
           const uint64_t t_r4w = __builtin_amdgcn_s_memtime();
           STAMP_ADD(4, t_r4w - t_r3);
 #endif
-          continue;
         }
-        // B. the miss list, densely
-        const unsigned int M = min(*nmiss, (unsigned int)MCL);
-        if (tid == 0) s_missacc += M;
-        if (!BOV && tid == 0) s_nmiss[lr == 2 ? 0 : lr + 1] = 0;  // the previous round's list is done
-        // (MHMKC_BSPREAD: list entry q to lane q / 16 of wave q % 16, so every wave takes a share)
-        const unsigned int q0 = MHMKC_BSPREAD ? (unsigned int)(lane * (C_THREADS / 64) + wid) : (unsigned int)tid;
-        for (unsigned int q = q0; q < M; q += C_THREADS) {
-          uint64_t key[NL];
-#pragma unroll
-          for (int w = 0; w < NL; w++) key[w] = mkey[w * MCL + q];
-          const uint32_t e = me[q];
-          const int g = CMP ? cmp_group((uint32_t)key[NL - 1], kshl, (uint32_t)ng)
-                            : (int)__umulhi(slot_hash<NL>(key), (uint32_t)ng);
-          K v[GS];
-          read_group<GS>(last, g, v);
-          const int r = lds_insert<NL, GS>(t, key, g, examine_group<NL, GS>(t, key, g, v));
-          if (r >= 0) {
-            if (COLD)
-              lds_add_nr(t, r, e, &s_wave[wid]);
-            else if (lds_add(t, r, e) >= HOT)
-              lds_clamp(t, r, e);
-          } else if (r == -1) {
-            store_record<NL, PACKED, CMP>(planes_of(ps), defer_pos(), key, e);
-          } else {
-            s_err = 1;
-          }
-        }
-        // Without B_OVERLAP a barrier closes the round. With it, the next round's phase A starts while
-        // other waves still work off this list: its misses go to the other list buffer and counter, and a
-        // lookup that races an insert of phase B at worst misses and is resolved by its own phase B (slots
-        // are only ever claimed, so the deferral rule of lds_insert holds across the two phases).
-        if (!BOV) __syncthreads();
-#if MHMKC_STAMP
-        const uint64_t t_r4 = __builtin_amdgcn_s_memtime();
-        STAMP_ADD(4, t_r4 - t_r3);
-#endif
       }
     };
     // (s_wave holds the dummy words of the cold adds until finalize overwrites it after a barrier)
@@ -3032,7 +2473,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     // `cold` is the table's counter encoding (lds_add_nr / slot_count) of the instantiation that ran.
     // (one- and two-word keys only: with three and four key words the dynamic instantiation spilled 20-40 VGPRs
     // and made k_count 10-22 % slower, against 2 % faster at k = 21 and 63)
-    constexpr bool DYNS = kDynSweeps && WQ && WDEF && NL <= 2;
+    constexpr bool DYNS = NL <= DYN_SWEEP_MAX_NL;
     dyn_sweep = DYNS && has_spill && n < 0xC000u && (dyn_sweep || nw == NONE);
     const bool cold = DYNS ? dyn_sweep : n < 0xC000u;
     if constexpr (DYNS) {
@@ -3053,7 +2494,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
     if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
-    if (MHMKC_PF_UNCOND) {
+    {
       // the next bucket's first round, loaded while this one is finalized; unconditional (as the round prefetch:
       // a load under a branch was waited for at once): without a next bucket, or before a re-sweep (which loads
       // its own first round), it re-reads this bucket's first records, never used (cnt >= 1 keeps the read at
@@ -3062,12 +2503,8 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       if (nxt) bucket_at(nx_base, nx_end, ps_next, nb_next);
       const bool use_next = nxt && nb_next;
       prefetch(use_next ? ps_next : ps, use_next ? nb_next : (n ? n : 1u), 0, NONE, (uint32_t)tid);
-    } else if (last_sweep && b_next < p.n_buckets) {
-      bucket_at(nx_base, nx_end, ps_next, nb_next);
-      if (nb_next) prefetch(ps_next, nb_next, 0, NONE, (uint32_t)tid);
     }
 
-#if MHMKC_FIN2
     // finalize in two passes. 1: occupancy and count of every slot; the slots with count >= 2 (the only ones
     // that can survive) are listed in the miss-list space (free: phase B of the last round ended before the
     // barrier above). 2: the listed slots, dense over the lanes, get get_ext and the X/X purge. (One pass
@@ -3076,7 +2513,6 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     unsigned int *s_fin = (unsigned int *)(s_u64 + 3);  // [0] listed slots, [1] survivors (zeroed between buckets)
     uint32_t occ = 0;
     unsigned long long sum = 0;
-#if MHMKC_FINQ
     // pass 1 over quads of slots: an occupied slot has count >= 1 (every claim is followed by its add; a contig
     // entry's depth is >= 1) and a free one count 0, so the counters alone decide, read four slots at a time
     // (one ds_read_b128 per counter plane, consecutive lanes on consecutive quads: no bank conflicts)
@@ -3088,7 +2524,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       if (4 * qd < t.cap) {
         const uint4 c4 = *(const uint4 *)(t.cnt + 4 * qd);
         c[0] = c4.x, c[1] = c4.y, c[2] = c4.z, c[3] = c4.w;
-        if (kCold2 && cold) {  // slot_count's cold encoding, four at a time
+        if (cold) {  // slot_count's cold encoding, four at a time
           const uint4 a4 = *(const uint4 *)(t.ext + 4 * qd), b4 = *(const uint4 *)(t.ext + t.cap + 4 * qd);
           const uint32_t a[4] = {a4.x, a4.y, a4.z, a4.w}, bb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
@@ -3121,18 +2557,6 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
                 (uint16_t)(4 * qd + i);
       }
     }
-#else
-#pragma unroll
-    for (int j = 0; j < SPT; j++) {
-      const int slot = tid + j * C_THREADS;
-      if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != (K)KEY_EMPTY) {
-        occ++;
-        const uint32_t c32 = slot_count(t, slot, cold);
-        sum += c32;
-        if (c32 >= 2) flist[atomicAdd(&s_fin[0], 1u)] = (uint16_t)slot;
-      }
-    }
-#endif
     __syncthreads();
     const uint32_t n_list = s_fin[0];
     uint32_t surv_mask = 0, spos[SPT];
@@ -3213,88 +2637,6 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         p.out_right[g] = R_[j];
       }
     }
-#else
-    // finalize in one pass: decisions in registers, wave-prefix offsets, one global reservation
-    uint32_t occ = 0, surv_mask = 0;
-    unsigned long long sum = 0;
-    uint16_t c16[SPT];
-    char L[SPT], R_[SPT];
-#pragma unroll
-    for (int j = 0; j < SPT; j++) {
-      const int slot = tid + j * C_THREADS;
-      c16[j] = 0;
-      L[j] = R_[j] = 0;
-      if (slot < t.cap && t.keys[(NL - 1) * t.cap + slot] != (K)KEY_EMPTY) {
-        occ++;
-        const uint32_t c32 = slot_count(t, slot, cold);
-        sum += c32;
-        if (slot_survives(t, slot, p, c32, c16[j], L[j], R_[j])) surv_mask |= 1u << j;
-      }
-    }
-    const uint32_t mine = __popc(surv_mask);
-    uint32_t incl = mine;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += y;
-    }
-    if (lane == 63) s_wave[wid] = incl;
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t acc = 0;
-      for (int w = 0; w < C_THREADS / 64; w++) {
-        const uint32_t c = s_wave[w];
-        s_wave[w] = acc;
-        acc += c;
-      }
-      unsigned long long gb = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
-      if (acc && gb + acc > p.out_cap) {
-        atomicOr(p.err, 16u);
-        gb = ~0ull;
-      }
-      s_gbase = gb;
-      my_out += acc;
-    }
-    __syncthreads();
-    if (s_gbase == ~0ull) surv_mask = 0;
-    unsigned long long g = s_gbase + s_wave[wid] + (incl - mine);
-#pragma unroll
-    for (int j = 0; j < SPT; j++) {
-      if ((surv_mask >> j) & 1u) {
-        const int slot = tid + j * C_THREADS;
-        uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
-        if (RK::C32) {  // key = cunmix(global fine bucket digits | stored bits)
-          const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
-          const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
-          ok[0] = cunmix(y, B) << (64 - B);
-        } else if (RK::M2) {  // key = m2_unmix(global fine bucket digits | stored L' bits, R')
-          const int rb = p.k - p.coarse_bits - p.fine_bits;
-          const uint64_t L = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
-          uint64_t kw[2];
-          m2_unmix(L, t.keys[t.cap + slot], p.k, kw);
-          ok[0] = kw[0];
-          ok[1] = kw[1];
-        } else if (RK::MX) {  // key = mx_unmix(global fine bucket digits | stored w0' bits, r[1..])
-          const int rb = 64 - p.coarse_bits - p.fine_bits;
-          uint64_t r[NL], kw[NL];
-          r[0] = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
-#pragma unroll
-          for (int w = 1; w < NL; w++) r[w] = t.keys[w * t.cap + slot];
-          mx_unmix<NL>(r, kw);
-#pragma unroll
-          for (int w = 0; w < NL; w++) ok[w] = kw[w];
-        } else {
-#pragma unroll
-          for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
-        }
-        for (int w = NL; w < p.nlo; w++) ok[w] = 0;
-        p.out_counts[g] = c16[j];
-        p.out_left[g] = L[j];
-        p.out_right[g] = R_[j];
-        g++;
-      }
-    }
-#endif
     my_occ += occ;
     my_purged += occ;  // minus the survivors, in 64 bits: with two passes a lane's survivors are not its slots
     my_purged -= mine;
@@ -3311,7 +2653,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       ps = pd;
       pd = t_;
       nw = NONE;
-    } else if (WDEF) {  // each wave re-reads its own deferred records; the rounds cover the largest share
+    } else {  // each wave re-reads its own deferred records; the rounds cover the largest share
       nw = s_wdef[wid];
       uint32_t mx = 0;
 #pragma unroll
@@ -3404,10 +2746,9 @@ static hipError_t do_extract_hist(const ExtractParams &p, hipStream_t s) {
 
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
-  constexpr int T = kTile<NL>();
-  const size_t tile_b = tile_lds_bytes<NL>() + (RecKind<NL, CMP>::M2 && kM2Walk ? m2walk_lds_bytes() : 0);
-  const size_t lds = kEStagedNL<NL>() ? staged_cnt_bytes(p.n_bins) + std::max(tile_b, staged_area_bytes(NL, kECap<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS))
-                              : tile_lds_bytes<NL>() + scatter_lds_bytes(p.n_bins);
+  const size_t lds = staged_cnt_bytes(p.n_bins) +
+                     std::max(tile_lds_bytes<NL>(),
+                              staged_area_bytes(NL, kECap<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS));
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
   k_extract_scatter<NL, PK, CMP><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p);
@@ -3426,8 +2767,7 @@ static hipError_t do_part_hist(const PartitionParams &p, hipStream_t s) {
 template <int NL, bool PK, bool CMP = false>
 static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
   const uint32_t nf = 1u << p.fine_bits;
-  const size_t lds = kPStaged ? staged_cnt_bytes(nf) + staged_area_bytes(NL, kPTile<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS)
-                              : scatter_lds_bytes(nf);
+  const size_t lds = staged_cnt_bytes(nf) + staged_area_bytes(NL, kPTile<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS);
   hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
   k_part_scatter<NL, PK, CMP><<<dim3(p.grid), dim3(kPThreads<NL>()), lds, s>>>(p);
@@ -3586,7 +2926,7 @@ hipError_t launch_smer_pack(const SmerParams &p, int nl, hipStream_t s) {
 template <int NL, bool PK, bool CMP, bool HIST>
 static hipError_t do_smer_extract(const ExtractParams &p, const SmerSource &src, hipStream_t s) {
   constexpr int T = kTile<NL>();
-  constexpr int SF = (RecKind<NL, CMP>::M2 && kM2Aos) ? SF_AOS2 : SF_WORDS;
+  constexpr int SF = RecKind<NL, CMP>::M2 ? SF_AOS2 : SF_WORDS;
   const size_t lds = HIST ? (size_t)p.n_bins * 4 : staged_cnt_bytes(p.n_bins) + staged_area_bytes(NL, T, PK, SF);
   hipError_t e = allow_lds(k_smer_extract<NL, PK, CMP, HIST>, lds);
   if (e != hipSuccess) return e;

@@ -215,28 +215,17 @@ constexpr int STAT_ALLOC = 16;
 // k_count's cold sweeps (< 0xC000 records) hand their waves the rounds' record slots dynamically; their deferred
 // records go to a per-workgroup spill area of this many records (and from there back to the bucket's own region)
 constexpr uint32_t SPILL_RECORDS = 0xC000;  // stats[8..13]: k_count phase stamps in MHMKC_STAMP builds
+// ... for keys of at most this many words (with three and four key words the dynamic instantiation spilled 20-40 VGPRs
+// and made k_count 10-22 % slower): the host allocates the spill area only for them
+constexpr int DYN_SWEEP_MAX_NL = 2;
 
-// threads of the extract / partition workgroups (each thread takes tile / E_THREADS windows or records)
-#ifndef MHMKC_ETHREADS
-#define MHMKC_ETHREADS 256
-#endif
-constexpr int E_THREADS = MHMKC_ETHREADS;
-constexpr int E_NSUB = 8;
-#ifndef MHMKC_CPAD
-#define MHMKC_CPAD 1
-#endif
-constexpr uint32_t CPAD = MHMKC_CPAD;  // cursor spacing in u64 words (segment i's cursor at i * CPAD)  // segments per coarse bucket: one per group of blocks sharing an XCD
-// k_count workgroups per CU (persistent): 1 = one 1024-thread workgroup with all 160 KB of LDS; 2 = two of
-// 512 threads with half the LDS each (one can count while the other waits at a barrier)
-#ifndef MHMKC_CSPLIT
-#define MHMKC_CSPLIT 1
-#endif
-constexpr int C_SPLIT = MHMKC_CSPLIT;
-#ifndef MHMKC_CTHREADS
-#define MHMKC_CTHREADS (1024 / MHMKC_CSPLIT)
-#endif
-constexpr int C_THREADS = MHMKC_CTHREADS;
-constexpr size_t C_LDS = 163840 / C_SPLIT;
+// Workgroup shapes (each measured against its neighbours on MI355X).
+constexpr int E_THREADS = 256;  // default threads of the extract / partition workgroups
+constexpr int E_NSUB = 8;       // segments per coarse bucket: one per group of workgroups sharing an XCD
+// k_count: one persistent 1024-thread workgroup per CU with all 160 KB of LDS (two 512-thread workgroups with half
+// the LDS each measured slower once the fine partition's cost is counted, §4.2)
+constexpr int C_THREADS = 1024;
+constexpr size_t C_LDS = 163840;
 
 // Hash bits stored in a packed record next to the ext code (bits [6, 6 + hbits) of the last word).
 inline int stored_hash_bits(int k, int nl, bool packed) {
@@ -245,90 +234,30 @@ inline int stored_hash_bits(int k, int nl, bool packed) {
   return room >= 16 ? 16 : (room >= 8 ? room : 0);
 }
 
-// Bases per extract tile (== records per S chunk) for NL words per key.
-#ifndef MHMKC_TILE1
-#define MHMKC_TILE1 4096
-#endif
-// two-word keys: 4096-base tiles of 16 windows per thread (78 KB of LDS, two workgroups per CU) measured faster
-// than 2048 (k = 63 extract 9.29 -> 8.52 ms, k = 33 10.10 -> 9.68 ms; 512 threads x 4096: 8.84 ms, 512 x 8192:
-// 11.2 ms); three and four words keep 2048 (their records would not fit the registers at 16 per thread)
-#ifndef MHMKC_TILE2
-#define MHMKC_TILE2 4096
-#endif
-// three-word keys: 1536-base tiles, so that the staged 24-byte records of three workgroups fit a CU's LDS (2048: two
-// workgroups, k = 77 extract 14.70 -> 13.05 ms); four-word keys keep 2048 (1536 still leaves two workgroups of
-// 32-byte records: 16.08 -> 19.09 ms; 1024: 16.03)
-#ifndef MHMKC_TILE3
-#define MHMKC_TILE3 1536
-#endif
-#ifndef MHMKC_TILE4
-#define MHMKC_TILE4 2048
-#endif
-inline int tile_bases(int nl) {
-  return nl == 1 ? MHMKC_TILE1 : nl == 2 ? MHMKC_TILE2 : nl == 3 ? MHMKC_TILE3 : MHMKC_TILE4;
-}
-// threads of an extract workgroup (tile_bases / threads windows each)
-#ifndef MHMKC_ETHREADS1
-#define MHMKC_ETHREADS1 E_THREADS
-#endif
-#ifndef MHMKC_ETHREADS2
-#define MHMKC_ETHREADS2 E_THREADS
-#endif
-#ifndef MHMKC_ETHREADS3
-#define MHMKC_ETHREADS3 MHMKC_ETHREADS2  // three-word keys
-#endif
-#ifndef MHMKC_ETHREADS4
-#define MHMKC_ETHREADS4 256  // four-word keys: 2048-base tiles, 8 windows per thread (512 threads: 13.23 -> 12.83 ms before the
-                             // capped stage area; with it 256 threads at 128 VGPRs fit four workgroups: 12.97 -> 10.04 ms)
-#endif
-// records per partition chunk (one E_THREADS workgroup)
-#ifndef MHMKC_PTILE1
-#define MHMKC_PTILE1 4096
-#endif
-#ifndef MHMKC_PTILE2
-#define MHMKC_PTILE2 2048
-#endif
-#ifndef MHMKC_PTILE3
-#define MHMKC_PTILE3 4096  // three-word keys
-#endif
-// partition workgroup threads; three- and four-word keys take longer chunks with more threads (the chunk's runs
-// per fine bucket grow, the LDS per wave stays)
-#ifndef MHMKC_PTHREADS1
-#define MHMKC_PTHREADS1 E_THREADS
-#endif
-#ifndef MHMKC_PTHREADS2
-#define MHMKC_PTHREADS2 E_THREADS
-#endif
-#ifndef MHMKC_PTHREADS3
-#define MHMKC_PTHREADS3 512
-#endif
-#ifndef MHMKC_PTILE4
-#define MHMKC_PTILE4 3072  // four-word keys (LDS: the staged chunk + 2048 bins' counters fit 160 KB)
-#endif
-inline int chunk_records(int nl) {
-  return nl == 1 ? MHMKC_PTILE1 : nl == 2 ? MHMKC_PTILE2 : nl == 3 ? MHMKC_PTILE3 : MHMKC_PTILE4;
-}
-// Mixed two-word records (33 <= k <= 63) as one 16-byte record in the first of their two planes' space, in the
-// coarse slabs and the fine buckets (0: two u64 planes)
-#ifndef MHMKC_M2AOS
-#define MHMKC_M2AOS 1
-#endif
+// Bases per extract tile, by key words. Two-word keys: 4096-base tiles of 16 windows per thread (78 KB of LDS before
+// the capped stage, two workgroups per CU) measured faster than 2048 (k = 63 extract 9.29 -> 8.52 ms). Three-word
+// keys: 1536-base tiles, so that the staged 24-byte records of three workgroups fit a CU's LDS (2048: k = 77 14.70 ->
+// 13.05 ms); four-word keys keep 2048 (1536: 16.08 -> 19.09 ms).
+constexpr int TILE_BASES[5] = {0, 4096, 4096, 1536, 2048};
+inline int tile_bases(int nl) { return TILE_BASES[nl]; }
+// threads of an extract workgroup (tile_bases / threads windows each); four-word keys: 8 windows per thread at 256
+// threads and 128 VGPRs fit four workgroups per CU (512 threads: 13.23 ms, 256: 10.04 ms at k = 99)
+constexpr int E_THREADS_NL[5] = {0, 256, 256, 256, 256};
+// records per partition chunk and threads per partition workgroup; three- and four-word keys take longer chunks over
+// more threads (the chunk's runs per fine bucket grow, the LDS per wave stays; four-word: the staged chunk + 2048
+// bins' counters fit 160 KB)
+constexpr int P_TILE[5] = {0, 4096, 2048, 4096, 3072};
+constexpr int P_THREADS[5] = {0, 256, 256, 512, 512};
+inline int chunk_records(int nl) { return P_TILE[nl]; }
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS); compact records keep
 // 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
-// k_count LDS: table (keys, count, 4 extension words per slot) + 192 B of scalars + the miss list of a
-// round's phase B (key words + ext code per entry); together <= 160 KiB.
-#ifndef MHMKC_CAP2
-#define MHMKC_CAP2 4000
-#endif
-#ifndef MHMKC_CAP3
-#define MHMKC_CAP3 3264
-#endif
-#ifndef MHMKC_CAP4
-#define MHMKC_CAP4 2752
-#endif
+// k_count LDS: table (keys, count, 4 extension words per slot) + 192 B of scalars + the miss queues of the waves
+// (key words + ext code per entry); together <= 160 KiB. Two-word keys: 3800 / 4200 slots measured slower than 4000,
+// three / four-word keys 2880 / 2400 slower than 3264 / 2752 (§4.2).
+constexpr int COUNT_CAP[5] = {0, 5120, 4000, 3264, 2752};
 __host__ __device__ constexpr int count_key_bytes(bool cmp) { return cmp ? 4 : 8; }
 __host__ __device__ constexpr int count_cap(int nl, bool cmp = false) {
-  return ((cmp ? 6144 : nl == 1 ? 5120 : nl == 2 ? MHMKC_CAP2 : nl == 3 ? MHMKC_CAP3 : MHMKC_CAP4) / C_SPLIT) & ~3;
+  return (cmp ? 6144 : COUNT_CAP[nl]) & ~3;
 }
 __host__ __device__ constexpr size_t count_table_bytes(int nl, bool cmp = false) {
   return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 256;  // + k_count's scalars

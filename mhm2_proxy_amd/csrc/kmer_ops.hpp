@@ -77,26 +77,12 @@ MHM_HD uint64_t murmur3_h1(const uint64_t *w) {
   return h1;
 }
 
-#ifndef MHMKC_PART_HASH
-#define MHMKC_PART_HASH 0
-#endif
-// Hash that assigns a k-mer to its rank / coarse bucket / fine bucket. 0: Kmer::hash (MurmurHash3 h1);
-// 1: a two-multiply mixer (the partition is internal: any function gives the same table).
+// Hash that assigns a k-mer of the unmixed record kinds to its rank / coarse bucket / fine bucket: Kmer::hash
+// (MurmurHash3 h1). (A two-multiply mixer saved 1.1 ms of extraction at k = 77 and cost 3.4 ms of partition and
+// counting through its less even digits, §4.2.)
 template <int NL>
 MHM_HD uint64_t part_hash(const uint64_t *w) {
-#if MHMKC_PART_HASH == 0
   return murmur3_h1<NL>(w);
-#else
-  uint64_t h = w[0];
-#pragma unroll
-  for (int i = 1; i < NL; i++) h = (h ^ (h >> 31)) * 0x9E3779B97F4A7C15ull + w[i];
-  h ^= h >> 32;
-  h *= 0xD6E8FEB86659FD93ull;
-  h ^= h >> 32;
-  h *= 0xD6E8FEB86659FD93ull;
-  h ^= h >> 32;
-  return h;
-#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -105,33 +91,14 @@ MHM_HD uint64_t part_hash(const uint64_t *w) {
 // of y) need not be stored: a coarse-bucketed record keeps the low B - cb bits of y next to the ext
 // code (<= 40 bits: a u32 plane + a byte plane), a fine-bucketed record the low B - cb - fb bits
 // (<= 32 bits: one u32 plane), and k_count rebuilds the key as cunmix(bucket digits | stored bits).
-// cmix is fmix64's xorshift-multiply chain over B bits: x ^= x >> s with s >= B/2 is its own inverse
-// on B bits, and an odd multiplier is invertible modulo 2^B.
-constexpr uint64_t CMIX_M1 = 0xff51afd7ed558ccdull, CMIX_M2 = 0xc4ceb9fe1a85ec53ull;
+// cmix is a Feistel network on the two halves of the B key bits (a = B/2 low bits, b = B - a <= 21 high bits; a
+// Feistel round is invertible whatever its round function). The round function takes bits [11, 11 + n) of the low
+// 32 bits of a 24 x 24-bit product: one full-rate v_mul_u32_u24, where fmix64's xorshift-multiply chain needs
+// quarter-rate 64-bit multiplies. Three rounds: the bucket digits are the top bits of the third round's L
+// (L ^ f(R) ^ f(R ^ f(L ^ f(R)))), k_count's home group the bits below them and the top of the second round's R; a
+// fourth round only re-mixed R (two rounds: extraction 4.915 -> 4.913 ms, not worth the weaker digits).
 constexpr int CMP_MIN_K = 10, CMP_MAX_K = 21;
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-constexpr uint64_t inv_odd(uint64_t a) {  // a^-1 mod 2^64 (Newton: the correct low bits double per step)
-  uint64_t x = a;
-  for (int i = 0; i < 6; i++) x *= 2 - a * x;
-  return x;
-}
-constexpr uint64_t CMIX_I1 = inv_odd(CMIX_M1), CMIX_I2 = inv_odd(CMIX_M2);
-
-#ifndef MHMKC_FEISTEL
-#define MHMKC_FEISTEL 1
-#endif
-// MHMKC_FEISTEL (default): a Feistel network on the two halves of the B key bits (a = B/2 low bits, b = B - a <= 21
-// high bits; a Feistel round is invertible whatever its round function). The round function takes bits [11, 11 + n)
-// of the low 32 bits of a 24 x 24-bit product: one full-rate v_mul_u32_u24, where the xorshift-multiply chain over
-// 64 bits needs quarter-rate 64-bit multiplies (extraction is VALU-bound). Three rounds (CMIX_ROUNDS): the bucket
-// digits are the top bits of the third round's L (L ^ f(R) ^ f(R ^ f(L ^ f(R)))), k_count's home group the bits
-// below them and the top of the second round's R; a fourth round only re-mixed R.
-#ifndef MHMKC_CMIX_ROUNDS
-#define MHMKC_CMIX_ROUNDS 3
-#endif
-constexpr uint32_t FEISTEL_K[4] = {0x9E3779u, 0x85EBCAu, 0xC2B2AEu, 0x27D4EBu};
+constexpr uint32_t FEISTEL_K[3] = {0x9E3779u, 0x85EBCAu, 0xC2B2AEu};
 // 24 x 24-bit product, low 32 bits (v_mul_u32_u24, full rate; a plain masked product can come out as the
 // quarter-rate v_mul_lo_u32 when the compiler loses track of the mask). b must be wave-uniform (an SGPR operand:
 // every caller passes a constant).
@@ -151,49 +118,25 @@ MHM_HD void cmix_lr(uint32_t &L, uint32_t &R, int a, int b) {
   L ^= feistel_f(R, FEISTEL_K[0], b);
   R ^= feistel_f(L, FEISTEL_K[1], a);
   L ^= feistel_f(R, FEISTEL_K[2], b);
-  if (MHMKC_CMIX_ROUNDS > 3) R ^= feistel_f(L, FEISTEL_K[3], a);
 }
 MHM_HD void cunmix_lr(uint32_t &L, uint32_t &R, int a, int b) {
-  if (MHMKC_CMIX_ROUNDS > 3) R ^= feistel_f(L, FEISTEL_K[3], a);
   L ^= feistel_f(R, FEISTEL_K[2], b);
   R ^= feistel_f(L, FEISTEL_K[1], a);
   L ^= feistel_f(R, FEISTEL_K[0], b);
 }
 
 MHM_HD uint64_t cmix(uint64_t x, int B) {
-#if MHMKC_FEISTEL
   const int a = B >> 1, b = B - a;
   uint32_t R = (uint32_t)x & ((1u << a) - 1), L = (uint32_t)(x >> a);
   cmix_lr(L, R, a, b);
   return ((uint64_t)L << a) | R;
-#else
-  const uint64_t m = (1ull << B) - 1;
-  const int s = (B + 1) >> 1;
-  x ^= x >> s;
-  x = (x * CMIX_M1) & m;
-  x ^= x >> s;
-  x = (x * CMIX_M2) & m;
-  x ^= x >> s;
-  return x;
-#endif
 }
 
 MHM_HD uint64_t cunmix(uint64_t y, int B) {
-#if MHMKC_FEISTEL
   const int a = B >> 1, b = B - a;
   uint32_t R = (uint32_t)y & ((1u << a) - 1), L = (uint32_t)(y >> a);
   cunmix_lr(L, R, a, b);
   return ((uint64_t)L << a) | R;
-#else
-  const uint64_t m = (1ull << B) - 1;
-  const int s = (B + 1) >> 1;
-  y ^= y >> s;
-  y = (y * CMIX_I2) & m;
-  y ^= y >> s;
-  y = (y * CMIX_I1) & m;
-  y ^= y >> s;
-  return y;
-#endif
 }
 
 // Partition hash of a compact key word (2k bits, left-aligned): the mixed key, left-aligned, so that the
@@ -204,34 +147,19 @@ MHM_HD bool compact_ok(int k, int nl) { return nl == 1 && k >= CMP_MIN_K && k <=
 
 // ------------------------------------------------------------------------------------------------
 // Mixed two-word records (33 <= k <= 63, NL = 2). The 2k key bits are split into halves of
-// k bits, L (bases 0 .. k/2-ish, the top k bits) and R (the low k bits), and put through a 3-round Feistel
+// k bits, L (bases 0 .. k/2-ish, the top k bits) and R (the low k bits), and put through a 2-round Feistel
 // network, (L', R') = m2_mix(key). The coarse and fine digits are the top bits of L', so a record keeps
 //   w[0] = (L' below the digits) << 6 | ext code,   w[1] = R'
 // (16 B, no byte plane, no stored hash bits), and k_count rebuilds the key as m2_unmix(digits | w[0] >> 6, w[1]).
-// The round function is one 64-bit multiply folded onto itself (every output bit depends on every input
-// bit); MurmurHash3 of two words takes eight such multiplies, in extraction and again in the fine partition.
-constexpr uint64_t M2_K[3] = {0x9E3779B97F4A7C15ull, 0xC2B2AE3D27D4EB4Full, 0xD6E8FEB86659FD93ull};
+// The round functions hash their k-bit input to 32 bits with full-rate 24-bit multiplies and xor them into the 32
+// bits that are used downstream: the top 32 bits of L (the bucket digits are the top bits of L'), the low 32 bits
+// of R (k_count's home group is the low 16 bits of R'). A Feistel round is a bijection whatever its round function
+// and wherever it xors, so the other bits may pass unmixed. Two rounds: the digits are top(L) ^ h(R), R (the last
+// ~k/2 bases) being all but unique per k-mer, and the home group is low(R) ^ h(L'); a third round only re-mixed L.
+// (Three rounds of a 64-bit multiply folded onto itself, four quarter-rate VALU ops each, were round 2's first mix.)
 constexpr int M2_MIN_K = 33, M2_MAX_K = 63;
-MHM_HD uint64_t m2_f(uint64_t v, uint64_t c) {
-  const uint64_t p = (v ^ (v >> 31)) * c;
-  return p ^ (p >> 32);
-}
 MHM_HD bool mixed2_ok(int k, int nl) { return nl == 2 && k >= M2_MIN_K && k <= M2_MAX_K; }
-
-// MHMKC_M2FAST (default): the round functions hash their k-bit input to 32 bits with full-rate 24-bit multiplies
-// and xor them into the 32 bits that are used downstream: the top 32 bits of L (the bucket digits are the top
-// bits of L'), the low 32 bits of R (k_count's home group is the low 16 bits of R'). A Feistel round is a
-// bijection whatever its round function and wherever it xors, so the other bits may pass unmixed. Each 64-bit
-// multiply of m2_f is four quarter-rate VALU ops, and extraction at k = 63 is VALU-bound. Two rounds: the digits
-// are top(L) ^ h(R), R (the last ~k/2 bases) being all but unique per k-mer, and the home group is
-// low(R) ^ h(L'); a third round only re-mixed L.
-#ifndef MHMKC_M2FAST
-#define MHMKC_M2FAST 1
-#endif
-#ifndef MHMKC_M2_ROUNDS
-#define MHMKC_M2_ROUNDS 2
-#endif
-constexpr uint32_t M2_C[6] = {0x9E3779u, 0x85EBCBu, 0xC2B2AFu, 0x27D4EBu, 0x165667u, 0x3A2659u};
+constexpr uint32_t M2_C[4] = {0x9E3779u, 0x85EBCBu, 0xC2B2AFu, 0x27D4EBu};
 MHM_HD uint32_t m2_h(uint64_t v, uint32_t c1, uint32_t c2) {  // <= 63-bit v -> 32 bits
   const uint32_t hi = (uint32_t)(v >> 32);
   uint32_t u = (uint32_t)v ^ ((hi << 7) | (hi >> 25));
@@ -245,28 +173,12 @@ MHM_HD uint32_t m2_h(uint64_t v, uint32_t c1, uint32_t c2) {  // <= 63-bit v -> 
 
 // The rounds on the halves: (L, R) -> (L', R'), k bits each, and back.
 MHM_HD void m2_mix_lr(uint64_t &L, uint64_t &R, int k) {
-#if MHMKC_M2FAST
   L ^= (uint64_t)m2_h(R, M2_C[0], M2_C[1]) << (k - 32);
   R ^= (uint64_t)m2_h(L, M2_C[2], M2_C[3]);
-  if (MHMKC_M2_ROUNDS > 2) L ^= (uint64_t)m2_h(R, M2_C[4], M2_C[5]) << (k - 32);
-#else
-  const uint64_t m = (1ull << k) - 1;
-  L ^= m2_f(R, M2_K[0]) & m;
-  R ^= m2_f(L, M2_K[1]) & m;
-  L ^= m2_f(R, M2_K[2]) & m;
-#endif
 }
 MHM_HD void m2_unmix_lr(uint64_t &L, uint64_t &R, int k) {
-#if MHMKC_M2FAST
-  if (MHMKC_M2_ROUNDS > 2) L ^= (uint64_t)m2_h(R, M2_C[4], M2_C[5]) << (k - 32);
   R ^= (uint64_t)m2_h(L, M2_C[2], M2_C[3]);
   L ^= (uint64_t)m2_h(R, M2_C[0], M2_C[1]) << (k - 32);
-#else
-  const uint64_t m = (1ull << k) - 1;
-  L ^= m2_f(R, M2_K[2]) & m;
-  R ^= m2_f(L, M2_K[1]) & m;
-  L ^= m2_f(R, M2_K[0]) & m;
-#endif
 }
 
 // key words (Kmer::longs layout, k bases) -> (L', R'), k bits each

@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include "../../include/mhmkc.h"
+#include "../../include/mhmkc_debug.h"
 #include "kcount_launch.hpp"
 #include "kmer_ops.hpp"
 
@@ -38,6 +39,21 @@ thread_local std::string g_create_error;
 
 // device bytes held by this process's handles (live, and the most at any time): mhmkc_stats.device_bytes[_peak]
 std::atomic<uint64_t> g_dev_live{0}, g_dev_peak{0};
+
+// Test-only switches (include/mhmkc_debug.h, mhmkc_debug_set): they force the rare paths the parity tests check
+// (exact layouts, tiny LDS tables, a full output, a failing file read, ...). Process-wide; none is set in production.
+struct DebugKnobs {
+  int64_t exact = 0;          // exact (histogram) layouts for every slab and finish pass
+  int64_t cap = 0;            // LDS table slots of k_count (0: the kernel's)
+  int64_t fine_bits = -1;     // fine bits (-1: from the sketch)
+  int64_t out_cap = -1;       // output rows the first finish pass allocates (-1: from the sketch)
+  int64_t fq_read_fail = -1;  // mhmkc_add_fastq_file: the read of this block fails
+  int64_t wide_records = 0;   // key-word records instead of the mixed ones (created handles)
+  int64_t smer = 1;           // 0: the minimizer owner at k >= 33 takes the record exchange + hand-off
+  int64_t chunk_bytes = 0;    // H2D chunk of a host batch (0: CHUNK_BYTES)
+  int64_t cb0[4] = {0, 0, 0, 0};  // coarse bits by key words (0: the default)
+};
+DebugKnobs g_dbg;
 
 struct DevBuf {
   void *p = nullptr;
@@ -375,7 +391,7 @@ struct mhmkc {
     if (!sh) return;
     if (compact) {
       ps.w[0] = (uint64_t *)((uint32_t *)ps.w[0] - sh);
-    } else if (mixed2 && MHMKC_M2AOS) {
+    } else if (mixed2) {  // one 16-byte record per entry in the first plane's place
       ps.w[0] -= 2 * sh;
       if (ps.w[1]) ps.w[1] -= sh;
     } else {
@@ -406,20 +422,9 @@ struct mhmkc {
   int qcut_pending = 20;  // quality cutoff of the batch being added (add_seqs encodes quality as case)
 };
 
-// Fine partition target: distinct keys per fine bucket <= FINE_LOAD x LDS table slots.
-// (MHMKC_FINE_LOAD overrides it, for A/B runs.)
-static const double FINE_LOAD = [] {
-  const char *env = getenv("MHMKC_FINE_LOAD");
-  return env && atof(env) > 0 ? atof(env) : 0.7;
-}();
-// Load of the LDS table k_count uses per bucket, after the fine partition is fixed (0 = the whole table, the
-// default: a table fitted to 0.6-0.8 of the estimate was measured slower, 6.28 -> 7.14-10.2 ms at C2, because
-// the home-group hit rate falls with the load faster than the per-slot clear and finalize work does).
-static const double CAP_LOAD = [] {
-  const char *env = getenv("MHMKC_CAP_LOAD");
-  return env ? atof(env) : 0.0;
-}();
-
+// Fine partition target: distinct keys per fine bucket <= FINE_LOAD x LDS table slots (0.5: k = 77 count 10.35 ->
+// 12.42 ms; 0.9: the same fine bits at C2).
+constexpr double FINE_LOAD = 0.7;
 // HyperLogLog estimate (Flajolet et al. 2007) with the linear-counting correction for small counts.
 static double hll_estimate(const std::vector<uint32_t> &reg) {
   const double m = (double)reg.size();
@@ -473,9 +478,8 @@ int mhmkc::extract(Slab *sl, bool exact) {
   if (!sl->recv) {  // (the received supermers' tile index is made once by smer_exchange)
     prof_begin(MHMKC_STAGE_TILEIDX);
     e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
-    // the tiles' read-start bitmaps (MHMKC_TSB=0: load_tile builds them from the offsets)
-    static const bool tsb_on = !(getenv("MHMKC_TSB") && !atoi(getenv("MHMKC_TSB")));
-    if (e == hipSuccess && tsb_on) {
+    // the tiles' read-start bitmaps (k_tile_starts: one dependent global round trip fewer per extraction tile)
+    if (e == hipSuccess) {
       const size_t words = (size_t)sl->tiles * mhm::tile_starts_words(nl);
       if ((e = grow(d_tsb, words * 4 + 64)) == hipSuccess) {
         e = mhm::launch_tile_starts(sl->rv, d_tiles.as<uint32_t>(), d_tsb.as<uint32_t>(), sl->tiles, nl, stream);
@@ -527,23 +531,9 @@ int mhmkc::extract(Slab *sl, bool exact) {
     return hip_fail(e, "cursor H2D");
   p.out = sl->planes;
   prof_begin(MHMKC_STAGE_ESCAT);
-#ifdef MHMKC_ESTAMP
-  (void)hipMemsetAsync(d_hist.p, 0, 2048, stream);
-#endif
   e = sl->recv ? mhm::launch_smer_extract(p, rsrc, nl, packed, false, stream) : mhm::launch_extract_scatter(p, nl, packed, stream);
   prof_end();
   if (e != hipSuccess) return hip_fail(e, "extract_scatter");
-#ifdef MHMKC_ESTAMP
-  {  // diagnostics build: extraction phase cycles summed over waves (k_extract_scatter stamps into hist[0..3])
-    unsigned long long hh[256], h[4] = {0, 0, 0, 0};
-    (void)hipMemcpyAsync(hh, d_hist.p, 2048, hipMemcpyDeviceToHost, stream);
-    (void)hipStreamSynchronize(stream);
-    for (int i = 0; i < 256; i++) h[i & 3] += hh[i];
-    const double t = (double)(h[0] + h[1] + h[2] + h[3]);
-    fprintf(stderr, "extract stamps: tile %.1f%% list %.1f%% walk %.1f%% scatter %.1f%%\n", 100 * h[0] / t,
-            100 * h[1] / t, 100 * h[2] / t, 100 * h[3] / t);
-  }
-#endif
   if ((e = hipMemcpyAsync(hc, dcur, (size_t)nseg * 8 + 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
     return hip_fail(e, "cursor D2H");
   if (!sl->ev && (e = hipEventCreateWithFlags(&sl->ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "slab event");
@@ -585,7 +575,7 @@ int mhmkc::add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known) {
   st.occurrences += wins;
   st.slabs++;
   if (smer) return smer_build(sl);
-  int rc = extract(sl, getenv("MHMKC_DEBUG_EXACT") != nullptr);  // tests force the exact layout
+  int rc = extract(sl, g_dbg.exact != 0);
   return rc ? rc : pump();
 }
 
@@ -641,7 +631,7 @@ int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads
   if (n_reads == 0) return MHMKC_OK;
   if (n_reads >= 0xffffffffull) return fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
   uint64_t chunk = CHUNK_BYTES;
-  if (const char *env = getenv("MHMKC_CHUNK_BYTES")) chunk = std::max<uint64_t>(64, strtoull(env, nullptr, 10));
+  if (g_dbg.chunk_bytes) chunk = std::max<uint64_t>(64, (uint64_t)g_dbg.chunk_bytes);
   hipError_t e;
   Arena *ar = new_arena();
   if ((e = grow(ar->bytes, n_bases + 64)) != hipSuccess || (e = grow(ar->offs, (n_reads + 1) * 8)) != hipSuccess)
@@ -818,7 +808,7 @@ int mhmkc::exchange(std::vector<Source> &srcs) {
   mhm::PlaneSet rps{};
   if ((rc = set_planes(d_recv, recv_total, rps))) return rc;
   // 4. transfers, per peer in slab and plane order on both sides
-  const bool aos = mixed2 && MHMKC_M2AOS;  // one 16-byte record per entry in the first plane's place
+  const bool aos = mixed2;  // one 16-byte record per entry in the first plane's place
   const int np = (compact || aos) ? 1 : nl;
   const size_t wb = compact ? 4 : aos ? 16 : 8;  // bytes of a word-plane entry
   std::vector<Xfer> snd, rcv;
@@ -923,7 +913,7 @@ int mhmkc::xround(Slab *sl, bool done) {
     off += pn.second;
   }
   // 3. transfers, per peer in plane order on both sides (as exchange())
-  const bool aos = mixed2 && MHMKC_M2AOS;
+  const bool aos = mixed2;
   const int np = (compact || aos) ? 1 : nl;
   const size_t wb = compact ? 4 : aos ? 16 : 8;
   std::vector<Xfer> snd, rcv;
@@ -1170,7 +1160,7 @@ int mhmkc::smer_records(uint32_t lo, uint32_t hi, std::vector<Source> &srcs) {
   rs->n = 0;
   rs->bin_lo = lo;
   rs->bin_hi = (lo == 0 && hi == nb) ? 0 : hi;
-  if ((rc = extract(rs, getenv("MHMKC_DEBUG_EXACT") != nullptr))) return rc;
+  if ((rc = extract(rs, g_dbg.exact != 0))) return rc;
   for (int pass = 0; rs->pending; pass++) {
     bool redo = false;
     if ((rc = resolve_one(rs, redo))) return rc;
@@ -1403,7 +1393,13 @@ int mhmkc::finish_passes(uint64_t owned) const {
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 1;
   double need = (double)owned * (double)(compact ? 4 : rec_bytes()) * 1.3;  // capped fine records
   if (smer) need += (double)owned * (double)rec_bytes() * 1.1;              // the received windows' coarse records
-  const double have = 0.8 * (double)fr + (double)d_r2.cap + (smer_slab ? (double)smer_slab->buf.cap : 0.0);
+  // what every pass shares: k_count's spill area, the fine tables of the largest pass (at most 2^11 fine buckets per
+  // coarse bucket, base + cursor + histogram), the output (sized later from the sketch; survivors are a fraction of
+  // the records: 1/24 at C2, 1/16 at C4, budgeted at 1/8)
+  const double fixed = (nl <= mhm::DYN_SWEEP_MAX_NL ? (double)n_cu * mhm::SPILL_RECORDS * (compact ? 4 : rec_bytes()) : 0.0) +
+                       (double)no * 2048.0 * 24.0 + (double)owned / 8.0 * (8.0 * nlo + 4.0);
+  const double have = 0.8 * (double)fr + (double)d_r2.cap + (smer_slab ? (double)smer_slab->buf.cap : 0.0) +
+                      (double)d_spill.cap + (double)d_out_keys.cap - fixed;
   int P = 1;
   while (P < (int)no && need / P > have) P *= 2;
   return std::min<int>(P, (int)std::max(1u, no));
@@ -1497,7 +1493,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
 
   const int T = mhm::chunk_records(nl);  // records per partition chunk
   const uint32_t cap_slots = (uint32_t)mhm::count_cap(nl, compact);
-  bool exact_env = getenv("MHMKC_DEBUG_EXACT") != nullptr;  // tests only
+  const bool exact_dbg = g_dbg.exact != 0;
   uint64_t out_cap = 0, out_used = 0;  // output rows allocated / written by the earlier passes
   unsigned long long acc_stats[mhm::STAT_ALLOC] = {0};
   double est_fine = 0;  // estimated distinct keys per fine bucket (0: no estimate)
@@ -1604,7 +1600,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
         const uint64_t avg_coarse = owned / std::max<uint32_t>(no, 1);
         while (fb < 11 && (avg_coarse >> fb) > (uint64_t)cap_slots * 4) fb++;
       }
-      if (const char *env = getenv("MHMKC_DEBUG_FINE_BITS")) fb = std::min(11, std::max(0, atoi(env)));  // tests only
+      if (g_dbg.fine_bits >= 0) fb = (int)std::min<int64_t>(11, g_dbg.fine_bits);
       fb = std::max(fb, min_fine_bits());
       nf = 1u << fb;
       est_fine /= nf;
@@ -1613,7 +1609,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       // bounds them by the distinct keys, of which half is a generous guess (C2: 52M survivors of 207M distinct)
       out_cap = owned / 2;
       if (est > 0) out_cap = std::min<uint64_t>(out_cap, (uint64_t)(0.5 * est * no) + (1u << 20));
-      if (const char *env = getenv("MHMKC_DEBUG_OUT_CAP")) out_cap = strtoull(env, nullptr, 10);  // tests only
+      if (g_dbg.out_cap >= 0) out_cap = (uint64_t)g_dbg.out_cap;
       out_cap += ctg_n + 1;
       if ((e = grow(d_out_keys, out_cap * 8 * nlo)) != hipSuccess || (e = grow(d_out_counts, out_cap * 2)) != hipSuccess ||
           (e = grow(d_out_left, out_cap)) != hipSuccess || (e = grow(d_out_right, out_cap)) != hipSuccess ||
@@ -1665,19 +1661,14 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     cp.fine_bits = fb;
     cp.bucket0 = (own_lo + c0) << fb;
     cp.n_buckets = n_fine;
-    cp.grid = (uint32_t)std::max(0, n_cu * mhm::C_SPLIT);  // persistent workgroups filling every CU's LDS
+    cp.grid = (uint32_t)std::max(0, n_cu);  // persistent workgroups filling every CU's LDS
     cp.k = k;
     cp.cap = mhm::count_cap(nl, compact);
-    // The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
-    // LDS table (C2: 0.44). The table k_count clears and finalizes per bucket is cut to CAP_LOAD of the estimate
-    // (multiples of 64 slots): both passes cost per slot, not per key.
-    if (est_fine > 0 && CAP_LOAD > 0) {
-      const double want = est_fine / CAP_LOAD;
-      const uint32_t fit = (uint32_t)std::min<double>(cp.cap, std::max(1024.0, std::ceil(want / 64.0) * 64.0));
-      cp.cap = std::min(cp.cap, (int)fit);
-    }
+    // (The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
+    // LDS table, 0.44 at C2; a table cut to 0.6-0.8 of the estimate was measured slower, 6.28 -> 7.14-10.2 ms: the
+    // home-group hit rate falls faster than the per-slot clear and finalize work.)
     st.table_slots = (uint64_t)cp.cap;
-    if (const char *env = getenv("MHMKC_DEBUG_CAP")) cp.cap = std::min(cp.cap, std::max(64, atoi(env)) & ~3);  // tests only
+    if (g_dbg.cap) cp.cap = std::min<int>(cp.cap, (int)std::max<int64_t>(64, g_dbg.cap) & ~3);
     cp.dmin_thres = dmin;
     cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
     cp.nlo = nlo;
@@ -1690,11 +1681,11 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     cp.ctg_bucket = d_ctg_bucket.as<uint32_t>();
     cp.ctg_done = d_ctg_done.as<uint8_t>();
     cp.ctg_base = c0 << fb;
-    if (cp.grid) {  // (MHMKC_DYN builds: dynamic cold sweeps defer into it)
+    if (cp.grid && nl <= mhm::DYN_SWEEP_MAX_NL) {  // dynamic cold sweeps defer into it (one- and two-word keys)
       if ((rc = set_planes(d_spill, (uint64_t)cp.grid * mhm::SPILL_RECORDS, cp.spill, true))) return rc;
     }
 
-    bool exact = exact_env;
+    bool exact = exact_dbg;
     unsigned long long stats[mhm::STAT_ALLOC], cursor_end = 0;
     for (int attempt = 0;; attempt++) {
       if (attempt >= 4) return fail(MHMKC_EHIP, "internal: finish pass %d did not settle", pass);
@@ -1783,7 +1774,8 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   finished = true;
   if (errf & 1u) return fail(MHMKC_EBADCHAR, "input byte with a base code > 4 (not A,C,G,T,N)");
   if (errf & 8u) return fail(MHMKC_EHIP, "internal: supermer spans inconsistent");
-  if (getenv("MHMKC_PRINT_STAMPS")) {  // k_count phase cycles of an MHMKC_STAMP build (diagnostics)
+#if MHMKC_STAMP
+  {  // k_count phase cycles of an MHMKC_STAMP build (diagnostics)
     const char *names[6] = {"clear", "loadwait", "insert", "barrier", "overflow", "finalize"};
     double tot = 0;
     for (int i = 0; i < 6; i++) tot += (double)acc_stats[8 + i];
@@ -1791,6 +1783,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f%%", names[i], tot > 0 ? 100.0 * acc_stats[8 + i] / tot : 0.0);
     fprintf(stderr, " (total %.3g wave-cycles)\n", tot);
   }
+#endif
   st.distinct = acc_stats[mhm::STAT_DISTINCT];
   st.n_out = acc_stats[mhm::STAT_NOUT];
   st.purged = acc_stats[mhm::STAT_PURGED];
@@ -1966,20 +1959,17 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   h->hbits = mhm::stored_hash_bits(k, nl, h->packed);
   // supermer exchange: the reference's owner (MHMKC_OWNER_MINIMIZER) with keys of two or more
   // words is reached by shipping supermers, each rank then counting all of its k-mers over the whole hash range;
-  // MHMKC_SMER=0 keeps the record exchange + hand-off (A/B, tests)
-  const char *smer_env = getenv("MHMKC_SMER");
-  h->smer = cfg->output_owner == MHMKC_OWNER_MINIMIZER && cfg->n_ranks > 1 && nl >= 2 && !(smer_env && !atoi(smer_env));
+  // (the test knob smer = 0 keeps the record exchange + hand-off)
+  h->smer = cfg->output_owner == MHMKC_OWNER_MINIMIZER && cfg->n_ranks > 1 && nl >= 2 && g_dbg.smer != 0;
   int extra = 0;
   while ((1 << extra) < cfg->n_ranks && extra < 3) extra++;
   if (h->smer) extra = 0;
   // coarse bits by key words: three- and four-word keys take 128 coarse buckets (half the extraction's cursor atomics
   // per record and runs twice as long at ~0.5 records per base; k = 99 38.9 -> 34.8 ms per C2 step, k = 77 31.4 -> 31.0).
-  // MHMKC_CB0 / MHMKC_CB0_2 / MHMKC_CB0_3 override them for A/B runs, checked below.
-  auto cb_env = [](const char *name, int dflt) {
-    const char *v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-  };
-  const int cb0 = nl >= 3 ? cb_env("MHMKC_CB0_3", 7) : nl == 2 ? cb_env("MHMKC_CB0_2", 8) : cb_env("MHMKC_CB0", 8);
+  // (7 coarse bits for two-word keys: k = 63 23.00 -> 23.31 ms.) The test knobs cb0 / cb0_2 / cb0_3 override them,
+  // checked below.
+  const int cb_knob = (int)g_dbg.cb0[nl >= 3 ? 3 : nl];
+  const int cb0 = cb_knob ? cb_knob : nl >= 3 ? 7 : 8;
   // A mixed record keeps the key bits below the coarse digit, shifted up by the 6-bit ext code, in its first 64-bit
   // word: three/four-word keys (64 bits of w0') need cb >= 7 (at cb = 6 with no fine bits the mask shift reaches 64
   // and a key bit is lost: a wrong table, not an error), two-word keys (k bits of L') cb >= k - 58. The coarse
@@ -1993,19 +1983,18 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
     return MHMKC_EUNSUPPORTED;
   }
   h->cb = cb0 + extra;
-  // compact records for 10 <= k <= 21 (MHMKC_WIDE_RECORDS=1 keeps the 8-byte records: A/B and tests)
-  const char *wide = getenv("MHMKC_WIDE_RECORDS");
-  h->compact = mhm::compact_ok(k, nl) && 2 * k - h->cb <= 34 && !(wide && atoi(wide));
+  // compact records for 10 <= k <= 21 (the test knob wide_records keeps the key-word records: the tests compare both)
+  const bool wide = g_dbg.wide_records != 0;
+  h->compact = mhm::compact_ok(k, nl) && 2 * k - h->cb <= 34 && !wide;
   if (h->compact) h->hbits = 0;
   // mixed two-word records for 33 <= k <= 63 (the same switch keeps the plain key words)
-  h->mixed2 = mhm::mixed2_ok(k, nl) && !(wide && atoi(wide));
+  h->mixed2 = mhm::mixed2_ok(k, nl) && !wide;
   if (h->mixed2) {
     h->packed = true;  // the ext code sits in w[0]
     h->hbits = 0;
   }
-  // mixed three- and four-word records for 64 < k < 128 (MHMKC_MIXED3=0: the key words + stored MurmurHash3 bits)
-  const char *mx_env = getenv("MHMKC_MIXED3");
-  h->mixed3 = mhm::mixed3_ok(k, nl) && !(wide && atoi(wide)) && !(mx_env && !atoi(mx_env));
+  // mixed three- and four-word records for 64 < k < 128
+  h->mixed3 = mhm::mixed3_ok(k, nl) && !wide;
   if (h->mixed3) {
     h->packed = true;  // the ext code sits in w[0]
     h->hbits = 0;
@@ -2285,15 +2274,6 @@ int mhmkc::add_fastq(const char *d_text, uint64_t n, bool pairs, uint64_t *consu
         (e = hipMemcpyAsync(hs, fst, 32, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipStreamSynchronize(stream)) != hipSuccess)
       return hip_fail(e, "fastq merge D2H");
-    if (getenv("MHMKC_PRINT_STAMPS")) {  // k_fq_merge phase cycles of an MHMKC_MGSTAMP build (diagnostics)
-      unsigned long long ms[6] = {0, 0, 0, 0, 0, 0};
-      if (hipMemcpy(ms, fst + 4, sizeof ms, hipMemcpyDeviceToHost) == hipSuccess && (ms[0] | ms[1] | ms[2] | ms[3])) {
-        const double t = (double)(ms[0] + ms[3]), tail = (double)ms[3] - (double)ms[1] - (double)ms[2];
-        fprintf(stderr, "k_fq_merge stamps: stage %.1f%% filter %.1f%% scans %.1f%% tail %.1f%% (%.0f cycles/pair); "
-                "%.2f scans and %.2f filter rounds per pair\n", 100 * ms[0] / t, 100 * ms[1] / t, 100 * ms[2] / t,
-                100 * tail / t, t / std::max<double>(1, P), ms[4] / std::max<double>(1, P), ms[5] / std::max<double>(1, P));
-      }
-    }
     st.fq_pairs = P;
     st.fq_merged = hs[1];
     st.fq_ambiguous = hs[2];
@@ -2412,9 +2392,8 @@ static int add_fastq_file(mhmkc_t h, const char *path, bool pairs) {
   }
   char *buf[2] = {h->fq_file_buf.as<char>(), h->fq_file_buf.as<char>() + slot};
   bool added = false;  // some block's reads are in the round (a later failure leaves the round partial)
-  // tests only: the read of block MHMKC_DEBUG_FQ_READ_FAIL fails (a file that shrinks or turns unreadable mid-call)
-  const char *fail_env = getenv("MHMKC_DEBUG_FQ_READ_FAIL");
-  const uint64_t fail_block = fail_env && *fail_env ? strtoull(fail_env, nullptr, 10) : ~0ull;
+  // tests only: the read of block fq_read_fail fails (a file that shrinks or turns unreadable mid-call)
+  const uint64_t fail_block = g_dbg.fq_read_fail >= 0 ? (uint64_t)g_dbg.fq_read_fail : ~0ull;
   // block i's data: file bytes [i * block, min(size, (i + 1) * block)), read in parallel pieces
   auto read_block = [&](uint64_t i, char *dst) -> bool {
     if (i == fail_block) return false;
@@ -2804,5 +2783,25 @@ int mhmkc_set_profiling(mhmkc_t h, int on) {
 }
 
 const char *mhmkc_last_error(mhmkc_t h) { return h ? h->err.c_str() : g_create_error.c_str(); }
+
+int mhmkc_debug_set(const char *knob, int64_t value) {
+  if (!knob) return MHMKC_EINVAL;
+  const std::string k = knob;
+  if (k == "exact") g_dbg.exact = value;
+  else if (k == "cap") g_dbg.cap = value;
+  else if (k == "fine_bits") g_dbg.fine_bits = value;
+  else if (k == "out_cap") g_dbg.out_cap = value;
+  else if (k == "fq_read_fail") g_dbg.fq_read_fail = value;
+  else if (k == "wide_records") g_dbg.wide_records = value;
+  else if (k == "smer") g_dbg.smer = value;
+  else if (k == "chunk_bytes") g_dbg.chunk_bytes = value;
+  else if (k == "cb0") g_dbg.cb0[1] = value;
+  else if (k == "cb0_2") g_dbg.cb0[2] = value;
+  else if (k == "cb0_3") g_dbg.cb0[3] = value;
+  else return MHMKC_EINVAL;
+  return MHMKC_OK;
+}
+
+void mhmkc_debug_reset(void) { g_dbg = DebugKnobs(); }
 
 }  // extern "C"

@@ -422,9 +422,13 @@ class KmerCounter:
             raise RuntimeError("fetch before finish")
         n = self.n_out
         if out is not None:
-            if (len(out) < n or out.keys.shape[1] != self.n_longs or out.keys.dtype != np.uint64
+            # (the native copy writes n * 8 * n_longs, n * 2, n and n bytes: the dtypes must be those widths)
+            if (len(out) < n or out.keys.ndim != 2 or out.keys.shape[1] != self.n_longs or out.keys.dtype != np.uint64
+                    or out.counts.dtype != np.uint16 or out.left.dtype.itemsize != 1 or out.right.dtype.itemsize != 1
+                    or min(len(out.counts), len(out.left), len(out.right)) < n
                     or not all(a.flags.c_contiguous for a in (out.keys, out.counts, out.left, out.right))):
-                raise ValueError("out: contiguous arrays of at least n_out rows with n_longs key words")
+                raise ValueError("out: contiguous arrays of at least n_out rows: keys uint64 [n, n_longs], counts "
+                                 "uint16, left / right one byte per row")
             keys, counts, left, right = out.keys[:n], out.counts[:n], out.left[:n], out.right[:n]
         else:
             keys = np.empty((n, self.n_longs), dtype=np.uint64)

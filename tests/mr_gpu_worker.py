@@ -36,10 +36,10 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     from common import ctg_set, synth_set
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    for key, val in opts.get("env", {}).items():
-        os.environ[key] = val
-    for key, val in opts.get("env_by_rank", {}).get(rank, {}).items():
-        os.environ[key] = val
+    from conftest import apply_env
+
+    apply_env(opts.get("env", {}))
+    apply_env(opts.get("env_by_rank", {}).get(rank, {}))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if opts.get("contigs"):
         b, o, seqs, depths = ctg_set(seed=opts["seed"], n_reads=opts.get("n_reads", 300))

@@ -22,6 +22,7 @@ def declared(header: Path) -> list:
 def test_headers_match_binding_lists():
     assert declared(ROOT / "include" / "mhmkc.h") == sorted(N.ABI_SYMBOLS)
     assert declared(ROOT / "include" / "mhmkc_synth.h") == sorted(N.SYNTH_SYMBOLS)
+    assert declared(ROOT / "include" / "mhmkc_debug.h") == sorted(N.DEBUG_SYMBOLS)
 
 
 def test_lib_exports_every_declared_symbol():
@@ -29,9 +30,10 @@ def test_lib_exports_every_declared_symbol():
 
     build.build_lib()  # hipcc cross-compiles gfx950 here without a GPU
     lib = N.lib()
-    for name in declared(ROOT / "include" / "mhmkc.h"):
+    for name in declared(ROOT / "include" / "mhmkc.h") + declared(ROOT / "include" / "mhmkc_debug.h"):
         assert hasattr(lib, name), name
     assert lib.mhmkc_abi_version() == 12
+    assert lib.mhmkc_debug_set(b"no_such_knob", 1) == -1
 
 
 def test_synth_exports_every_declared_symbol():
@@ -146,12 +148,12 @@ def test_map_hash_matches_the_adapter():
     assert got == [map_hash([0x1B1B1B1B1B000000]), map_hash([1, 0x1B1B1B1B1B000000, 2**64 - 1])]
 
 
-@pytest.mark.parametrize("k,env,value", [(77, "MHMKC_CB0_3", "6"), (99, "MHMKC_CB0_3", "5"), (63, "MHMKC_CB0_2", "4"),
-                                         (21, "MHMKC_CB0", "12"), (99, "MHMKC_CB0_3", "12")])
-def test_create_rejects_coarse_bits(k, env, value, monkeypatch):
+@pytest.mark.parametrize("k,name,value", [(77, "cb0_3", 6), (99, "cb0_3", 5), (63, "cb0_2", 4), (21, "cb0", 12),
+                                          (99, "cb0_3", 12)])
+def test_create_rejects_coarse_bits(k, name, value, knob):
     """VERDICT r3 (weak 10): a coarse-bit count the mixed records cannot hold (three/four-word keys need >= 7, two-word
     keys k - 58; at most 11 bins' bits) is refused at create time, not counted into a wrong table."""
-    monkeypatch.setenv(env, value)
+    knob(name, value)
     cfg = N.MhmkcConfig()
     N.lib().mhmkc_config_init(C.byref(cfg))
     cfg.k = k

@@ -125,9 +125,9 @@ def test_gpu_fastq_file_errors(tmp_path, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fail_block", [1, 2])
-def test_gpu_fastq_file_read_failure_after_first_block(tmp_path, monkeypatch, fail_block):
+def test_gpu_fastq_file_read_failure_after_first_block(tmp_path, monkeypatch, fail_block, knob):
     """the background read of a later block fails (a file that shrinks or turns unreadable mid-call,
-    injected with MHMKC_DEBUG_FQ_READ_FAIL): the earlier blocks' reads are already in the round, so the call fails
+    injected with the test knob fq_read_fail): the earlier blocks' reads are already in the round, so the call fails
     with MHMKC_EINVAL and finish refuses the round (MHMKC_ESTATE) until reset."""
     import mhm2_proxy_amd as m
     b, o = c.synth_set(400, 20000, 38)
@@ -135,7 +135,7 @@ def test_gpu_fastq_file_read_failure_after_first_block(tmp_path, monkeypatch, fa
     path = _write(tmp_path, "reads.fq", t)
     monkeypatch.setenv("MHMKC_FQ_BLOCK", "5000")
     assert len(t) > 4 * 5000
-    monkeypatch.setenv("MHMKC_DEBUG_FQ_READ_FAIL", str(fail_block))
+    knob("fq_read_fail", fail_block)
     with m.KmerCounter(21, device=0) as cnt:
         with pytest.raises(m.MhmkcError) as e:
             cnt.add_fastq_file(path)
@@ -143,7 +143,7 @@ def test_gpu_fastq_file_read_failure_after_first_block(tmp_path, monkeypatch, fa
         with pytest.raises(m.MhmkcError) as e2:
             cnt.finish()
         assert str(e2.value).startswith("MHMKC_ESTATE"), str(e2.value)
-        monkeypatch.delenv("MHMKC_DEBUG_FQ_READ_FAIL")
+        knob("fq_read_fail", -1)
         cnt.reset()
         cnt.add_fastq_file(path)
         cnt.finish()

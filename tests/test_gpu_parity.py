@@ -70,11 +70,11 @@ def test_hot_kmer_saturation(k):
 
 
 @pytest.mark.parametrize("k", [21, 63, 99])
-def test_exact_partition_path(k, monkeypatch):
+def test_exact_partition_path(k, knob):
     """The histogram-sized (exact) partition path, forced for ordinary input."""
     b, o = synth_set(2500, 12000, 17 + k)
     exp = oracle_table(b, o, k)
-    monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+    knob("exact", 1)
     got, st = hip_table(b, o, k)
     assert_tables_equal(got, exp, "exact path")
     check_stats(st)
@@ -98,15 +98,15 @@ def test_batches_equal_single(k):
 
 
 @pytest.mark.parametrize("k,wide", [(21, True), (15, False), (17, False), (63, False), (77, False), (99, False)])
-def test_forced_overflow_sweeps(k, wide, monkeypatch):
+def test_forced_overflow_sweeps(k, wide, knob):
     """Tiny LDS tables force the multi-sweep path (a closed table overflows whole keys to the next sweep).
     Compact records (k <= 21) need >= 2k - 34 fine bits, so k = 15, 17 cover them with one fine bucket."""
     b, o = synth_set(3000, 50000, 13)
     exp = oracle_table(b, o, k)
-    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
-    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    knob("cap", 64)
+    knob("fine_bits", 0)
     if wide:
-        monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
+        knob("wide_records", 1)
     got, st = hip_table(b, o, k)
     assert st["overflow_sweeps"] > 0
     assert_tables_equal(got, exp, "forced overflow")
@@ -114,17 +114,17 @@ def test_forced_overflow_sweeps(k, wide, monkeypatch):
 
 
 @pytest.mark.parametrize("k,wide", [(15, False), (21, True), (63, False), (77, False)])
-def test_forced_overflow_hot_sweep(k, wide, monkeypatch):
+def test_forced_overflow_hot_sweep(k, wide, knob):
     """A hot first sweep (>= 0xC000 records: the checked round loop with its round barrier and clamp) that
     overflows a 64-slot table: the poly-A k-mer's bucket also holds ~100-200 distinct keys of the random reads,
     so keys are deferred with the per-wave defer positions, then counted by a re-sweep with its own round bound
     (no earlier test overflowed a non-cold sweep)."""
     b, o = hot_set()
     exp = oracle_table(b, o, k)
-    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
-    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    knob("cap", 64)
+    knob("fine_bits", 0)
     if wide:
-        monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
+        knob("wide_records", 1)
     got, st = hip_table(b, o, k)
     assert st["max_bucket"] >= 0xC000, st["max_bucket"]
     assert st["overflow_sweeps"] > 0
@@ -266,22 +266,22 @@ def test_contig_pass_order_kept_across_calls():
 
 
 @pytest.mark.parametrize("k,wide", [(21, True), (17, False), (63, False)])
-def test_contig_pass_with_overflow_sweeps(k, wide, monkeypatch):
+def test_contig_pass_with_overflow_sweeps(k, wide, knob):
     """Tiny LDS tables: read entries are spread over several sweeps of a bucket; a contig k-mer must meet
     its read entry in whichever sweep holds it, and only count as contig-only after the last sweep."""
     b, o, seqs, depths = ctg_set(seed=91, n_reads=600)
-    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
-    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    knob("cap", 64)
+    knob("fine_bits", 0)
     if wide:
-        monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
+        knob("wide_records", 1)
     got, st = ctg_table(b, o, seqs, depths, k)
     assert st["overflow_sweeps"] > 0
     assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, k), "contigs + overflow sweeps")
 
 
-def test_contig_pass_exact_partition(monkeypatch):
+def test_contig_pass_exact_partition(knob):
     b, o, seqs, depths = ctg_set(seed=92)
-    monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+    knob("exact", 1)
     got, _ = ctg_table(b, o, seqs, depths, 33)
     assert_tables_equal(got, oracle_ctg_table(b, o, seqs, depths, 33), "contigs, exact partition")
 
@@ -306,13 +306,13 @@ def test_analyze_kmers_with_contigs():
 
 
 @pytest.mark.parametrize("k", [21, 19])
-def test_compact_overflow_at_min_fine_bits(k, monkeypatch):
+def test_compact_overflow_at_min_fine_bits(k, knob):
     """Compact records at their smallest fine partition (2k - 34 fine bits at k = 21): ~120 distinct
     k-mers per fine bucket against 64-slot tables, so most buckets need several sweeps."""
     b, o = synth_set(60000, 4_000_000, 23)
     exp = oracle_table(b, o, k)
-    monkeypatch.setenv("MHMKC_DEBUG_CAP", "64")
-    monkeypatch.setenv("MHMKC_DEBUG_FINE_BITS", "0")
+    knob("cap", 64)
+    knob("fine_bits", 0)
     got, st = hip_table(b, o, k)
     assert st["overflow_sweeps"] > 0
     assert_tables_equal(got, exp, "compact overflow")
@@ -320,17 +320,17 @@ def test_compact_overflow_at_min_fine_bits(k, monkeypatch):
 
 
 @pytest.mark.parametrize("k", [21, 12, 33, 47, 63, 65, 77, 95, 99, 127])
-def test_compact_equals_wide_records(k, monkeypatch):
+def test_compact_equals_wide_records(k, knob):
     """The mixed record layouts (compact 4/5-byte at k <= 21, two-word m2_mix at 33 <= k <= 63, three- and four-word
     mx_mix at 64 < k < 128; the key rebuilt from the bucket digits) and the plain key-word records give the same
     table, through the capped and the exact partition paths."""
     b, o = synth_set(20000, 300000, 31)
     cmp_t, st_c = hip_table(b, o, k)
-    monkeypatch.setenv("MHMKC_WIDE_RECORDS", "1")
+    knob("wide_records", 1)
     wide_t, st_w = hip_table(b, o, k)
     assert_tables_equal(cmp_t, wide_t, "compact vs wide")
-    monkeypatch.delenv("MHMKC_WIDE_RECORDS")
-    monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+    knob("wide_records", 0)
+    knob("exact", 1)
     exact_t, _ = hip_table(b, o, k)
     assert_tables_equal(exact_t, wide_t, "compact exact vs wide")
     for key in ("distinct", "n_out", "purged", "count_sum"):
@@ -350,11 +350,11 @@ def test_distinct_sketch_estimate(k):
 
 
 @pytest.mark.parametrize("k,chunk", [(21, 700), (63, 1000), (33, 100000)])
-def test_host_chunks_equal_oracle(k, chunk, monkeypatch):
+def test_host_chunks_equal_oracle(k, chunk, knob):
     """mhmkc_add_reads copies a host batch in chunks of whole reads, each extracted as a slice view (an aligned
     byte base plus a head offset) as soon as it lands: ragged reads (empty, shorter than k, N runs, poly-A)
     over many chunk boundaries give the oracle's table."""
-    monkeypatch.setenv("MHMKC_CHUNK_BYTES", str(chunk))
+    knob("chunk_bytes", chunk)
     b, o = edge_case_set(seed=17 + k)
     with m.KmerCounter(k) as c:
         c.add_packed_reads(b, o)
@@ -413,12 +413,12 @@ def _hot_key_last_bucket(k: int) -> str:
     rng = np.random.default_rng(k)
     nl = k // 32 + 1
     B = 2 * k
-    FK = (0x9E3779, 0x85EBCA, 0xC2B2AE, 0x27D4EB)  # kmer_ops.hpp cunmix (Feistel, MHMKC_FEISTEL)
+    FK = (0x9E3779, 0x85EBCA, 0xC2B2AE, 0x27D4EB)  # kmer_ops.hpp cunmix (Feistel)
 
     def f(v, c, n):
         return ((((v ^ (v >> 9)) & 0xffffff) * c & 0xffffffff) >> 11) & ((1 << n) - 1)
 
-    def cunmix(y):  # three rounds (MHMKC_CMIX_ROUNDS)
+    def cunmix(y):  # three rounds
         a, bb = B >> 1, B - (B >> 1)
         R, L = y & ((1 << a) - 1), y >> a
         L ^= f(R, FK[2], bb)
@@ -426,7 +426,7 @@ def _hot_key_last_bucket(k: int) -> str:
         L ^= f(R, FK[0], bb)
         return (L << a) | R
 
-    M2C = (0x9E3779, 0x85EBCB, 0xC2B2AF, 0x27D4EB, 0x165667, 0x3A2659)  # kmer_ops.hpp m2_h (MHMKC_M2FAST)
+    M2C = (0x9E3779, 0x85EBCB, 0xC2B2AF, 0x27D4EB, 0x165667, 0x3A2659)  # kmer_ops.hpp m2_h
     M32 = 0xffffffff
 
     def m2_h(v, c1, c2):
@@ -438,7 +438,7 @@ def _hot_key_last_bucket(k: int) -> str:
         u = ((u & 0xffffff) * c2) & M32
         return u ^ (u >> 16)
 
-    def m2_unmix(L, R):  # (L', R') -> key words; two rounds (MHMKC_M2_ROUNDS)
+    def m2_unmix(L, R):  # (L', R') -> key words; two rounds
         R ^= m2_h(L, M2C[2], M2C[3])
         L ^= m2_h(R, M2C[0], M2C[1]) << (k - 32)
         x = (L << k) | R  # 2k bits, left-aligned in 128
@@ -529,7 +529,7 @@ def long_ragged_set(k: int, seed: int = 61):
 
 
 @pytest.mark.parametrize("k", [33, 47, 63, 77, 99, 21])
-def test_valid_window_walk_long_and_ragged_reads(k, monkeypatch):
+def test_valid_window_walk_long_and_ragged_reads(k, knob):
     """Two-word extraction over the listed valid windows == the oracle, for reads of length 0 .. 9000 (reads
     crossing several extraction tiles), whole and as host chunks (slice views with a head offset). At k = 77, 99
     the long reads count nearly every window of a tile, more than the extraction stages at once (kECap: 1024
@@ -539,7 +539,7 @@ def test_valid_window_walk_long_and_ragged_reads(k, monkeypatch):
     got, st = hip_table(b, o, k)
     assert_tables_equal(got, exp, f"long/ragged reads, k={k}")
     check_stats(st)
-    monkeypatch.setenv("MHMKC_CHUNK_BYTES", "5000")
+    knob("chunk_bytes", 5000)
     got2, _ = hip_table(b, o, k)
     assert_tables_equal(got2, exp, f"long/ragged reads in 5000-byte chunks, k={k}")
 
@@ -582,13 +582,13 @@ def test_finish_passes_with_contigs(k, passes, monkeypatch):
 
 
 @pytest.mark.parametrize("k,passes,exact", [(21, "1", False), (21, "3", False), (63, "2", True), (99, "1", False)])
-def test_output_overflow_redoes_the_pass(k, passes, exact, monkeypatch):
-    """An output sized too small (MHMKC_DEBUG_OUT_CAP rows) fills: the pass writes nothing past it, the output grows to
+def test_output_overflow_redoes_the_pass(k, passes, exact, monkeypatch, knob):
+    """An output sized too small (the test knob out_cap: rows) fills: the pass writes nothing past it, the output grows to
     the rows its cursor counted (the earlier passes' rows kept) and the pass is redone; the table is unchanged."""
     monkeypatch.setenv("MHMKC_PASSES", passes)
-    monkeypatch.setenv("MHMKC_DEBUG_OUT_CAP", "100")
+    knob("out_cap", 100)
     if exact:
-        monkeypatch.setenv("MHMKC_DEBUG_EXACT", "1")
+        knob("exact", 1)
     b, o = synth_set(2500, 12000, 620 + k)
     got, st = hip_table(b, o, k)
     assert st["out_reruns"] >= 1

@@ -81,13 +81,13 @@ def test_minimizer_owner_handoff(k, world, seed, tmp_path):
         assert sum(int(p["smer_count"]) for p in parts) > 0 and sum(int(p["handoff_sent"]) for p in parts) == 0
 
 
-@pytest.mark.parametrize("k,world,env", [(63, 2, {"MHMKC_SMER": "0"}), (99, 2, {"MHMKC_SMER": "0"}),
-                                         (63, 3, {"MHMKC_DEBUG_EXACT": "1"}), (33, 2, {"MHMKC_CHUNK_BYTES": "3000"}),
+@pytest.mark.parametrize("k,world,env", [(63, 2, {"knob:smer": "0"}), (99, 2, {"knob:smer": "0"}),
+                                         (63, 3, {"knob:exact": "1"}), (33, 2, {"knob:chunk_bytes": "3000"}),
                                          (63, 3, {"MHMKC_PASSES": "3"}), (99, 2, {"MHMKC_PASSES": "5"}),
-                                         (55, 2, {"MHMKC_PASSES": "4", "MHMKC_DEBUG_EXACT": "1"}),
-                                         (63, 2, {"MHMKC_PASSES": "2", "MHMKC_DEBUG_OUT_CAP": "50"})])
+                                         (55, 2, {"MHMKC_PASSES": "4", "knob:exact": "1"}),
+                                         (63, 2, {"MHMKC_PASSES": "2", "knob:out_cap": "50"})])
 def test_supermer_exchange_variants(k, world, env, tmp_path):
-    """MHMKC_OWNER_MINIMIZER at k >= 33 ships supermers; MHMKC_SMER=0 keeps the record exchange +
+    """MHMKC_OWNER_MINIMIZER at k >= 33 ships supermers; the test knob smer = 0 keeps the record exchange +
     hand-off; the exact (histogram) layout of the received records; many H2D chunks = many supermer slabs."""
     seed = 900 + k
     parts = run_ranks(k, world, tmp_path, seed=seed, minimizer=True, env=env)
@@ -98,7 +98,7 @@ def test_supermer_exchange_variants(k, world, env, tmp_path):
     for r, p in enumerate(parts):
         keys = np.ascontiguousarray(p["keys"][:, :nl], dtype=np.uint64)
         assert all(L.orc_kmer_target_rank(keys[i].ctypes.data, k, nl, world) == r for i in range(len(keys)))
-    smer = env.get("MHMKC_SMER", "1") != "0"
+    smer = env.get("knob:smer", "1") != "0"
     assert (sum(int(p["smer_count"]) for p in parts) > 0) == smer
     assert (sum(int(p["handoff_sent"]) for p in parts) > 0) == (not smer)
 
@@ -106,9 +106,9 @@ def test_supermer_exchange_variants(k, world, env, tmp_path):
 @pytest.mark.parametrize("k,world,opts", [
     (21, 2, {}), (33, 3, {}), (63, 2, {}), (99, 2, {}), (21, 3, {"minimizer": True}),
     (21, 3, {"env": {"MHMKC_PASSES": "3"}}), (21, 2, {"minimizer": True, "env": {"MHMKC_PASSES": "2"}}),
-    (21, 2, {"env_by_rank": {0: {"MHMKC_CHUNK_BYTES": "2000"}}}),   # rank 0: ~20 slabs, rank 1: a few
+    (21, 2, {"env_by_rank": {0: {"knob:chunk_bytes": "2000"}}}),   # rank 0: ~20 slabs, rank 1: a few
     (63, 3, {"idle_rank": 0}),                                          # a rank with no slab at all
-    (21, 2, {"env": {"MHMKC_DEBUG_EXACT": "1"}}),
+    (21, 2, {"env": {"knob:exact": "1"}}),
     (33, 2, {"env": {"MHMKC_XPIECES": "7"}, "n_reads": 3000, "genome": 20000})])
 def test_pipelined_exchange(k, world, opts, tmp_path):
     """The pipelined record exchange (MHMKC_XPIPE=1): one collective round per slab inside the add
@@ -210,7 +210,7 @@ def test_contigs_on_one_rank(k, world, minimizer, tmp_path):
 def test_multirank_dmin_and_many_chunks(tmp_path):
     """Two ranks, each host batch cut into ~45 H2D chunks (slice views with a head offset), dmin_thres = 3."""
     parts = run_ranks(21, 2, tmp_path, seed=9, dmin=3, n_reads=1200, genome=20000,
-                      env={"MHMKC_CHUNK_BYTES": "1000"})
+                      env={"knob:chunk_bytes": "1000"})
     b, o = synth_set(1200, 20000, 9)
     check_parts(parts, 21, oracle_table(b, o, 21, dmin_thres=3), "2 ranks, dmin 3, many H2D chunks")
 

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-pmc}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 rm -rf $OUT
-ARGS=${ARGS:-"--steps 1 --warmup 1 --no-cpu-baseline --no-profile-events"}
+ARGS=${ARGS:-"--steps 1 --warmup 1 --no-cpu-baseline --no-profile-events --h2d-steps 0 --no-kmermap"}
 cd /tmp
 i=0
 GROUPS_DEFAULT=(
