@@ -126,8 +126,8 @@ def handoff_ms(counter, k: int, threads: int, runs: int = 3):
     §8(d)): tools/bin/libmhmkc_handoff.so runs include/mhmkc_kcount.hpp's load_ordered on the counter's handle, which
     is what HashTableInserter::insert_into_local_hashtable does after mhmkc_finish (the device sort into the map's slot
     order, chunked D2H on a helper thread, the parallel fill of a fresh map; src/kcount/kcount_cpu.cpp:503-522). The
-    first run includes the device sort; later runs reuse the sorted rows (the sort is ~1.5 ms at C2). Every run fills a
-    fresh map (its page faults included), and a sample of the rows is looked up afterwards (untimed)."""
+    first run includes the device sort (ms_cold); later runs reuse the sorted rows (the sort is ~1.5 ms at C2). Every
+    run fills a fresh map (its page faults included); a sample of the rows is looked up after every run (untimed)."""
     import ctypes as C
 
     lib_path = ROOT / "tools" / "bin" / "libmhmkc_handoff.so"
@@ -145,8 +145,8 @@ def handoff_ms(counter, k: int, threads: int, runs: int = 3):
             return {"error": "library error in the hand-off"}
         ms.append(t)
         parts.append({n_: round(v, 1) for n_, v in zip(("first_fetch_incl_sort", "fill", "wait_fetch"), pa)})
-    return {"ms": round(sorted(ms)[len(ms) // 2], 1), "statistic": f"median of {runs} runs", "runs_ms": [round(x, 1) for x in ms],
-            "rows": counter.n_out,
+    return {"ms": round(sorted(ms)[len(ms) // 2], 1), "statistic": f"median of {runs} runs",
+            "ms_cold": round(ms[0], 1), "runs_ms": [round(x, 1) for x in ms], "rows": counter.n_out,
             "map_size": int(size.value), "sample_rows_bad": int(bad.value), "threads": threads, "parts_ms": parts,
             "kind": "C++ adapter load_ordered (HashTableInserter::insert_into_local_hashtable): device sort by KmerMap "
                     "slot, 4M-row chunks D2H on a helper thread overlapped with the parallel fill of a fresh "

@@ -207,8 +207,9 @@ def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts:
     def say(what):
         print(f"[rank {rank} {time.time() - t0:6.1f}s] {what}", flush=True)
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MHMKC_XPIPE=opts.get("xpipe", "1"),
-                      MHMKC_PASSES=str(opts.get("passes", 4)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MHMKC_XPIPE=opts.get("xpipe", "1"))
+    if opts.get("passes"):
+        os.environ["MHMKC_PASSES"] = str(opts["passes"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     R = opts["reads_per_rank"]
     g = m.synth_genome(opts["genome"], opts["seed"])
@@ -216,11 +217,25 @@ def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts:
     del g
     say(f"{R} reads")
     owner = m.MHMKC_OWNER_MINIMIZER if opts.get("owner") == "minimizer" else m.MHMKC_OWNER_HASH
-    c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner)
+    if opts.get("rccl"):  # libmhmkc's RCCL path, as the 8-GPU run takes it (per-rank NCCL_HOSTID: rccl_same_gpu_env)
+        rccl_same_gpu_env(rank)
+        obj = [m.comm_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, comm_id=obj[0], output_owner=owner)
+    else:
+        c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(), output_owner=owner)
     dist.barrier()
     t1 = time.time()
-    c.add_packed_reads(b, o)
-    del b, o
+    if opts.get("device_batch"):  # one device batch (bench.py's path: cut into MHMKC_XPIECES pipelined slabs)
+        import torch
+
+        bt = torch.from_numpy(b).cuda()
+        ot = torch.from_numpy(o.view(np.int64)).cuda()
+        del b, o
+        c.add_tensors(bt, ot)
+    else:
+        c.add_packed_reads(b, o)
+        del b, o
     c.finish()
     t_count = time.time() - t1
     st = c.stats()

@@ -336,3 +336,35 @@ def test_c3_c4_eight_ranks_vs_cpu_restatement(cfg, tmp_path):
         bad = np.flatnonzero(got != exp)
         assert bad.size == 0, f"{cfg} part {p}: {bad.size} rows differ"
     assert rows == fps.size
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("k,owner", [(21, "hash"), (63, "minimizer")])
+def test_rccl_eight_ranks_vs_cpu_restatement(k, owner, tmp_path):
+    """the 8-GPU run's code path at 8 ranks. Eight ranks share the one GPU over libmhmkc's RCCL
+    exchange (ncclCommInitRank from mhmkc_comm_id, the pipelined rounds' ncclAllGather and grouped
+    ncclSend/ncclRecv; per-rank NCCL_HOSTID, RCCL's socket transport), each with 250k reads given as one device batch
+    (bench.py's path, cut into pipelined slabs): k = 21 with the hash-range owner (record exchange), k = 63 with the
+    reference's owner (supermer exchange; every row checked on its get_kmer_target_rank). The union of the 8 tables
+    equals the multi-threaded CPU restatement (oracle/kcount_mt.c) row for row (sorted 64-bit row fingerprints)."""
+    import torch.multiprocessing as mp
+
+    import mr_gpu_worker
+
+    world, R, genome = 8, 250_000, 10_000_000
+    opts = {"reads_per_rank": R, "genome": genome, "seed": 8, "owner": owner, "passes": 0, "n_parts": 1,
+            "rccl": True, "device_batch": True}
+    mp.spawn(mr_gpu_worker.run_share_full, args=(world, free_port(), k, str(tmp_path), opts), nprocs=world, join=True)
+    stats = [dict(np.load(tmp_path / f"rank{r}_stats.npz")) for r in range(world)]
+    assert sum(int(s["owned_records"]) for s in stats) == sum(int(s["occurrences"]) for s in stats) == \
+        world * R * (150 - k - 1)
+    assert sum(int(s["bytes_sent"]) for s in stats) == sum(int(s["bytes_recv"]) for s in stats) > 0
+    if owner == "hash":
+        assert all(int(s["xchg_rounds"]) >= 2 for s in stats)  # the pipelined rounds ran
+    fps = np.sort(np.concatenate([np.load(tmp_path / f"rank{r}_fps.npy") for r in range(world)]))
+    g = m.synth_genome(genome, 8)
+    b, o = m.synth_reads(g, world * R, 150, 8, threads=16)
+    t = O.kcount_mt(b, o, k, threads=16)
+    exp = np.sort(O.row_fingerprints(*t.fetch(), k))
+    assert fps.size == exp.size, f"{fps.size} GPU rows vs {exp.size}"
+    assert np.array_equal(fps, exp), f"{int((fps != exp).sum())} rows differ"
