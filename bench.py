@@ -606,6 +606,11 @@ def main():
                           # extraction ended (the rest overlapped extraction)
                           "ms_transfers_rank0": round(st["ms_xchg"], 3) if st["xchg_rounds"] else None,
                           "ms_exposed_rank0": round(st["ms_xchg_exposed"], 3) if st["xchg_rounds"] else None,
+                          # the incremental fine partition: rounds partitioned as they landed, and
+                          # the device time from the last transfer's end to the finished table
+                          "inc_rounds_rank0": st["inc_rounds"], "inc_fallbacks_rank0": st["inc_fallbacks"],
+                          "inc_redone_coarse_rank0": st["inc_redone_coarse"],
+                          "ms_finish_tail_rank0": round(st["ms_finish_tail"], 3),
                           "GBps_rank0": round(st["bytes_sent"] / (per_step["exchange"] * 1e-3) / 1e9, 2)
                           if per_step.get("exchange") else None}
                          if world > 1 and st else None),

@@ -129,6 +129,10 @@ typedef struct {
   uint64_t out_reruns;     /* finish passes redone because the output (sized from the distinct-key sketch) was full */
   uint64_t device_bytes;   /* device memory held by this process's handles after the finish */
   uint64_t device_bytes_peak; /* ... the most it held at any time */
+  uint64_t inc_rounds;     /* pipelined record exchange: rounds fine-partitioned as they landed (0: all at finish) */
+  uint64_t inc_fallbacks;  /* ... finishes whose incremental count failed and were redone from the sources */
+  double ms_finish_tail;   /* device time from the last transfer's end (or finish's start) to the finished table */
+  uint64_t inc_redone_coarse; /* ... coarse buckets whose capped fine layout overflowed (skew), counted again exactly */
 } mhmkc_stats;
 
 enum {

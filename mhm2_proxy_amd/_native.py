@@ -116,6 +116,10 @@ class MhmkcStats(C.Structure):
         ("out_reruns", C.c_uint64),
         ("device_bytes", C.c_uint64),
         ("device_bytes_peak", C.c_uint64),
+        ("inc_rounds", C.c_uint64),
+        ("inc_fallbacks", C.c_uint64),
+        ("ms_finish_tail", C.c_double),
+        ("inc_redone_coarse", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -35,6 +35,10 @@ FILL = ROOT / "tools" / "bin" / "kmermap_fill"
 FILL_DEPS = [ROOT / "tools" / "cpp" / "kmermap_fill.cpp", ROOT / "include" / "mhmkc_kcount.hpp", ROOT / "include" / "mhmkc.h"]
 HANDOFF = ROOT / "tools" / "bin" / "libmhmkc_handoff.so"
 HANDOFF_DEPS = [ROOT / "tools" / "cpp" / "handoff.cpp", ROOT / "include" / "mhmkc_kcount.hpp", ROOT / "include" / "mhmkc.h"]
+# test infrastructure: the restated traversal over a given table (the multi-rank multi-k chain, tests/test_c5_scale.py)
+DBJG = ROOT / "tools" / "bin" / "libmhmkc_dbjg.so"
+DBJG_DEPS = [ROOT / "tools" / "cpp" / "dbjg_lib.cpp", ROOT / "include" / "mhmkc_dbjg.hpp",
+             ROOT / "include" / "mhmkc_kcount.hpp", ROOT / "include" / "mhmkc.h"]
 
 
 def source_build_id() -> str:
@@ -150,12 +154,23 @@ def build_handoff(force: bool = False) -> Path:
     return HANDOFF
 
 
+def build_dbjg(force: bool = False) -> Path:
+    if force or _stale(DBJG, DBJG_DEPS + [LIB]):
+        DBJG.parent.mkdir(parents=True, exist_ok=True)
+        tmp = DBJG.with_suffix(".tmp")
+        _run(["g++", "-O2", "-std=c++17", "-pthread", "-fPIC", "-shared", "-I", ROOT / "include", DBJG_DEPS[0], "-L",
+              PKG, "-lmhmkc", "-lz", "-Wl,-rpath,$ORIGIN/../../mhm2_proxy_amd", "-o", tmp])
+        tmp.replace(DBJG)
+    return DBJG
+
+
 def build_all(force: bool = False) -> None:
     build_lib(force)
     build_synth(force)
     build_oracle(force)
     build_fill(force)
     build_handoff(force)
+    build_dbjg(force)
 
 
 if __name__ == "__main__":

@@ -1472,7 +1472,10 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_sketch(PartitionParams p, u
   atomicAdd(&s_ext, ext_adds);
   __syncthreads();
   for (int i = threadIdx.x; i < SKETCH_M; i += NT)
-    if (reg[i]) atomicMax(&hll[i], reg[i]);
+    if (reg[i]) {
+      atomicMax(&hll[i], reg[i]);
+      if (!(blockIdx.x & 1u)) atomicMax(&hll[SKETCH_M + 1 + i], reg[i]);  // the even chunks' sketch (about half)
+    }
   if (threadIdx.x == 0 && s_ext) atomicAdd(&hll[SKETCH_M], s_ext);  // (one add per workgroup)
 }
 
@@ -2493,7 +2496,9 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP_ADD(3, t_f0 - t_b0);  // (the sweep's end barrier: the waves' imbalance; cold sweeps have no round barrier)
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
-    if (p.ctg_n) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
+    // (a skipped coarse bucket's fine buckets are empty, k_inc_fixup, and its contig k-mers wait for the launch
+    // that counts it)
+    if (p.ctg_n && !(p.coarse_skip && p.coarse_skip[b >> p.fine_bits])) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
     {
       // the next bucket's first round, loaded while this one is finalized; unconditional (as the round prefetch:
       // a load under a branch was waited for at once): without a next bucket, or before a re-sweep (which loads
@@ -2815,6 +2820,31 @@ hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *o
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void k_inc_fixup(const unsigned long long *coarse_base,
+                                                  const unsigned long long *coarse_fcap, int fine_bits,
+                                                  unsigned long long *cursor, uint8_t *skip, unsigned int *err) {
+  const uint32_t c = blockIdx.x, nf = 1u << fine_bits;
+  const unsigned long long b0 = coarse_base[c], fcap = coarse_fcap[c];
+  unsigned long long *cur = cursor + ((uint64_t)c << fine_bits);
+  int over = 0;
+  for (uint32_t f = threadIdx.x; f < nf; f += 256) over |= cur[f] > b0 + (f + 1) * fcap;
+  over = __syncthreads_or(over);
+  if (over)
+    for (uint32_t f = threadIdx.x; f < nf; f += 256) cur[f] = b0 + f * fcap;
+  if (threadIdx.x == 0) {
+    skip[c] = (uint8_t)over;
+    if (c == 0) atomicAnd(err, ~2u);
+  }
+}
+
+hipError_t launch_inc_fixup(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap,
+                            uint32_t n_coarse, int fine_bits, unsigned long long *cursor, uint8_t *skip,
+                            unsigned int *err, hipStream_t s) {
+  if (!n_coarse) return hipSuccess;
+  k_inc_fixup<<<dim3(n_coarse), dim3(256), 0, s>>>(coarse_base, coarse_fcap, fine_bits, cursor, skip, err);
+  return hipGetLastError();
+}
+
 hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap,
                             uint32_t n_coarse, int fine_bits, unsigned long long *base, unsigned long long *cursor,
                             hipStream_t s) {
@@ -2878,6 +2908,31 @@ hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s
   if (!p.n_buckets) return hipSuccess;
   if (p.compact) return MHM_DISPATCH_MIXED(nl, do_count, (p, s));
   MHM_DISPATCH(nl, packed, do_count, (p, s));
+}
+
+// ------------------------------------------------------------------------------------------------
+// exchange: dense send planes (one workgroup per filled segment; consecutive lanes copy consecutive elements)
+
+template <typename V>
+__global__ __launch_bounds__(256) void k_seg_gather(const SegCopy *segs, const V *src, V *dst) {
+  const SegCopy sc = segs[blockIdx.x];
+  const V *s = src + sc.src;
+  V *d = dst + sc.dst;
+  for (uint64_t i = threadIdx.x; i < sc.n; i += 256) d[i] = s[i];
+}
+
+hipError_t launch_seg_gather(const SegCopy *segs, uint32_t n_segs, const void *src, void *dst, int elem_bytes,
+                             hipStream_t s) {
+  if (!n_segs) return hipSuccess;
+  const dim3 grid(n_segs), block(256);
+  switch (elem_bytes) {
+    case 1: k_seg_gather<uint8_t><<<grid, block, 0, s>>>(segs, (const uint8_t *)src, (uint8_t *)dst); break;
+    case 4: k_seg_gather<uint32_t><<<grid, block, 0, s>>>(segs, (const uint32_t *)src, (uint32_t *)dst); break;
+    case 8: k_seg_gather<uint2><<<grid, block, 0, s>>>(segs, (const uint2 *)src, (uint2 *)dst); break;
+    case 16: k_seg_gather<uint4><<<grid, block, 0, s>>>(segs, (const uint4 *)src, (uint4 *)dst); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------

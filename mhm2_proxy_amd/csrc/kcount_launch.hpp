@@ -166,6 +166,8 @@ struct CountParams {
   PlaneSet spill;                     // deferred records of cold sweeps: SPILL_RECORDS per workgroup (fine record
                                       // layout; planes of grid * SPILL_RECORDS entries); w[0] == nullptr: none
   uint8_t *ctg_done;                  // [ctg_n] applied (zeroed before the launch)
+  const uint8_t *coarse_skip;         // [n_buckets >> fine_bits] or null: a local coarse bucket whose fine buckets are
+                                      // counted by a later launch (k_inc_fixup emptied them): no contig k-mers here
 };
 
 // Contig pass state word of one folded contig k-mer (kcount_ctg.hip).
@@ -281,6 +283,13 @@ size_t tile_starts_words(int nl);
 // not a valid PackedReads CSR (offs[0] != 0, decreasing, a read longer than 65535, offs[n] != n_bases)
 hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, unsigned int *err, hipStream_t s);
 // capped fine layout: base/cursor of bucket (c, d) = coarse_base[c] + d * coarse_fcap[c]
+// The incremental layout after its last round: a coarse bucket with a fine bucket past its capped
+// segment (k_part_scatter wrote none of that bucket's overflowing runs) gets skip[c] = 1 and all its fine buckets
+// emptied (cursor = base), so k_count counts the others and the host redoes just the skipped coarse buckets; err bit 1
+// (the overflow flag, which would void the k_count launch) is cleared.
+hipError_t launch_inc_fixup(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap,
+                            uint32_t n_coarse, int fine_bits, unsigned long long *cursor, uint8_t *skip,
+                            unsigned int *err, hipStream_t s);
 hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigned long long *coarse_fcap,
                             uint32_t n_coarse, int fine_bits, unsigned long long *base, unsigned long long *cursor,
                             hipStream_t s);
@@ -291,13 +300,24 @@ hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 // HyperLogLog sketch of the distinct keys in chunks [0, n_chunks) of p's chunk table (one coarse bucket):
-// hll[SKETCH_M] registers, max-merged, and hll[SKETCH_M] += the records' extension adds (zero them first).
+// hll[SKETCH_M] registers, max-merged, and hll[SKETCH_M] += the records' extension adds; hll[SKETCH_M + 1 ..
+// 2 SKETCH_M + 1) the registers of the even-numbered chunks alone (a second sample point for the growth of the distinct
+// keys with the records). Zero all 2 SKETCH_M + 1 words first.
 constexpr int SKETCH_M = 1024;
+constexpr int SKETCH_WORDS = 2 * SKETCH_M + 1;
 hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
                          hipStream_t s);
 hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor,
                        uint32_t n, hipStream_t s);
 hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s);
+// The exchange's send side: the filled part of every capped segment a peer owns, copied back to back into a dense
+// send plane (a slab's owned range has up to the capped slack between its segments, which the wire need not carry).
+// Elements of elem_bytes (1, 4, 8 or 16); segs in elements.
+struct SegCopy {
+  uint64_t src, dst, n;
+};
+hipError_t launch_seg_gather(const SegCopy *segs, uint32_t n_segs, const void *src, void *dst, int elem_bytes,
+                             hipStream_t s);
 
 // FASTQ ingest (fastq.hip): text -> PackedRead bytes. FQ_CHUNK bytes of text per count / lines block.
 constexpr int FQ_CHUNK = 4096;

@@ -170,6 +170,24 @@ struct Source {
   std::vector<uint64_t> count;  // [n_owned * NSUB]
 };
 
+// The run table of a fine partition over coarse buckets [c0, c1) (local) of a list of sources: one entry per
+// non-empty (source, segment) span; the device expands it into chunks of T records ordered by XCD class (coarse % 8),
+// then coarse bucket, segment, source (xcd_chunk). n_c0: the chunks up to the end of coarse bucket c0 (all of c0's
+// records when c0 % 8 == 0: the sketch's sample); n_c0_even: its records in even-numbered chunks.
+struct RunTable {
+  std::vector<mhm::SRun> runs;
+  std::vector<mhm::PlaneSet> ps;
+  uint64_t n_chunks = 0, n_c0 = 0, xcd_max = 0, rec_c0 = 0, rec_c0_even = 0;
+  uint64_t xcd_start[9] = {0};
+};
+
+// One exchange round's fine partition on pstream (the incremental partition): its run table (kept
+// until the round's copies ran) and device tables.
+struct IncRound {
+  RunTable rt;
+  DevBuf chunks, srcs;
+};
+
 // One device-to-device transfer of the exchange: `bytes` at `ptr` to (or from) rank `peer`.
 struct Xfer {
   int peer;
@@ -235,6 +253,32 @@ struct mhmkc {
   hipEvent_t ev_xdone = nullptr, ev_xext = nullptr;
   std::vector<hipEvent_t> x_ev;  // per round: start / end of the round's transfer on xstream
   int xround(Slab *sl, bool done);
+  // incremental fine partition: the rounds' records are fine-partitioned on pstream as they land,
+  // into a capped layout fixed after the first round (fine bits from the round's distinct-key sketch, extrapolated;
+  // capacities from the windows every rank announced); finish then only counts, unless the layout overflowed
+  bool inc = false, inc_tried = false;
+  hipStream_t pstream = nullptr;
+  hipEvent_t ev_pdone = nullptr;
+  uint64_t inc_expect = 0, inc_announced = 0;  // this rank's windows announced by its add calls / not yet added
+  uint64_t x_expect_all = 0;                   // all ranks' announced windows (the latest round's all-gather)
+  std::vector<uint64_t> x_r0_coarse;           // round 0: records of each owned coarse bucket (all senders)
+  uint64_t x_r0_total = 0;                     // round 0: records of all senders' slabs (every coarse bucket)
+  std::vector<int> x_round_slab;               // per round: the index of this rank's slab sent in it, or -1
+  std::vector<IncRound *> inc_pool;
+  size_t inc_parted = 0;                       // rounds whose partition is enqueued
+  double inc_distinct = 0;                     // the extrapolated distinct keys of the owned range
+  double inc_ext_per_rec = 0;                  // extension adds per record of the sketch sample (stats)
+  mhm::PlaneSet inc_r2{};                      // the fine records' planes of the incremental layout (in d_r2)
+  std::vector<uint64_t> inc_cfit;              // its capped layout (host copy, kept until finish)
+  hipEvent_t ev_tail0 = nullptr;               // finish: the exchange is over, what is left is counting
+  uint64_t inc_out_est = 0;
+  int inc_setup();
+  int inc_round(size_t r);
+  void round_sources(size_t r, std::vector<Source> &srcs) const;
+  int finish_inc(bool &done, uint64_t *n_out_ret);
+  void make_runs(const std::vector<Source> &srcs, uint32_t c0, uint32_t c1, int T, RunTable &rt) const;
+  int upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_t s, mhm::PartitionParams &pp);
+  int fine_layout(const std::vector<uint64_t> &per_coarse, std::vector<uint64_t> &cfit, uint64_t &r2_size) const;
   int pump();
   int resolve_one(Slab *sl, bool &redo);
   std::vector<hipEvent_t> chunk_ev;  // one per H2D chunk in flight (pool)
@@ -246,6 +290,8 @@ struct mhmkc {
   bool ord_ready = false;  // set by order_rows, cleared by finish / reset
   int order_rows();
   DevBuf d_spill;  // k_count: the deferred records of cold sweeps, mhm::SPILL_RECORDS per persistent workgroup
+  DevBuf d_cfit;   // capped fine layout: per coarse bucket of the pass its first record and fine-bucket capacity
+  DevBuf d_inc_skip;  // incremental count: per owned coarse bucket, 1 = overflowed its capped layout (k_inc_fixup)
   // supermer exchange (smer): owner bytes of a slab's tiles; the received supermers (codes, good bits, descriptors),
   // their window counts / prefix, per-tile first supermer, scan scratch
   bool smer = false;
@@ -258,6 +304,9 @@ struct mhmkc {
   int smer_exchange(std::vector<Source> &srcs);
   int smer_records(uint32_t lo, uint32_t hi, std::vector<Source> &srcs);
   PinBuf x_send, x_recv;  // host-staged exchange
+  DevBuf d_xsend, d_xsegs;  // pipelined exchange: the round's dense send planes and their segment list
+  std::vector<mhm::SegCopy> x_segs;
+  uint64_t x_send_cap = 0;
   // FASTQ ingest (fastq.hip): text staging, chunk counts, newline positions, record lengths, scan scratch,
   // the packed reads of the last batch, first error
   DevBuf d_fq_text, d_fq_chunk, d_fq_lines, d_fq_len, d_fq_tmp, d_fq_bytes, d_fq_offs, d_fq_err;
@@ -312,15 +361,15 @@ struct mhmkc {
     (void)hipEventCreate(&e);
     return e;
   }
-  void prof_begin(int stage) {
+  void prof_begin(int stage, hipStream_t s = nullptr) {
     if (!profiling) return;
     Prof p{stage, take_event(), take_event()};
-    (void)hipEventRecord(p.a, stream);
+    (void)hipEventRecord(p.a, s ? s : stream);
     prof.push_back(p);
   }
-  void prof_end() {
+  void prof_end(hipStream_t s = nullptr) {
     if (!profiling || prof.empty()) return;
-    (void)hipEventRecord(prof.back().b, stream);
+    (void)hipEventRecord(prof.back().b, s ? s : stream);
   }
   void prof_collect() {
     for (auto &p : prof) {
@@ -372,12 +421,14 @@ struct mhmkc {
 
   // Record planes for n records: NL u64 word planes (+ a byte plane when the ext code is not packed);
   // compact: a u32 plane (w[0]) + a byte plane for coarse-bucketed records, the u32 plane alone for fine.
-  int set_planes(DevBuf &buf, uint64_t n, mhm::PlaneSet &ps, bool fine = false) {
+  // (sync = false: the buffer is known idle, e.g. for the incremental partition, which must not wait for the main
+  // stream's extraction)
+  int set_planes(DevBuf &buf, uint64_t n, mhm::PlaneSet &ps, bool fine = false, bool sync = true) {
     const uint64_t m = std::max<uint64_t>(n, 1);
     const size_t plane = align_up(m * (compact ? 4 : 8), 256);
     const size_t extb = (compact ? !fine : !packed) ? align_up(m, 256) : 0;
     const int np = compact ? 1 : nl;
-    hipError_t e = grow(buf, plane * np + extb);
+    hipError_t e = sync ? grow(buf, plane * np + extb) : buf.ensure(plane * np + extb);
     if (e != hipSuccess) return hip_fail(e, "allocating record planes");
     char *b = buf.as<char>();
     for (int w = 0; w < 4; w++) ps.w[w] = w < np ? (uint64_t *)(b + plane * w) : nullptr;
@@ -415,6 +466,12 @@ struct mhmkc {
   int exchange(std::vector<Source> &srcs);
   int gather_ctgs(std::vector<uint8_t> &gb, std::vector<uint64_t> &go, std::vector<uint64_t> &gw,
                   std::vector<uint16_t> &gd);
+  // every rank's contigs, gathered once per finish (prepare_ctgs runs again, locally, when an incremental count
+  // falls back to the passes on this rank only)
+  bool ctg_gathered = false;
+  std::vector<uint8_t> ctg_gbytes;
+  std::vector<uint64_t> ctg_goffs, ctg_gwin;
+  std::vector<uint16_t> ctg_gdepth;
   int handoff();
   int finish(uint64_t *n_out_ret);
   int finish_passes(uint64_t owned) const;
@@ -574,6 +631,13 @@ int mhmkc::add_view(const mhm::ReadsView &rv, uint64_t wins, bool wins_known) {
   sl->n = 0;
   st.occurrences += wins;
   st.slabs++;
+  // (the windows an add call announced for its whole batch, inc_expect, cover its slabs; any other slab adds its own)
+  if (inc_announced >= wins) {
+    inc_announced -= wins;
+  } else {
+    inc_expect += wins - inc_announced;
+    inc_announced = 0;
+  }
   if (smer) return smer_build(sl);
   int rc = extract(sl, g_dbg.exact != 0);
   return rc ? rc : pump();
@@ -632,6 +696,15 @@ int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads
   if (n_reads >= 0xffffffffull) return fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
   uint64_t chunk = CHUNK_BYTES;
   if (g_dbg.chunk_bytes) chunk = std::max<uint64_t>(64, (uint64_t)g_dbg.chunk_bytes);
+  if (xpipe) {  // the batch's windows, announced to the other ranks by the exchange rounds (the incremental layout)
+    uint64_t w = 0;
+    for (uint64_t r = 0; r < n_reads; r++) {
+      const uint64_t L = offs[r + 1] >= offs[r] ? offs[r + 1] - offs[r] : 0;
+      w += L > (uint64_t)k + 1 ? L - k - 1 : 0;
+    }
+    inc_expect += w;
+    inc_announced += w;
+  }
   hipError_t e;
   Arena *ar = new_arena();
   if ((e = grow(ar->bytes, n_bases + 64)) != hipSuccess || (e = grow(ar->offs, (n_reads + 1) * 8)) != hipSuccess)
@@ -871,26 +944,44 @@ int mhmkc::xround(Slab *sl, bool done) {
     if ((rc = resolve_one(sl, redo))) return rc;
     if (redo && pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
   }
-  // 1. every rank's flags (done, has a slab) and its slab's segment counts and starts (capped slabs have gaps)
-  const size_t per = 2 * (size_t)nseg + 3;
+  // 1. every rank's flags (done, has a slab), the windows it announced, its slab's segment counts and starts (capped
+  //    slabs have gaps)
+  const size_t per = 2 * (size_t)nseg + 4;
   std::vector<uint64_t> mine(per, 0), all((size_t)g * per, 0);
   mine[0] = done;
   mine[1] = sl != nullptr;
+  mine[2] = inc_expect;
   if (sl) {
-    std::copy(sl->counts.begin(), sl->counts.end(), mine.begin() + 2);
-    std::copy(sl->bases.begin(), sl->bases.end(), mine.begin() + 2 + nseg);
+    std::copy(sl->counts.begin(), sl->counts.end(), mine.begin() + 3);
+    std::copy(sl->bases.begin(), sl->bases.end(), mine.begin() + 3 + nseg);
   }
   if ((rc = allgather_host(mine.data(), all.data(), 8 * per, xstream))) return rc;
   auto row = [&](int r) { return all.data() + (size_t)r * per; };
   bool all_done = true;
-  for (int p = 0; p < g; p++) all_done &= row(p)[0] != 0;
-  // 2. receive layout: one span per peer with a slab this round, its records of my owned range
+  x_expect_all = 0;
+  for (int p = 0; p < g; p++) {
+    all_done &= row(p)[0] != 0;
+    x_expect_all += row(p)[2];
+  }
+  if (x_rounds == 0) {  // round 0's shares of the owned coarse buckets: the incremental partition's layout (inc_setup)
+    x_r0_coarse.assign(no, 0);
+    x_r0_total = 0;
+    for (int p = 0; p < g; p++) {
+      if (!row(p)[1]) continue;
+      const uint64_t *pc = row(p) + 3;
+      for (uint32_t i = 0; i < nseg; i++) x_r0_total += pc[i];
+      for (uint32_t i = 0; i < no * NSUB; i++) x_r0_coarse[i / NSUB] += pc[own_lo * NSUB + i];
+    }
+  }
+  // 2. receive layout: one span per peer with a slab this round, its records of my owned range, dense (the sender
+  //    copies each capped segment's records back to back, step 3)
   std::vector<std::pair<int, uint64_t>> rsp;
   uint64_t recv_total = 0;
   for (int p = 0; p < g; p++) {
     if (p == me || !row(p)[1]) continue;
-    const uint64_t *pb = row(p) + 2 + nseg;
-    const uint64_t n = pb[own_hi * NSUB] - pb[own_lo * NSUB];
+    const uint64_t *pc = row(p) + 3;
+    uint64_t n = 0;
+    for (uint32_t i = own_lo * NSUB; i < own_hi * NSUB; i++) n += pc[i];
     rsp.push_back({p, n});
     recv_total += n;
   }
@@ -904,27 +995,51 @@ int mhmkc::xround(Slab *sl, bool done) {
     sp.off = off;
     sp.start.resize((size_t)no * NSUB);
     sp.count.resize((size_t)no * NSUB);
-    const uint64_t *pc = row(pn.first) + 2, *pb = row(pn.first) + 2 + nseg;
+    const uint64_t *pc = row(pn.first) + 3;
+    uint64_t o = off;
     for (uint32_t i = 0; i < no * NSUB; i++) {
-      sp.start[i] = off + (pb[own_lo * NSUB + i] - pb[own_lo * NSUB]);
+      sp.start[i] = o;
       sp.count[i] = pc[own_lo * NSUB + i];
+      o += sp.count[i];
     }
     rp->spans.push_back(std::move(sp));
     off += pn.second;
   }
-  // 3. transfers, per peer in plane order on both sides (as exchange())
+  // 3. transfers, per peer in plane order on both sides (as exchange()). The send side copies the filled part of every
+  //    segment a peer owns back to back into the send planes (k_seg_gather on xstream, after the slab's extraction):
+  //    a slab's owned range carries the capped segments' slack (4 % + a constant), which the wire need not (bytes
+  //    per occurrence at 8 ranks 4.79 -> 4.375, the records' 5 B x 7/8)
   const bool aos = mixed2;
   const int np = (compact || aos) ? 1 : nl;
   const size_t wb = compact ? 4 : aos ? 16 : 8;
   std::vector<Xfer> snd, rcv;
+  x_segs.clear();
+  uint64_t send_total = 0;
+  std::vector<uint64_t> peer_off(g + 1, 0);
   if (sl) {
     for (int p = 0; p < g; p++) {
+      peer_off[p] = send_total;
       if (p == me) continue;
-      const uint32_t lo = owner_lo(p), hi = owner_lo(p + 1);
-      const uint64_t a = sl->bases[lo * NSUB], b = sl->bases[hi * NSUB];
-      if (b == a) continue;
-      for (int w = 0; w < np; w++) snd.push_back({p, (char *)sl->planes.w[w] + a * wb, (b - a) * wb});
-      if (sl->planes.ext) snd.push_back({p, sl->planes.ext + a, b - a});
+      for (uint32_t i = owner_lo(p) * NSUB; i < owner_lo(p + 1) * NSUB; i++)
+        if (sl->counts[i]) {
+          x_segs.push_back({sl->bases[i], send_total, sl->counts[i]});
+          send_total += sl->counts[i];
+        }
+    }
+    peer_off[g] = send_total;
+  }
+  mhm::PlaneSet sps{};
+  if (send_total) {
+    // (xstream may still send the previous round from the send planes: a larger allocation waits for it)
+    const uint64_t need = send_total;
+    if (x_send_cap < need && (e = hipStreamSynchronize(xstream)) != hipSuccess) return hip_fail(e, "exchange stream");
+    if ((rc = set_planes(d_xsend, need, sps, false, false))) return rc;
+    x_send_cap = std::max(x_send_cap, need);
+    for (int p = 0; p < g; p++) {
+      const uint64_t a = peer_off[p], b = p + 1 < g ? peer_off[p + 1] : send_total;
+      if (p == me || b == a) continue;
+      for (int w = 0; w < np; w++) snd.push_back({p, (char *)sps.w[w] + a * wb, (b - a) * wb});
+      if (sps.ext) snd.push_back({p, sps.ext + a, b - a});
     }
   }
   off = 0;
@@ -943,10 +1058,31 @@ int mhmkc::xround(Slab *sl, bool done) {
   }
   if (sl && (e = hipStreamWaitEvent(xstream, sl->ev, 0)) != hipSuccess) return hip_fail(e, "exchange wait");
   (void)hipEventRecord(x_ev[2 * x_rounds], xstream);
+  if (!x_segs.empty()) {
+    const size_t sb = x_segs.size() * sizeof(mhm::SegCopy);
+    if (d_xsegs.cap < sb && (e = hipStreamSynchronize(xstream)) != hipSuccess) return hip_fail(e, "exchange stream");
+    if ((e = d_xsegs.ensure(sb)) != hipSuccess) return hip_fail(e, "exchange segments");
+    mhm::SegCopy *ds = d_xsegs.as<mhm::SegCopy>();
+    // (x_segs lives in the handle until the next round, which first waits for this one's copy: the H2D is on xstream)
+    if ((e = hipMemcpyAsync(ds, x_segs.data(), sb, hipMemcpyHostToDevice, xstream)) != hipSuccess)
+      return hip_fail(e, "exchange segments");
+    for (int w = 0; w < np && e == hipSuccess; w++)
+      e = mhm::launch_seg_gather(ds, (uint32_t)x_segs.size(), sl->planes.w[w], sps.w[w], (int)wb, xstream);
+    if (e == hipSuccess && sl->planes.ext)
+      e = mhm::launch_seg_gather(ds, (uint32_t)x_segs.size(), sl->planes.ext, sps.ext, 1, xstream);
+    if (e != hipSuccess) return hip_fail(e, "exchange gather");
+  }
   if ((rc = move(snd, rcv, xstream))) return rc;
   (void)hipEventRecord(x_ev[2 * x_rounds + 1], xstream);
+  x_round_slab.push_back(sl ? (int)(std::find(slabs.begin(), slabs.begin() + (long)n_slabs, sl) - slabs.begin()) : -1);
   x_rounds++;
   x_all_done = all_done;
+  // the incremental partition: its layout once round 0 has landed (while round 1's transfer and the
+  // next slab's extraction run), then every round on pstream as it lands
+  if (!inc_tried && x_rounds >= 2 && (rc = inc_setup())) return rc;
+  if (inc)
+    for (; inc_parted < x_rounds; inc_parted++)
+      if ((rc = inc_round(inc_parted))) return rc;
   return MHMKC_OK;
 }
 
@@ -1227,16 +1363,16 @@ int mhmkc::gather_ctgs(std::vector<uint8_t> &gb, std::vector<uint64_t> &go, std:
 
 int mhmkc::prepare_ctgs() {
   ctg_n = 0;
-  std::vector<uint8_t> gb;
-  std::vector<uint64_t> go, gw;
-  std::vector<uint16_t> gd;
   const std::vector<uint8_t> *cb_ = &ctg_bytes;
   const std::vector<uint64_t> *co = &ctg_offs, *cw = &ctg_win;
   const std::vector<uint16_t> *cd = &ctg_depth;
   if (G() > 1) {
-    int rc = gather_ctgs(gb, go, gw, gd);
-    if (rc) return rc;
-    cb_ = &gb, co = &go, cw = &gw, cd = &gd;
+    if (!ctg_gathered) {  // (collective: every rank gathers exactly once per finish)
+      int rc = gather_ctgs(ctg_gbytes, ctg_goffs, ctg_gwin, ctg_gdepth);
+      if (rc) return rc;
+      ctg_gathered = true;
+    }
+    cb_ = &ctg_gbytes, co = &ctg_goffs, cw = &ctg_gwin, cd = &ctg_gdepth;
   }
   const uint64_t W = cw->back();
   if (!W) return MHMKC_OK;
@@ -1421,11 +1557,221 @@ hipError_t mhmkc::grow_keep(DevBuf &b, size_t used, size_t need) {
   return hipSuccess;
 }
 
+void mhmkc::make_runs(const std::vector<Source> &srcs, uint32_t c0, uint32_t c1, int T, RunTable &rt) const {
+  rt.runs.clear();
+  rt.ps.clear();
+  rt.n_chunks = rt.n_c0 = rt.xcd_max = rt.rec_c0 = rt.rec_c0_even = 0;
+  for (auto &sr : srcs) rt.ps.push_back(sr.planes);
+  for (uint32_t x = 0; x < 8; x++) {
+    rt.xcd_start[x] = rt.n_chunks;
+    for (uint32_t c = c0 + ((x + 8 - c0 % 8) % 8); c < c1; c += 8) {
+      for (uint32_t q = 0; q < NSUB; q++)
+        for (size_t s_ = 0; s_ < srcs.size(); s_++) {
+          const uint32_t i = c * NSUB + q;
+          const uint64_t cnt = srcs[s_].count[i];
+          if (!cnt) continue;
+          rt.runs.push_back({srcs[s_].start[i], cnt, (uint32_t)s_, c - c0, (uint32_t)rt.n_chunks, 0});
+          if (c == c0) {  // (the sketch launches one workgroup per chunk: its even chunks are the half sample)
+            rt.rec_c0 += cnt;
+            for (uint64_t j = 0; j < cnt; j += (uint64_t)T)
+              if (!((rt.n_chunks + j / T) & 1)) rt.rec_c0_even += std::min<uint64_t>((uint64_t)T, cnt - j);
+          }
+          rt.n_chunks += (cnt + T - 1) / T;
+        }
+      if (c == c0) rt.n_c0 = rt.n_chunks;
+    }
+  }
+  rt.xcd_start[8] = rt.n_chunks;
+  for (int x = 0; x < 8; x++) rt.xcd_max = std::max(rt.xcd_max, rt.xcd_start[x + 1] - rt.xcd_start[x]);
+}
+
+// The run table on the device (buf: runs | chunk index, expanded on s; sbuf: the plane sets), and the partition
+// parameters that point at it. The host vectors of rt must live until the copies on s ran.
+int mhmkc::upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_t s, mhm::PartitionParams &pp) {
+  const int T = mhm::chunk_records(nl);
+  if (rt.n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
+  hipError_t e;
+  const size_t rb = align_up(std::max<size_t>(1, rt.runs.size()) * sizeof(mhm::SRun), 256);
+  const bool main = s == stream;  // (main stream: earlier kernels may still read the buffers, grow waits for them)
+  if ((e = main ? grow(buf, rb + 4 * (rt.n_chunks + 1) + 256) : buf.ensure(rb + 4 * (rt.n_chunks + 1) + 256)) != hipSuccess)
+    return hip_fail(e, "chunk table");
+  const size_t sb = std::max<size_t>(1, rt.ps.size()) * sizeof(mhm::PlaneSet) + 64;
+  if ((e = main ? grow(sbuf, sb) : sbuf.ensure(sb)) != hipSuccess) return hip_fail(e, "source table");
+  mhm::SRun *d_runs = buf.as<mhm::SRun>();
+  uint32_t *d_chunk_run = (uint32_t *)(buf.as<char>() + rb);
+  if (!rt.runs.empty()) {
+    if ((e = hipMemcpyAsync(d_runs, rt.runs.data(), rt.runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, s)) !=
+        hipSuccess)
+      return hip_fail(e, "run table H2D");
+    if ((e = mhm::launch_chunk_runs(d_runs, (uint32_t)rt.runs.size(), d_chunk_run, T, s)) != hipSuccess)
+      return hip_fail(e, "chunk index");
+  }
+  if (!rt.ps.empty() &&
+      (e = hipMemcpyAsync(sbuf.p, rt.ps.data(), rt.ps.size() * sizeof(mhm::PlaneSet), hipMemcpyHostToDevice, s)) !=
+          hipSuccess)
+    return hip_fail(e, "source H2D");
+  pp.runs = d_runs;
+  pp.chunk_run = d_chunk_run;
+  pp.n_runs = (uint32_t)rt.runs.size();
+  pp.n_chunks = (uint32_t)rt.n_chunks;
+  for (int x = 0; x < 9; x++) pp.xcd_start[x] = (uint32_t)rt.xcd_start[x];
+  pp.grid = (uint32_t)(8 * rt.xcd_max);
+  pp.srcs = sbuf.as<mhm::PlaneSet>();
+  pp.k = k;
+  pp.coarse_bits = cb;
+  pp.fine_bits = fb;
+  pp.hbits = hbits;
+  pp.compact = mixed();
+  pp.err = d_err.as<unsigned int>();
+  return MHMKC_OK;
+}
+
+// The capped fine layout of coarse buckets with these (expected) record counts: every fine bucket of coarse bucket c
+// gets 1.25x its share + 256 records (multiples of 16: k_count loads compact records in quads).
+int mhmkc::fine_layout(const std::vector<uint64_t> &per_coarse, std::vector<uint64_t> &cfit, uint64_t &r2_size) const {
+  const size_t np_ = per_coarse.size();
+  cfit.assign(2 * np_, 0);  // [coarse_base | coarse_fcap]
+  r2_size = 0;
+  for (size_t c = 0; c < np_; c++) {
+    const uint64_t ex = per_coarse[c] >> fb;
+    const uint64_t fcap = align_up(ex + ex / 4 + 256, 16);
+    cfit[c] = r2_size;
+    cfit[np_ + c] = fcap;
+    r2_size += fcap << fb;
+  }
+  return MHMKC_OK;
+}
+
+// The sources of exchange round r: this rank's slab of the round (its owned range in place) and the received spans.
+void mhmkc::round_sources(size_t r, std::vector<Source> &srcs) const {
+  srcs.clear();
+  if (r < x_round_slab.size() && x_round_slab[r] >= 0) {
+    const Slab *sl = slabs[(size_t)x_round_slab[r]];
+    Source src;
+    src.planes = sl->planes;
+    src.start.assign(sl->bases.begin() + own_lo * NSUB, sl->bases.begin() + own_hi * NSUB);
+    src.count.assign(sl->counts.begin() + own_lo * NSUB, sl->counts.begin() + own_hi * NSUB);
+    srcs.push_back(std::move(src));
+  }
+  if (r < n_parts)
+    for (auto &sp : parts[r]->spans) {
+      Source src;
+      src.planes = parts[r]->planes;
+      src.start = sp.start;
+      src.count = sp.count;
+      srcs.push_back(std::move(src));
+    }
+}
+
+// The incremental partition's layout, after round 0 has landed. The fine bits need the distinct keys
+// per coarse bucket, which round 0 samples: a HyperLogLog sketch of its records of the first owned coarse bucket, and a
+// second one of about half of them (the even chunks), give the distinct keys D at two sample sizes n; with
+// D(n) = G + e n (the genome's k-mers are all seen after a few x of coverage, sequencing errors add new keys in
+// proportion to the reads) they extrapolate to the bucket's expected records N. The expected records per coarse bucket
+// are the windows every rank announced (its add calls' batches) times the bucket's share of round 0. A later add call
+// beyond the announcement, or a skewed input, overflows a capped fine bucket: finish then redoes the partition from the
+// sources, which every round keeps.
+int mhmkc::inc_setup() {
+  inc_tried = true;
+  const uint32_t no = n_owned();
+  if (!pstream || x_expect_all == 0 || x_r0_total == 0 || n_parts < 1 || g_dbg.exact || no == 0) return MHMKC_OK;
+  hipError_t e;
+  std::vector<Source> srcs;
+  round_sources(0, srcs);
+  const int T = mhm::chunk_records(nl);
+  IncRound sk;
+  make_runs(srcs, 0, 1, T, sk.rt);  // the first owned coarse bucket of round 0
+  if (!sk.rt.n_c0 || sk.rt.rec_c0 < 4096) return MHMKC_OK;
+  mhm::PartitionParams sp{};
+  if ((e = hipStreamWaitEvent(pstream, x_ev[1], 0)) != hipSuccess) return hip_fail(e, "partition stream");
+  int rc = upload_runs(sk.rt, sk.chunks, sk.srcs, pstream, sp);
+  if (rc) return rc;
+  std::vector<uint32_t> reg(mhm::SKETCH_WORDS);
+  prof_begin(MHMKC_STAGE_OTHER, pstream);
+  if ((e = d_hll.ensure(4 * mhm::SKETCH_WORDS + 64)) != hipSuccess ||
+      (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_WORDS, pstream)) != hipSuccess ||
+      (e = mhm::launch_sketch(sp, (uint32_t)sk.rt.n_c0, d_hll.as<unsigned int>(), nl, packed, pstream)) != hipSuccess)
+    return hip_fail(e, "distinct sketch");
+  prof_end(pstream);
+  if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * mhm::SKETCH_WORDS, hipMemcpyDeviceToHost, pstream)) != hipSuccess ||
+      (e = hipStreamSynchronize(pstream)) != hipSuccess)
+    return hip_fail(e, "sketch D2H");
+  sk.chunks.release();
+  sk.srcs.release();
+  const double d_f = hll_estimate(std::vector<uint32_t>(reg.begin(), reg.begin() + mhm::SKETCH_M));
+  const double d_h = hll_estimate(std::vector<uint32_t>(reg.begin() + mhm::SKETCH_M + 1, reg.end()));
+  const double n_f = (double)sk.rt.rec_c0, n_h = (double)sk.rt.rec_c0_even;
+  inc_ext_per_rec = (double)reg[mhm::SKETCH_M] / n_f;
+  // the expected records of every owned coarse bucket (at least what round 0 brought)
+  std::vector<uint64_t> per_coarse(no);
+  for (uint32_t c = 0; c < no; c++)
+    per_coarse[c] = std::max<uint64_t>(x_r0_coarse[c], (uint64_t)((double)x_expect_all * (double)x_r0_coarse[c] / (double)x_r0_total));
+  const double n_exp = (double)per_coarse[0];
+  const double slope = (n_f > n_h && d_f > d_h) ? (d_f - d_h) / (n_f - n_h) : 0.0;
+  const double d_n = std::min(std::max(d_f + slope * (n_exp - n_f), d_f), d_f * n_exp / n_f);
+  const uint32_t cap_slots = (uint32_t)mhm::count_cap(nl, compact);
+  int f = 4;
+  while (f < 11 && d_n / (double)(1u << f) > FINE_LOAD * cap_slots) f++;
+  if (g_dbg.fine_bits >= 0) f = (int)std::min<int64_t>(11, g_dbg.fine_bits);
+  fb = std::max(f, min_fine_bits());
+  nf = 1u << fb;
+  uint64_t r2_size = 0;
+  fine_layout(per_coarse, inc_cfit, r2_size);
+  // room for it (the finish then needs no more than the output and k_count's spill area)
+  size_t fr = 0, tot = 0;
+  const double rec_b = compact ? 4.0 : (double)rec_bytes();
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess ||
+      (double)r2_size * rec_b > 0.7 * (double)fr + (double)d_r2.cap)
+    return MHMKC_OK;
+  const uint32_t n_fine = no << fb;
+  if ((rc = set_planes(d_r2, r2_size, inc_r2, true, false))) return rc;
+  if ((e = d_fine_base.ensure((size_t)n_fine * 8)) != hipSuccess ||
+      (e = d_fine_cursor.ensure((size_t)n_fine * 8)) != hipSuccess || (e = d_cfit.ensure(16 * (size_t)no + 64)) != hipSuccess)
+    return hip_fail(e, "fine layout");
+  unsigned long long *cf = d_cfit.as<unsigned long long>();
+  if ((e = hipMemcpyAsync(cf, inc_cfit.data(), 16 * (size_t)no, hipMemcpyHostToDevice, pstream)) != hipSuccess ||
+      (e = mhm::launch_init_fine(cf, cf + no, no, fb, d_fine_base.as<unsigned long long>(),
+                                 d_fine_cursor.as<unsigned long long>(), pstream)) != hipSuccess)
+    return hip_fail(e, "fine layout");
+  inc_distinct = d_n * no;
+  inc = true;
+  return MHMKC_OK;
+}
+
+// Round r's records into the incremental layout, on pstream once the round's transfer has landed.
+int mhmkc::inc_round(size_t r) {
+  const uint32_t no = n_owned();
+  while (inc_pool.size() <= r) inc_pool.push_back(new IncRound());
+  IncRound *ir = inc_pool[r];
+  std::vector<Source> srcs;
+  round_sources(r, srcs);
+  make_runs(srcs, 0, no, mhm::chunk_records(nl), ir->rt);
+  if (!ir->rt.n_chunks) return MHMKC_OK;
+  hipError_t e;
+  if ((e = hipStreamWaitEvent(pstream, x_ev[2 * r + 1], 0)) != hipSuccess) return hip_fail(e, "partition stream");
+  mhm::PartitionParams pp{};
+  int rc = upload_runs(ir->rt, ir->chunks, ir->srcs, pstream, pp);
+  if (rc) return rc;
+  unsigned long long *cf = d_cfit.as<unsigned long long>();
+  pp.fine_hist = nullptr;
+  pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
+  pp.coarse_base = cf;
+  pp.coarse_fcap = cf + no;
+  pp.out = inc_r2;
+  prof_begin(MHMKC_STAGE_SSCAT, pstream);
+  e = mhm::launch_part_scatter(pp, nl, packed, pstream);
+  prof_end(pstream);
+  if (e != hipSuccess) return hip_fail(e, "part_scatter");
+  st.inc_rounds++;
+  return MHMKC_OK;
+}
+
 int mhmkc::finish(uint64_t *n_out_ret) {
   if (partial) return fail(MHMKC_ESTATE, "a failed mhmkc_add_fastq_file left part of the file in this round; call mhmkc_reset");
   int rc = begin_round();
   if (rc) return rc;
   ord_ready = false;
+  ctg_gathered = false;
   if ((rc = resolve_slabs())) return rc;
   hipError_t e;
   const uint32_t no = n_owned();
@@ -1451,6 +1797,12 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     st.xchg_rounds = x_rounds;
     st.ms_xchg = x_ms;
     st.ms_xchg_exposed = exposed;
+    if (inc) {  // every round's partition is enqueued on pstream (xround): the count waits for them
+      for (; inc_parted < x_rounds; inc_parted++)
+        if ((rc = inc_round(inc_parted))) return rc;
+      if ((e = hipEventRecord(ev_pdone, pstream)) != hipSuccess || (e = hipStreamWaitEvent(stream, ev_pdone, 0)) != hipSuccess)
+        return hip_fail(e, "partition stream");
+    }
     if (profiling) {
       st.ms_kernel[MHMKC_STAGE_XCHG] += x_ms;
       st.launches[MHMKC_STAGE_XCHG] += x_rounds;
@@ -1481,6 +1833,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       srcs.push_back(std::move(src));
     }
   }
+  (void)hipEventRecord(ev_tail0, stream);  // (the exchange is over: what follows on the stream is the count)
   uint64_t owned = smer ? smer_nwin : 0;  // (the received windows' records are extracted per pass)
   for (auto &s : srcs)
     for (uint32_t i = 0; i < no * NSUB; i++) owned += s.count[i];
@@ -1488,8 +1841,6 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   st.coarse_record_bytes = rec_bytes();
   st.fine_record_bytes = compact ? 4 : rec_bytes();
   smer_seen = 0;
-  const int passes = finish_passes(owned);
-  st.finish_passes = (uint64_t)passes;
 
   const int T = mhm::chunk_records(nl);  // records per partition chunk
   const uint32_t cap_slots = (uint32_t)mhm::count_cap(nl, compact);
@@ -1499,8 +1850,145 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   double est_fine = 0;  // estimated distinct keys per fine bucket (0: no estimate)
   unsigned int errf = 0;
   st.fine_buckets = 0;
-  for (int pass = 0; pass < passes; pass++) {
-    const uint32_t c0 = (uint32_t)((uint64_t)no * pass / passes), c1 = (uint32_t)((uint64_t)no * (pass + 1) / passes);
+  // k_count's parameters for the fine buckets of a pass that starts at local coarse bucket c0 (all but the records
+  // and the output, which the attempts set)
+  int rc_cp = MHMKC_OK;
+  auto count_params = [&](uint32_t c0, uint32_t n_fine) {
+    mhm::CountParams cp{};
+    cp.bucket_base = d_fine_base.as<unsigned long long>();
+    cp.bucket_end = d_fine_cursor.as<unsigned long long>();
+    cp.hbits = hbits;
+    cp.compact = mixed();
+    cp.coarse_bits = cb;
+    cp.fine_bits = fb;
+    cp.bucket0 = (own_lo + c0) << fb;
+    cp.n_buckets = n_fine;
+    cp.grid = (uint32_t)std::max(0, n_cu);  // persistent workgroups filling every CU's LDS
+    cp.k = k;
+    cp.cap = mhm::count_cap(nl, compact);
+    // (The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
+    // LDS table, 0.44 at C2; a table cut to 0.6-0.8 of the estimate was measured slower, 6.28 -> 7.14-10.2 ms: the
+    // home-group hit rate falls faster than the per-slot clear and finalize work.)
+    st.table_slots = (uint64_t)cp.cap;
+    if (g_dbg.cap) cp.cap = std::min<int>(cp.cap, (int)std::max<int64_t>(64, g_dbg.cap) & ~3);
+    cp.dmin_thres = dmin;
+    cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
+    cp.nlo = nlo;
+    cp.out_cursor = d_out_cursor.as<unsigned long long>();
+    cp.stats = d_stats.as<unsigned long long>();
+    cp.err = d_err.as<unsigned int>();
+    cp.ctg_n = ctg_n;
+    for (int w = 0; w < 4; w++) cp.ctg_keys[w] = w < nl ? d_ctg_keys[w].as<uint64_t>() : nullptr;
+    cp.ctg_state = d_ctg_state.as<uint32_t>();
+    cp.ctg_bucket = d_ctg_bucket.as<uint32_t>();
+    cp.ctg_done = d_ctg_done.as<uint8_t>();
+    cp.ctg_base = c0 << fb;
+    if (cp.grid && nl <= mhm::DYN_SWEEP_MAX_NL)  // dynamic cold sweeps defer into it (one- and two-word keys)
+      rc_cp = set_planes(d_spill, (uint64_t)cp.grid * mhm::SPILL_RECORDS, cp.spill, true);
+    if (rc_cp) cp.grid = 0;
+    return cp;
+  };
+  auto grow_output = [&](uint64_t rows) -> int {
+    hipError_t e_;
+    if ((e_ = grow(d_out_keys, rows * 8 * nlo)) != hipSuccess || (e_ = grow(d_out_counts, rows * 2)) != hipSuccess ||
+        (e_ = grow(d_out_left, rows)) != hipSuccess || (e_ = grow(d_out_right, rows)) != hipSuccess ||
+        (e_ = grow(d_out_cursor, 8)) != hipSuccess)
+      return hip_fail(e_, "output");
+    return MHMKC_OK;
+  };
+
+  // The incremental partition put every round's records into their fine buckets already: count them.
+  // A coarse bucket with a fine bucket past its capped segment (skewed input: a very frequent k-mer) is emptied by
+  // k_inc_fixup and skipped by k_count; the passes below then count just those coarse buckets again, from the sources,
+  // with exact bucket sizes. A full output grows and counts again (the layout stays). Anything else unexpected sends
+  // the whole finish through the passes.
+  bool inc_done = false;
+  std::vector<std::pair<uint32_t, uint32_t>> ranges;  // the local coarse ranges the passes below count
+  if (inc) {
+    const uint32_t n_fine = no << fb;
+    nf = 1u << fb;
+    st.distinct_estimate = (uint64_t)inc_distinct;
+    st.lds_ext_adds = (uint64_t)(inc_ext_per_rec * (double)owned);
+    if ((rc = prepare_ctgs())) return rc;
+    out_cap = std::min<uint64_t>(owned / 2, (uint64_t)(0.5 * inc_distinct) + (1u << 20));
+    if (g_dbg.out_cap >= 0) out_cap = (uint64_t)g_dbg.out_cap;
+    out_cap += ctg_n + 1;
+    if ((rc = grow_output(out_cap))) return rc;
+    mhm::CountParams cp = count_params(0, n_fine);
+    if (rc_cp) return rc_cp;
+    if ((e = d_inc_skip.ensure((size_t)no + 64)) != hipSuccess) return hip_fail(e, "skip flags");
+    unsigned long long *cf = d_cfit.as<unsigned long long>();
+    prof_begin(MHMKC_STAGE_OTHER);
+    e = mhm::launch_inc_fixup(cf, cf + no, no, fb, d_fine_cursor.as<unsigned long long>(), d_inc_skip.as<uint8_t>(),
+                              d_err.as<unsigned int>(), stream);
+    prof_end();
+    if (e != hipSuccess) return hip_fail(e, "layout fixup");
+    cp.recs = inc_r2;
+    cp.coarse_skip = d_inc_skip.as<uint8_t>();
+    std::vector<uint8_t> skip(no);
+    for (int attempt = 0; attempt < 4 && !inc_done; attempt++) {
+      cp.out_keys = d_out_keys.as<uint64_t>();
+      cp.out_counts = d_out_counts.as<uint16_t>();
+      cp.out_left = d_out_left.as<char>();
+      cp.out_right = d_out_right.as<char>();
+      cp.out_cap = out_cap;
+      unsigned long long stats[mhm::STAT_ALLOC], cursor_end = 0;
+      const unsigned long long cur0 = 0;
+      prof_begin(MHMKC_STAGE_OTHER);
+      e = hipMemcpyAsync(d_out_cursor.p, &cur0, 8, hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipMemsetAsync(d_stats.p, 0, 8 * mhm::STAT_ALLOC, stream);
+      if (e == hipSuccess && ctg_n) e = hipMemsetAsync(d_ctg_done.p, 0, ctg_n, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "count setup");
+      prof_begin(MHMKC_STAGE_COUNT);
+      e = mhm::launch_count(cp, nl, packed, stream);
+      prof_end();
+      if (e != hipSuccess) return hip_fail(e, "count");
+      (void)hipEventRecord(ev_end, stream);
+      if ((e = hipMemcpyAsync(stats, d_stats.p, sizeof stats, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(&errf, d_err.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(&cursor_end, d_out_cursor.p, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(skip.data(), d_inc_skip.p, no, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+          (e = hipStreamSynchronize(stream)) != hipSuccess)
+        return hip_fail(e, "finish");
+      if (errf & 2u) break;  // (not expected: k_inc_fixup cleared it)
+      if (errf & 16u) {  // the output is full: grow it to the rows the cursor counted, count again
+        out_cap = cursor_end + cursor_end / 16 + 1024;
+        if ((rc = grow_output(out_cap))) return rc;
+        st.out_reruns++;
+        errf &= ~16u;
+        if ((e = hipMemcpy(d_err.p, &errf, 4, hipMemcpyHostToDevice)) != hipSuccess) return hip_fail(e, "flag reset");
+        continue;
+      }
+      if (stats[mhm::STAT_N - 1]) return fail(MHMKC_EHIP, "internal: LDS probe bound exceeded");
+      for (int i = 0; i < mhm::STAT_ALLOC; i++) acc_stats[i] = stats[i];
+      out_used = cursor_end;
+      st.fine_buckets = n_fine;
+      inc_done = true;
+    }
+    if (inc_done) {
+      for (uint32_t c = 0; c < no; c++) {
+        if (!skip[c]) continue;
+        st.inc_redone_coarse++;
+        if (!ranges.empty() && ranges.back().second == c)
+          ranges.back().second = c + 1;
+        else
+          ranges.push_back({c, c + 1});
+      }
+    } else {
+      st.inc_fallbacks++;
+      errf &= ~(2u | 16u);
+      if ((e = hipMemcpy(d_err.p, &errf, 4, hipMemcpyHostToDevice)) != hipSuccess) return hip_fail(e, "flag reset");
+    }
+  }
+  if (!inc_done) {
+    const int passes = finish_passes(owned);
+    for (int q = 0; q < passes; q++)
+      ranges.push_back({(uint32_t)((uint64_t)no * q / passes), (uint32_t)((uint64_t)no * (q + 1) / passes)});
+  }
+  st.finish_passes = (inc_done ? 1 : 0) + (uint64_t)ranges.size();
+  for (size_t pass = 0; pass < ranges.size(); pass++) {
+    const uint32_t c0 = ranges[pass].first, c1 = ranges[pass].second;
     const uint32_t np_ = c1 - c0;  // coarse buckets of this pass
     if (!np_) continue;
     const size_t n_srcs0 = srcs.size();
@@ -1546,9 +2034,10 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       return hip_fail(e, "chunk table");
     mhm::SRun *d_runs = d_chunks.as<mhm::SRun>();
     uint32_t *d_chunk_run = (uint32_t *)(d_chunks.as<char>() + align_up(runs.size() * sizeof(mhm::SRun), 256));
-    if ((e = grow(d_srcs, std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 16 * (size_t)np_)) != hipSuccess)
+    if ((e = grow(d_srcs, std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 64)) != hipSuccess ||
+        (e = grow(d_cfit, 16 * (size_t)np_ + 64)) != hipSuccess)
       return hip_fail(e, "source table");
-    unsigned long long *d_cfit = (unsigned long long *)(d_srcs.as<char>() + align_up(ps.size() * sizeof(mhm::PlaneSet), 16));
+    unsigned long long *cfit_d = d_cfit.as<unsigned long long>();
     // the tables are small: their copies are waited for below (the host vectors go out of scope)
     if (!runs.empty()) {
       if ((e = hipMemcpyAsync(d_runs, runs.data(), runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, stream)) !=
@@ -1561,7 +2050,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
                                            hipMemcpyHostToDevice, stream)) != hipSuccess)
       return hip_fail(e, "source H2D");
 
-    if (pass == 0) {
+    if (pass == 0 && !inc_done) {  // (a redo after the incremental count keeps its fine bits, contigs and output)
       // fine bits: at most FINE_LOAD x the LDS table slots of distinct keys per fine bucket, with
       // the distinct keys of the first owned coarse bucket estimated by a HyperLogLog sketch (the ratio of distinct
       // keys to records grows with k and the error rate, so the record count alone misjudges it); the same fine bits
@@ -1581,8 +2070,8 @@ int mhmkc::finish(uint64_t *n_out_ret) {
         sp.compact = mixed();
         std::vector<uint32_t> reg(mhm::SKETCH_M + 1);
         prof_begin(MHMKC_STAGE_OTHER);
-        if ((e = grow(d_hll, 4 * mhm::SKETCH_M + 64)) != hipSuccess ||
-            (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_M + 4, stream)) != hipSuccess ||
+        if ((e = grow(d_hll, 4 * mhm::SKETCH_WORDS + 64)) != hipSuccess ||
+            (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_WORDS, stream)) != hipSuccess ||
             (e = mhm::launch_sketch(sp, (uint32_t)n_c0, d_hll.as<unsigned int>(), nl, packed, stream)) != hipSuccess)
           return hip_fail(e, "distinct sketch");
         prof_end();
@@ -1611,10 +2100,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       if (est > 0) out_cap = std::min<uint64_t>(out_cap, (uint64_t)(0.5 * est * no) + (1u << 20));
       if (g_dbg.out_cap >= 0) out_cap = (uint64_t)g_dbg.out_cap;
       out_cap += ctg_n + 1;
-      if ((e = grow(d_out_keys, out_cap * 8 * nlo)) != hipSuccess || (e = grow(d_out_counts, out_cap * 2)) != hipSuccess ||
-          (e = grow(d_out_left, out_cap)) != hipSuccess || (e = grow(d_out_right, out_cap)) != hipSuccess ||
-          (e = grow(d_out_cursor, 8)) != hipSuccess)
-        return hip_fail(e, "output");
+      if ((rc = grow_output(out_cap))) return rc;
     }
     const uint32_t n_fine = np_ * nf;
     st.fine_buckets += n_fine;
@@ -1629,7 +2115,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       cfit[np_ + c] = fcap;
       r2_size += fcap << fb;
     }
-    if ((e = hipMemcpyAsync(d_cfit, cfit.data(), 16 * (size_t)np_, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    if ((e = hipMemcpyAsync(cfit_d, cfit.data(), 16 * (size_t)np_, hipMemcpyHostToDevice, stream)) != hipSuccess)
       return hip_fail(e, "layout H2D");
     if ((e = grow(d_fine_hist, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine histogram");
     if ((e = grow(d_fine_base, (size_t)n_fine * 8)) != hipSuccess) return hip_fail(e, "fine bases");
@@ -1652,40 +2138,9 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     pp.fine_cursor = d_fine_cursor.as<unsigned long long>();
     pp.err = d_err.as<unsigned int>();
 
-    mhm::CountParams cp{};
-    cp.bucket_base = d_fine_base.as<unsigned long long>();
-    cp.bucket_end = d_fine_cursor.as<unsigned long long>();
-    cp.hbits = hbits;
-    cp.compact = mixed();
-    cp.coarse_bits = cb;
-    cp.fine_bits = fb;
-    cp.bucket0 = (own_lo + c0) << fb;
-    cp.n_buckets = n_fine;
-    cp.grid = (uint32_t)std::max(0, n_cu);  // persistent workgroups filling every CU's LDS
-    cp.k = k;
-    cp.cap = mhm::count_cap(nl, compact);
-    // (The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
-    // LDS table, 0.44 at C2; a table cut to 0.6-0.8 of the estimate was measured slower, 6.28 -> 7.14-10.2 ms: the
-    // home-group hit rate falls faster than the per-slot clear and finalize work.)
-    st.table_slots = (uint64_t)cp.cap;
-    if (g_dbg.cap) cp.cap = std::min<int>(cp.cap, (int)std::max<int64_t>(64, g_dbg.cap) & ~3);
-    cp.dmin_thres = dmin;
-    cp.dyn_mult = 1.0 - cfg.dyn_min_depth;
-    cp.nlo = nlo;
-    cp.out_cursor = d_out_cursor.as<unsigned long long>();
-    cp.stats = d_stats.as<unsigned long long>();
-    cp.err = d_err.as<unsigned int>();
-    cp.ctg_n = ctg_n;
-    for (int w = 0; w < 4; w++) cp.ctg_keys[w] = w < nl ? d_ctg_keys[w].as<uint64_t>() : nullptr;
-    cp.ctg_state = d_ctg_state.as<uint32_t>();
-    cp.ctg_bucket = d_ctg_bucket.as<uint32_t>();
-    cp.ctg_done = d_ctg_done.as<uint8_t>();
-    cp.ctg_base = c0 << fb;
-    if (cp.grid && nl <= mhm::DYN_SWEEP_MAX_NL) {  // dynamic cold sweeps defer into it (one- and two-word keys)
-      if ((rc = set_planes(d_spill, (uint64_t)cp.grid * mhm::SPILL_RECORDS, cp.spill, true))) return rc;
-    }
-
-    bool exact = exact_dbg;
+    mhm::CountParams cp = count_params(c0, n_fine);
+    if (rc_cp) return rc_cp;
+    bool exact = exact_dbg || inc_done;  // (a coarse bucket the incremental count skipped is known to be skewed)
     unsigned long long stats[mhm::STAT_ALLOC], cursor_end = 0;
     for (int attempt = 0;; attempt++) {
       if (attempt >= 4) return fail(MHMKC_EHIP, "internal: finish pass %d did not settle", pass);
@@ -1707,7 +2162,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       if (e == hipSuccess && ctg_n) e = hipMemsetAsync(d_ctg_done.p, 0, ctg_n, stream);  // (earlier passes' are done)
       if (e == hipSuccess && exact) e = hipMemsetAsync(d_fine_hist.p, 0, (size_t)n_fine * 8, stream);
       if (e == hipSuccess && !exact)
-        e = mhm::launch_init_fine(d_cfit, d_cfit + np_, np_, fb, d_fine_base.as<unsigned long long>(),
+        e = mhm::launch_init_fine(cfit_d, cfit_d + np_, np_, fb, d_fine_base.as<unsigned long long>(),
                                   d_fine_cursor.as<unsigned long long>(), stream);
       prof_end();
       if (e != hipSuccess) return hip_fail(e, "fine layout");
@@ -1724,8 +2179,8 @@ int mhmkc::finish(uint64_t *n_out_ret) {
         prof_end();
         if (e != hipSuccess) return hip_fail(e, "scan");
       } else {
-        pp.coarse_base = d_cfit;
-        pp.coarse_fcap = d_cfit + np_;
+        pp.coarse_base = cfit_d;
+        pp.coarse_fcap = cfit_d + np_;
       }
       pp.out = r2;
       prof_begin(MHMKC_STAGE_SSCAT);
@@ -1771,6 +2226,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
                 (unsigned long long)smer_seen, (unsigned long long)smer_nwin);
   float ms = 0;
   if (hipEventElapsedTime(&ms, ev_begin, ev_end) == hipSuccess) st.ms_total = ms;
+  if (hipEventElapsedTime(&ms, ev_tail0, ev_end) == hipSuccess) st.ms_finish_tail = ms;
   finished = true;
   if (errf & 1u) return fail(MHMKC_EBADCHAR, "input byte with a base code > 4 (not A,C,G,T,N)");
   if (errf & 8u) return fail(MHMKC_EHIP, "internal: supermer spans inconsistent");
@@ -2037,8 +2493,11 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   const char *xp_env = getenv("MHMKC_XPIPE");
   h->xpipe = cfg->n_ranks > 1 && !h->smer && xp_env && atoi(xp_env);
   if (const char *env = getenv("MHMKC_XPIECES")) h->xpieces = std::max(1, std::min(64, atoi(env)));
-  if (h->xpipe && ((e = hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking)) != hipSuccess ||
-                   (e = hipEventCreate(&h->ev_xdone)) != hipSuccess || (e = hipEventCreate(&h->ev_xext)) != hipSuccess)) {
+  if ((e = hipEventCreate(&h->ev_tail0)) != hipSuccess ||
+      (h->xpipe && ((e = hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking)) != hipSuccess ||
+                    (e = hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking)) != hipSuccess ||
+                    (e = hipEventCreateWithFlags(&h->ev_pdone, hipEventDisableTiming)) != hipSuccess ||
+                    (e = hipEventCreate(&h->ev_xdone)) != hipSuccess || (e = hipEventCreate(&h->ev_xext)) != hipSuccess))) {
     g_create_error = std::string("exchange stream: ") + hipGetErrorString(e);
     mhmkc_destroy(h);
     return MHMKC_EHIP;
@@ -2064,7 +2523,16 @@ void mhmkc_destroy(mhmkc_t h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
   if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+  if (h->pstream) (void)hipStreamSynchronize(h->pstream);
   if (h->comm) ncclCommDestroy(h->comm);
+  for (IncRound *q : h->inc_pool) {
+    q->chunks.release();
+    q->srcs.release();
+    delete q;
+  }
+  if (h->pstream) (void)hipStreamDestroy(h->pstream);
+  if (h->ev_pdone) (void)hipEventDestroy(h->ev_pdone);
+  if (h->ev_tail0) (void)hipEventDestroy(h->ev_tail0);
   for (RecvPart *q : h->parts) {
     q->buf.release();
     delete q;
@@ -2091,7 +2559,7 @@ void mhmkc_destroy(mhmkc_t h) {
                     &h->d_out_keys, &h->d_out_counts, &h->d_out_left,   &h->d_out_right,  &h->d_out_cursor,
                     &h->d_recv,     &h->d_xg,         &h->d_hll,        &h->d_dest,       &h->d_ohist,
                     &h->d_out2_keys, &h->d_out2_counts, &h->d_out2_left, &h->d_out2_right, &h->d_mh, &h->d_ord,
-                    &h->d_spill,
+                    &h->d_spill,      &h->d_cfit,       &h->d_xsend,      &h->d_xsegs,
                     &h->d_owners, &h->d_rcodes, &h->d_rgood, &h->d_rdesc, &h->d_rnwin, &h->d_rwpre, &h->d_rtiles,
                     &h->d_rtmp,
                     &h->d_fqa_bytes, &h->d_fqa_offs,
@@ -2145,19 +2613,44 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_
     if (cut[0] != 0)
       return h->fail(MHMKC_EINVAL, "device read offsets are not a PackedReads CSR (offs[0] == 0, non-decreasing, reads "
                                    "<= 65535 bases, offs[n_reads] == n_bases)");
+    std::vector<mhm::ReadsView> rvs(P);
     for (uint64_t i = 0; i < P; i++) {
       const uint64_t r0 = n_reads * i / P, r1 = n_reads * (i + 1) / P;
       if (cut[i + 1] < cut[i] || cut[P] != n_bases)
         return h->fail(MHMKC_EINVAL, "device read offsets are not a PackedReads CSR (offs[n_reads] == n_bases)");
-      mhm::ReadsView rv{};
+      mhm::ReadsView &rv = rvs[i];
+      rv = mhm::ReadsView{};
       rv.obase = cut[i] & ~15ull;
       rv.head = (uint32_t)(cut[i] - rv.obase);
       rv.bytes = d_bytes + rv.obase;
       rv.offs = d_offs + r0;
       rv.n_reads = r1 - r0;
       rv.n_bases = cut[i + 1] - rv.obase;
-      if ((rc = h->add_view(rv, 0, false))) return rc;
     }
+    // every piece's windows (and the CSR checks) in one go: the batch's windows are announced to the other ranks by
+    // the exchange rounds (the incremental partition's layout), then the pieces become slabs
+    std::vector<uint64_t> wins(P, 0);
+    unsigned int ef = 0;
+    if ((e = h->grow(h->d_hist, (size_t)(h->nb + P) * 8 + 64)) != hipSuccess) return h->hip_fail(e, "histogram");
+    unsigned long long *d_wins = h->d_hist.as<unsigned long long>() + h->nb;
+    h->prof_begin(MHMKC_STAGE_TILEIDX);
+    e = hipMemsetAsync(d_wins, 0, 8 * P, h->stream);
+    for (uint64_t i = 0; i < P && e == hipSuccess; i++)
+      e = mhm::launch_count_windows(rvs[i], h->k, d_wins + i, h->d_err.as<unsigned int>(), h->stream);
+    h->prof_end();
+    if (e == hipSuccess) e = hipMemcpyAsync(wins.data(), d_wins, 8 * P, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&ef, h->d_err.p, 4, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return h->hip_fail(e, "window count");
+    if (ef & 4u)
+      return h->fail(MHMKC_EINVAL, "device read offsets are not a PackedReads CSR (offs[0] == 0, non-decreasing, reads "
+                                   "<= 65535 bases, offs[n_reads] == n_bases)");
+    uint64_t tot = 0;
+    for (uint64_t w : wins) tot += w;
+    h->inc_expect += tot;
+    h->inc_announced += tot;
+    for (uint64_t i = 0; i < P; i++)
+      if ((rc = h->add_view(rvs[i], wins[i], true))) return rc;
     return MHMKC_OK;
   }
   mhm::ReadsView rv{d_bytes, d_offs, n_reads, n_bases, 0, 0, 0};
@@ -2752,7 +3245,14 @@ int mhmkc_reset(mhmkc_t h) {
   if (!h) return MHMKC_EINVAL;
   hipError_t e = hipStreamSynchronize(h->stream);
   if (e == hipSuccess && h->xstream) e = hipStreamSynchronize(h->xstream);
+  if (e == hipSuccess && h->pstream) e = hipStreamSynchronize(h->pstream);
   if (e != hipSuccess) return h->hip_fail(e, "reset");
+  h->inc = h->inc_tried = false;
+  h->inc_parted = 0;
+  h->inc_expect = h->inc_announced = h->x_expect_all = h->x_r0_total = 0;
+  h->x_r0_coarse.clear();
+  h->x_round_slab.clear();
+  h->inc_distinct = h->inc_ext_per_rec = 0;
   h->prof_collect();
   h->n_slabs = 0;
   h->n_parts = 0;

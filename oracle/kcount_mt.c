@@ -92,6 +92,35 @@ static inline uint32_t mt_range(const uint64_t *key, int nl, uint32_t n_ranges) 
   return (uint32_t)(((x >> 32) * (uint64_t)n_ranges) >> 32);
 }
 
+/* contig records of one partition, in contig order (the contig pass is order dependent): key words, ext codes
+ * (left << 3 | right; A0 C1 G2 T3, 4 = none: 'N', or a base below the quality cutoff) and the contig's depth */
+typedef struct {
+  uint64_t *keys;
+  uint8_t *ext;
+  uint16_t *depth;
+  uint64_t n, cap;
+} mt_cbin;
+
+static int cbin_push(mt_cbin *b, const uint64_t *key, int nl, uint8_t e, uint16_t d) {
+  if (b->n == b->cap) {
+    uint64_t nc = b->cap ? 2 * b->cap : 1024;
+    uint64_t *nk = (uint64_t *)realloc(b->keys, nc * 8 * (size_t)nl);
+    if (!nk) return 0;
+    b->keys = nk;
+    uint8_t *ne = (uint8_t *)realloc(b->ext, nc);
+    if (!ne) return 0;
+    b->ext = ne;
+    uint16_t *nd = (uint16_t *)realloc(b->depth, nc * 2);
+    if (!nd) return 0;
+    b->depth = nd;
+    b->cap = nc;
+  }
+  memcpy(b->keys + b->n * nl, key, 8 * (size_t)nl);
+  b->ext[b->n] = e;
+  b->depth[b->n++] = d;
+  return 1;
+}
+
 typedef struct {
   /* input */
   const uint8_t *bytes;
@@ -116,6 +145,7 @@ typedef struct {
   int nthreads;
   int next_part;
   pthread_mutex_t lock;
+  const mt_cbin *cbins; /* [MT_PARTS]: the contig pass's records, or NULL */
 } mt_shared;
 
 typedef struct {
@@ -192,6 +222,84 @@ static void *mt_extract(void *arg) {
   return NULL;
 }
 
+/* The contig pass's records (add_ctg_kmers, src/kcount/kcount.cpp:100-138 -> process_seq with count = depth, depth 0
+ * -> 1, kcount_cpu.cpp:73-103 -> get_kmers_and_exts, :307-335): the interior windows of every contig of >= k + 2
+ * bases, in contig order, binned by partition like the reads' records. Case is quality (upper = good); 'N' keys as G
+ * and is no extension. Returns 0 on a character the reference DIEs on (:453-458) or allocation failure. */
+static int mt_ctg_records(const char *chars, const uint64_t *offs, const uint16_t *depths, uint64_t n_ctgs, int k,
+                          int nl, uint32_t range, uint32_t n_ranges, mt_cbin *cbins) {
+  const int klast = k - 32 * (nl - 1);
+  const uint64_t lastmask = klast >= 32 ? ~0ULL : ~(~0ULL >> (2 * klast));
+  uint8_t *code = NULL, *ext = NULL;
+  uint64_t cap = 0;
+  int ok = 1;
+  for (uint64_t c = 0; c < n_ctgs && ok; c++) {
+    const uint64_t L = offs[c + 1] - offs[c];
+    if (L < (uint64_t)k + 2) continue; /* kcount.cpp:128 */
+    if (L > cap) {
+      free(code);
+      free(ext);
+      cap = L;
+      code = (uint8_t *)malloc(cap);
+      ext = (uint8_t *)malloc(cap);
+      if (!code || !ext) return 0;
+    }
+    const char *s = chars + offs[c];
+    for (uint64_t j = 0; j < L; j++) {
+      const char b = s[j], u = (b >= 'a' && b <= 'z') ? (char)(b - 32) : b;
+      int t;
+      switch (u) {
+        case 'A': t = 0; break;
+        case 'C': t = 1; break;
+        case 'G': t = 2; break;
+        case 'T': t = 3; break;
+        case 'N': t = 4; break;
+        default: ok = 0; t = 4;
+      }
+      code[j] = (uint8_t)(t == 4 ? 2 : t);
+      ext[j] = (uint8_t)((b >= 'A' && b <= 'Z' && t < 4) ? t : 4);
+    }
+    if (!ok) break;
+    const uint16_t depth = depths[c] ? depths[c] : 1;
+    uint64_t fw[MT_MAXNL] = {0}, rc[MT_MAXNL] = {0};
+    for (int j = 0; j < k; j++) {
+      const uint64_t t = code[j];
+      fw[j >> 5] |= t << (62 - 2 * (j & 31));
+      const int q = k - 1 - j;
+      rc[q >> 5] |= (3 - t) << (62 - 2 * (q & 31));
+    }
+    for (uint64_t i = 0; i + k < L && ok; i++) {
+      if (i >= 1) {
+        const uint64_t t = code[i + k - 1];
+        for (int m = 0; m < nl - 1; m++) fw[m] = (fw[m] << 2) | (fw[m + 1] >> 62);
+        fw[nl - 1] = ((fw[nl - 1] << 2) | (t << (64 - 2 * klast))) & lastmask;
+        for (int m = nl - 1; m > 0; m--) rc[m] = (rc[m] >> 2) | (rc[m - 1] << 62);
+        rc[0] = (rc[0] >> 2) | ((3 - t) << 62);
+        rc[nl - 1] &= lastmask;
+      }
+      if (i == 0) continue;
+      int l = ext[i - 1], r = ext[i + k];
+      int use_rc = 0;
+      for (int m = 0; m < nl; m++)
+        if (rc[m] != fw[m]) {
+          use_rc = rc[m] < fw[m];
+          break;
+        }
+      const uint64_t *key = use_rc ? rc : fw;
+      if (n_ranges > 1 && mt_range(key, nl, n_ranges) != range) continue;
+      if (use_rc) {
+        const int nl_ = r < 4 ? 3 - r : 4, nr_ = l < 4 ? 3 - l : 4;
+        l = nl_;
+        r = nr_;
+      }
+      ok = cbin_push(&cbins[mt_hash(key, nl) >> 56], key, nl, (uint8_t)((l << 3) | r), depth);
+    }
+  }
+  free(code);
+  free(ext);
+  return ok;
+}
+
 /* get_ext (kcount_cpu.cpp:173-182, get_sorted :133-145: descending count, ties to the higher char) */
 static char mt_get_ext(const uint32_t *e, uint32_t count, int dmin, double dyn_mult) {
   static const char ch[4] = {'A', 'C', 'G', 'T'};
@@ -216,7 +324,10 @@ static char mt_get_ext(const uint32_t *e, uint32_t count, int dmin, double dyn_m
 typedef struct {
   uint32_t count;
   uint32_t l[4], r[4];
+  uint32_t from_ctg; /* KmerExtsCounts::from_ctg (kcount_cpu.cpp:191-196) */
 } mt_val;
+
+static char mt_ext_char(int code) { return code < 4 ? "ACGT"[code] : 'N'; }
 
 /* phase 2: count and finalize whole partitions (every record of a partition, from every thread) */
 static void *mt_count(void *arg) {
@@ -234,6 +345,7 @@ static void *mt_count(void *arg) {
     if (p < 0) break;
     uint64_t n = 0;
     for (int t = 0; t < sh->nthreads; t++) n += sh->w[t].bins[p].n;
+    if (sh->cbins) n += sh->cbins[p].n;
     if (!n) continue;
     uint64_t cap = 1024;
     while (cap < n + n / 2) cap <<= 1; /* distinct <= records: load <= 2/3 */
@@ -273,6 +385,56 @@ static void *mt_count(void *arg) {
         if ((e >> 3) < 4) v->l[e >> 3]++;
         if ((e & 7) < 4) v->r[e & 7]++;
         w->occ++;
+      }
+    }
+    /* the contig pass over this partition, in contig order, after every read (insert_supermer_from_ctg,
+     * kcount_cpu.cpp:356-406) */
+    const mt_cbin *cb = sh->cbins ? &sh->cbins[p] : NULL;
+    for (uint64_t i = 0; cb && i < cb->n; i++) {
+      const uint64_t *key = cb->keys + i * nl;
+      uint64_t s = (mt_hash(key, nl) * 0x9E3779B97F4A7C15ULL) >> 8 & (cap - 1);
+      int is_new = 0;
+      for (;;) {
+        if (!used[s]) {
+          used[s] = 1;
+          memcpy(tk + s * nl, key, 8 * (size_t)nl);
+          memset(&tv[s], 0, sizeof(mt_val));
+          w->distinct++;
+          is_new = 1;
+          break;
+        }
+        if (memcmp(tk + s * nl, key, 8 * (size_t)nl) == 0) break;
+        s = (s + 1) & (cap - 1);
+      }
+      mt_val *v = &tv[s];
+      const int l = cb->ext[i] >> 3, r = cb->ext[i] & 7;
+      uint32_t c = cb->depth[i];
+      int insert_it = 0;
+      if (is_new) {
+        insert_it = 1;
+      } else if (!v->from_ctg) { /* a read k-mer: replaced when it is a singleton or not UU */
+        const uint32_t vc = v->count > 65535 ? 65535 : v->count;
+        if (vc == 1) {
+          insert_it = 1;
+        } else {
+          const char L = mt_get_ext(v->l, vc, w->dmin, w->dyn_mult), R = mt_get_ext(v->r, vc, w->dmin, w->dyn_mult);
+          insert_it = L == 'X' || L == 'F' || R == 'X' || R == 'F';
+        }
+      } else if (v->count) { /* an earlier contig's k-mer: the lower depth, or 0 (purged) when they disagree */
+        insert_it = 1;
+        const char L = mt_get_ext(v->l, v->count, w->dmin, w->dyn_mult);
+        const char R = mt_get_ext(v->r, v->count, w->dmin, w->dyn_mult);
+        if (L != mt_ext_char(l) || R != mt_ext_char(r))
+          c = 0;
+        else if (v->count < c)
+          c = v->count;
+      }
+      if (insert_it) {
+        memset(v, 0, sizeof *v);
+        v->count = c;
+        v->from_ctg = 1;
+        if (l < 4) v->l[l] = c;
+        if (r < 4) v->r[r] = c;
       }
     }
     for (uint64_t s = 0; s < cap; s++) {
@@ -343,9 +505,10 @@ typedef struct {
 /* The part `range` of n_ranges of the table (the k-mers with mt_range(key) == range): a table too large for host
  * memory at once (C3: 1.28e10 occurrences) is built and compared one part at a time. Returns NULL on bad input (a
  * base code > 4: the reference DIEs) or allocation failure. */
-mt_table *orc_kcount_mt_range(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int k, int n_longs,
-                              int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads, int range,
-                              int n_ranges) {
+mt_table *orc_kcount_mt_ctgs_range(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, const char *ctg_chars,
+                                   const uint64_t *ctg_offs, const uint16_t *ctg_depths, uint64_t n_ctgs, int k,
+                                   int n_longs, int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads,
+                                   int range, int n_ranges) {
   const int nl = k / 32 + 1;
   if (k < 1 || k > 127 || k % 32 == 0 || n_longs < nl || n_longs > 8) return NULL;
   if (threads < 1) threads = 1;
@@ -372,13 +535,18 @@ mt_table *orc_kcount_mt_range(const uint8_t *bytes, const uint64_t *offs, uint64
   for (uint64_t r = 0; r < n_reads; r++)
     if (offs[r + 1] < offs[r] || offs[r + 1] - offs[r] > 65535) return NULL;
   for (int t = 0; t < threads; t++) pthread_create(&tid[t], NULL, mt_extract, &w[t]);
-  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
   int fail = 0;
+  mt_cbin *cbins = n_ctgs ? (mt_cbin *)calloc(MT_PARTS, sizeof(mt_cbin)) : NULL;
+  if (n_ctgs && (!cbins || !mt_ctg_records(ctg_chars, ctg_offs, ctg_depths, n_ctgs, k, nl, (uint32_t)range,
+                                           n_ranges < 1 ? 1u : (uint32_t)n_ranges, cbins)))
+    fail = 1;
+  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
   for (int t = 0; t < threads; t++) fail |= w[t].fail;
   mt_shared sh;
   sh.w = w;
   sh.nthreads = threads;
   sh.next_part = 0;
+  sh.cbins = cbins;
   pthread_mutex_init(&sh.lock, NULL);
   mt_arg *args = (mt_arg *)calloc((size_t)threads, sizeof(mt_arg));
   if (!args) fail = 1;
@@ -437,9 +605,24 @@ mt_table *orc_kcount_mt_range(const uint8_t *bytes, const uint64_t *offs, uint64
     free(w[t].out_l);
     free(w[t].out_r);
   }
+  if (cbins) {
+    for (int p = 0; p < MT_PARTS; p++) {
+      free(cbins[p].keys);
+      free(cbins[p].ext);
+      free(cbins[p].depth);
+    }
+    free(cbins);
+  }
   free(w);
   free(tid);
   return out;
+}
+
+mt_table *orc_kcount_mt_range(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int k, int n_longs,
+                              int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads, int range,
+                              int n_ranges) {
+  return orc_kcount_mt_ctgs_range(bytes, offs, n_reads, NULL, NULL, NULL, 0, k, n_longs, qual_cutoff, dmin_thres,
+                                  dyn_min_depth, threads, range, n_ranges);
 }
 
 /* The whole table (one range). */

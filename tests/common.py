@@ -47,12 +47,12 @@ def edge_case_set(seed: int = 5, n: int = 1500):
     return np.concatenate(out).astype(np.uint8), offs
 
 
-def hot_set(n_poly: int = 800, seed: int = 9):
+def hot_set(n_poly: int = 800, seed: int = 9, n_reads: int = 400, genome_len: int = 20000):
     """Enough poly-A reads that one canonical k-mer passes 65535 occurrences (u16 saturation) and its
-    extension counters pass the 0xC000 clamp of the LDS counters."""
-    b, o = synth_set(400, 20000, seed)
+    extension counters pass the 0xC000 clamp of the LDS counters (after n_reads random reads)."""
+    b, o = synth_set(n_reads, genome_len, seed)
     poly = np.full(150, 0 | (31 << 3), dtype=np.uint8)
-    reads = [b[o[i]:o[i + 1]] for i in range(400)] + [poly] * n_poly
+    reads = [b[o[i]:o[i + 1]] for i in range(n_reads)] + [poly] * n_poly
     lens = np.array([x.size for x in reads], dtype=np.uint64)
     offs = np.zeros(len(reads) + 1, dtype=np.uint64)
     np.cumsum(lens, out=offs[1:])
@@ -296,3 +296,41 @@ def paired_fastq_text(n_pairs: int, seed: int = 0, *, genome_len: int = 200_000,
                     "tab": f"@read{i}/{mate}\textra", "slash_comment": f"@read{i}/{mate} comment here"}[style]
             out.append(name.encode() + b"\n" + m.tobytes() + b"\n+\n" + q.tobytes() + b"\n")
     return b"".join(out)
+
+
+def paired_fastq_bulk(n_pairs: int, seed: int, genome_len: int, *, read_len: int = 150, frag_mean: int = 240,
+                      frag_sd: int = 40, subst: float = 0.005, n_rate: float = 0.001, low_q: float = 0.03,
+                      qual_offset: int = 33) -> bytes:
+    """paired_fastq_text's model at scale (vectorised, millions of pairs): fragments of a synthetic genome
+    (m.synth_genome) of read_len <= F <= 2 read_len + 60 bases, mate 1 its start, mate 2 the reverse complement of
+    its end, substitutions at random qualities, N bases, low-quality bases; names "@p<9 digits>/1" and "/2"."""
+    rng = np.random.default_rng(seed)
+    g = np.frombuffer(b"ACGT", dtype=np.uint8)[m.synth_genome(genome_len, seed).astype(np.int64) & 3]
+    comp = np.zeros(256, dtype=np.uint8)
+    for a, b in (b"AT", b"CG", b"GC", b"TA"):
+        comp[a] = b
+    L = read_len
+    F = np.clip(rng.normal(frag_mean, frag_sd, n_pairs), L, 2 * L + 60).astype(np.int64)
+    start = (rng.random(n_pairs) * (genome_len - F)).astype(np.int64)
+    col = np.arange(L, dtype=np.int64)
+    m1 = g[start[:, None] + col]
+    m2 = comp[g[(start + F - 1)[:, None] - col]]
+    recs = []
+    for mate, s in ((1, m1), (2, m2)):
+        q = rng.integers(30, 41, size=s.shape, dtype=np.uint8)
+        sub = rng.random(s.shape) < subst
+        s[sub] = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, size=int(sub.sum()))]
+        q[sub] = rng.integers(2, 41, size=int(sub.sum()), dtype=np.uint8)
+        s[rng.random(s.shape) < n_rate] = ord("N")
+        lq = rng.random(s.shape) < low_q
+        q[lq] = rng.integers(0, 12, size=int(lq.sum()), dtype=np.uint8)
+        name = np.empty((n_pairs, 14), dtype=np.uint8)  # "@p" + 9 digits + "/m" + "\n"
+        name[:, 0], name[:, 1] = ord("@"), ord("p")
+        idx = np.arange(n_pairs, dtype=np.int64)
+        for d in range(9):
+            name[:, 10 - d] = 48 + (idx // 10 ** d) % 10
+        name[:, 11], name[:, 12], name[:, 13] = ord("/"), 48 + mate, ord("\n")
+        nl = np.full((n_pairs, 1), ord("\n"), dtype=np.uint8)
+        plus = np.frombuffer(b"+\n", dtype=np.uint8)[None, :].repeat(n_pairs, 0)
+        recs.append(np.concatenate([name, s, nl, plus, (q + qual_offset).astype(np.uint8), nl], axis=1))
+    return np.stack(recs, axis=1).reshape(-1).tobytes()

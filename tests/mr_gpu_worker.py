@@ -46,11 +46,13 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
     elif opts.get("hot"):  # common.hot_set: random reads first, then the poly-A reads
         from common import hot_set
 
-        b, o = hot_set()
+        b, o = hot_set(**opts.get("hot_args", {}))
         seqs, depths = [], np.zeros(0, np.uint16)
     else:
         b, o = synth_set(opts.get("n_reads", 1200), opts.get("genome", 9000), opts["seed"])
         seqs, depths = [], np.zeros(0, np.uint16)
+    if "ctg_seqs" in opts:
+        seqs, depths = opts["ctg_seqs"], opts["ctg_depths"]
     n = o.size - 1
     lo, hi = shard(n, rank, world)
     if opts.get("cuts"):  # explicit read ranges: rank r takes [cuts[r], cuts[r + 1])
@@ -92,7 +94,8 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
              owned=st["owned_records"], count_sum=st["count_sum"], distinct=st["distinct"], purged=st["purged"],
              n_out=st["n_out"], handoff_sent=st["handoff_sent"], handoff_recv=st["handoff_recv"],
              ctg_kmers=st["ctg_kmers"], smer_count=st["smer_count"], smer_words=st["smer_words"],
-             xchg_rounds=st["xchg_rounds"], exact_reruns=st["exact_reruns"])
+             xchg_rounds=st["xchg_rounds"], exact_reruns=st["exact_reruns"], inc_rounds=st["inc_rounds"],
+             inc_fallbacks=st["inc_fallbacks"], inc_redone_coarse=st["inc_redone_coarse"])
     c.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -256,6 +259,92 @@ def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts:
     np.savez(Path(out_dir) / f"rank{rank}_stats.npz", seconds=t_count,
              **{key: st[key] for key in ("occurrences", "owned_records", "bytes_sent", "bytes_recv", "exact_reruns",
                                          "smer_count", "n_out", "distinct", "finish_passes", "out_reruns",
-                                         "device_bytes", "device_bytes_peak", "xchg_rounds", "ms_xchg")})
+                                         "device_bytes", "device_bytes_peak", "xchg_rounds", "ms_xchg",
+                                         "inc_rounds", "inc_fallbacks", "ms_finish_tail", "inc_redone_coarse")})
     dist.barrier()
+    dist.destroy_process_group()
+
+
+def read_ctgs(path):
+    """The contig file mhmkc_dbjg_traverse writes ("<seq> <uint16 depth>" lines): (seqs, depths)."""
+    seqs, depths = [], []
+    with open(path) as f:
+        for line in f:
+            s, d = line.split()
+            seqs.append(s)
+            depths.append(int(d))
+    return seqs, np.array(depths, dtype=np.uint16)
+
+
+def run_c5(rank: int, world: int, port: int, k_unused: int, out_dir: str, opts: dict):
+    """One rank of the C5-shaped multi-k chain (src/contigging.cpp:93-158, src/kcount/kcount.cpp:
+    100-138): the merged reads (out_dir/merged.npz, the device merge of the paired set, checked by the parent) sharded
+    over the ranks. For every k of opts["ks"] the rank counts its shard plus its block of the previous round's contigs
+    (add_ctg_kmers; the blocks in rank order are the traversal's order, the order the contig pass applies them in)
+    with opts["owner"] over RCCL (opts["rccl"]) or the host transport, and saves its rows; rank 0 then traverses the
+    union of the ranks' tables (the restated dbjg, tools/cpp/dbjg_lib.cpp) into out_dir/ctgs_k<next>.txt."""
+    import ctypes as C
+    import time
+
+    import torch.distributed as dist
+
+    import mhm2_proxy_amd as m
+
+    t0 = time.time()
+
+    def say(what):
+        print(f"[c5 rank {rank} {time.time() - t0:6.1f}s] {what}", flush=True)
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    z = np.load(Path(out_dir) / "merged.npz")
+    b, o = z["bytes"], z["offs"]
+    lo, hi = shard(o.size - 1, rank, world)
+    b, o = b[int(o[lo]):int(o[hi])].copy(), (o[lo:hi + 1] - o[lo]).astype(np.uint64)
+    owner = m.MHMKC_OWNER_MINIMIZER if opts.get("owner") == "minimizer" else m.MHMKC_OWNER_HASH
+    if opts.get("rccl"):
+        rccl_same_gpu_env(rank)
+    ks = opts["ks"]
+    for i, k in enumerate(ks):
+        if opts.get("rccl"):
+            obj = [m.comm_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, comm_id=obj[0], output_owner=owner)
+        else:
+            c = m.KmerCounter(k, device=0, rank=rank, n_ranks=world, transport=m.TorchDistTransport(),
+                              output_owner=owner)
+        c.add_packed_reads(b, o)
+        if i:
+            seqs, depths = read_ctgs(Path(out_dir) / f"ctgs_k{k}.txt")
+            a, e = shard(len(seqs), rank, world)
+            c.add_ctgs(seqs[a:e], depths[a:e])
+        c.finish()
+        t = c.fetch()
+        st = c.stats()
+        c.close()
+        nl = k // 32 + 1
+        np.savez(Path(out_dir) / f"k{k}_rank{rank}.npz", keys=np.ascontiguousarray(t.keys[:, :nl]), counts=t.counts,
+                 left=t.left, right=t.right, ctg_kmers=st["ctg_kmers"], bytes_sent=st["bytes_sent"],
+                 xchg_rounds=st["xchg_rounds"], smer_count=st["smer_count"])
+        say(f"k={k}: {len(t)} rows, {st['ctg_kmers']} contig k-mers")
+        del t
+        dist.barrier()
+        if rank == 0 and i + 1 < len(ks):
+            parts = [np.load(Path(out_dir) / f"k{k}_rank{r}.npz") for r in range(world)]
+            keys = np.ascontiguousarray(np.concatenate([p["keys"] for p in parts]), dtype=np.uint64)
+            counts = np.ascontiguousarray(np.concatenate([p["counts"] for p in parts]), dtype=np.uint16)
+            left = np.ascontiguousarray(np.concatenate([p["left"] for p in parts])).view(np.uint8)
+            right = np.ascontiguousarray(np.concatenate([p["right"] for p in parts])).view(np.uint8)
+            from mhm2_proxy_amd import build as B
+
+            L = C.CDLL(str(B.DBJG))
+            L.mhmkc_dbjg_traverse.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                              C.c_char_p]
+            L.mhmkc_dbjg_traverse.restype = C.c_int64
+            n_ctgs = L.mhmkc_dbjg_traverse(k, keys.ctypes.data, counts.ctypes.data, left.ctypes.data,
+                                           right.ctypes.data, keys.shape[0],
+                                           os.fsencode(str(Path(out_dir) / f"ctgs_k{ks[i + 1]}.txt")))
+            assert n_ctgs > 0, f"k={k}: traversal gave {n_ctgs}"
+            say(f"k={k}: traversed the union ({keys.shape[0]} rows) into {n_ctgs} contigs")
+        dist.barrier()
     dist.destroy_process_group()

@@ -50,6 +50,8 @@ def oracle() -> C.CDLL:
         L.orc_kcount_mt.restype = VP
         L.orc_kcount_mt_range.argtypes = [VP, VP, U64, I, I, I, I, C.c_double, I, I, I]
         L.orc_kcount_mt_range.restype = VP
+        L.orc_kcount_mt_ctgs_range.argtypes = [VP, VP, U64, C.c_char_p, VP, VP, U64, I, I, I, I, C.c_double, I, I, I]
+        L.orc_kcount_mt_ctgs_range.restype = VP
         L.orc_mt_ranges.argtypes = [VP, U64, I, I, I, VP]
         L.orc_mt_ranges.restype = None
         L.orc_row_fingerprints.argtypes = [VP, VP, VP, VP, U64, I, I, VP]
@@ -193,6 +195,21 @@ def kcount_ctgs(packed_bytes, offsets, ctg_seqs, ctg_depths, k, n_longs=None, qu
     d = np.ascontiguousarray(ctg_depths, dtype=np.uint16)
     ptr = oracle().orc_kcount_ctgs(b.ctypes.data, o.ctypes.data, o.size - 1, blob, co.ctypes.data, d.ctypes.data,
                                    len(ctg_seqs), k, nl, qual_cutoff, dmin_thres, dyn_min_depth)
+    return OracleTable(ptr, nl, k)
+
+
+def kcount_mt_ctgs(packed_bytes, offsets, ctg_blob: bytes, ctg_offs, ctg_depths, k, threads=8, part=0, n_parts=1,
+                   qual_cutoff=20, dmin_thres=2, dyn_min_depth=0.9) -> OracleTable:
+    """The multi-threaded restatement with the contig pass (oracle/kcount_mt.c orc_kcount_mt_ctgs_range): contigs
+    back to back in ctg_blob (ASCII, case = quality), ctg_offs their n + 1 offsets, in the order they are applied."""
+    nl = k // 32 + 1
+    b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    co = np.ascontiguousarray(ctg_offs, dtype=np.uint64)
+    d = np.ascontiguousarray(ctg_depths, dtype=np.uint16)
+    ptr = oracle().orc_kcount_mt_ctgs_range(b.ctypes.data, o.ctypes.data, o.size - 1, ctg_blob, co.ctypes.data,
+                                            d.ctypes.data, d.size, k, nl, qual_cutoff, dmin_thres, dyn_min_depth,
+                                            threads, part, n_parts)
     return OracleTable(ptr, nl, k)
 
 

@@ -196,6 +196,33 @@ def test_hot_kmer_on_one_rank(k, xpipe, rccl, tmp_path):
     assert int(parts[1]["exact_reruns"]) >= 1
 
 
+@pytest.mark.parametrize("k,ctgs", [(21, False), (33, False), (21, True)])
+def test_hot_kmer_incremental_redo(k, ctgs, tmp_path):
+    """The incremental partition with a skewed rank: 800 poly-A reads after 60k random reads, on
+    rank 1. The poly-A k-mer's fine bucket overflows its capped segment; k_inc_fixup empties that coarse bucket,
+    k_count skips it (and its contig k-mers), and the finish counts just it again with exact sizes; no full fallback.
+    The union equals the oracle."""
+    from common import hot_set
+
+    world, hot_args = 2, {"n_reads": 60000, "genome_len": 200000, "n_poly": 800, "seed": 4}
+    opts = {"hot": True, "hot_args": hot_args, "env": {"MHMKC_XPIPE": "1"}}
+    b, o = hot_set(**hot_args)
+    if ctgs:  # contigs over the hot range too: a skipped coarse bucket's contig k-mers wait for the redo
+        seqs = ["A" * 200, "A" * 30 + "CGTACGGATC" * 10, "T" * 90]
+        g = b[:5000] & 7
+        seqs += ["".join("ACGTN"[int(x)] for x in g[i:i + 400]) for i in range(0, 4000, 400)]
+        depths = np.array([5, 0, 300] + [7] * 10, dtype=np.uint16)
+        opts.update(ctg_seqs=seqs, ctg_depths=depths)
+        exp = oracle_ctg_table(b, o, seqs, depths, k)
+    else:
+        exp = oracle_table(b, o, k)
+    parts = run_ranks(k, world, tmp_path, seed=0, **opts)
+    check_parts(parts, k, exp, f"hot k-mer, incremental partition, k={k}, contigs={ctgs}")
+    assert all(int(p["inc_rounds"]) >= 2 and int(p["inc_fallbacks"]) == 0 for p in parts), \
+        [(int(p["inc_rounds"]), int(p["inc_fallbacks"])) for p in parts]
+    assert int(parts[1]["inc_redone_coarse"]) >= 1 and int(parts[0]["inc_redone_coarse"]) == 0
+
+
 @pytest.mark.parametrize("k,world,minimizer", [(21, 2, False), (63, 3, True), (33, 3, False)])
 def test_contigs_on_one_rank(k, world, minimizer, tmp_path):
     """every contig added on rank 0 only (the others add none): still applied in that one order
@@ -361,6 +388,10 @@ def test_rccl_eight_ranks_vs_cpu_restatement(k, owner, tmp_path):
     assert sum(int(s["bytes_sent"]) for s in stats) == sum(int(s["bytes_recv"]) for s in stats) > 0
     if owner == "hash":
         assert all(int(s["xchg_rounds"]) >= 2 for s in stats)  # the pipelined rounds ran
+        # ... and were fine-partitioned as they landed, with no fallback to the finish's partition
+        assert all(int(s["inc_rounds"]) >= 2 and int(s["inc_fallbacks"]) == 0 for s in stats), \
+            [(int(s["inc_rounds"]), int(s["inc_fallbacks"]), int(s["inc_redone_coarse"]))
+             for s in stats]
     fps = np.sort(np.concatenate([np.load(tmp_path / f"rank{r}_fps.npy") for r in range(world)]))
     g = m.synth_genome(genome, 8)
     b, o = m.synth_reads(g, world * R, 150, 8, threads=16)

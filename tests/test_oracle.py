@@ -263,6 +263,25 @@ def test_mt_range_parts_union_is_the_table(k, parts):
     assert not np.array_equal(np.sort(O.row_fingerprints(keys, c2, lft, rgt, k)), fw)
 
 
+@pytest.mark.parametrize("k,dmin", [(21, 2), (33, 2), (63, 3), (99, 2), (21, 1)])
+def test_mt_contig_pass_equals_oracle(k, dmin):
+    """kcount_mt's contig pass (the C5-shaped multi-k check's reference, tests/test_c5_scale.py) == the single-threaded
+    restatement (orc_kcount_ctgs, itself pinned to tests/ref_literal.py above) on common.ctg_set: duplicates at other
+    depths (min rule), mutated copies (disagreeing contigs purged, read k-mers replaced), novel keys, N bases,
+    lowercase, contigs shorter than k + 2, depths 0 to 65535; whole, and built in 3 key-range parts."""
+    for seed in (31, 32):
+        b, o, seqs, depths = ctg_set(seed=seed + k, n_reads=400)
+        exp = np.sort(O.row_fingerprints(*O.kcount_ctgs(b, o, seqs, depths, k, dmin_thres=dmin).fetch(), k))
+        blob = "".join(seqs).encode("ascii")
+        co = np.zeros(len(seqs) + 1, dtype=np.uint64)
+        np.cumsum([len(s) for s in seqs], out=co[1:])
+        got = O.kcount_mt_ctgs(b, o, blob, co, depths, k, threads=3, dmin_thres=dmin).fetch()
+        assert np.array_equal(np.sort(O.row_fingerprints(*got, k)), exp)
+        parts = [O.row_fingerprints(*O.kcount_mt_ctgs(b, o, blob, co, depths, k, threads=2, part=p, n_parts=3,
+                                                      dmin_thres=dmin).fetch(), k) for p in range(3)]
+        assert np.array_equal(np.sort(np.concatenate(parts)), exp)
+
+
 @pytest.mark.parametrize("k,world", [(21, 8), (63, 8), (77, 3)])
 def test_batch_target_ranks(k, world):
     b, o = synth_set(400, 5000, 720 + k)
