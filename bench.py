@@ -609,7 +609,7 @@ def main():
                           # the incremental fine partition: rounds partitioned as they landed, and
                           # the device time from the last transfer's end to the finished table
                           "inc_rounds_rank0": st["inc_rounds"], "inc_fallbacks_rank0": st["inc_fallbacks"],
-                          "inc_redone_coarse_rank0": st["inc_redone_coarse"],
+                          "inc_redone_coarse_rank0": st["inc_redone_coarse"], "inc_slack_rank0": round(st["inc_slack"], 3),
                           "ms_finish_tail_rank0": round(st["ms_finish_tail"], 3),
                           "GBps_rank0": round(st["bytes_sent"] / (per_step["exchange"] * 1e-3) / 1e9, 2)
                           if per_step.get("exchange") else None}

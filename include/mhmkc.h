@@ -133,6 +133,7 @@ typedef struct {
   uint64_t inc_fallbacks;  /* ... finishes whose incremental count failed and were redone from the sources */
   double ms_finish_tail;   /* device time from the last transfer's end (or finish's start) to the finished table */
   uint64_t inc_redone_coarse; /* ... coarse buckets whose capped fine layout overflowed (skew), counted again exactly */
+  double inc_slack;           /* ... the capped fine buckets' slack over their expected records (0.25 .. 2) */
 } mhmkc_stats;
 
 enum {

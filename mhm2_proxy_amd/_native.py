@@ -120,6 +120,7 @@ class MhmkcStats(C.Structure):
         ("inc_fallbacks", C.c_uint64),
         ("ms_finish_tail", C.c_double),
         ("inc_redone_coarse", C.c_uint64),
+        ("inc_slack", C.c_double),
     ]
 
     def as_dict(self) -> dict:

@@ -1445,12 +1445,15 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParam
 // It also counts the extension adds of these records (the LDS op mix of k_count, reported in the stats as
 // a sample of the whole).
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(kPThreads<NL>()) void k_sketch(PartitionParams p, unsigned int *hll) {
+__global__ __launch_bounds__(kPThreads<NL>()) void k_sketch(PartitionParams p, unsigned int *hll, unsigned int *fhist) {
   constexpr int NT = kPThreads<NL>(), T = kPTile<NL>(), W = T / NT;
   __shared__ unsigned int reg[SKETCH_M];
+  __shared__ unsigned int fh[SKETCH_FH];
   __shared__ unsigned int s_ext;
   if (threadIdx.x == 0) s_ext = 0;
   for (int i = threadIdx.x; i < SKETCH_M; i += NT) reg[i] = 0;
+  if (fhist)
+    for (int i = threadIdx.x; i < SKETCH_FH; i += NT) fh[i] = 0;
   const SChunk ch = chunk_of<T>(p, blockIdx.x);
   const PlaneSet src = p.srcs[ch.src];
   uint64_t rk[W][NL];
@@ -1468,9 +1471,13 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_sketch(PartitionParams p, u
     for (int w = 0; w < NL; w++) h = fmix64(h ^ (w == RecKind<NL, CMP>::XW ? rk[j][w] & ~low_mask : rk[j][w]));
     const uint32_t rho = (uint32_t)__clzll(h | (uint64_t)(SKETCH_M - 1)) + 1;  // first 1 among the top bits
     atomicMax(&reg[h & (SKETCH_M - 1)], rho);
+    if (fhist) atomicAdd(&fh[fine_digit<NL, PACKED, CMP>(rk[j], p)], 1u);
   }
   atomicAdd(&s_ext, ext_adds);
   __syncthreads();
+  if (fhist)
+    for (int i = threadIdx.x; i < SKETCH_FH; i += NT)
+      if (fh[i]) atomicAdd(&fhist[i], fh[i]);
   for (int i = threadIdx.x; i < SKETCH_M; i += NT)
     if (reg[i]) {
       atomicMax(&hll[i], reg[i]);
@@ -2886,16 +2893,17 @@ hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_
 }
 
 template <int NL, bool PK, bool CMP = false>
-static hipError_t do_sketch(const PartitionParams &p, uint32_t n, unsigned int *hll, hipStream_t s) {
-  k_sketch<NL, PK, CMP><<<dim3(n), dim3(kPThreads<NL>()), 0, s>>>(p, hll);
+static hipError_t do_sketch(const PartitionParams &p, uint32_t n, unsigned int *hll, bool fh, hipStream_t s) {
+  k_sketch<NL, PK, CMP><<<dim3(n), dim3(kPThreads<NL>()), 0, s>>>(p, hll, fh ? hll + SKETCH_WORDS : nullptr);
   return hipGetLastError();
 }
 
 hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
-                         hipStream_t s) {
+                         hipStream_t s, bool fine_hist) {
   if (!n_chunks) return hipSuccess;
-  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_sketch, (p, n_chunks, hll, s));
-  MHM_DISPATCH(nl, packed, do_sketch, (p, n_chunks, hll, s));
+  if (fine_hist && p.fine_bits != SKETCH_FB) return hipErrorInvalidValue;
+  if (p.compact) return MHM_DISPATCH_MIXED(nl, do_sketch, (p, n_chunks, hll, fine_hist, s));
+  MHM_DISPATCH(nl, packed, do_sketch, (p, n_chunks, hll, fine_hist, s));
 }
 
 hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor, uint32_t n,

@@ -302,11 +302,14 @@ hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hi
 // HyperLogLog sketch of the distinct keys in chunks [0, n_chunks) of p's chunk table (one coarse bucket):
 // hll[SKETCH_M] registers, max-merged, and hll[SKETCH_M] += the records' extension adds; hll[SKETCH_M + 1 ..
 // 2 SKETCH_M + 1) the registers of the even-numbered chunks alone (a second sample point for the growth of the distinct
-// keys with the records). Zero all 2 SKETCH_M + 1 words first.
+// keys with the records). Zero all 2 SKETCH_M + 1 words first. fine_hist (p.fine_bits =
+// SKETCH_FB): also the records per fine digit, hll[SKETCH_WORDS ..) (SKETCH_FH more words, zeroed too), from which the
+// incremental layout learns how unevenly the records fall on fine buckets (a key's copies all land in one).
 constexpr int SKETCH_M = 1024;
 constexpr int SKETCH_WORDS = 2 * SKETCH_M + 1;
+constexpr int SKETCH_FB = 11, SKETCH_FH = 1 << SKETCH_FB;
 hipError_t launch_sketch(const PartitionParams &p, uint32_t n_chunks, unsigned int *hll, int nl, bool packed,
-                         hipStream_t s);
+                         hipStream_t s, bool fine_hist = false);
 hipError_t launch_scan(const unsigned long long *in, unsigned long long *base, unsigned long long *cursor,
                        uint32_t n, hipStream_t s);
 hipError_t launch_count(const CountParams &p, int nl, bool packed, hipStream_t s);

@@ -243,7 +243,7 @@ struct mhmkc {
   // pipelined exchange (xpipe): slabs [0, xq) have been sent, one round per slab, on xstream while
   // the next slab is extracted; received records land in parts [0, n_parts)
   bool xpipe = false;
-  int xpieces = 4;  // a device batch is cut into this many slabs (so that there is a next slab to overlap)
+  int xpieces = 8;  // a device batch is cut into this many slabs (so that there is a next slab to overlap)
   hipStream_t xstream = nullptr;
   std::vector<RecvPart *> parts;
   size_t n_parts = 0, xq = 0;
@@ -278,7 +278,8 @@ struct mhmkc {
   int finish_inc(bool &done, uint64_t *n_out_ret);
   void make_runs(const std::vector<Source> &srcs, uint32_t c0, uint32_t c1, int T, RunTable &rt) const;
   int upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_t s, mhm::PartitionParams &pp);
-  int fine_layout(const std::vector<uint64_t> &per_coarse, std::vector<uint64_t> &cfit, uint64_t &r2_size) const;
+  int fine_layout(const std::vector<uint64_t> &per_coarse, double slack, std::vector<uint64_t> &cfit,
+                  uint64_t &r2_size) const;
   int pump();
   int resolve_one(Slab *sl, bool &redo);
   std::vector<hipEvent_t> chunk_ev;  // one per H2D chunk in flight (pool)
@@ -292,6 +293,7 @@ struct mhmkc {
   DevBuf d_spill;  // k_count: the deferred records of cold sweeps, mhm::SPILL_RECORDS per persistent workgroup
   DevBuf d_cfit;   // capped fine layout: per coarse bucket of the pass its first record and fine-bucket capacity
   DevBuf d_inc_skip;  // incremental count: per owned coarse bucket, 1 = overflowed its capped layout (k_inc_fixup)
+  double inc_slack = 0;  // the incremental layout's fine-bucket slack (inc_setup)
   // supermer exchange (smer): owner bytes of a slab's tiles; the received supermers (codes, good bits, descriptors),
   // their window counts / prefix, per-tile first supermer, scan scratch
   bool smer = false;
@@ -1627,14 +1629,15 @@ int mhmkc::upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_
 }
 
 // The capped fine layout of coarse buckets with these (expected) record counts: every fine bucket of coarse bucket c
-// gets 1.25x its share + 256 records (multiples of 16: k_count loads compact records in quads).
-int mhmkc::fine_layout(const std::vector<uint64_t> &per_coarse, std::vector<uint64_t> &cfit, uint64_t &r2_size) const {
+// gets (1 + slack) x its share + 256 records (multiples of 16: k_count loads compact records in quads).
+int mhmkc::fine_layout(const std::vector<uint64_t> &per_coarse, double slack, std::vector<uint64_t> &cfit,
+                       uint64_t &r2_size) const {
   const size_t np_ = per_coarse.size();
   cfit.assign(2 * np_, 0);  // [coarse_base | coarse_fcap]
   r2_size = 0;
   for (size_t c = 0; c < np_; c++) {
     const uint64_t ex = per_coarse[c] >> fb;
-    const uint64_t fcap = align_up(ex + ex / 4 + 256, 16);
+    const uint64_t fcap = align_up(ex + (uint64_t)((double)ex * slack) + 256, 16);
     cfit[c] = r2_size;
     cfit[np_ + c] = fcap;
     r2_size += fcap << fb;
@@ -1686,20 +1689,23 @@ int mhmkc::inc_setup() {
   if ((e = hipStreamWaitEvent(pstream, x_ev[1], 0)) != hipSuccess) return hip_fail(e, "partition stream");
   int rc = upload_runs(sk.rt, sk.chunks, sk.srcs, pstream, sp);
   if (rc) return rc;
-  std::vector<uint32_t> reg(mhm::SKETCH_WORDS);
+  // (the records per fine digit too, at SKETCH_FB bits, when the stored key bits below the coarse digit have them)
+  const bool fh_ok = !(compact && 2 * k - cb < mhm::SKETCH_FB) && !(mixed2 && k - cb < mhm::SKETCH_FB);
+  const size_t words = mhm::SKETCH_WORDS + (size_t)mhm::SKETCH_FH;
+  std::vector<uint32_t> reg(words);
+  if (fh_ok) sp.fine_bits = mhm::SKETCH_FB;
   prof_begin(MHMKC_STAGE_OTHER, pstream);
-  if ((e = d_hll.ensure(4 * mhm::SKETCH_WORDS + 64)) != hipSuccess ||
-      (e = hipMemsetAsync(d_hll.p, 0, 4 * mhm::SKETCH_WORDS, pstream)) != hipSuccess ||
-      (e = mhm::launch_sketch(sp, (uint32_t)sk.rt.n_c0, d_hll.as<unsigned int>(), nl, packed, pstream)) != hipSuccess)
+  if ((e = d_hll.ensure(4 * words + 64)) != hipSuccess || (e = hipMemsetAsync(d_hll.p, 0, 4 * words, pstream)) != hipSuccess ||
+      (e = mhm::launch_sketch(sp, (uint32_t)sk.rt.n_c0, d_hll.as<unsigned int>(), nl, packed, pstream, fh_ok)) != hipSuccess)
     return hip_fail(e, "distinct sketch");
   prof_end(pstream);
-  if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * mhm::SKETCH_WORDS, hipMemcpyDeviceToHost, pstream)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(reg.data(), d_hll.p, 4 * words, hipMemcpyDeviceToHost, pstream)) != hipSuccess ||
       (e = hipStreamSynchronize(pstream)) != hipSuccess)
     return hip_fail(e, "sketch D2H");
   sk.chunks.release();
   sk.srcs.release();
   const double d_f = hll_estimate(std::vector<uint32_t>(reg.begin(), reg.begin() + mhm::SKETCH_M));
-  const double d_h = hll_estimate(std::vector<uint32_t>(reg.begin() + mhm::SKETCH_M + 1, reg.end()));
+  const double d_h = hll_estimate(std::vector<uint32_t>(reg.begin() + mhm::SKETCH_M + 1, reg.begin() + mhm::SKETCH_WORDS));
   const double n_f = (double)sk.rt.rec_c0, n_h = (double)sk.rt.rec_c0_even;
   inc_ext_per_rec = (double)reg[mhm::SKETCH_M] / n_f;
   // the expected records of every owned coarse bucket (at least what round 0 brought)
@@ -1715,8 +1721,27 @@ int mhmkc::inc_setup() {
   if (g_dbg.fine_bits >= 0) f = (int)std::min<int64_t>(11, g_dbg.fine_bits);
   fb = std::max(f, min_fine_bits());
   nf = 1u << fb;
+  // The slack of the capped fine buckets: a key's copies all land in one fine bucket, so at high coverage the buckets'
+  // loads spread wider than the record count alone says (small buckets most: a test's 1000-record buckets of 24
+  // genome k-mers x 40 copies). The sampled coarse bucket's loads per fine bucket (without its fullest, where a very
+  // frequent k-mer would sit) give their coefficient of variation; 5 of it, at least 1/4, at most 2.
+  double slack = 0.25;
+  if (fh_ok) {
+    const uint32_t G = 1u << fb, per = 1u << (mhm::SKETCH_FB - fb);
+    std::vector<double> ld(G, 0.0);
+    for (uint32_t i = 0; i < (uint32_t)mhm::SKETCH_FH; i++) ld[i / per] += reg[mhm::SKETCH_WORDS + i];
+    std::sort(ld.begin(), ld.end());
+    ld.pop_back();
+    double m = 0, v = 0;
+    for (double x : ld) m += x;
+    m /= (double)ld.size();
+    for (double x : ld) v += (x - m) * (x - m);
+    v /= (double)ld.size();
+    if (m > 0) slack = std::min(2.0, std::max(0.25, 5.0 * std::sqrt(v) / m));
+  }
+  inc_slack = slack;
   uint64_t r2_size = 0;
-  fine_layout(per_coarse, inc_cfit, r2_size);
+  fine_layout(per_coarse, slack, inc_cfit, r2_size);
   // room for it (the finish then needs no more than the output and k_count's spill area)
   size_t fr = 0, tot = 0;
   const double rec_b = compact ? 4.0 : (double)rec_bytes();
@@ -1908,6 +1933,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     const uint32_t n_fine = no << fb;
     nf = 1u << fb;
     st.distinct_estimate = (uint64_t)inc_distinct;
+    st.inc_slack = inc_slack;
     st.lds_ext_adds = (uint64_t)(inc_ext_per_rec * (double)owned);
     if ((rc = prepare_ctgs())) return rc;
     out_cap = std::min<uint64_t>(owned / 2, (uint64_t)(0.5 * inc_distinct) + (1u << 20));
@@ -3128,7 +3154,7 @@ int mhmkc_set_transport(mhmkc_t h, const mhmkc_transport *t) {
   h->has_xp = true;
   // A host-staged transport moves a few GB/s, so the last exchange round (the one no extraction overlaps) is
   // what a step waits for: cut the batch finer (2 ranks, C2: 252 -> 57 ms exposed for 4 % more bytes, DESIGN.md
-  // §3.5e). RCCL over xGMI keeps 4 pieces, where the pieces' slack bytes cost more than their overlap gains.
+  // §3.5e). RCCL over xGMI takes 8 (the sends carry no slack since round 5, §3.5f).
   if (!getenv("MHMKC_XPIECES")) h->xpieces = 16;
   return MHMKC_OK;
 }

@@ -95,7 +95,7 @@ def run(rank: int, world: int, port: int, k: int, out_dir: str, opts: dict):
              n_out=st["n_out"], handoff_sent=st["handoff_sent"], handoff_recv=st["handoff_recv"],
              ctg_kmers=st["ctg_kmers"], smer_count=st["smer_count"], smer_words=st["smer_words"],
              xchg_rounds=st["xchg_rounds"], exact_reruns=st["exact_reruns"], inc_rounds=st["inc_rounds"],
-             inc_fallbacks=st["inc_fallbacks"], inc_redone_coarse=st["inc_redone_coarse"])
+             inc_fallbacks=st["inc_fallbacks"], inc_redone_coarse=st["inc_redone_coarse"], inc_slack=st["inc_slack"])
     c.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -260,7 +260,7 @@ def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts:
              **{key: st[key] for key in ("occurrences", "owned_records", "bytes_sent", "bytes_recv", "exact_reruns",
                                          "smer_count", "n_out", "distinct", "finish_passes", "out_reruns",
                                          "device_bytes", "device_bytes_peak", "xchg_rounds", "ms_xchg",
-                                         "inc_rounds", "inc_fallbacks", "ms_finish_tail", "inc_redone_coarse")})
+                                         "inc_rounds", "inc_fallbacks", "ms_finish_tail", "inc_redone_coarse", "inc_slack")})
     dist.barrier()
     dist.destroy_process_group()
 

@@ -220,7 +220,8 @@ def test_hot_kmer_incremental_redo(k, ctgs, tmp_path):
     check_parts(parts, k, exp, f"hot k-mer, incremental partition, k={k}, contigs={ctgs}")
     assert all(int(p["inc_rounds"]) >= 2 and int(p["inc_fallbacks"]) == 0 for p in parts), \
         [(int(p["inc_rounds"]), int(p["inc_fallbacks"])) for p in parts]
-    assert int(parts[1]["inc_redone_coarse"]) >= 1 and int(parts[0]["inc_redone_coarse"]) == 0
+    # the poly-A k-mer's coarse bucket is redone on its owner; the other buckets fit their slack
+    assert 1 <= sum(int(p["inc_redone_coarse"]) for p in parts) <= 2, [int(p["inc_redone_coarse"]) for p in parts]
 
 
 @pytest.mark.parametrize("k,world,minimizer", [(21, 2, False), (63, 3, True), (33, 3, False)])
