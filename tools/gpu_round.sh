@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r05}
 MARK=${MARK:-"gpu and not slow"}
-timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest tests -x -v -m "$MARK" --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
+timeout -k 10 ${TEST_LIMIT:-900} python -u -m pytest tests -x -v -m "$MARK" --timeout 170 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1; rc=$?
 echo "pytest exit $rc" >> gpurun_out/pytest_gpu_$TAG.log
 tail -5 gpurun_out/pytest_gpu_$TAG.log
 # test failures (1) still allow the measurements; a crash, abort or time limit ends the call
