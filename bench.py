@@ -454,6 +454,11 @@ def main():
                                    "lds_TBps": round(lds_b / (ms_launch * 1e-3) / 1e12, 3),
                                    "ops": {"records": st["owned_records"], "phase_b_records": st["lds_misses"],
                                            "ext_adds": st["lds_ext_adds"]}}}
+        # the issue roofline beside it: the fraction of the kernel's cycles its SIMDs spent issuing VALU instructions
+        # (PMC, tools/pmc_traffic.py); extraction and counting are issue-bound, not HBM-bound
+        valu = pmc.get("valu_issue_frac", {}).get(stage)
+        if valu is not None:
+            extra["valu_issue_frac"] = valu
         return {"bound": "hbm", "kernel": "k_" + stage, "achieved": hbm["achieved"], "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": hbm["frac"], "traffic": traffic, "traffic_source": pmc.get("source"),
                 "algorithmic_bytes": int(alg), "avg_launch_ms": round(ms_launch, 4), **extra}

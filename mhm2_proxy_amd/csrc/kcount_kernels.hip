@@ -360,6 +360,37 @@ struct WalkSpan {
     e_r = (lr << 3) | rr;  // reverse complement: complemented and swapped
     return (last < lp) && (lp + k < end) && (lp > beg);
   }
+  // The validity of all W windows at once (W + k + 1 <= 64): window i is valid iff no read starts in
+  // [lp0 + i, lp0 + i + k] (then `last` < lp in step) and it is inside the data. One OR-window of width k + 1 over the
+  // span's read-start bits (log steps) replaces step's per-window start test, compare and select (the extraction is
+  // VALU-issue bound).
+  __device__ __forceinline__ uint32_t valid_mask(const uint32_t *start, int k) const {
+    const uint64_t X = __brevll(((uint64_t)bits32(start, lp0) << 32) | bits32(start, lp0 + 32));  // bit j: lp0 + j
+    uint64_t A = X | (X >> 1);
+    A |= A >> 2;
+    A |= A >> 4;  // bit j: a start in [j, j + 8)
+    const int w = k + 1;
+    if (w > 16) {
+      A |= A >> 8;
+      A |= A >> (w - 16);
+    } else {
+      A |= A >> (w - 8);
+    }
+    uint32_t m = ~(uint32_t)A;
+    const int hi = end - lp0 - k, lo = beg - lp0;  // valid iff lo < i < hi
+    m &= hi >= 32 ? ~0u : hi <= 0 ? 0u : (1u << hi) - 1u;
+    m &= lo < 0 ? ~0u : lo >= 31 ? 0u : ~0u << (lo + 1);
+    return m;
+  }
+  // step without the validity (valid_mask)
+  __device__ __forceinline__ void step_ext(int i, uint32_t &cr, uint32_t &e_f, uint32_t &e_r) {
+    cr = (uint32_t)(incoming >> (62 - 2 * i)) & 3u;
+    const bool gl = (gl_bits >> (31 - i)) & 1u, gr = (gr_bits >> (31 - i)) & 1u;
+    const uint32_t l = gl ? cl : (uint32_t)EXT_NONE, r = gr ? cr : (uint32_t)EXT_NONE;
+    const uint32_t lr = gr ? cr ^ 3u : (uint32_t)EXT_NONE, rr = gl ? cl ^ 3u : (uint32_t)EXT_NONE;
+    e_f = (l << 3) | r;
+    e_r = (lr << 3) | rr;
+  }
 };
 
 // Compact-record walk (10 <= k <= 21, §3.7): the windows of walk_windows with the key kept right-aligned in its
@@ -378,10 +409,13 @@ __device__ __forceinline__ void walk_c32_lh(const uint64_t *fwd, const uint32_t 
   const uint64_t mB = (1ull << B) - 1, rmask = (1ull << rb) - 1;
   uint64_t fw = WalkSpan<1>::codes64(fwd, sp.lp0) >> (64 - B);
   uint64_t rc = rev2(~fw) >> (64 - B);
+  static_assert(W + 21 + 1 <= 64, "valid_mask covers the span");
+  const uint32_t vm = sp.valid_mask(start, k);
 #pragma unroll
   for (int i = 0; i < W; i++) {
     uint32_t cr, e_f, e_r;
-    const bool valid = sp.step(i, k, cr, e_f, e_r);
+    sp.step_ext(i, cr, e_f, e_r);
+    const bool valid = (vm >> i) & 1u;
     const bool use_rc = rc < fw;
     const uint64_t x = use_rc ? rc : fw;
     const uint32_t e = use_rc ? e_r : e_f;
