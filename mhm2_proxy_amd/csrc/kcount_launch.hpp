@@ -245,11 +245,11 @@ inline int tile_bases(int nl) { return TILE_BASES[nl]; }
 // threads of an extract workgroup (tile_bases / threads windows each); four-word keys: 8 windows per thread at 256
 // threads and 128 VGPRs fit four workgroups per CU (512 threads: 13.23 ms, 256: 10.04 ms at k = 99)
 constexpr int E_THREADS_NL[5] = {0, 256, 256, 256, 256};
-// records per partition chunk and threads per partition workgroup; three- and four-word keys take longer chunks over
-// more threads (the chunk's runs per fine bucket grow, the LDS per wave stays; four-word: the staged chunk + 2048
-// bins' counters fit 160 KB)
-constexpr int P_TILE[5] = {0, 4096, 2048, 4096, 3072};
-constexpr int P_THREADS[5] = {0, 256, 256, 512, 512};
+// records per partition chunk and threads per partition workgroup; two-, three- and four-word keys take longer chunks
+// over more threads (the chunk's runs per fine bucket grow, the LDS per wave stays; four-word: the staged chunk + 2048
+// bins' counters fit 160 KB; two-word 3072 over 512: k = 63 5.59 -> 5.50 ms, k = 33 7.49 -> 7.33)
+constexpr int P_TILE[5] = {0, 4096, 3072, 4096, 3072};
+constexpr int P_THREADS[5] = {0, 256, 512, 512, 512};
 inline int chunk_records(int nl) { return P_TILE[nl]; }
 // LDS hash-table slots of the count kernel for NL words per key (~143 KB of LDS); compact records keep
 // 32-bit keys (the stored bits of the mixed key), 24 bytes per slot instead of 28.
