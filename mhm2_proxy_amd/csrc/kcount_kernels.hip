@@ -382,6 +382,28 @@ struct WalkSpan {
     m &= lo < 0 ? ~0u : lo >= 31 ? 0u : ~0u << (lo + 1);
     return m;
   }
+  // valid_mask for 32 < k < 64 (two-word keys: W + k + 1 <= 80 positions): the OR-window over the span's first 64
+  // positions, and a start at lp0 + 64 + j in the next 32 invalidates the windows i >= 64 + j - k
+  __device__ __forceinline__ uint32_t valid_mask_wide(const uint32_t *start, int k) const {
+    const uint64_t X = __brevll(((uint64_t)bits32(start, lp0) << 32) | bits32(start, lp0 + 32));
+    uint64_t A = X | (X >> 1);
+    A |= A >> 2;
+    A |= A >> 4;
+    A |= A >> 8;
+    A |= A >> 16;  // bit j: a start in [j, j + 32)
+    A |= A >> (k + 1 - 32);
+    uint32_t P = __brev(bits32(start, lp0 + 64));  // bit j: a start at lp0 + 64 + j
+    P |= P << 1;
+    P |= P << 2;
+    P |= P << 4;
+    P |= P << 8;
+    P |= P << 16;  // bit j: a start in [lp0 + 64, lp0 + 64 + j]
+    uint32_t m = ~(uint32_t)(A | ((uint64_t)P << (64 - k)));
+    const int hi = end - lp0 - k, lo = beg - lp0;
+    m &= hi >= 32 ? ~0u : hi <= 0 ? 0u : (1u << hi) - 1u;
+    m &= lo < 0 ? ~0u : lo >= 31 ? 0u : ~0u << (lo + 1);
+    return m;
+  }
   // step without the validity (valid_mask)
   __device__ __forceinline__ void step_ext(int i, uint32_t &cr, uint32_t &e_f, uint32_t &e_r) {
     cr = (uint32_t)(incoming >> (62 - 2 * i)) & 3u;
@@ -454,10 +476,13 @@ __device__ __forceinline__ void walk_m2(const uint64_t *fwd, const uint32_t *goo
     rL = rw[0] >> (64 - k);
     rR = ((rw[0] << (2 * k - 64)) | (rw[1] >> (128 - 2 * k))) & mk;
   }
+  static_assert(W + 63 + 1 <= 96, "valid_mask_wide covers the span");
+  const uint32_t vm = sp.valid_mask_wide(start, k);
 #pragma unroll
   for (int i = 0; i < W; i++) {
     uint32_t cr, e_f, e_r;
-    const bool valid = sp.step(i, k, cr, e_f, e_r);
+    sp.step_ext(i, cr, e_f, e_r);
+    const bool valid = (vm >> i) & 1u;
     const bool use_rc = (rL < fL) | ((rL == fL) & (rR < fR));
     uint64_t L = use_rc ? rL : fL, R = use_rc ? rR : fR;
     const uint32_t e = use_rc ? e_r : e_f;
