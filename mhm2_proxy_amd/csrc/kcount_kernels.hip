@@ -682,7 +682,7 @@ __host__ __device__ constexpr size_t staged_area_bytes(int nl, int T, bool packe
 // CAP < W * NT: the stage area holds CAP records and the records go out in rounds of CAP (bin order), so a
 // workgroup whose windows are mostly not counted (k = 77, 99 on 150-base reads: 48 %, 33 % counted) needs LDS for
 // the records it has, not for one per window.
-template <int NL, bool PACKED, int W, int SF, int NT = E_THREADS, int CAP = W * NT>
+template <int NL, bool PACKED, int W, int SF, int NT = E_THREADS, int CAP = W * NT, int BPT = 8>  // BPT: as scatter_staged_c40
 __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], const uint32_t (&inf)[W], uint32_t nb,
                                                unsigned char *smem, unsigned char *area,
                                                unsigned long long *cursor, uint32_t cstride, const PlaneSet &out,
@@ -705,10 +705,10 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   // Reserve each bin's run in the global layout. The returned offsets stay in registers while the bins are
   // scanned and the records staged, so the atomics' round trip overlaps that LDS work (a bin count up to
   // SCATTER_MAX_BINS = 8 * NT).
-  unsigned long long off[8];
-  uint32_t cnt[8];
+  unsigned long long off[BPT];
+  uint32_t cnt[BPT];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < BPT; i++) {
     const uint32_t b = threadIdx.x + i * NT;
     off[i] = 0;
     cnt[i] = 0;
@@ -747,7 +747,7 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   // recomputing the segment end (a 64-bit multiply per record)
   if (r0 == 0) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < BPT; i++) {
     const uint32_t b = threadIdx.x + i * NT;
     if (b < nb) {
       const bool over = lim.cap && cnt[i] && off[i] + cnt[i] > lim.end(b);
@@ -784,7 +784,8 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
 
 // scatter_staged for compact 40-bit records held as lo / hi words (walk_c32_lh): the window's rank in its bin
 // goes into hi's free bits 19..30 instead of a register of its own (bins <= 2048, T <= 4096).
-template <int W, int NT, bool HB = true>  // HB: the record's top byte goes to the ext plane (false: u32 records)
+template <int W, int NT, bool HB = true, int BPT = 8>  // HB: the record's top byte goes to the ext plane (false: u32
+// records); BPT: bins per thread, nb <= BPT * NT (1: the usual 256 fine bins over 256 threads in 21 fewer VGPRs)
 __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (&hi)[W], uint32_t nb,
                                                    unsigned char *smem, unsigned char *area,
                                                    unsigned long long *cursor, const PlaneSet &out,
@@ -802,10 +803,10 @@ __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (
   for (int j = 0; j < W; j++)
     if (hi[j] >> 31) hi[j] |= atomicAdd(&lcnt[hi[j] & 0x7ffu], 1u) << 19;
   __syncthreads();
-  unsigned long long off[8];
-  uint32_t cnt[8];
+  unsigned long long off[BPT];
+  uint32_t cnt[BPT];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < BPT; i++) {
     const uint32_t b = threadIdx.x + i * NT;
     off[i] = 0;
     cnt[i] = 0;
@@ -829,7 +830,7 @@ __device__ __forceinline__ void scatter_staged_c40(uint32_t (&lo)[W], uint32_t (
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < BPT; i++) {
     const uint32_t b = threadIdx.x + i * NT;
     if (b < nb) {
       const bool over = lim.cap && cnt[i] && off[i] + cnt[i] > lim.end(b);
@@ -873,7 +874,7 @@ constexpr int kEWaves() {
   return NL == 4 ? 4 : 1;
 }
 
-template <int NL, bool PACKED, bool CMP>
+template <int NL, bool PACKED, bool CMP, int BPT = 8>
 __global__ __launch_bounds__(kEThreads<NL>()) __attribute__((amdgpu_waves_per_eu(kEWaves<NL>()))) void k_extract_scatter(ExtractParams p) {
   constexpr int ET = kEThreads<NL>(), T = kTile<NL>(), W = T / ET;
   const int kk = p.k;
@@ -895,7 +896,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) __attribute__((amdgpu_waves_per_eu
   if constexpr (RecKind<NL, CMP>::C32) {
     uint32_t lo[W], hi[W];
     walk_c32_lh<W>(fwd, good, start, tile, p.reads.n_bases, p.reads.head, kk, p.coarse_bits, lo, hi);
-    scatter_staged_c40<W, ET>(lo, hi, p.n_bins, smem, area, p.cursor + sub * p.n_bins, p.out, lim, p.ovf);
+    scatter_staged_c40<W, ET, true, BPT>(lo, hi, p.n_bins, smem, area, p.cursor + sub * p.n_bins, p.out, lim, p.ovf);
     return;
   }
   uint64_t rk[W][NL];
@@ -931,7 +932,7 @@ __global__ __launch_bounds__(kEThreads<NL>()) __attribute__((amdgpu_waves_per_eu
                      });
   }
   constexpr int SF = RecKind<NL, CMP>::M2 ? SF_AOS2 : SF_WORDS;
-  scatter_staged<NL, PACKED, W, SF, ET, kECap<NL>()>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1,
+  scatter_staged<NL, PACKED, W, SF, ET, kECap<NL>(), BPT>(rk, inf, p.n_bins, smem, area, p.cursor + sub * p.n_bins, 1,
                                                      p.out, lim, p.ovf);
 }
 
@@ -1431,7 +1432,7 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_part_hist(PartitionParams p
   }
 }
 
-template <int NL, bool PACKED, bool CMP>
+template <int NL, bool PACKED, bool CMP, int BPT = 8>
 __global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParams p) {
   constexpr int NT = kPThreads<NL>(), T = kPTile<NL>(), W = T / NT;
   static_assert(T % NT == 0 && NT % 64 == 0, "whole records per thread, whole waves");
@@ -1468,7 +1469,7 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParam
       lim = BinLimit{p.coarse_base[ch.coarse_local], fc, fc};
     }
     __syncthreads();
-    scatter_staged_c40<W, NT, false>(lo, hi, nf, smem, smem + staged_cnt_bytes(nf),
+    scatter_staged_c40<W, NT, false, BPT>(lo, hi, nf, smem, smem + staged_cnt_bytes(nf),
                                      p.fine_cursor + (uint64_t)ch.coarse_local * nf, p.out, lim, p.err);
     return;
   }
@@ -1494,7 +1495,7 @@ __global__ __launch_bounds__(kPThreads<NL>()) void k_part_scatter(PartitionParam
   }
   unsigned long long *cur = p.fine_cursor + (uint64_t)ch.coarse_local * nf;
   constexpr int SF = RecKind<NL, CMP>::M2 ? SF_AOS2 : SF_WORDS;
-  scatter_staged<NL, PACKED, W, SF, NT>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
+  scatter_staged<NL, PACKED, W, SF, NT, W * NT, BPT>(rk, inf, nf, smem, smem + staged_cnt_bytes(nf), cur, 1, p.out, lim, p.err);
 }
 
 // Distinct-key sketch (HyperLogLog, SKETCH_M registers) over the records of one coarse bucket, from which
@@ -2820,6 +2821,12 @@ static hipError_t do_extract_scatter(const ExtractParams &p, hipStream_t s) {
   const size_t lds = staged_cnt_bytes(p.n_bins) +
                      std::max(tile_lds_bytes<NL>(),
                               staged_area_bytes(NL, kECap<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C40 : SF_WORDS));
+  if (p.n_bins <= (uint32_t)kEThreads<NL>()) {  // one coarse bin per thread (one rank: 256 bins), see do_part_scatter
+    hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP, 1>, lds);
+    if (e != hipSuccess) return e;
+    k_extract_scatter<NL, PK, CMP, 1><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p);
+    return hipGetLastError();
+  }
   hipError_t e = allow_lds(k_extract_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
   k_extract_scatter<NL, PK, CMP><<<dim3(p.n_tiles), dim3(kEThreads<NL>()), lds, s>>>(p);
@@ -2839,6 +2846,14 @@ template <int NL, bool PK, bool CMP = false>
 static hipError_t do_part_scatter(const PartitionParams &p, hipStream_t s) {
   const uint32_t nf = 1u << p.fine_bits;
   const size_t lds = staged_cnt_bytes(nf) + staged_area_bytes(NL, kPTile<NL>(), PK, RecKind<NL, CMP>::C32 ? SF_C32 : SF_WORDS);
+  // one fine bin per thread when the launch has no more, not the eight of the most (the bin registers: five
+  // workgroups per CU at k = 21, part_scatter 2.64 -> 2.45 ms; two bins per thread at k = 63 measured 5.46 -> 5.55)
+  if (nf <= (uint32_t)kPThreads<NL>()) {
+    hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP, 1>, lds);
+    if (e != hipSuccess) return e;
+    k_part_scatter<NL, PK, CMP, 1><<<dim3(p.grid), dim3(kPThreads<NL>()), lds, s>>>(p);
+    return hipGetLastError();
+  }
   hipError_t e = allow_lds(k_part_scatter<NL, PK, CMP>, lds);
   if (e != hipSuccess) return e;
   k_part_scatter<NL, PK, CMP><<<dim3(p.grid), dim3(kPThreads<NL>()), lds, s>>>(p);
