@@ -2125,6 +2125,17 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
+  // The finalize keeps its survivors' key words in registers (one- to three-word keys; four key words would
+  // hold SPT x NL x 2 more VGPRs) when the slots it lists fit KJ per thread, so that it clears the table while the
+  // output reservation is in flight; a bucket with more listed slots writes its output from the table first.
+#ifndef MHMKC_KREG_NL
+#define MHMKC_KREG_NL 3
+#endif
+#ifndef MHMKC_KJ
+#define MHMKC_KJ 2
+#endif
+  constexpr bool KREG = NL <= MHMKC_KREG_NL;
+  constexpr int KJ = KREG ? (MHMKC_KJ < SPT ? MHMKC_KJ : SPT) : 1;
 
 #define tid (count_tid<NL>())  // (see count_tid; #undef after the kernel)
 #define lane (count_tid<NL>() & 63)
@@ -2237,10 +2248,32 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #if MHMKC_STAMP
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
 #endif
-  if (tid == 0) {  // (the first sweep's clear ends with a barrier)
+  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
+  auto clear_table = [&]() {
+    uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
+    const int n_ones = t.cap * (int)sizeof(K) / 16;
+    for (int i = tid; i < n_ones; i += C_THREADS) ones[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    uint4 *zeros = (uint4 *)t.cnt;
+    const int n_zeros = t.cap * 20 / 16;
+    for (int i = tid; i < n_zeros; i += C_THREADS) zeros[i] = make_uint4(0, 0, 0, 0);
+  };
+  // a sweep's scalars: deferral counters, dynamic slot counter, error flag
+  auto reset_sweep = [&]() {
+    if (tid == 0) {
+      s_ovf = 0;
+      s_err = 0;
+      s_next = 2 * (C_THREADS / 64);  // (slots s and 16 + s are wave s's own: already prefetched / next)
+    }
+    if (tid < C_THREADS / 64) s_wdef[tid] = 0;
+  };
+  if (tid == 0) {
     s_missacc = 0;
     s_u64[3] = 0;  // finalize's counters
   }
+  // the first sweep's table; every later sweep's is cleared by the finalize before it
+  clear_table();
+  reset_sweep();
+  __syncthreads();
   // this workgroup's spill area (dynamic sweeps: their deferred records; the sweep after reads them from there)
   const Src spill{(uint64_t)blockIdx.x * SPILL_RECORDS, 1u};
   const bool has_spill = p.spill.w[0] != nullptr;
@@ -2269,26 +2302,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // a dependent round trip there (unconditional: without a next bucket it re-reads this bucket's, never used)
   const uint32_t b_ext = b_next < p.n_buckets ? b_next : b;
   const uint64_t nx_base = p.bucket_base[b_ext], nx_end = p.bucket_end[b_ext];
-  while (true) {  // sweeps of bucket b
-    STAMP(t_sw0);
-    {  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
-      uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
-      const int n_ones = t.cap * (int)sizeof(K) / 16;
-      for (int i = tid; i < n_ones; i += C_THREADS) ones[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
-      uint4 *zeros = (uint4 *)t.cnt;
-      const int n_zeros = t.cap * 20 / 16;
-      for (int i = tid; i < n_zeros; i += C_THREADS) zeros[i] = make_uint4(0, 0, 0, 0);
-    }
-    if (tid == 0) {
-      s_ovf = 0;
-      s_err = 0;
-    }
-    if (tid < C_THREADS / 64) s_wdef[tid] = 0;
-    if (tid == 0) s_next = 2 * (C_THREADS / 64);  // (slots s and 16 + s are wave s's own: already prefetched / next)
-    __syncthreads();
-    STAMP(t_sw1);
-    STAMP_ADD(0, t_sw1 - t_sw0);
-
+  while (true) {  // sweeps of bucket b (the table is clear and the sweep's scalars reset)
     // R records per thread per round, the next round prefetched into registers, so that every CU keeps
     // R * 8 KB of record loads in flight. A round has two phases:
     //   A. every lane looks its records up in their home group; found keys are counted at once, a new key with an
@@ -2563,6 +2577,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP_ADD(3, t_f0 - t_b0);  // (the sweep's end barrier: the waves' imbalance; cold sweeps have no round barrier)
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
+    // what a next sweep of this bucket needs, read before the finalize resets the sweep's scalars
+    const uint32_t n_def = s_ovf;
+    const bool err_sw = s_err != 0;
+    uint32_t nw_def = 0, mx_def = 0;
+    if (!last_sweep) {
+      nw_def = s_wdef[wid];
+#pragma unroll
+      for (int w = 0; w < C_THREADS / 64; w++) mx_def = mx_def > s_wdef[w] ? mx_def : s_wdef[w];
+      // this wave's deferred records (global stores of the rounds) are released before the finalize's barriers; the
+      // next sweep's loads acquire them after the last one
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    }
     // (a skipped coarse bucket's fine buckets are empty, k_inc_fixup, and its contig k-mers wait for the launch
     // that counts it)
     if (p.ctg_n && !(p.coarse_skip && p.coarse_skip[b >> p.fine_bits])) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
@@ -2631,19 +2657,28 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     }
     __syncthreads();
     const uint32_t n_list = s_fin[0];
-    uint32_t surv_mask = 0, spos[SPT];
-    uint16_t c16[SPT], fslot[SPT];
-    char L[SPT], R_[SPT];
+    // per listed slot of this thread: sp = slot | output position << 16 (both < 2^16), row = count | L << 16 | R << 24
+    uint32_t surv_mask = 0, sp[SPT], row[SPT];
+    // (uniform) the survivors' key words go to registers: the table may be cleared before the output is written
+    const bool kfast = KREG && n_list <= (uint32_t)(KJ * C_THREADS);
+    K kreg[KJ][NL];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
       const uint32_t i = (uint32_t)tid + (uint32_t)j * C_THREADS;
-      spos[j] = 0;
-      fslot[j] = 0;
+      sp[j] = 0;
+      row[j] = 0;
       bool sv = false;
       if (i < n_list) {
         const int slot = flist[i];
-        fslot[j] = (uint16_t)slot;
-        sv = slot_survives(t, slot, p, slot_count(t, slot, cold), c16[j], L[j], R_[j]);
+        sp[j] = (uint32_t)slot;
+        uint16_t c16;
+        char L, R_;
+        sv = slot_survives(t, slot, p, slot_count(t, slot, cold), c16, L, R_);
+        row[j] = (uint32_t)c16 | (uint32_t)(uint8_t)L << 16 | (uint32_t)(uint8_t)R_ << 24;
+        if (KREG && j < KJ && sv) {
+#pragma unroll
+          for (int w = 0; w < NL; w++) kreg[j < KJ ? j : 0][w] = t.keys[w * t.cap + slot];
+        }
       }
       // one reservation per wave for its survivors (ballot + lane prefix)
       const uint64_t bal = __ballot(sv);
@@ -2653,15 +2688,27 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         sb = __builtin_amdgcn_readfirstlane(sb);
         if (sv) {
           surv_mask |= 1u << j;
-          spos[j] = sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          sp[j] |= (sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))) << 16;
         }
       }
     }
     const uint32_t mine = __popc(surv_mask);
     __syncthreads();
+    // The survivors take one global reservation. With their key words in registers (kfast) the table is cleared for
+    // the next sweep while it is in flight, and the output rows are written after one barrier with the next sweep's
+    // rounds right behind them (two barriers fewer per bucket than clearing at the sweep's start).
+    unsigned long long gret = 0;
+    uint32_t acc = 0;
     if (tid == 0) {
-      const uint32_t acc = s_fin[1];
-      unsigned long long gb = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      acc = s_fin[1];
+      if (acc) gret = atomicAdd(p.out_cursor, (unsigned long long)acc);
+    }
+    STAMP(t_c0);
+    if (kfast) clear_table();
+    STAMP(t_c1);
+    reset_sweep();  // (every thread read what it needs of the sweep's scalars above)
+    if (tid == 0) {
+      unsigned long long gb = gret;
       if (acc && gb + acc > p.out_cap) {  // the output is full: write nothing, flag the launch (the cursor still
         atomicOr(p.err, 16u);             // counts: the host grows the output to it and redoes the pass)
         gb = ~0ull;
@@ -2676,49 +2723,56 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
       if ((surv_mask >> j) & 1u) {
-        const int slot = fslot[j];
-        const unsigned long long g = s_gbase + spos[j];
+        const int slot = (int)(sp[j] & 0xffffu);
+        // the key words: from registers (kfast: every listed slot is one of a thread's first KJ) or from the table
+        auto kw_of = [&](int w) -> K { return (KREG && j < KJ && kfast) ? kreg[j < KJ ? j : 0][w] : t.keys[w * t.cap + slot]; };
+        const unsigned long long g = s_gbase + (sp[j] >> 16);
         uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
         if (RK::C32) {  // key = cunmix(global fine bucket digits | stored bits)
           const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
-          const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (kw_of(0) >> EXT_BITS);
           ok[0] = cunmix(y, B) << (64 - B);
         } else if (RK::M2) {  // key = m2_unmix(global fine bucket digits | stored L' bits, R')
           const int rb = p.k - p.coarse_bits - p.fine_bits;
-          const uint64_t L = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          const uint64_t L = ((uint64_t)(p.bucket0 + b) << rb) | (kw_of(0) >> EXT_BITS);
           uint64_t kw[2];
-          m2_unmix(L, t.keys[t.cap + slot], p.k, kw);
+          m2_unmix(L, kw_of(1), p.k, kw);
           ok[0] = kw[0];
           ok[1] = kw[1];
         } else if (RK::MX) {  // key = mx_unmix(global fine bucket digits | stored w0' bits, r[1..])
           const int rb = 64 - p.coarse_bits - p.fine_bits;
           uint64_t r[NL], kw[NL];
-          r[0] = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          r[0] = ((uint64_t)(p.bucket0 + b) << rb) | (kw_of(0) >> EXT_BITS);
 #pragma unroll
-          for (int w = 1; w < NL; w++) r[w] = t.keys[w * t.cap + slot];
+          for (int w = 1; w < NL; w++) r[w] = kw_of(w);
           mx_unmix<NL>(r, kw);
 #pragma unroll
           for (int w = 0; w < NL; w++) ok[w] = kw[w];
         } else {
 #pragma unroll
-          for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
+          for (int w = 0; w < NL; w++) ok[w] = kw_of(w);
         }
         for (int w = NL; w < p.nlo; w++) ok[w] = 0;
-        p.out_counts[g] = c16[j];
-        p.out_left[g] = L[j];
-        p.out_right[g] = R_[j];
+        p.out_counts[g] = (uint16_t)row[j];
+        p.out_left[g] = (char)(row[j] >> 16);
+        p.out_right[g] = (char)(row[j] >> 24);
       }
     }
     my_occ += occ;
     my_purged += occ;  // minus the survivors, in 64 bits: with two passes a lane's survivors are not its slots
     my_purged -= mine;
     my_sum += sum;
-    __syncthreads();
+    if (!kfast) {  // the output read the table: clear it after
+      __syncthreads();
+      clear_table();
+      __syncthreads();
+    }
     STAMP(t_f1);
-    STAMP_ADD(5, t_f1 - t_f0);
-    if (s_err && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
+    STAMP_ADD(0, t_c1 - t_c0);
+    STAMP_ADD(5, t_f1 - t_f0 - (t_c1 - t_c0));
+    if (err_sw && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
     if (last_sweep) break;
-    n = s_ovf;
+    n = n_def;
     lim = n;
     if (dyn_sweep) {  // the deferred records, dense in pd, are the next sweep's; the region it read takes its deferrals
       const Src t_ = ps;
@@ -2726,19 +2780,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       pd = t_;
       nw = NONE;
     } else {  // each wave re-reads its own deferred records; the rounds cover the largest share
-      nw = s_wdef[wid];
-      uint32_t mx = 0;
-#pragma unroll
-      for (int w = 0; w < C_THREADS / 64; w++) mx = mx > s_wdef[w] ? mx : s_wdef[w];
-      lim = (mx + (uint32_t)(64 * R) - 1) / (uint32_t)(64 * R) * RND;
+      nw = nw_def;
+      lim = (mx_def + (uint32_t)(64 * R) - 1) / (uint32_t)(64 * R) * RND;
     }
     my_sweeps++;
-    // overflow records were written by this workgroup: make them visible to its own loads
+    // the deferred records of every wave (released before the finalize's barriers) are visible to this wave's loads
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    __syncthreads();
   }  // sweeps
   if (b_next >= p.n_buckets) break;
-  b = b_next;  // the finalize above ended with a barrier: the table may be cleared for the next bucket
+  b = b_next;  // (the finalize cleared the table for the next bucket)
   ps = ps_next;
   n = nb_next;
   pd = spill;
