@@ -2247,6 +2247,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned long long &s_missacc = s_u64[4];  // phase-B records of this workgroup (the LDS op mix, stats)
 #if MHMKC_STAMP
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+  const uint64_t st_wg0 = __builtin_amdgcn_s_memtime();
 #endif
   // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
   auto clear_table = [&]() {
@@ -2798,6 +2799,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #if MHMKC_STAMP
   if (lane == 0)
     for (int i = 0; i < 6; i++) atomicAdd(&p.stats[8 + i], (unsigned long long)st_acc[i]);
+  if (tid == 0) {  // the workgroup's cycles: sum and largest (the launch's tail)
+    const uint64_t el = __builtin_amdgcn_s_memtime() - st_wg0;
+    atomicAdd(&p.stats[14], (unsigned long long)el);
+    atomicMax(&p.stats[15], (unsigned long long)el);
+  }
 #endif
   // block reduction of the statistics
   my_occ = wave_sum_u64(my_occ);

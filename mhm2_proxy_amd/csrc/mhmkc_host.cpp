@@ -2263,7 +2263,8 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     for (int i = 0; i < 6; i++) tot += (double)acc_stats[8 + i];
     fprintf(stderr, "k_count stamps:");
     for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f%%", names[i], tot > 0 ? 100.0 * acc_stats[8 + i] / tot : 0.0);
-    fprintf(stderr, " (total %.3g wave-cycles)\n", tot);
+    fprintf(stderr, " (total %.3g wave-cycles); workgroup cycles mean %.4g max %.4g\n", tot,
+            (double)acc_stats[14] / std::max(1, n_cu), (double)acc_stats[15]);
   }
 #endif
   st.distinct = acc_stats[mhm::STAT_DISTINCT];
