@@ -1912,18 +1912,15 @@ __device__ __forceinline__ void lds_clamp(const CountLds<K> &t, int slot, uint32
 #define STAMP_ADD(i, v)
 #endif
 
-// Final decision for one table slot: insert_into_local_hashtable (src/kcount/kcount_cpu.cpp:503-517):
-// count < 2 -> purged; left/right = get_ext(count) (kcount_cpu.cpp:173-182, with the exact double
-// expression of the dynamic threshold); both 'X' -> purged.
-template <typename K>
-__device__ __forceinline__ bool slot_survives(const CountLds<K> &t, int slot, const CountParams &p, uint32_t c32,
-                                              uint16_t &c16, char &L, char &R) {
+// Final decision for one listed table slot (count >= 2): insert_into_local_hashtable
+// (src/kcount/kcount_cpu.cpp:503-517): left/right = get_ext(count) (kcount_cpu.cpp:173-182, with the exact double
+// expression of the dynamic threshold); both 'X' -> purged. The caller reads the slot's count word and its four
+// extension words together (one LDS round trip: a listed slot always has count >= 2, so nothing waits for the count).
+__device__ __forceinline__ bool slot_survives(uint32_t c32, uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3,
+                                              const CountParams &p, uint16_t &c16, char &L, char &R) {
   const uint32_t c = c32 > 65535u ? 65535u : c32;
   c16 = (uint16_t)c;
-  if (c < 2) return false;
   const int thr = dyn_threshold(c, p.dyn_mult, p.dmin_thres);
-  const uint32_t e0 = t.ext[slot], e1 = t.ext[t.cap + slot];
-  const uint32_t e2 = t.ext[2 * t.cap + slot], e3 = t.ext[3 * t.cap + slot];
   L = ext_choice(e0 & 0xffffu, e0 >> 16, e1 & 0xffffu, e1 >> 16, thr);
   R = ext_choice(e2 & 0xffffu, e2 >> 16, e3 & 0xffffu, e3 >> 16, thr);
   return !(L == 'X' && R == 'X');
@@ -2674,12 +2671,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         sp[j] = (uint32_t)slot;
         uint16_t c16;
         char L, R_;
-        sv = slot_survives(t, slot, p, slot_count(t, slot, cold), c16, L, R_);
-        row[j] = (uint32_t)c16 | (uint32_t)(uint8_t)L << 16 | (uint32_t)(uint8_t)R_ << 24;
-        if (KREG && j < KJ && sv) {
+        const uint32_t cw = t.cnt[slot], e0 = t.ext[slot], e1 = t.ext[t.cap + slot], e2 = t.ext[2 * t.cap + slot],
+                       e3 = t.ext[3 * t.cap + slot];
+        if (KREG && j < KJ) {  // (with the counters: the same round trip)
 #pragma unroll
           for (int w = 0; w < NL; w++) kreg[j < KJ ? j : 0][w] = t.keys[w * t.cap + slot];
         }
+        // slot_count's cold encoding from the words already read
+        const uint32_t c32 = !cold ? cw
+                             : (cw >> 31) ? cw & 0x7fffffffu
+                                          : cw + (e0 & 0xffffu) + (e0 >> 16) + (e1 & 0xffffu) + (e1 >> 16);
+        sv = slot_survives(c32, e0, e1, e2, e3, p, c16, L, R_);
+        row[j] = (uint32_t)c16 | (uint32_t)(uint8_t)L << 16 | (uint32_t)(uint8_t)R_ << 24;
       }
       // one reservation per wave for its survivors (ballot + lane prefix)
       const uint64_t bal = __ballot(sv);
