@@ -71,6 +71,8 @@ def parse():
                          "in blocks into pinned memory, each block parsed and counted while the next is read "
                          "(mhmkc_add_fastq_file): the step includes the file read and the H2D")
     ap.add_argument("--no-profile-events", action="store_true")
+    ap.add_argument("--profile-level", type=int, choices=(1, 2), default=None,
+                    help="stage events: 1 every stage, 2 the heavy stages (default for packed input)")
     ap.add_argument("--no-kmermap", dest="kmermap", action="store_false",
                     help="skip timing the hand-off into the C++ adapter's KmerMap")
     ap.add_argument("--transport", choices=("rccl", "host", "rccl-same-gpu"), default="rccl",
@@ -378,7 +380,11 @@ def main():
     counter = m.KmerCounter(k, device=local, rank=rank, n_ranks=world, comm_id=cid,
                             transport=m.TorchDistTransport() if host_xp else None,
                             output_owner=m.MHMKC_OWNER_MINIMIZER if args.owner == "minimizer" else m.MHMKC_OWNER_HASH)
-    counter.set_profiling(not args.no_profile_events)
+    # events around the heavy stages only (each event record is a marker the next launch waits behind: all stages
+    # measured 0.07-0.2 ms per step slower than none)
+    # (FASTQ inputs time their ingest as stage "other": every stage)
+    counter.set_profiling(0 if args.no_profile_events else args.profile_level if args.profile_level is not None
+                          else 1 if args.input != "packed" else 2)
 
     def step():
         counter.reset()
@@ -570,7 +576,11 @@ def main():
             "roofline": roofline,
             "rooflines": rooflines,
             "cpu_baseline": cpu,
-            "stages_ms_per_step": {s_: round(v, 3) for s_, v in per_step.items() if launches.get(s_)},
+            # (events around the heavy stages only, mhmkc_set_profiling level 2: "rest" is the step's time outside
+            # them: the tile index, layouts, small copies and the host's turns between launches)
+            "stages_ms_per_step": {**{s_: round(v, 3) for s_, v in per_step.items() if launches.get(s_)},
+                                   "rest": round(elapsed / steps * 1e3 - sum(v for s_, v in per_step.items()
+                                                                            if launches.get(s_)), 3)},
             "achieved_measured_GBps_whole_step": round(
                 sum(pmc["per_launch_bytes"][s_] * launches[s_] / steps for s_ in launched
                     if s_ not in ("other", "tileidx")) / (elapsed / steps) / 1e9, 1)

@@ -334,7 +334,8 @@ struct mhmkc {
   bool partial = false;  // a failed mhmkc_add_fastq_file left part of a file in the round (finish refuses it)
   uint64_t n_out = 0;
   mhmkc_stats st{};
-  bool profiling = false;
+  int profiling = 0;        // mhmkc_set_profiling: 0 off, 1 every stage, 2 the heavy stages
+  bool prof_open = false;   // the last prof_begin recorded its event (its prof_end records the other)
   std::vector<Prof> prof;
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_begin = nullptr, ev_end = nullptr, ev_h2d0 = nullptr, ev_h2d1 = nullptr;
@@ -363,14 +364,18 @@ struct mhmkc {
     (void)hipEventCreate(&e);
     return e;
   }
+  // profiling 1: every stage; 2: the heavy stages only (extraction, partition, exchange, count), so that the timed
+  // region carries few event records (each one a marker the next launch waits behind)
   void prof_begin(int stage, hipStream_t s = nullptr) {
-    if (!profiling) return;
+    prof_open = profiling == 1 || (profiling == 2 && stage != MHMKC_STAGE_TILEIDX && stage != MHMKC_STAGE_OTHER);
+    if (!prof_open) return;
     Prof p{stage, take_event(), take_event()};
     (void)hipEventRecord(p.a, s ? s : stream);
     prof.push_back(p);
   }
   void prof_end(hipStream_t s = nullptr) {
-    if (!profiling || prof.empty()) return;
+    if (!prof_open || prof.empty()) return;
+    prof_open = false;
     (void)hipEventRecord(prof.back().b, s ? s : stream);
   }
   void prof_collect() {
@@ -3305,7 +3310,7 @@ int mhmkc_reset(mhmkc_t h) {
 
 int mhmkc_set_profiling(mhmkc_t h, int on) {
   if (!h) return MHMKC_EINVAL;
-  h->profiling = on != 0;
+  h->profiling = on <= 0 ? 0 : on == 2 ? 2 : 1;
   return MHMKC_OK;
 }
 

@@ -455,8 +455,9 @@ class KmerCounter:
         self._check(N.lib().mhmkc_reset(self._h))
         self.n_out = None
 
-    def set_profiling(self, on: bool = True) -> None:
-        self._check(N.lib().mhmkc_set_profiling(self._h, 1 if on else 0))
+    def set_profiling(self, on: "bool | int" = True) -> None:
+        """Per-stage event timing (stats()["ms_kernel"]): True / 1 every stage, 2 the heavy stages only, False off."""
+        self._check(N.lib().mhmkc_set_profiling(self._h, int(on) if on is not True else 1))
 
 
 class TorchDistTransport:
