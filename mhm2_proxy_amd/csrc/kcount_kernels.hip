@@ -141,6 +141,9 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
   const int64_t gA = (int64_t)tile * (T / 32) - 1;
   for (int g = threadIdx.x; g < NG; g += blockDim.x) {
     const int64_t gi = gA + g;
+    // the group's read-start word first, so that its load is in flight with the bases' (issued after them it was
+    // a second global round trip per tile: the bases' loads are waited for and decoded before it)
+    const uint32_t sw = tile_starts ? gload(tile_starts + (uint64_t)tile * NG + g) : 0u;
     uint64_t f = 0;
     uint32_t gd = 0;
     if (gi >= 0 && (uint64_t)gi * 32 < rv.n_bases) {
@@ -184,7 +187,7 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
     }
     fwd[g] = f;
     good[g] = gd;
-    start[g] = tile_starts ? gload(tile_starts + (uint64_t)tile * NG + g) : 0u;
+    start[g] = sw;
   }
   __syncthreads();
   if (tile_starts) return;  // (uniform) the bitmap came precomputed: no dependent load of the tile's first read
@@ -1350,24 +1353,27 @@ __device__ __forceinline__ bool xcd_chunk(const PartitionParams &p, uint32_t &c)
   return c < p.xcd_start[x + 1];
 }
 
-// The chunk a partition workgroup works on: its run from the per-chunk run index, then its tile of it.
+// The chunk a partition workgroup works on: one 24-byte load of the span k_chunk_runs expanded (the run index and
+// then the run cost two dependent global round trips before the chunk's records could be loaded).
 template <int T>
 __device__ __forceinline__ SChunk chunk_of(const PartitionParams &p, uint32_t c) {
-  const SRun r = p.runs[p.chunk_run[c]];
-  const uint64_t o = (uint64_t)(c - r.chunk0) * T;
-  SChunk ch;
-  ch.start = r.start + o;
-  ch.count = (uint32_t)(r.count - o < (uint64_t)T ? r.count - o : (uint64_t)T);
-  ch.src = r.src;
-  ch.coarse_local = r.coarse_local;
-  ch.pad = 0;
-  return ch;
+  return p.chunks[c];
 }
 
-__global__ __launch_bounds__(256) void k_chunk_runs(const SRun *runs, uint32_t *chunk_run, int tile) {
+// Every run's chunks (one workgroup per run): chunk i of a run is records [i T, min((i + 1) T, count)) of it.
+__global__ __launch_bounds__(256) void k_chunk_runs(const SRun *runs, SChunk *chunks, int tile) {
   const SRun r = runs[blockIdx.x];
   const uint32_t n = (uint32_t)((r.count + tile - 1) / tile);
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) chunk_run[r.chunk0 + i] = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint64_t o = (uint64_t)i * tile;
+    SChunk ch;
+    ch.start = r.start + o;
+    ch.count = (uint32_t)(r.count - o < (uint64_t)tile ? r.count - o : (uint64_t)tile);
+    ch.src = r.src;
+    ch.coarse_local = r.coarse_local;
+    ch.pad = 0;
+    chunks[r.chunk0 + i] = ch;
+  }
 }
 
 // All W records of a thread are loaded before any is processed (W * 8 B * NL in flight per lane). The
@@ -1672,6 +1678,16 @@ struct CountLds {
   uint32_t *ext;   // [4][cap]: (A|C<<16, G|T<<16) left, then right
   int cap;         // multiple of 4: slots are probed in groups of 4
 };
+
+// An LDS fetch-add whose result is used later (k_count's dynamic slot counter, read at the end of the round): the
+// address goes through an opaque move, so the atomic optimizer does not expand the add for a uniform address (a
+// reduction over the active lanes that waits for the result at once: an LDS round trip at the top of every round).
+typedef __attribute__((address_space(3))) unsigned int lds_u32_t;
+__device__ __forceinline__ uint32_t lds_add_late(unsigned int *p, uint32_t v) {
+  lds_u32_t *q = (lds_u32_t *)p;
+  asm volatile("" : "+v"(q));
+  return __hip_atomic_fetch_add(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Groups a key may probe before its record is deferred to the next sweep of its bucket.
 constexpr int C_PROBE = 64;
@@ -2327,7 +2343,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         uint64_t ck[R][NL];
         uint32_t ce[R];
         uint32_t ca = 0;  // DYN: the slot after cn (lane 0 asks now, the answer is read at the end of the round)
-        if (DYN && lane == 0) ca = atomicAdd(&s_next, 1u);
+        if (DYN && lane == 0) ca = lds_add_late(&s_next, 1u);
         const uint32_t cr0 = DYN ? cc / NWV * RND : r0;                              // the slot's round
         const uint32_t vt = DYN ? cc % NWV * 64u + (uint32_t)lane : (uint32_t)tid;  // its thread slot
         // record j of this lane is valid iff j * vstep < vrem: the records left from this lane's first one (a dense
@@ -3019,9 +3035,9 @@ hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hi
   MHM_DISPATCH(nl, packed, do_part_scatter, (p, s));
 }
 
-hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_run, int tile, hipStream_t s) {
+hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, SChunk *chunks, int tile, hipStream_t s) {
   if (!n_runs) return hipSuccess;
-  k_chunk_runs<<<dim3(n_runs), dim3(256), 0, s>>>(runs, chunk_run, tile);
+  k_chunk_runs<<<dim3(n_runs), dim3(256), 0, s>>>(runs, chunks, tile);
   return hipGetLastError();
 }
 
