@@ -701,22 +701,9 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   uint32_t *stage32 = (uint32_t *)area;
   uint16_t *sbin = C32 ? (uint16_t *)(stage32 + T) : (uint16_t *)(stage + NL * T);
   uint8_t *sext = (uint8_t *)(sbin + T);
-  // One- and two-word records (BATCH): every rank atomic issued before any result is used (see scatter_staged_c40);
-  // uncounted windows add 0 to a word of their own lane in goff (free until the bins' offsets are written). Three- and
-  // four-word records keep one atomic per counted window: the batched phases cost their kernels a wave per SIMD.
-  constexpr bool BATCH = NL <= 2;
   uint32_t rank[W];
-  if constexpr (BATCH) {
-    uint32_t *const dummy = (uint32_t *)goff + (threadIdx.x & 63u);
 #pragma unroll
-    for (int j = 0; j < W; j++) {
-      const bool v = inf[j] >> 31;
-      rank[j] = atomicAdd(v ? &lcnt[inf[j] & 0xffffu] : dummy, v ? 1u : 0u);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
-  }
+  for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
   __syncthreads();
   // Reserve each bin's run in the global layout. The returned offsets stay in registers while the bins are
   // scanned and the records staged, so the atomics' round trip overlaps that LDS work (a bin count up to
@@ -739,17 +726,11 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   const uint32_t total = block_excl_scan<NT>(lstart, (int)nb, wsum);
   for (uint32_t r0 = 0; r0 < total; r0 += CAP) {  // (uniform) one round when CAP = W * NT
   if (r0) __syncthreads();  // the previous round's copy-out has read the stage area
-  // the bins' run starts of all W records read first (BATCH, see scatter_staged_c40)
-  uint32_t st_[BATCH ? W : 1];
-  if constexpr (BATCH) {
-#pragma unroll
-    for (int j = 0; j < W; j++) st_[j] = lstart[inf[j] & 0xffffu];
-  }
 #pragma unroll
   for (int j = 0; j < W; j++) {
     if (inf[j] >> 31) {
       const uint32_t d = inf[j] & 0xffffu;
-      const uint32_t pos = (BATCH ? st_[BATCH ? j : 0] : lstart[d]) + rank[j] - r0;  // (earlier rounds' records wrap to >= CAP)
+      const uint32_t pos = lstart[d] + rank[j] - r0;  // (earlier rounds' records wrap to >= CAP)
       if (CAP < W * NT && pos >= (uint32_t)CAP) continue;
       if (C32) {
         stage32[pos] = (uint32_t)rk[j][0];
@@ -779,38 +760,26 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   }
   }
   __syncthreads();
-  // the copy-out in batches of CB records whose LDS reads are all issued before the first global store (see
-  // scatter_staged_c40)
-  constexpr int NJ = CAP / NT, CB = !BATCH ? 1 : NJ % 4 == 0 ? 4 : NJ % 2 == 0 ? 2 : 1;
 #pragma unroll
-  for (int j0 = 0; j0 < NJ; j0 += CB) {
-    uint32_t d[CB], ls[CB], xe[CB];
-    unsigned long long go[CB];
-    uint64_t v[CB][NL];
-#pragma unroll
-    for (int jj = 0; jj < CB; jj++) d[jj] = sbin[threadIdx.x + (j0 + jj) * NT];  // (past total: stale, unused)
-#pragma unroll
-    for (int jj = 0; jj < CB; jj++) {
-      const uint32_t sp = threadIdx.x + (j0 + jj) * NT;
-      const uint32_t dd = d[jj] < nb ? d[jj] : 0u;
-      go[jj] = goff[dd];
-      ls[jj] = lstart[dd];
+  for (int j = 0; j < CAP / NT; j++) {
+    const uint32_t sp = threadIdx.x + j * NT, pos = sp + r0;  // stage slot, position in the workgroup's run
+    if (pos < total) {
+      const uint32_t d = sbin[sp];
+      const unsigned long long go = goff[d];
+      if (go == ~0ull) continue;
+      const unsigned long long dst = go + (pos - lstart[d]);
+      uint64_t v[NL];
       if (C32) {
-        v[jj][0] = (uint64_t)stage32[sp] | (SF == SF_C40 ? (uint64_t)sext[sp] << 32 : 0ull);
+        v[0] = (uint64_t)stage32[sp] | (SF == SF_C40 ? (uint64_t)sext[sp] << 32 : 0ull);
       } else if (SF == SF_AOS2) {
         const ulonglong2 q = ((const ulonglong2 *)stage)[sp];
-        v[jj][0] = q.x;
-        v[jj][NL - 1] = q.y;
+        v[0] = q.x;
+        v[NL - 1] = q.y;
       } else {
 #pragma unroll
-        for (int w = 0; w < NL; w++) v[jj][w] = stage[w * T + sp];
+        for (int w = 0; w < NL; w++) v[w] = stage[w * T + sp];
       }
-      xe[jj] = PACKED ? 0u : sext[sp];
-    }
-#pragma unroll
-    for (int jj = 0; jj < CB; jj++) {
-      const uint32_t sp = threadIdx.x + (j0 + jj) * NT, pos = sp + r0;  // stage slot, position in the workgroup's run
-      if (pos < total && go[jj] != ~0ull) store_out<NL, PACKED, SF>(out, go[jj] + (pos - ls[jj]), v[jj], xe[jj]);
+      store_out<NL, PACKED, SF>(out, dst, v, PACKED ? 0u : sext[sp]);
     }
   }
   }  // rounds
