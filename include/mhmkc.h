@@ -321,9 +321,7 @@ int mhmkc_get_stats(mhmkc_t h, mhmkc_stats *s);
  * (KmerDHT::clear_stores + a fresh HashTableInserter, src/kcount/kcount.cpp:156). */
 int mhmkc_reset(mhmkc_t h);
 
-/* Per-stage HIP-event timing (mhmkc_stats.ms_kernel). Off by default. on = 1: every stage; on = 2: the extraction,
- * partition, exchange and count stages only (fewer event records in the timed stream: MHMKC_STAGE_TILEIDX and
- * MHMKC_STAGE_OTHER then read 0). */
+/* Per-stage HIP-event timing (mhmkc_stats.ms_kernel). Off by default. */
 int mhmkc_set_profiling(mhmkc_t h, int on);
 
 /* Last error message of the handle (or of the last failed mhmkc_create when h is NULL). */
