@@ -321,7 +321,8 @@ int mhmkc_get_stats(mhmkc_t h, mhmkc_stats *s);
  * (KmerDHT::clear_stores + a fresh HashTableInserter, src/kcount/kcount.cpp:156). */
 int mhmkc_reset(mhmkc_t h);
 
-/* Per-stage HIP-event timing (mhmkc_stats.ms_kernel). Off by default. */
+/* Per-stage HIP-event timing (mhmkc_stats.ms_kernel). Off by default (0); 1: every stage; 2: the heavy stages only
+ * (extraction scatter, fine scatter, exchange, count), whose events cost the step less. */
 int mhmkc_set_profiling(mhmkc_t h, int on);
 
 /* Last error message of the handle (or of the last failed mhmkc_create when h is NULL). */

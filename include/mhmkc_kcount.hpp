@@ -455,7 +455,10 @@ class KmerMap {
       for (uint64_t i = 0; i < n; i++) {
         const uint64_t hw = hash_words(keys + i * nl);
         if ((hw >> 32) != fs_prev32_) break;
-        bool d = tag_[locate(key_type(keys + i * nl), hw)] != 0;
+        const key_type ki(keys + i * nl);
+        bool d = tag_[locate(ki, hw)] != 0;
+        // (an earlier chunk's row placed past the last slot waits in fs_wrapped_, not yet in the map)
+        for (size_t j = fs_wrapped_.size(); j-- > 0 && !d;) d = fs_wrapped_[j].first == ki;
         for (uint64_t j = 0; j < i && !d; j++) d = same(i, j);
         lead.push_back(d);
       }
@@ -755,10 +758,19 @@ void load_ordered(mhmkc_t h, KmerMap<MAX_K> &map, uint64_t n, int threads = 0, u
   auto t0 = clk::now();
   int rc = n_ch ? fetch(0) : MHMKC_OK;
   lt.first_fetch = ms_since(t0);
+  // the prefetch thread is joined on every way out of an iteration (a fill that throws would otherwise destroy a
+  // joinable std::thread: std::terminate)
+  struct Joiner {
+    std::thread t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  };
   for (uint64_t c = 0; c < n_ch; c++) {
     check(rc, h, "mhmkc_fetch_ordered_range");
     int rc_next = MHMKC_OK;
-    std::thread f;
+    Joiner jf;
+    std::thread &f = jf.t;
     if (c + 1 < n_ch) f = std::thread([&, c] { rc_next = fetch(c + 1); });
     const Chunk &b = buf[c & 1];
     auto t1 = clk::now();

@@ -26,6 +26,7 @@
 
 #define MT_MAXNL 4
 #define MT_PARTS 256
+#define MT_DIG 6 /* digest words per key range: rows, xor, sum, sum of fmix (of the row fingerprints), distinct, occurrences */
 
 /* MurmurHash3_x64_128 h1 of the key words, seed 313 (src/hash_funcs.c:77-170,185-190; Kmer::hash,
  * src/kmer.cpp:465-468): the thread partition and the table slot. */
@@ -69,6 +70,7 @@ typedef struct {
 
 static int bin_push(mt_bin *b, const uint64_t *key, int nl, uint8_t e) {
   if (b->n == b->cap) {
+    /* (doubling: a 1.25x growth made a pass holding four key ranges' records 2.5x slower, reallocs copying) */
     uint64_t nc = b->cap ? 2 * b->cap : 4096;
     uint64_t *nk = (uint64_t *)realloc(b->keys, nc * 8 * (size_t)nl);
     if (!nk) return 0;
@@ -126,7 +128,9 @@ typedef struct {
   const uint8_t *bytes;
   const uint64_t *offs;
   uint64_t r0, r1;
-  uint32_t range, n_ranges; /* keep only the k-mers with mt_range == range */
+  uint32_t range, n_ranges; /* keep only the k-mers with mt_range in [range, range + n_sel) */
+  uint32_t n_sel;           /* key ranges binned by one extraction pass (bins [n_sel][MT_PARTS]) */
+  uint64_t *dig;            /* orc_kcount_mt_digests: per selected range rows, xor, sum of row fingerprints */
   int k, nl, qcut, dmin;
   double dyn_mult; /* 1.0 - DYN_MIN_DEPTH, in double as the reference computes it */
   int nthreads;
@@ -143,7 +147,7 @@ typedef struct {
 typedef struct {
   mt_work *w;
   int nthreads;
-  int next_part;
+  int next_part, n_part_bins; /* partitions to count: n_sel x MT_PARTS */
   pthread_mutex_t lock;
   const mt_cbin *cbins; /* [MT_PARTS]: the contig pass's records, or NULL */
 } mt_shared;
@@ -206,14 +210,18 @@ static void *mt_extract(void *arg) {
           break;
         }
       const uint64_t *key = use_rc ? rc : fw;
-      if (w->n_ranges > 1 && mt_range(key, nl, w->n_ranges) != w->range) continue;
+      uint32_t sel = 0;
+      if (w->n_ranges > 1) {
+        sel = mt_range(key, nl, w->n_ranges) - w->range;
+        if (sel >= w->n_sel) continue;
+      }
       if (use_rc) { /* complement and swap (comp_nucleotide, src/utils.cpp:121-143) */
         const int nl_ = rr < 4 ? 3 - rr : 4, nr_ = l < 4 ? 3 - l : 4;
         l = nl_;
         rr = nr_;
       }
       const uint64_t h = mt_hash(key, nl);
-      if (!bin_push(&w->bins[h >> 56], key, nl, (uint8_t)((l << 3) | rr))) {
+      if (!bin_push(&w->bins[sel * MT_PARTS + (h >> 56)], key, nl, (uint8_t)((l << 3) | rr))) {
         w->fail = 1;
         return NULL;
       }
@@ -340,7 +348,7 @@ static void *mt_count(void *arg) {
   uint8_t *used = NULL;
   for (;;) {
     pthread_mutex_lock(&sh->lock);
-    const int p = sh->next_part < MT_PARTS ? sh->next_part++ : -1;
+    const int p = sh->next_part < sh->n_part_bins ? sh->next_part++ : -1;
     pthread_mutex_unlock(&sh->lock);
     if (p < 0) break;
     uint64_t n = 0;
@@ -363,6 +371,7 @@ static void *mt_count(void *arg) {
       }
     }
     memset(used, 0, cap);
+    const uint64_t distinct0 = w->distinct, occ0 = w->occ;
     for (int t = 0; t < sh->nthreads; t++) {
       const mt_bin *b = &sh->w[t].bins[p];
       for (uint64_t i = 0; i < b->n; i++) {
@@ -450,6 +459,17 @@ static void *mt_count(void *arg) {
         w->purged++;
         continue;
       }
+      if (w->dig) { /* digest only: the row's fingerprint (orc_row_fingerprints) into its range's sums */
+        uint64_t h = 0x243F6A8885A308D3ULL;
+        for (int q = 0; q < nl; q++) h = mt_fmix(h ^ tk[s * nl + q]) + 0x9E3779B97F4A7C15ULL;
+        h = mt_fmix(h ^ ((uint64_t)c | (uint64_t)(uint8_t)L << 16 | (uint64_t)(uint8_t)R << 24));
+        uint64_t *d = w->dig + MT_DIG * (size_t)(p / MT_PARTS);
+        d[0]++;
+        d[1] ^= h;
+        d[2] += h;
+        d[3] += mt_fmix(h);
+        continue;
+      }
       if (w->n_out == w->cap_out) {
         const uint64_t nc = w->cap_out ? 2 * w->cap_out : 1 << 16;
         uint64_t *ok = (uint64_t *)realloc(w->out_keys, nc * 8 * (size_t)nl);
@@ -471,6 +491,10 @@ static void *mt_count(void *arg) {
       w->out_l[w->n_out] = L;
       w->out_r[w->n_out] = R;
       w->n_out++;
+    }
+    if (w->dig) {
+      w->dig[MT_DIG * (size_t)(p / MT_PARTS) + 4] += w->distinct - distinct0;
+      w->dig[MT_DIG * (size_t)(p / MT_PARTS) + 5] += w->occ - occ0;
     }
     for (int t = 0; t < sh->nthreads; t++) { /* this partition's records are done */
       mt_bin *b = &sh->w[t].bins[p];
@@ -505,12 +529,15 @@ typedef struct {
 /* The part `range` of n_ranges of the table (the k-mers with mt_range(key) == range): a table too large for host
  * memory at once (C3: 1.28e10 occurrences) is built and compared one part at a time. Returns NULL on bad input (a
  * base code > 4: the reference DIEs) or allocation failure. */
-mt_table *orc_kcount_mt_ctgs_range(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, const char *ctg_chars,
-                                   const uint64_t *ctg_offs, const uint16_t *ctg_depths, uint64_t n_ctgs, int k,
-                                   int n_longs, int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads,
-                                   int range, int n_ranges) {
+/* The core of both: n_sel consecutive ranges from `range` in one extraction pass; dig != NULL: no table, the rows'
+ * fingerprint digests per range (MT_DIG words each) into dig, and a non-NULL return on success (an empty table). */
+static mt_table *mt_run(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, const char *ctg_chars,
+                        const uint64_t *ctg_offs, const uint16_t *ctg_depths, uint64_t n_ctgs, int k, int n_longs,
+                        int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads, int range, int n_ranges,
+                        int n_sel, uint64_t *dig) {
   const int nl = k / 32 + 1;
   if (k < 1 || k > 127 || k % 32 == 0 || n_longs < nl || n_longs > 8) return NULL;
+  if (n_sel < 1 || (n_sel > 1 && n_ctgs) || range + n_sel > (n_ranges < 1 ? 1 : n_ranges)) return NULL;
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   mt_work *w = (mt_work *)calloc((size_t)threads, sizeof(mt_work));
@@ -529,8 +556,10 @@ mt_table *orc_kcount_mt_ctgs_range(const uint8_t *bytes, const uint64_t *offs, u
     w[t].nthreads = threads;
     w[t].range = (uint32_t)range;
     w[t].n_ranges = n_ranges < 1 ? 1u : (uint32_t)n_ranges;
-    w[t].bins = (mt_bin *)calloc(MT_PARTS, sizeof(mt_bin));
-    if (!w[t].bins) return NULL;
+    w[t].n_sel = (uint32_t)n_sel;
+    w[t].bins = (mt_bin *)calloc((size_t)n_sel * MT_PARTS, sizeof(mt_bin));
+    w[t].dig = dig ? (uint64_t *)calloc(MT_DIG * (size_t)n_sel, 8) : NULL;
+    if (!w[t].bins || (dig && !w[t].dig)) return NULL;
   }
   for (uint64_t r = 0; r < n_reads; r++)
     if (offs[r + 1] < offs[r] || offs[r + 1] - offs[r] > 65535) return NULL;
@@ -546,6 +575,7 @@ mt_table *orc_kcount_mt_ctgs_range(const uint8_t *bytes, const uint64_t *offs, u
   sh.w = w;
   sh.nthreads = threads;
   sh.next_part = 0;
+  sh.n_part_bins = n_sel * MT_PARTS;
   sh.cbins = cbins;
   pthread_mutex_init(&sh.lock, NULL);
   mt_arg *args = (mt_arg *)calloc((size_t)threads, sizeof(mt_arg));
@@ -593,13 +623,19 @@ mt_table *orc_kcount_mt_ctgs_range(const uint8_t *bytes, const uint64_t *offs, u
       }
       out->reads = n_reads;
     }
+    if (out && dig) {
+      memset(dig, 0, MT_DIG * 8 * (size_t)n_sel);
+      for (int t = 0; t < threads; t++)
+        for (int q = 0; q < MT_DIG * n_sel; q++) dig[q] = (q % MT_DIG == 1) ? dig[q] ^ w[t].dig[q] : dig[q] + w[t].dig[q];
+    }
   }
   for (int t = 0; t < threads; t++) {
-    for (int p = 0; p < MT_PARTS; p++) {
+    for (int p = 0; p < n_sel * MT_PARTS; p++) {
       free(w[t].bins[p].keys);
       free(w[t].bins[p].ext);
     }
     free(w[t].bins);
+    free(w[t].dig);
     free(w[t].out_keys);
     free(w[t].out_counts);
     free(w[t].out_l);
@@ -616,6 +652,46 @@ mt_table *orc_kcount_mt_ctgs_range(const uint8_t *bytes, const uint64_t *offs, u
   free(w);
   free(tid);
   return out;
+}
+
+mt_table *orc_kcount_mt_ctgs_range(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, const char *ctg_chars,
+                                   const uint64_t *ctg_offs, const uint16_t *ctg_depths, uint64_t n_ctgs, int k,
+                                   int n_longs, int qual_cutoff, int dmin_thres, double dyn_min_depth, int threads,
+                                   int range, int n_ranges) {
+  return mt_run(bytes, offs, n_reads, ctg_chars, ctg_offs, ctg_depths, n_ctgs, k, n_longs, qual_cutoff, dmin_thres,
+                dyn_min_depth, threads, range, n_ranges, 1, NULL);
+}
+
+/* Row-fingerprint digests (orc_row_fingerprints: MT_DIG words per range, see mt_run) of the key ranges [range, range +
+ * n_sel) of n_ranges, from one extraction pass over the reads (the extraction is half of a range's time): the at-scale
+ * gates compare them with the GPU's rows of the same ranges (orc_fp_digests) without building the tables. Returns 0,
+ * or -1 on bad input or allocation failure. */
+int orc_kcount_mt_digests(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int k, int qual_cutoff,
+                          int dmin_thres, double dyn_min_depth, int threads, int range, int n_sel, int n_ranges,
+                          uint64_t *dig) {
+  mt_table *t = mt_run(bytes, offs, n_reads, NULL, NULL, NULL, 0, k, k / 32 + 1, qual_cutoff, dmin_thres,
+                       dyn_min_depth, threads, range, n_ranges, n_sel, dig);
+  if (!t) return -1;
+  free(t->out_keys);
+  free(t->out_counts);
+  free(t->out_left);
+  free(t->out_right);
+  free(t);
+  return 0;
+}
+
+/* The same digests of a GPU table's row fingerprints fps[n] by their key range parts[n] (orc_mt_ranges), ranges
+ * [0, n_ranges): MT_DIG words each (distinct and occurrences left 0). */
+void orc_fp_digests(const uint64_t *fps, const uint8_t *parts, uint64_t n, int n_ranges, uint64_t *dig) {
+  memset(dig, 0, MT_DIG * 8 * (size_t)n_ranges);
+  for (uint64_t i = 0; i < n; i++) {
+    if (parts[i] >= n_ranges) continue;
+    uint64_t *d = dig + MT_DIG * (size_t)parts[i];
+    d[0]++;
+    d[1] ^= fps[i];
+    d[2] += fps[i];
+    d[3] += mt_fmix(fps[i]);
+  }
 }
 
 mt_table *orc_kcount_mt_range(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int k, int n_longs,

@@ -258,7 +258,7 @@ def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts:
     say(f"{fps.size} row fingerprints saved")
     np.savez(Path(out_dir) / f"rank{rank}_stats.npz", seconds=t_count,
              **{key: st[key] for key in ("occurrences", "owned_records", "bytes_sent", "bytes_recv", "exact_reruns",
-                                         "smer_count", "n_out", "distinct", "finish_passes", "out_reruns",
+                                         "smer_count", "n_out", "distinct", "count_sum", "finish_passes", "out_reruns",
                                          "device_bytes", "device_bytes_peak", "xchg_rounds", "ms_xchg",
                                          "inc_rounds", "inc_fallbacks", "ms_finish_tail", "inc_redone_coarse", "inc_slack")})
     dist.barrier()

@@ -52,6 +52,10 @@ def oracle() -> C.CDLL:
         L.orc_kcount_mt_range.restype = VP
         L.orc_kcount_mt_ctgs_range.argtypes = [VP, VP, U64, C.c_char_p, VP, VP, U64, I, I, I, I, C.c_double, I, I, I]
         L.orc_kcount_mt_ctgs_range.restype = VP
+        L.orc_kcount_mt_digests.argtypes = [VP, VP, U64, I, I, I, C.c_double, I, I, I, I, VP]
+        L.orc_kcount_mt_digests.restype = I
+        L.orc_fp_digests.argtypes = [VP, VP, U64, I, VP]
+        L.orc_fp_digests.restype = None
         L.orc_mt_ranges.argtypes = [VP, U64, I, I, I, VP]
         L.orc_mt_ranges.restype = None
         L.orc_row_fingerprints.argtypes = [VP, VP, VP, VP, U64, I, I, VP]
@@ -151,6 +155,66 @@ def kcount_mt_range(packed_bytes, offsets, k, part, n_parts, threads=8, qual_cut
     ptr = oracle().orc_kcount_mt_range(b.ctypes.data, o.ctypes.data, o.size - 1, k, nl, qual_cutoff, dmin_thres,
                                        dyn_min_depth, threads, part, n_parts)
     return OracleTable(ptr, nl, k)
+
+
+MT_DIG = 6  # digest words per key range (oracle/kcount_mt.c): rows, xor, sum, sum of fmix, distinct, occurrences
+
+
+def kcount_mt_digests(packed_bytes, offsets, k, part0, n_sel, n_parts, threads=8, qual_cutoff=20, dmin_thres=2,
+                      dyn_min_depth=0.9) -> np.ndarray:
+    """Row-fingerprint digests of the restatement's key-range parts [part0, part0 + n_sel) of n_parts, from one pass
+    over the reads (oracle/kcount_mt.c orc_kcount_mt_digests): (n_sel, MT_DIG) uint64."""
+    b = np.ascontiguousarray(packed_bytes, dtype=np.uint8)
+    o = np.ascontiguousarray(offsets, dtype=np.uint64)
+    out = np.zeros((n_sel, MT_DIG), dtype=np.uint64)
+    rc = oracle().orc_kcount_mt_digests(b.ctypes.data, o.ctypes.data, o.size - 1, k, qual_cutoff, dmin_thres,
+                                        dyn_min_depth, threads, part0, n_sel, n_parts, out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("orc_kcount_mt_digests failed (bad input or out of memory)")
+    return out
+
+
+def fp_digests(fps, parts, n_parts) -> np.ndarray:
+    """The same digests of row fingerprints fps by their key-range parts (mt_ranges): (n_parts, MT_DIG) uint64, the
+    distinct and occurrence words 0."""
+    f = np.ascontiguousarray(fps, dtype=np.uint64)
+    p = np.ascontiguousarray(parts, dtype=np.uint8)
+    out = np.zeros((n_parts, MT_DIG), dtype=np.uint64)
+    oracle().orc_fp_digests(f.ctypes.data, p.ctypes.data, f.size, n_parts, out.ctypes.data)
+    return out
+
+
+FP_CHAIN0 = 0x243F6A8885A308D3
+
+
+def _fmix(x):
+    m = (1 << 64) - 1
+    x ^= x >> 33
+    x = (x * 0xff51afd7ed558ccd) & m
+    x ^= x >> 33
+    x = (x * 0xc4ceb9fe1a85ec53) & m
+    return x ^ (x >> 33)
+
+
+def _fmix_inv(x):
+    m = (1 << 64) - 1
+    x ^= x >> 33  # (x >> 33 >> 33 == 0: an xor-shift by 33 is its own inverse on 64 bits)
+    x = (x * pow(0xc4ceb9fe1a85ec53, -1, 1 << 64)) & m
+    x ^= x >> 33
+    x = (x * pow(0xff51afd7ed558ccd, -1, 1 << 64)) & m
+    return x ^ (x >> 33)
+
+
+def fp_row_values(fp, key_words):
+    """(count, left, right) of the row whose fingerprint is fp if its key is key_words (orc_row_fingerprints inverted:
+    the final fmix undone and the key's chain removed), else None."""
+    h = FP_CHAIN0
+    for w in key_words:
+        h = (_fmix(h ^ int(w)) + 0x9E3779B97F4A7C15) & ((1 << 64) - 1)
+    v = _fmix_inv(int(fp)) ^ h
+    if v >> 32:
+        return None
+    return v & 0xFFFF, chr((v >> 16) & 0xFF), chr((v >> 24) & 0xFF)
 
 
 def mt_ranges(keys, k, n_parts):

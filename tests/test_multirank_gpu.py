@@ -270,8 +270,8 @@ def test_ranks_sharing_gpu_counters(k, tmp_path):
 
 
 # The whole -m gpu suite must finish inside the round-end driver's test step (900 s): the checks below that the
-# eight-rank C3/C4 test supersedes run only with MHMKC_SCALE_TESTS=1, and that test compares half of its key-range
-# parts by default (all eight with the variable set).
+# eight-rank C3/C4 test supersedes run only with MHMKC_SCALE_TESTS=1. The eight-rank RCCL test (the driver's 8-GPU
+# code path) runs before the full-size C3/C4 test, which is last in the file.
 SCALE_TESTS = os.environ.get("MHMKC_SCALE_TESTS") == "1"
 
 
@@ -325,68 +325,6 @@ def test_device_offsets_not_from_zero_refused(xpipe, tmp_path):
     assert codes == [-1] * world, codes
 
 
-@pytest.mark.slow
-@pytest.mark.timeout(1150)
-@pytest.mark.parametrize("cfg", ["C3", "C4"])
-def test_c3_c4_eight_ranks_vs_cpu_restatement(cfg, tmp_path):
-    """VERDICT r3 item 1: C3 (1e8 x 150 bp, G = 500 Mbp, seed 3, k = 21, hash-range owner) and C4 (the same reads at
-    k = 63 with MHMKC_OWNER_MINIMIZER: the supermer exchange) as configured, as 8 ranks of 12.5M reads sharing the one
-    GPU over the host transport (C3: the incremental partition of the exchange rounds; C4: 4 finish passes per rank,
-    each extracting its received supermers). The union of the 8 tables is
-    compared with the multi-threaded CPU restatement (oracle/kcount_mt.c) row by row, one key-range part at a time
-    (kcount_mt_range: the 1e8-read table does not fit host memory at once): in each part the sorted lists of 64-bit
-    row fingerprints (key words, count, left, right) must be equal. C4 also checks every row's target rank."""
-    import torch.multiprocessing as mp
-
-    import mr_gpu_worker
-
-    world, n_parts = 8, 8
-    k, owner = (21, "hash") if cfg == "C3" else (63, "minimizer")
-    opts = {"reads_per_rank": 12_500_000, "genome": 500_000_000, "seed": 3, "owner": owner, "passes": 4,
-            "n_parts": n_parts}
-    t0 = time.time()
-    mp.spawn(mr_gpu_worker.run_share_full, args=(world, free_port(), k, str(tmp_path), opts), nprocs=world, join=True)
-    stats = [dict(np.load(tmp_path / f"rank{r}_stats.npz")) for r in range(world)]
-    assert sum(int(s["owned_records"]) for s in stats) == sum(int(s["occurrences"]) for s in stats) == \
-        100_000_000 * (150 - k - 1)
-    assert sum(int(s["bytes_sent"]) for s in stats) == sum(int(s["bytes_recv"]) for s in stats) > 0
-    # C3 (records over the pipelined exchange): the incremental partition puts every round into its fine buckets as it
-    # lands and then counts the owned range once (DESIGN.md §3.5f; MHMKC_PASSES splits only a finish without it);
-    # C4 (supermers, extracted on the owner per pass) counts in the 4 passes asked for
-    for s in stats:
-        if int(s["inc_rounds"]) > 0:
-            assert int(s["inc_fallbacks"]) == 0 and int(s["finish_passes"]) >= 1
-        else:
-            assert int(s["finish_passes"]) == 4
-    print(f"[parent {time.time() - t0:6.1f}s] {cfg}: 8 ranks counted; per rank: "
-          + ", ".join(f"{float(s['seconds']):.1f} s / {int(s['device_bytes_peak']) / 2**30:.1f} GiB peak" for s in stats),
-          flush=True)
-    parts = np.concatenate([np.load(tmp_path / f"rank{r}_parts.npy") for r in range(world)])
-    fps = np.concatenate([np.load(tmp_path / f"rank{r}_fps.npy") for r in range(world)])
-    assert fps.size == sum(int(s["n_out"]) for s in stats)
-    g = m.synth_genome(500_000_000, 3)
-    b, o = m.synth_reads(g, world * 12_500_000, 150, 3, threads=16)
-    del g
-    print(f"[parent {time.time() - t0:6.1f}s] {o.size - 1} reads regenerated", flush=True)
-    rows = 0
-    checked = range(n_parts) if SCALE_TESTS else range(0, n_parts, 2)  # (the key-range parts are random halves)
-    if os.environ.get("MHMKC_C34_PARTS"):  # (a chosen subset, e.g. to re-check one part)
-        checked = [int(x) for x in os.environ["MHMKC_C34_PARTS"].split(",")]
-    for p in checked:
-        t = O.kcount_mt_range(b, o, k, p, n_parts, threads=16)
-        exp = np.sort(O.row_fingerprints(*t.fetch(), k))
-        del t
-        got = np.sort(fps[parts == p])
-        rows += exp.size
-        print(f"[parent {time.time() - t0:6.1f}s] part {p}: {exp.size} rows (CPU) vs {got.size} (GPU)", flush=True)
-        assert got.size == exp.size, f"{cfg} part {p}: {got.size} GPU rows vs {exp.size}"
-        bad = np.flatnonzero(got != exp)
-        assert bad.size == 0, (f"{cfg} part {p}: {bad.size} sorted positions differ; "
-                               f"{np.setdiff1d(got, exp).size} GPU rows not in the CPU table, "
-                               f"{np.setdiff1d(exp, got).size} CPU rows not in the GPU table")
-    assert rows == fps.size if SCALE_TESTS else rows == int(np.isin(parts, list(checked)).sum())
-
-
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("k,owner", [(21, "hash"), (63, "minimizer")])
 def test_rccl_eight_ranks_vs_cpu_restatement(k, owner, tmp_path):
@@ -421,3 +359,112 @@ def test_rccl_eight_ranks_vs_cpu_restatement(k, owner, tmp_path):
     exp = np.sort(O.row_fingerprints(*t.fetch(), k))
     assert fps.size == exp.size, f"{fps.size} GPU rows vs {exp.size}"
     assert np.array_equal(fps, exp), f"{int((fps != exp).sum())} rows differ"
+
+
+def _diagnose_part(p, fps, parts, sizes, b, o, k, n_parts):
+    """The rows of key-range part p where the GPU's union differs from the CPU restatement: each GPU-only row is
+    matched to a CPU-only row by key (oracle_lib.fp_row_values inverts the row fingerprint), so a line names the key,
+    the rank that emitted it and both tables' count / left / right."""
+    t = O.kcount_mt_range(b, o, k, p, n_parts, threads=16)
+    keys, c, lft, rgt = t.fetch()
+    del t
+    exp = O.row_fingerprints(keys, c, lft, rgt, k)
+    gi = np.flatnonzero(parts == p)
+    got = fps[gi]
+    only_gpu = np.flatnonzero(~np.isin(got, exp))
+    only_cpu = np.flatnonzero(~np.isin(exp, got))
+    ends = np.cumsum(sizes)
+    lines = [f"part {p}: {got.size} GPU rows, {exp.size} CPU rows; {only_gpu.size} GPU-only, {only_cpu.size} CPU-only"]
+    matched = set()
+    for i in only_gpu[:16]:
+        rank = int(np.searchsorted(ends, gi[i], side="right"))
+        hit = None
+        for j in only_cpu[:256]:
+            v = O.fp_row_values(got[i], keys[j])
+            if v is not None:
+                hit = (j, v)
+                break
+        if hit:
+            j, v = hit
+            matched.add(int(j))
+            lines.append(f"  key {[hex(int(x)) for x in keys[j]]} rank {rank}: GPU count {v[0]} L {v[1]} R {v[2]}, "
+                         f"CPU count {int(c[j])} L {chr(int(lft[j]))} R {chr(int(rgt[j]))}")
+        else:
+            lines.append(f"  GPU-only row (rank {rank}, fingerprint {int(got[i]):#x}): key not among the CPU-only rows")
+    for j in only_cpu[:16]:
+        if int(j) not in matched:
+            lines.append(f"  CPU-only row key {[hex(int(x)) for x in keys[j]]} count {int(c[j])} L {chr(int(lft[j]))} "
+                         f"R {chr(int(rgt[j]))}: no GPU row with this key and other values")
+    return lines
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(1150)
+@pytest.mark.parametrize("cfg", ["C3", "C4"])
+def test_c3_c4_eight_ranks_vs_cpu_restatement(cfg, tmp_path):
+    """VERDICT r3 item 1: C3 (1e8 x 150 bp, G = 500 Mbp, seed 3, k = 21, hash-range owner) and C4 (the same reads at
+    k = 63 with MHMKC_OWNER_MINIMIZER: the supermer exchange) as configured, as 8 ranks of 12.5M reads sharing the one
+    GPU over the host transport (C3: the incremental partition of the exchange rounds; C4: 4 finish passes per rank,
+    each extracting its received supermers). The union of the 8 tables is compared with the multi-threaded CPU
+    restatement (oracle/kcount_mt.c) in all 8 key-range parts (the 1e8-read table does not fit host memory at once):
+    per part the row count and three 64-bit sums of the row fingerprints (key words, count, left, right) must be
+    equal (orc_kcount_mt_digests builds four parts' digests from one pass over the reads). A differing part is then
+    built in full and its differing rows are named: key, rank, GPU and CPU count / left / right. Every rank's counts
+    add up to its owned records, and the GPU's distinct keys equal the CPU's. C4 also checks every row's target
+    rank (in the workers)."""
+    import torch.multiprocessing as mp
+
+    import mr_gpu_worker
+
+    world, n_parts, per_pass = 8, 8, 4
+    k, owner = (21, "hash") if cfg == "C3" else (63, "minimizer")
+    opts = {"reads_per_rank": 12_500_000, "genome": 500_000_000, "seed": 3, "owner": owner, "passes": 4,
+            "n_parts": n_parts}
+    t0 = time.time()
+    mp.spawn(mr_gpu_worker.run_share_full, args=(world, free_port(), k, str(tmp_path), opts), nprocs=world, join=True)
+    stats = [dict(np.load(tmp_path / f"rank{r}_stats.npz")) for r in range(world)]
+    occ_total = 100_000_000 * (150 - k - 1)
+    assert sum(int(s["owned_records"]) for s in stats) == sum(int(s["occurrences"]) for s in stats) == occ_total
+    assert sum(int(s["bytes_sent"]) for s in stats) == sum(int(s["bytes_recv"]) for s in stats) > 0
+    # C3 (records over the pipelined exchange): the incremental partition puts every round into its fine buckets as it
+    # lands and then counts the owned range once (DESIGN.md §3.5f; MHMKC_PASSES splits only a finish without it);
+    # C4 (supermers, extracted on the owner per pass) counts in the 4 passes asked for
+    for s in stats:
+        if int(s["inc_rounds"]) > 0:
+            assert int(s["inc_fallbacks"]) == 0 and int(s["finish_passes"]) >= 1
+        else:
+            assert int(s["finish_passes"]) == 4
+    print(f"[parent {time.time() - t0:6.1f}s] {cfg}: 8 ranks counted; per rank: "
+          + ", ".join(f"{float(s['seconds']):.1f} s / {int(s['device_bytes_peak']) / 2**30:.1f} GiB peak" for s in stats),
+          flush=True)
+    sizes = [int(s["n_out"]) for s in stats]
+    parts = np.concatenate([np.load(tmp_path / f"rank{r}_parts.npy") for r in range(world)])
+    fps = np.concatenate([np.load(tmp_path / f"rank{r}_fps.npy") for r in range(world)])
+    assert fps.size == sum(sizes)
+    got = O.fp_digests(fps, parts, n_parts)
+    g = m.synth_genome(500_000_000, 3)
+    b, o = m.synth_reads(g, world * 12_500_000, 150, 3, threads=16)
+    del g
+    print(f"[parent {time.time() - t0:6.1f}s] {o.size - 1} reads regenerated", flush=True)
+    exp = np.zeros_like(got)
+    bad = []
+    for p0 in range(0, n_parts, per_pass):
+        exp[p0:p0 + per_pass] = O.kcount_mt_digests(b, o, k, p0, per_pass, n_parts, threads=16)
+        for p in range(p0, p0 + per_pass):
+            same = (got[p, :4] == exp[p, :4]).all()
+            print(f"[parent {time.time() - t0:6.1f}s] part {p}: {int(exp[p, 0])} rows (CPU) vs {int(got[p, 0])} (GPU)"
+                  f"{'' if same else ': DIFFERENT'}", flush=True)
+            if not same:
+                bad.append(p)
+    cpu_distinct, gpu_distinct = int(exp[:, 4].sum()), sum(int(s["distinct"]) for s in stats)
+    assert int(exp[:, 5].sum()) == occ_total
+    sums = [(int(s["count_sum"]), int(s["owned_records"])) for s in stats]
+    msg = [f"{cfg}: parts {bad} differ; distinct keys GPU {gpu_distinct} CPU {cpu_distinct}; per-rank count sum - "
+           f"owned records {[a - z for a, z in sums]}"]
+    for p in bad[:2]:
+        msg += _diagnose_part(p, fps, parts, sizes, b, o, k, n_parts)
+    if bad:
+        print("\n".join(msg), flush=True)
+    assert not bad, "\n".join(msg)
+    assert all(a == z for a, z in sums), msg[0]
+    assert gpu_distinct == cpu_distinct, msg[0]
