@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--no-profile-events", action="store_true")
     ap.add_argument("--profile-level", type=int, choices=(1, 2), default=None,
                     help="stage events: 1 every stage, 2 the heavy stages (default for packed input)")
+    ap.add_argument("--no-k63", dest="k63", action="store_false",
+                    help="N = 1, C2: skip the second leg, C2's reads at k = 63 (C4's two-word Kmer<> path)")
     ap.add_argument("--no-kmermap", dest="kmermap", action="store_false",
                     help="skip timing the hand-off into the C++ adapter's KmerMap")
     ap.add_argument("--transport", choices=("rccl", "host", "rccl-same-gpu"), default="rccl",
@@ -443,7 +445,7 @@ def main():
             pmc = {}
     # measured for this workload only (the config's own sizes)
     pmc = {} if (args.reads_per_gpu or args.reads_total) else pmc.get("configs", {}).get(f"{args.config}/k{k}", {})
-    def roofline_of(stage):
+    def roofline_of(stage, stage_ms=stage_ms, launches=launches, st=st, k=k, pmc=pmc):
         """The roofline object of one stage's kernel: algorithmic HBM bytes per launch over the launch's HIP-event
         time, against the 8 TB/s HBM peak (k_count also carries its LDS-floor model)."""
         ms_launch = stage_ms[stage] / launches[stage]
@@ -547,6 +549,49 @@ def main():
                "window": "BASELINE.md:74-75: from the first H2D of the reads to the finished device table"}
         del hb, ho
 
+    # C4's one-GPU figure: the same resident reads counted at k = 63, the two-word Kmer<> path
+    # (mixed 16-byte records, two-word LDS table), timed like the headline leg; not `value`
+    k63 = None
+    if world == 1 and args.k63 and args.config == "C2" and args.input == "packed" and k != 63 and not args.reads_per_gpu:
+        c63 = m.KmerCounter(63, device=local)
+        c63.set_profiling(0 if args.no_profile_events else 2)
+
+        def step63():
+            c63.reset()
+            c63.add_tensors(bt, ot, n_bases=n_bases)
+            c63.finish()
+
+        for _ in range(args.warmup):
+            step63()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        sm63, la63, occ63, st63 = {}, {}, 0, None
+        for _ in range(args.steps):
+            step63()
+            st63 = c63.stats()
+            occ63 += st63["occurrences"]
+            for s_, v in st63["ms_kernel"].items():
+                sm63[s_] = sm63.get(s_, 0.0) + v
+                la63[s_] = la63.get(s_, 0) + st63["launches"][s_]
+        torch.cuda.synchronize()
+        el63 = time.perf_counter() - t1
+        pmc63 = {}
+        if Path(args.pmc_json).exists():
+            try:
+                pmc63 = json.loads(Path(args.pmc_json).read_text()).get("configs", {}).get("C2/k63", {})
+            except Exception:
+                pmc63 = {}
+        k63 = {"workload": f"C2's reads ({R} x {L} bp, genome {G} bp, seed {seed}) at k = 63: C4's two-word path on one GPU",
+               "value": round(occ63 / el63, 1), "unit": "k-mers/s", "ms_per_step": round(el63 / steps * 1e3, 3),
+               "steps": args.steps, "warmup": args.warmup,
+               "stages_ms_per_step": {**{s_: round(v / steps, 3) for s_, v in sm63.items() if la63.get(s_)},
+                                      "rest": round(el63 / steps * 1e3 - sum(v / steps for s_, v in sm63.items()
+                                                                               if la63.get(s_)), 3)},
+               "rooflines": {s_: roofline_of(s_, sm63, la63, st63, 63, pmc63)
+                             for s_ in ("extract_scatter", "part_scatter", "count") if la63.get(s_)},
+               "n_out": st63["n_out"], "distinct": st63["distinct"]}
+        c63.close()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(b, o, k, args.cpu_sample_reads, args.cpu_threads)
@@ -598,6 +643,7 @@ def main():
             "h2d_inclusive": h2d,
             "d2h_fetch": d2h,
             "kmermap": kmermap,
+            "k63": k63,
             "d2h_kmermap_ms": kmermap["ms"] if kmermap and "ms" in kmermap else None,
             "distinct_per_gpu": st["distinct"] if st else None,
             "n_out_per_gpu": st["n_out"] if st else None,

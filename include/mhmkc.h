@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 12
+#define MHMKC_ABI_VERSION 13
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -289,6 +289,15 @@ int mhmkc_fetch_ordered(mhmkc_t h, uint64_t *keys, uint16_t *counts, char *left,
  * adapter's insert_into_local_hashtable) never holds the whole table twice. */
 int mhmkc_fetch_ordered_range(mhmkc_t h, uint64_t row0, uint64_t n_rows, uint64_t *keys, uint16_t *counts, char *left,
                               char *right);
+
+/* Rows [row0, row0 + n_rows) of mhmkc_fetch_ordered's order, each with the slot it takes in a KmerMap of `capacity`
+ * slots (a power of two, 16 .. 2^32; home slot = the top log2(capacity) bits of mhmkc_map_hash) filled with the rows
+ * in this order from empty by linear probing, and its tag byte (0x80 | the low 7 bits of mhmkc_map_hash): slot i =
+ * max(home i, slot i-1 + 1), computed on the device (a prefix maximum), or 0xFFFFFFFF past the last slot (the map
+ * places that row itself). The C++ adapter's KmerMap then writes each row straight to its slot, with no hashing or
+ * probing on the host (insert_into_local_hashtable, src/kcount/kcount_cpu.cpp:503-522). slots / tags may be NULL. */
+int mhmkc_fetch_map_range(mhmkc_t h, uint64_t capacity, uint64_t row0, uint64_t n_rows, uint64_t *keys,
+                          uint16_t *counts, char *left, char *right, uint32_t *slots, uint8_t *tags);
 
 /* Device pointers of the finished table (valid until the next reset/destroy). */
 int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,

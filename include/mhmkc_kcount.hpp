@@ -376,6 +376,55 @@ class KmerMap {
     }
     chunk_loop(keys, counts, left, right, n);
   }
+  // fill_begin left the map ready for fill_chunk_slots: it was empty, the fill has several threads, and it has at most
+  // 2^32 slots
+  bool fill_by_slots() const { return fs_ordered_ && fs_pool_ != nullptr; }
+  // Rows with the slots and tags mhmkc_fetch_map_range computed on the device for this map's capacity (bucket_count()
+  // after fill_begin), in that order (the rows of all chunks, each chunk in turn): the fill threads write each row
+  // straight to its slot in one pass, with no hashing and no probing on the host; a row whose slot is 0xFFFFFFFF (past
+  // the last slot) is placed by put() at fill_end. The rows' keys must be unique (a finished table's are). Only between
+  // fill_begin and fill_end of a map for which fill_by_slots() is true, and not mixed with fill_chunk in one fill.
+  void fill_chunk_slots(const uint64_t *keys, const uint16_t *counts, const char *left, const char *right,
+                        const uint32_t *slots, const uint8_t *tags, uint64_t n) {
+    if (!n) return;
+    if (!fill_by_slots()) die("KmerMap::fill_chunk_slots: the map was not empty at fill_begin, or one fill thread");
+    const int nl = key_type::N_LONGS;
+    const int T = (int)std::min<uint64_t>((uint64_t)fs_pool_->size(), n / 4096 + 1);
+    std::vector<std::vector<uint64_t>> wrapped(T);
+    std::vector<uint64_t> placed(T, 0);
+    const std::function<void(int)> worker = [&](int t) {
+      if (t >= T) return;
+      const uint64_t a = n * (uint64_t)t / (uint64_t)T, b = n * (uint64_t)(t + 1) / (uint64_t)T;
+      uint64_t m = 0;
+      for (uint64_t i = a; i < b; i++) {
+        const uint32_t p = slots[i];
+        if (p == 0xffffffffu || p >= cap_) {
+          wrapped[t].push_back(i);
+          continue;
+        }
+        tag_[p] = tags[i];
+        value_type &v = slot_[p];
+        v.first = key_type(keys + i * nl);
+        v.second = KmerCounts();
+        v.second.count = counts[i];
+        v.second.left = left[i];
+        v.second.right = right[i];
+        m++;
+      }
+      placed[t] = m;
+    };
+    fs_pool_->run(worker);
+    for (int t = 0; t < T; t++) {
+      size_ += placed[t];
+      for (uint64_t i : wrapped[t]) {
+        KmerCounts kc;
+        kc.count = counts[i];
+        kc.left = left[i];
+        kc.right = right[i];
+        fs_wrapped_.emplace_back(key_type(keys + i * nl), kc);
+      }
+    }
+  }
   void fill_end() {
     flush_wrapped();
     fs_pool_.reset();
@@ -738,20 +787,33 @@ void load_ordered(mhmkc_t h, KmerMap<MAX_K> &map, uint64_t n, int threads = 0, u
     std::unique_ptr<uint64_t[]> keys;
     std::unique_ptr<uint16_t[]> counts;
     std::unique_ptr<char[]> left, right;
+    std::unique_ptr<uint32_t[]> slots;
+    std::unique_ptr<uint8_t[]> tags;
   } buf[2];
+  map.fill_begin(n, threads);
+  // into an empty map (the usual case): each row's slot and tag come from the device (mhmkc_fetch_map_range, a prefix
+  // maximum over the ordered rows' home slots), and the fill threads write the rows straight to their slots
+  const bool by_slots = map.fill_by_slots();
+  const uint64_t cap = map.bucket_count();
   for (auto &b : buf) {
     b.keys.reset(new uint64_t[m * nl]);
     b.counts.reset(new uint16_t[m]);
     b.left.reset(new char[m]);
     b.right.reset(new char[m]);
+    if (by_slots) {
+      b.slots.reset(new uint32_t[m]);
+      b.tags.reset(new uint8_t[m]);
+    }
   }
   auto fetch = [&](uint64_t c) {
     Chunk &b = buf[c & 1];
     const uint64_t r0 = c * m;
+    if (by_slots)
+      return mhmkc_fetch_map_range(h, cap, r0, std::min(m, n - r0), b.keys.get(), b.counts.get(), b.left.get(),
+                                   b.right.get(), b.slots.get(), b.tags.get());
     return mhmkc_fetch_ordered_range(h, r0, std::min(m, n - r0), b.keys.get(), b.counts.get(), b.left.get(),
                                      b.right.get());
   };
-  map.fill_begin(n, threads);
   const uint64_t n_ch = (n + m - 1) / m;
   // (the map's fresh memory is faulted in by the fill threads as they write it: a separate parallel pass to fault it in
   // while the first chunk was on the wire measured no faster)
@@ -774,7 +836,11 @@ void load_ordered(mhmkc_t h, KmerMap<MAX_K> &map, uint64_t n, int threads = 0, u
     if (c + 1 < n_ch) f = std::thread([&, c] { rc_next = fetch(c + 1); });
     const Chunk &b = buf[c & 1];
     auto t1 = clk::now();
-    map.fill_chunk(b.keys.get(), b.counts.get(), b.left.get(), b.right.get(), std::min(m, n - c * m));
+    if (by_slots)
+      map.fill_chunk_slots(b.keys.get(), b.counts.get(), b.left.get(), b.right.get(), b.slots.get(), b.tags.get(),
+                           std::min(m, n - c * m));
+    else
+      map.fill_chunk(b.keys.get(), b.counts.get(), b.left.get(), b.right.get(), std::min(m, n - c * m));
     lt.fill += ms_since(t1);
     t1 = clk::now();
     if (f.joinable()) f.join();

@@ -382,6 +382,11 @@ inline int minimizer_len_for(int k) { return k * 2 / 3 + 1 < 15 ? 15 : (k * 2 / 
 // mhmkc_fetch_ordered: the output rows in the order of the top 32 bits of mhmkc_map_hash (kcount_owner.hip)
 size_t map_order_scratch_bytes(uint64_t n, int nlo);
 hipError_t preload_owner_kernels();
+// mhmkc_fetch_map_range: each of the n ordered rows' slot in a KmerMap of cap (a power of two) slots filled in this
+// order from empty (0xFFFFFFFF: past the last slot) and its tag byte
+size_t map_slots_scratch_bytes(uint64_t n);
+hipError_t launch_map_slots(const uint64_t *keys, uint64_t n, int nlo, uint64_t cap, void *scratch, size_t scratch_bytes,
+                            uint32_t *slot, uint8_t *tag, hipStream_t s);
 hipError_t launch_map_order(const OutRows &in, uint64_t n, int nlo, void *scratch, size_t scratch_bytes, const OutRows &out,
                             hipStream_t s);
 // minimizer_hash_fast of n keys (nlo words each, the first k/32+1 used)

@@ -7,6 +7,7 @@
 // each output row and group the rows by owner for the exchange.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 
@@ -153,7 +154,50 @@ hipError_t packed_order(const OutRows &in, uint64_t n, void *scratch, size_t scr
   return hipGetLastError();
 }
 
+// mhmkc_fetch_map_range: every ordered row's home slot in a KmerMap of 2^(64 - shift) slots, minus its row index.
+// Linear probing that inserts rows in home order into an empty map puts row i at pos_i = max(home_i, pos_{i-1} + 1),
+// that is pos_i = i + max_{j <= i}(home_j - j) (a prefix maximum: include/mhmkc_kcount.hpp chunk_ordered).
+__global__ __launch_bounds__(O_THREADS) void k_map_home(const uint64_t *keys, uint64_t n, int nlo, int shift,
+                                                        long long *v) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    v[i] = (long long)(mhmkc_map_hash(keys + i * (uint64_t)nlo, nlo) >> shift) - (long long)i;
+}
+
+// The slot (0xFFFFFFFF past the last one: the map places that row itself) and the tag byte (0x80 | 7 hash bits) of
+// every ordered row.
+__global__ __launch_bounds__(O_THREADS) void k_map_slots(const uint64_t *keys, const long long *m, uint64_t n, int nlo,
+                                                         uint64_t cap, uint32_t *slot, uint8_t *tag) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t pos = i + (uint64_t)m[i];
+    slot[i] = pos < cap && pos < 0xffffffffull ? (uint32_t)pos : 0xffffffffu;
+    tag[i] = (uint8_t)(0x80u | (mhmkc_map_hash(keys + i * (uint64_t)nlo, nlo) & 0x7fu));
+  }
+}
+
 }  // namespace
+
+size_t map_slots_scratch_bytes(uint64_t n) {
+  size_t t = 0;
+  (void)rocprim::inclusive_scan(nullptr, t, (const long long *)nullptr, (long long *)nullptr, (size_t)n,
+                                rocprim::maximum<long long>());
+  return 2 * ((n + 63) / 64 * 64) * 8 + t + 512;
+}
+
+hipError_t launch_map_slots(const uint64_t *keys, uint64_t n, int nlo, uint64_t cap, void *scratch, size_t scratch_bytes,
+                            uint32_t *slot, uint8_t *tag, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (cap < 2 || (cap & (cap - 1)) || scratch_bytes < map_slots_scratch_bytes(n)) return hipErrorInvalidValue;
+  const size_t a = (n + 63) / 64 * 64;
+  long long *v = (long long *)scratch, *m = v + a;
+  void *tmp = m + a;
+  size_t tb = scratch_bytes - 2 * a * 8;
+  k_map_home<<<grid_for(n), O_THREADS, 0, s>>>(keys, n, nlo, __builtin_clzll(cap) + 1, v);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if ((e = rocprim::inclusive_scan(tmp, tb, v, m, (size_t)n, rocprim::maximum<long long>(), s)) != hipSuccess) return e;
+  k_map_slots<<<grid_for(n), O_THREADS, 0, s>>>(keys, m, n, nlo, cap, slot, tag);
+  return hipGetLastError();
+}
 
 // The code object of this file (the hand-off kernels and their rocPRIM sorts) is loaded at its first kernel use; a
 // handle asks for it at create, so that the first ordered fetch of a process does not pay the load (~40 ms).

@@ -290,6 +290,12 @@ struct mhmkc {
   mhm::OutRows ord{};      // the ordered rows (in d_r2 or d_ord), valid while ord_ready
   bool ord_ready = false;  // set by order_rows, cleared by finish / reset
   int order_rows();
+  char *ord_scratch = nullptr;  // the ordering's scratch (free once the rows are ordered) and its size
+  size_t ord_scratch_bytes = 0;
+  // mhmkc_fetch_map_range: each ordered row's KmerMap slot (u32) and tag (u8) for a map of map_cap slots
+  DevBuf d_mslot;
+  uint64_t map_cap = 0;  // the capacity d_mslot holds the slots of (0: none; cleared with ord_ready)
+  int map_slots(uint64_t cap);
   DevBuf d_spill;  // k_count: the deferred records of cold sweeps, mhm::SPILL_RECORDS per persistent workgroup
   DevBuf d_cfit;   // capped fine layout: per coarse bucket of the pass its first record and fine-bucket capacity
   DevBuf d_inc_skip;  // incremental count: per owned coarse bucket, 1 = overflowed its capped layout (k_inc_fixup)
@@ -3229,6 +3235,29 @@ int mhmkc::order_rows() {
   if (n && (e = mhm::launch_map_order(in, n, nlo, base, sb, ord, stream)) != hipSuccess)
     return hip_fail(e, "fetch_ordered sort");
   ord_ready = true;
+  ord_scratch = base;
+  ord_scratch_bytes = sb;
+  map_cap = 0;
+  return MHMKC_OK;
+}
+
+// The KmerMap slot and tag of every ordered row for a map of `cap` slots filled in this order from empty (a prefix
+// maximum on the device, kcount_owner.hip k_map_slots), computed once per capacity.
+int mhmkc::map_slots(uint64_t cap) {
+  int rc = order_rows();
+  if (rc) return rc;
+  if (map_cap == cap) return MHMKC_OK;
+  const uint64_t n = n_out;
+  hipError_t e;
+  if ((e = grow(d_mslot, n * 5 + 256)) != hipSuccess) return hip_fail(e, "map slots");
+  // the scan runs in the ordering's scratch (>= 40 B per row, the scan needs 16 B per row + its own temporary)
+  if (ord_scratch_bytes < mhm::map_slots_scratch_bytes(n)) return fail(MHMKC_EHIP, "internal: map slot scratch");
+  uint32_t *slot = d_mslot.as<uint32_t>();
+  uint8_t *tag = (uint8_t *)(slot + n);
+  if (n && (e = mhm::launch_map_slots(ord.keys, n, nlo, cap, ord_scratch, ord_scratch_bytes, slot, tag, stream)) !=
+               hipSuccess)
+    return hip_fail(e, "map slots");
+  map_cap = cap;
   return MHMKC_OK;
 }
 
@@ -3254,6 +3283,25 @@ int mhmkc_fetch_ordered_range(mhmkc_t h, uint64_t row0, uint64_t n_rows, uint64_
   if (e == hipSuccess && right) e = h->d2h(right, o.right + row0, n_rows);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fetch_ordered");
+}
+
+int mhmkc_fetch_map_range(mhmkc_t h, uint64_t capacity, uint64_t row0, uint64_t n_rows, uint64_t *keys,
+                          uint16_t *counts, char *left, char *right, uint32_t *slots, uint8_t *tags) {
+  if (!h) return MHMKC_EINVAL;
+  if (!h->finished) return h->fail(MHMKC_ESTATE, "fetch before finish");
+  if (capacity < 16 || (capacity & (capacity - 1)) || capacity > (1ull << 32))
+    return h->fail(MHMKC_EINVAL, "capacity must be a power of two in [16, 2^32]");
+  if (row0 > h->n_out || n_rows > h->n_out - row0) return h->fail(MHMKC_EINVAL, "row range past the table's end");
+  if (!n_rows) return MHMKC_OK;
+  int rc = h->map_slots(capacity);
+  if (rc) return rc;
+  const uint32_t *slot = h->d_mslot.as<uint32_t>();
+  const uint8_t *tag = (const uint8_t *)(slot + h->n_out);
+  hipError_t e = hipSuccess;
+  if (slots) e = h->d2h(slots, slot + row0, n_rows * 4);
+  if (e == hipSuccess && tags) e = h->d2h(tags, tag + row0, n_rows);
+  if (e != hipSuccess) return h->hip_fail(e, "fetch_map");
+  return mhmkc_fetch_ordered_range(h, row0, n_rows, keys, counts, left, right);
 }
 
 int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,
