@@ -127,7 +127,9 @@ def test_kmermap_parallel_fill(k, n, chunks, dups, tmp_path):
     chunk_ordered: positions as a running maximum over thread ranges, rows past the last slot wrapped through put), in
     one piece and streamed in chunks as load_ordered feeds it, holds every row with its values, exactly like the
     one-thread insert loop; repeated keys (also across chunk boundaries) keep their first row; unordered rows fall
-    back to the loop."""
+    back to the loop. --slots: the rows' slots and tags computed as the device computes them for mhmkc_fetch_map_range
+    (a prefix maximum of home slot minus row index), placed by KmerMap::fill_chunk_slots, rows past the last slot
+    through put."""
     import numpy as np
 
     from mhm2_proxy_amd import build as b
@@ -145,7 +147,8 @@ def test_kmermap_parallel_fill(k, n, chunks, dups, tmp_path):
     rng.integers(0, 65535, size=n, dtype=np.uint16).tofile(pre + ".counts")
     rng.integers(65, 90, size=n, dtype=np.uint8).tofile(pre + ".left")
     rng.integers(65, 90, size=n, dtype=np.uint8).tofile(pre + ".right")
-    for extra in (["4", "--sort", "--chunks", str(chunks)], ["4", "--chunks", str(chunks)]):
+    for extra in (["4", "--sort", "--chunks", str(chunks)], ["4", "--chunks", str(chunks)],
+                  ["4", "--slots", "--chunks", str(chunks)]):
         r = subprocess.run([str(tool), str(k), str(n), pre, *extra], capture_output=True, text=True)
         assert r.returncode == 0, r.stdout + r.stderr
         import json
