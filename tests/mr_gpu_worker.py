@@ -246,7 +246,11 @@ def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts:
         f"{st['device_bytes'] / 2**30:.1f} GiB (peak {st['device_bytes_peak'] / 2**30:.1f} GiB), sent "
         f"{st['bytes_sent'] / 2**30:.2f} GiB")
     t = c.fetch()
+    lr = lr_check(c, t)
     c.close()
+    if lr["bad_rows"].size:
+        say(f"{lr['bad_rows'].size} rows with left/right outside ACGTXF: {lr}")
+    np.savez(Path(out_dir) / f"rank{rank}_lr.npz", **lr)
     if owner == m.MHMKC_OWNER_MINIMIZER:
         off = np.flatnonzero(O.target_ranks(t.keys, k, world) != rank)
         assert off.size == 0, f"rank {rank}: {off.size} rows not on their target rank"
@@ -263,6 +267,40 @@ def run_share_full(rank: int, world: int, port: int, k: int, out_dir: str, opts:
                                          "inc_rounds", "inc_fallbacks", "ms_finish_tail", "inc_redone_coarse", "inc_slack")})
     dist.barrier()
     dist.destroy_process_group()
+
+
+VALID_EXT = np.frombuffer(b"ACGTXF", dtype=np.uint8)
+
+
+def lr_check(counter, t):
+    """Rows of a fetched table whose left / right byte is not one of get_ext's results (A C G T X F): their indices,
+    the bytes as fetched, the bytes of a second fetch, and the bytes in device memory read back by a separate small
+    copy of just those rows, which tells a transfer that lost bytes from a table written wrong on the device."""
+    left, right = np.asarray(t.left).view(np.uint8), np.asarray(t.right).view(np.uint8)
+    bad = np.flatnonzero(~(np.isin(left, VALID_EXT) & np.isin(right, VALID_EXT)))
+    out = {"bad_rows": bad.astype(np.int64), "n_rows": np.int64(left.size),
+           "first_left": left[bad], "first_right": right[bad]}
+    if bad.size:
+        t2 = counter.fetch()
+        out["second_left"] = np.asarray(t2.left).view(np.uint8)[bad]
+        out["second_right"] = np.asarray(t2.right).view(np.uint8)[bad]
+        import ctypes as C
+
+        import torch
+
+        dev = counter.device_output()
+        # the device bytes of the bad rows, one small hipMemcpy each (torch's own copy path, not libmhmkc's d2h)
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        dl, dr = np.zeros(bad.size, np.uint8), np.zeros(bad.size, np.uint8)
+        for j, i in enumerate(bad[:64]):
+            b1, b2 = C.c_uint8(0), C.c_uint8(0)
+            hip.hipMemcpy(C.byref(b1), C.c_void_p(dev["left"] + int(i)), 1, 2)
+            hip.hipMemcpy(C.byref(b2), C.c_void_p(dev["right"] + int(i)), 1, 2)
+            dl[j], dr[j] = b1.value, b2.value
+        out["device_left"], out["device_right"] = dl, dr
+        torch.cuda.synchronize()
+    return out
 
 
 def read_ctgs(path):

@@ -387,8 +387,9 @@ def _diagnose_part(p, fps, parts, sizes, b, o, k, n_parts):
         if hit:
             j, v = hit
             matched.add(int(j))
-            lines.append(f"  key {[hex(int(x)) for x in keys[j]]} rank {rank}: GPU count {v[0]} L {v[1]} R {v[2]}, "
-                         f"CPU count {int(c[j])} L {chr(int(lft[j]))} R {chr(int(rgt[j]))}")
+            row = int(gi[i]) - (int(ends[rank - 1]) if rank else 0)
+            lines.append(f"  key {[hex(int(x)) for x in keys[j]]} rank {rank} row {row}: GPU count {v[0]} L {v[1]!r} "
+                         f"R {v[2]!r}, CPU count {int(c[j])} L {chr(int(lft[j]))!r} R {chr(int(rgt[j]))!r}")
         else:
             lines.append(f"  GPU-only row (rank {rank}, fingerprint {int(got[i]):#x}): key not among the CPU-only rows")
     for j in only_cpu[:16]:
