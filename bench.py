@@ -143,12 +143,13 @@ def handoff_ms(counter, k: int, threads: int, runs: int = 3):
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
     ms, size, bad, parts = [], C.c_uint64(0), C.c_uint64(0), []
     for _ in range(runs):
-        pa = (C.c_double * 3)()
+        pa = (C.c_double * 5)()
         t = lib.mhmkc_handoff_ms(counter._h, k, threads, 0, C.byref(size), C.byref(bad), pa)
         if t < 0:
             return {"error": "library error in the hand-off"}
         ms.append(t)
-        parts.append({n_: round(v, 1) for n_, v in zip(("first_fetch_incl_sort", "fill", "wait_fetch"), pa)})
+        parts.append({n_: round(v, 1) for n_, v in zip(("first_fetch_incl_sort", "fill", "wait_fetch", "begin", "end"),
+                                                        pa)})
     return {"ms": round(sorted(ms)[len(ms) // 2], 1), "statistic": f"median of {runs} runs",
             "ms_cold": round(ms[0], 1), "runs_ms": [round(x, 1) for x in ms], "rows": counter.n_out,
             "map_size": int(size.value), "sample_rows_bad": int(bad.value), "threads": threads, "parts_ms": parts,

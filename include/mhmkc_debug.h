@@ -24,6 +24,7 @@ extern "C" {
  *   wide_records  1: key-word records instead of the compact / mixed ones
  *   smer          0: MHMKC_OWNER_MINIMIZER at k >= 33 takes the record exchange + hand-off, not supermers
  *   chunk_bytes   H2D chunk of a host batch (0: 128 MB)
+ *   d2h_chunk     staging chunk of a fetch into pageable host memory (0: 8 MB)
  *   cb0, cb0_2, cb0_3  coarse bits for one-, two-, three/four-word keys (0: 8, 8, 7) */
 int mhmkc_debug_set(const char *knob, int64_t value);
 /* Every knob back to its default. */

@@ -51,6 +51,7 @@ struct DebugKnobs {
   int64_t wide_records = 0;   // key-word records instead of the mixed ones (created handles)
   int64_t smer = 1;           // 0: the minimizer owner at k >= 33 takes the record exchange + hand-off
   int64_t chunk_bytes = 0;    // H2D chunk of a host batch (0: CHUNK_BYTES)
+  int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
   int64_t cb0[4] = {0, 0, 0, 0};  // coarse bits by key words (0: the default)
 };
 DebugKnobs g_dbg;
@@ -2301,7 +2302,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
 }
 
 hipError_t mhmkc::d2h(void *dst, const void *src, size_t bytes) {
-  constexpr size_t CH = 8ull << 20;
+  const size_t CH = g_dbg.d2h_chunk > 0 ? (size_t)g_dbg.d2h_chunk : 8ull << 20;
   hipError_t e;
   hipPointerAttribute_t pa{};
   const bool pinned = hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost;
@@ -2319,13 +2320,17 @@ hipError_t mhmkc::d2h(void *dst, const void *src, size_t bytes) {
     const size_t off = c * CH, len = std::min(CH, bytes - off);
     const char *sp = stg.buf[c & 1].as<char>();
     char *dp = (char *)dst + off;
+    // piece t is [cut(t), cut(t + 1)): quarters on 64-byte boundaries, the last one ending at len. (The pieces were
+    // once q = (len / 4 + 63) & ~63 long, which rounds down when len / 4 is a multiple of 64 and len is not one of 4:
+    // the chunk's last 1-3 bytes were never copied. It took the last two rows' left and right bytes of a C4 rank's
+    // 65,094,658-row table, the one-row C4 mismatch of rounds 4-5)
+    auto cut = [&](int t) { return t >= 4 ? len : std::min(len, (len / 4 * (size_t)t) & ~(size_t)63); };
     std::thread th[3];
-    const size_t q = (len / 4 + 63) & ~(size_t)63;
-    for (int t = 0; t < 3; t++) {
-      const size_t a = std::min(len, (t + 1) * q), b = std::min(len, (t + 2) * q);
-      th[t] = std::thread([=] { if (b > a) memcpy(dp + a, sp + a, b - a); });
+    for (int t = 1; t < 4; t++) {
+      const size_t a = cut(t), b = cut(t + 1);
+      th[t - 1] = std::thread([=] { if (b > a) memcpy(dp + a, sp + a, b - a); });
     }
-    memcpy(dp, sp, std::min(len, q));
+    memcpy(dp, sp, cut(1));
     for (auto &x : th) x.join();
   };
   e = hipSuccess;
@@ -3377,6 +3382,7 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
   else if (k == "wide_records") g_dbg.wide_records = value;
   else if (k == "smer") g_dbg.smer = value;
   else if (k == "chunk_bytes") g_dbg.chunk_bytes = value;
+  else if (k == "d2h_chunk") g_dbg.d2h_chunk = value;
   else if (k == "cb0") g_dbg.cb0[1] = value;
   else if (k == "cb0_2") g_dbg.cb0[2] = value;
   else if (k == "cb0_3") g_dbg.cb0[3] = value;

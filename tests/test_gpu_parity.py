@@ -619,3 +619,23 @@ def test_fetch_into_existing_buffers(k, pinned):
             got = c.fetch(ordered=ordered, out=out)
             assert len(got) == n
             assert_tables_equal(got, plain, f"fetch into existing buffers, ordered={ordered}")
+
+
+@pytest.mark.parametrize("chunk", [257, 258, 259, 1000, 4099])
+def test_fetch_staged_chunk_tails(chunk, knob):
+    """A fetch into pageable memory goes through pinned staging chunks, each copied out by four host threads. With
+    staging chunks of 257-259 bytes (quarters of 64.25-64.75 bytes) and other odd sizes, every byte of every array
+    (keys, counts, left, right; plain and ordered) arrives: the quarter split once rounded down and dropped a chunk's
+    last 1-3 bytes (the last two rows' left/right bytes of a C4 rank's 65,094,658-row table)."""
+    b, o = synth_set(2000, 10000, 1234)
+    with m.KmerCounter(63) as c:
+        c.add_packed_reads(b, o)
+        n = c.finish()
+        ref, ref_o = c.fetch(), c.fetch(ordered=True)  # small arrays: one DMA straight into them
+        assert n >= 2 * chunk  # (every array goes through the staging chunks)
+        knob("d2h_chunk", chunk)
+        got, got_o = c.fetch(), c.fetch(ordered=True)
+    for a, e in ((got, ref), (got_o, ref_o)):
+        assert np.array_equal(a.keys, e.keys) and np.array_equal(a.counts, e.counts)
+        assert np.array_equal(a.left, e.left) and np.array_equal(a.right, e.right)
+    assert np.isin(got.left.view(np.uint8), np.frombuffer(b"ACGTXF", np.uint8)).all()

@@ -6,7 +6,8 @@
 //                           double *parts_out)
 // returns the milliseconds from the first fetch to the filled map (-1 on a library error); *size_out = map size;
 // *bad_out = rows of a 1/64 sample (re-fetched afterwards, not timed) that the map does not hold with their values;
-// parts_out[3] (may be null) = load_ordered's first fetch (incl. the device sort), fill, fetch-wait ms.
+// parts_out[5] (may be null) = load_ordered's first fetch (incl. the device sort), fill, fetch-wait, begin (buffers +
+// fill_begin), fill_end ms.
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -31,6 +32,8 @@ static double run(mhmkc_t h, int k, int threads, uint64_t chunk_rows, uint64_t *
       parts_out[0] = lt.first_fetch;
       parts_out[1] = lt.fill;
       parts_out[2] = lt.wait_fetch;
+      parts_out[3] = lt.begin;
+      parts_out[4] = lt.end;
     }
     if (size_out) *size_out = map.size();
     // a sample of the rows, looked up with their values
