@@ -141,6 +141,9 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
   const int64_t gA = (int64_t)tile * (T / 32) - 1;
   for (int g = threadIdx.x; g < NG; g += blockDim.x) {
     const int64_t gi = gA + g;
+    // the group's read-start word first, so that its load is in flight with the bases' (issued after them it was
+    // a second global round trip per tile: the bases' loads are waited for and decoded before it)
+    const uint32_t sw = tile_starts ? gload(tile_starts + (uint64_t)tile * NG + g) : 0u;
     uint64_t f = 0;
     uint32_t gd = 0;
     if (gi >= 0 && (uint64_t)gi * 32 < rv.n_bases) {
@@ -184,7 +187,7 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
     }
     fwd[g] = f;
     good[g] = gd;
-    start[g] = tile_starts ? gload(tile_starts + (uint64_t)tile * NG + g) : 0u;
+    start[g] = sw;
   }
   __syncthreads();
   if (tile_starts) return;  // (uniform) the bitmap came precomputed: no dependent load of the tile's first read
@@ -698,9 +701,22 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   uint32_t *stage32 = (uint32_t *)area;
   uint16_t *sbin = C32 ? (uint16_t *)(stage32 + T) : (uint16_t *)(stage + NL * T);
   uint8_t *sext = (uint8_t *)(sbin + T);
+  // One- and two-word records (BATCH): every rank atomic issued before any result is used (see scatter_staged_c40);
+  // uncounted windows add 0 to a word of their own lane in goff (free until the bins' offsets are written). Three- and
+  // four-word records keep one atomic per counted window: the batched phases cost their kernels a wave per SIMD.
+  constexpr bool BATCH = NL <= 2;
   uint32_t rank[W];
+  if constexpr (BATCH) {
+    uint32_t *const dummy = (uint32_t *)goff + (threadIdx.x & 63u);
 #pragma unroll
-  for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
+    for (int j = 0; j < W; j++) {
+      const bool v = inf[j] >> 31;
+      rank[j] = atomicAdd(v ? &lcnt[inf[j] & 0xffffu] : dummy, v ? 1u : 0u);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < W; j++) rank[j] = (inf[j] >> 31) ? atomicAdd(&lcnt[inf[j] & 0xffffu], 1u) : 0u;
+  }
   __syncthreads();
   // Reserve each bin's run in the global layout. The returned offsets stay in registers while the bins are
   // scanned and the records staged, so the atomics' round trip overlaps that LDS work (a bin count up to
@@ -723,11 +739,17 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   const uint32_t total = block_excl_scan<NT>(lstart, (int)nb, wsum);
   for (uint32_t r0 = 0; r0 < total; r0 += CAP) {  // (uniform) one round when CAP = W * NT
   if (r0) __syncthreads();  // the previous round's copy-out has read the stage area
+  // the bins' run starts of all W records read first (BATCH, see scatter_staged_c40)
+  uint32_t st_[BATCH ? W : 1];
+  if constexpr (BATCH) {
+#pragma unroll
+    for (int j = 0; j < W; j++) st_[j] = lstart[inf[j] & 0xffffu];
+  }
 #pragma unroll
   for (int j = 0; j < W; j++) {
     if (inf[j] >> 31) {
       const uint32_t d = inf[j] & 0xffffu;
-      const uint32_t pos = lstart[d] + rank[j] - r0;  // (earlier rounds' records wrap to >= CAP)
+      const uint32_t pos = (BATCH ? st_[BATCH ? j : 0] : lstart[d]) + rank[j] - r0;  // (earlier rounds' records wrap to >= CAP)
       if (CAP < W * NT && pos >= (uint32_t)CAP) continue;
       if (C32) {
         stage32[pos] = (uint32_t)rk[j][0];
@@ -757,26 +779,38 @@ __device__ __forceinline__ void scatter_staged(const uint64_t (&rk)[W][NL], cons
   }
   }
   __syncthreads();
+  // the copy-out in batches of CB records whose LDS reads are all issued before the first global store (see
+  // scatter_staged_c40)
+  constexpr int NJ = CAP / NT, CB = !BATCH ? 1 : NJ % 4 == 0 ? 4 : NJ % 2 == 0 ? 2 : 1;
 #pragma unroll
-  for (int j = 0; j < CAP / NT; j++) {
-    const uint32_t sp = threadIdx.x + j * NT, pos = sp + r0;  // stage slot, position in the workgroup's run
-    if (pos < total) {
-      const uint32_t d = sbin[sp];
-      const unsigned long long go = goff[d];
-      if (go == ~0ull) continue;
-      const unsigned long long dst = go + (pos - lstart[d]);
-      uint64_t v[NL];
+  for (int j0 = 0; j0 < NJ; j0 += CB) {
+    uint32_t d[CB], ls[CB], xe[CB];
+    unsigned long long go[CB];
+    uint64_t v[CB][NL];
+#pragma unroll
+    for (int jj = 0; jj < CB; jj++) d[jj] = sbin[threadIdx.x + (j0 + jj) * NT];  // (past total: stale, unused)
+#pragma unroll
+    for (int jj = 0; jj < CB; jj++) {
+      const uint32_t sp = threadIdx.x + (j0 + jj) * NT;
+      const uint32_t dd = d[jj] < nb ? d[jj] : 0u;
+      go[jj] = goff[dd];
+      ls[jj] = lstart[dd];
       if (C32) {
-        v[0] = (uint64_t)stage32[sp] | (SF == SF_C40 ? (uint64_t)sext[sp] << 32 : 0ull);
+        v[jj][0] = (uint64_t)stage32[sp] | (SF == SF_C40 ? (uint64_t)sext[sp] << 32 : 0ull);
       } else if (SF == SF_AOS2) {
         const ulonglong2 q = ((const ulonglong2 *)stage)[sp];
-        v[0] = q.x;
-        v[NL - 1] = q.y;
+        v[jj][0] = q.x;
+        v[jj][NL - 1] = q.y;
       } else {
 #pragma unroll
-        for (int w = 0; w < NL; w++) v[w] = stage[w * T + sp];
+        for (int w = 0; w < NL; w++) v[jj][w] = stage[w * T + sp];
       }
-      store_out<NL, PACKED, SF>(out, dst, v, PACKED ? 0u : sext[sp]);
+      xe[jj] = PACKED ? 0u : sext[sp];
+    }
+#pragma unroll
+    for (int jj = 0; jj < CB; jj++) {
+      const uint32_t sp = threadIdx.x + (j0 + jj) * NT, pos = sp + r0;  // stage slot, position in the workgroup's run
+      if (pos < total && go[jj] != ~0ull) store_out<NL, PACKED, SF>(out, go[jj] + (pos - ls[jj]), v[jj], xe[jj]);
     }
   }
   }  // rounds
@@ -1350,24 +1384,27 @@ __device__ __forceinline__ bool xcd_chunk(const PartitionParams &p, uint32_t &c)
   return c < p.xcd_start[x + 1];
 }
 
-// The chunk a partition workgroup works on: its run from the per-chunk run index, then its tile of it.
+// The chunk a partition workgroup works on: one 24-byte load of the span k_chunk_runs expanded (the run index and
+// then the run cost two dependent global round trips before the chunk's records could be loaded).
 template <int T>
 __device__ __forceinline__ SChunk chunk_of(const PartitionParams &p, uint32_t c) {
-  const SRun r = p.runs[p.chunk_run[c]];
-  const uint64_t o = (uint64_t)(c - r.chunk0) * T;
-  SChunk ch;
-  ch.start = r.start + o;
-  ch.count = (uint32_t)(r.count - o < (uint64_t)T ? r.count - o : (uint64_t)T);
-  ch.src = r.src;
-  ch.coarse_local = r.coarse_local;
-  ch.pad = 0;
-  return ch;
+  return p.chunks[c];
 }
 
-__global__ __launch_bounds__(256) void k_chunk_runs(const SRun *runs, uint32_t *chunk_run, int tile) {
+// Every run's chunks (one workgroup per run): chunk i of a run is records [i T, min((i + 1) T, count)) of it.
+__global__ __launch_bounds__(256) void k_chunk_runs(const SRun *runs, SChunk *chunks, int tile) {
   const SRun r = runs[blockIdx.x];
   const uint32_t n = (uint32_t)((r.count + tile - 1) / tile);
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) chunk_run[r.chunk0 + i] = blockIdx.x;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint64_t o = (uint64_t)i * tile;
+    SChunk ch;
+    ch.start = r.start + o;
+    ch.count = (uint32_t)(r.count - o < (uint64_t)tile ? r.count - o : (uint64_t)tile);
+    ch.src = r.src;
+    ch.coarse_local = r.coarse_local;
+    ch.pad = 0;
+    chunks[r.chunk0 + i] = ch;
+  }
 }
 
 // All W records of a thread are loaded before any is processed (W * 8 B * NL in flight per lane). The
@@ -1673,6 +1710,16 @@ struct CountLds {
   int cap;         // multiple of 4: slots are probed in groups of 4
 };
 
+// An LDS fetch-add whose result is used later (k_count's dynamic slot counter, read at the end of the round): the
+// address goes through an opaque move, so the atomic optimizer does not expand the add for a uniform address (a
+// reduction over the active lanes that waits for the result at once: an LDS round trip at the top of every round).
+typedef __attribute__((address_space(3))) unsigned int lds_u32_t;
+__device__ __forceinline__ uint32_t lds_add_late(unsigned int *p, uint32_t v) {
+  lds_u32_t *q = (lds_u32_t *)p;
+  asm volatile("" : "+v"(q));
+  return __hip_atomic_fetch_add(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Groups a key may probe before its record is deferred to the next sweep of its bucket.
 constexpr int C_PROBE = 64;
 // First-group reads a lane keeps in flight in phase A (two-word keys: one at a time, measured 11.39 -> 11.24 ms at
@@ -1912,18 +1959,15 @@ __device__ __forceinline__ void lds_clamp(const CountLds<K> &t, int slot, uint32
 #define STAMP_ADD(i, v)
 #endif
 
-// Final decision for one table slot: insert_into_local_hashtable (src/kcount/kcount_cpu.cpp:503-517):
-// count < 2 -> purged; left/right = get_ext(count) (kcount_cpu.cpp:173-182, with the exact double
-// expression of the dynamic threshold); both 'X' -> purged.
-template <typename K>
-__device__ __forceinline__ bool slot_survives(const CountLds<K> &t, int slot, const CountParams &p, uint32_t c32,
-                                              uint16_t &c16, char &L, char &R) {
+// Final decision for one listed table slot (count >= 2): insert_into_local_hashtable
+// (src/kcount/kcount_cpu.cpp:503-517): left/right = get_ext(count) (kcount_cpu.cpp:173-182, with the exact double
+// expression of the dynamic threshold); both 'X' -> purged. The caller reads the slot's count word and its four
+// extension words together (one LDS round trip: a listed slot always has count >= 2, so nothing waits for the count).
+__device__ __forceinline__ bool slot_survives(uint32_t c32, uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3,
+                                              const CountParams &p, uint16_t &c16, char &L, char &R) {
   const uint32_t c = c32 > 65535u ? 65535u : c32;
   c16 = (uint16_t)c;
-  if (c < 2) return false;
   const int thr = dyn_threshold(c, p.dyn_mult, p.dmin_thres);
-  const uint32_t e0 = t.ext[slot], e1 = t.ext[t.cap + slot];
-  const uint32_t e2 = t.ext[2 * t.cap + slot], e3 = t.ext[3 * t.cap + slot];
   L = ext_choice(e0 & 0xffffu, e0 >> 16, e1 & 0xffffu, e1 >> 16, thr);
   R = ext_choice(e2 & 0xffffu, e2 >> 16, e3 & 0xffffu, e3 >> 16, thr);
   return !(L == 'X' && R == 'X');
@@ -2125,6 +2169,17 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   K *s_mkey = (K *)(smem + count_table_bytes(NL, RK::C32));
   uint32_t *s_me = (uint32_t *)(s_mkey + NL * MC);
   constexpr int SPT = (count_cap(NL, RK::C32) + C_THREADS - 1) / C_THREADS;  // table slots per thread (finalize)
+  // The finalize keeps its survivors' key words in registers (one- to three-word keys; four key words would
+  // hold SPT x NL x 2 more VGPRs) when the slots it lists fit KJ per thread, so that it clears the table while the
+  // output reservation is in flight; a bucket with more listed slots writes its output from the table first.
+#ifndef MHMKC_KREG_NL
+#define MHMKC_KREG_NL 3
+#endif
+#ifndef MHMKC_KJ
+#define MHMKC_KJ 2
+#endif
+  constexpr bool KREG = NL <= MHMKC_KREG_NL;
+  constexpr int KJ = KREG ? (MHMKC_KJ < SPT ? MHMKC_KJ : SPT) : 1;
 
 #define tid (count_tid<NL>())  // (see count_tid; #undef after the kernel)
 #define lane (count_tid<NL>() & 63)
@@ -2236,11 +2291,34 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   unsigned long long &s_missacc = s_u64[4];  // phase-B records of this workgroup (the LDS op mix, stats)
 #if MHMKC_STAMP
   uint64_t st_acc[6] = {0, 0, 0, 0, 0, 0};
+  const uint64_t st_wg0 = __builtin_amdgcn_s_memtime();
 #endif
-  if (tid == 0) {  // (the first sweep's clear ends with a barrier)
+  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
+  auto clear_table = [&]() {
+    uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
+    const int n_ones = t.cap * (int)sizeof(K) / 16;
+    for (int i = tid; i < n_ones; i += C_THREADS) ones[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    uint4 *zeros = (uint4 *)t.cnt;
+    const int n_zeros = t.cap * 20 / 16;
+    for (int i = tid; i < n_zeros; i += C_THREADS) zeros[i] = make_uint4(0, 0, 0, 0);
+  };
+  // a sweep's scalars: deferral counters, dynamic slot counter, error flag
+  auto reset_sweep = [&]() {
+    if (tid == 0) {
+      s_ovf = 0;
+      s_err = 0;
+      s_next = 2 * (C_THREADS / 64);  // (slots s and 16 + s are wave s's own: already prefetched / next)
+    }
+    if (tid < C_THREADS / 64) s_wdef[tid] = 0;
+  };
+  if (tid == 0) {
     s_missacc = 0;
     s_u64[3] = 0;  // finalize's counters
   }
+  // the first sweep's table; every later sweep's is cleared by the finalize before it
+  clear_table();
+  reset_sweep();
+  __syncthreads();
   // this workgroup's spill area (dynamic sweeps: their deferred records; the sweep after reads them from there)
   const Src spill{(uint64_t)blockIdx.x * SPILL_RECORDS, 1u};
   const bool has_spill = p.spill.w[0] != nullptr;
@@ -2269,26 +2347,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
   // a dependent round trip there (unconditional: without a next bucket it re-reads this bucket's, never used)
   const uint32_t b_ext = b_next < p.n_buckets ? b_next : b;
   const uint64_t nx_base = p.bucket_base[b_ext], nx_end = p.bucket_end[b_ext];
-  while (true) {  // sweeps of bucket b
-    STAMP(t_sw0);
-    {  // clear the table with 16-byte stores: last-word plane = EMPTY, counters = 0
-      uint4 *ones = (uint4 *)(t.keys + (NL - 1) * t.cap);
-      const int n_ones = t.cap * (int)sizeof(K) / 16;
-      for (int i = tid; i < n_ones; i += C_THREADS) ones[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
-      uint4 *zeros = (uint4 *)t.cnt;
-      const int n_zeros = t.cap * 20 / 16;
-      for (int i = tid; i < n_zeros; i += C_THREADS) zeros[i] = make_uint4(0, 0, 0, 0);
-    }
-    if (tid == 0) {
-      s_ovf = 0;
-      s_err = 0;
-    }
-    if (tid < C_THREADS / 64) s_wdef[tid] = 0;
-    if (tid == 0) s_next = 2 * (C_THREADS / 64);  // (slots s and 16 + s are wave s's own: already prefetched / next)
-    __syncthreads();
-    STAMP(t_sw1);
-    STAMP_ADD(0, t_sw1 - t_sw0);
-
+  while (true) {  // sweeps of bucket b (the table is clear and the sweep's scalars reset)
     // R records per thread per round, the next round prefetched into registers, so that every CU keeps
     // R * 8 KB of record loads in flight. A round has two phases:
     //   A. every lane looks its records up in their home group; found keys are counted at once, a new key with an
@@ -2315,7 +2374,7 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         uint64_t ck[R][NL];
         uint32_t ce[R];
         uint32_t ca = 0;  // DYN: the slot after cn (lane 0 asks now, the answer is read at the end of the round)
-        if (DYN && lane == 0) ca = atomicAdd(&s_next, 1u);
+        if (DYN && lane == 0) ca = lds_add_late(&s_next, 1u);
         const uint32_t cr0 = DYN ? cc / NWV * RND : r0;                              // the slot's round
         const uint32_t vt = DYN ? cc % NWV * 64u + (uint32_t)lane : (uint32_t)tid;  // its thread slot
         // record j of this lane is valid iff j * vstep < vrem: the records left from this lane's first one (a dense
@@ -2563,6 +2622,18 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     STAMP_ADD(3, t_f0 - t_b0);  // (the sweep's end barrier: the waves' imbalance; cold sweeps have no round barrier)
     // no deferred records: this is the bucket's last sweep, so start loading the next bucket now
     const bool last_sweep = s_ovf == 0;
+    // what a next sweep of this bucket needs, read before the finalize resets the sweep's scalars
+    const uint32_t n_def = s_ovf;
+    const bool err_sw = s_err != 0;
+    uint32_t nw_def = 0, mx_def = 0;
+    if (!last_sweep) {
+      nw_def = s_wdef[wid];
+#pragma unroll
+      for (int w = 0; w < C_THREADS / 64; w++) mx_def = mx_def > s_wdef[w] ? mx_def : s_wdef[w];
+      // this wave's deferred records (global stores of the rounds) are released before the finalize's barriers; the
+      // next sweep's loads acquire them after the last one
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    }
     // (a skipped coarse bucket's fine buckets are empty, k_inc_fixup, and its contig k-mers wait for the launch
     // that counts it)
     if (p.ctg_n && !(p.coarse_skip && p.coarse_skip[b >> p.fine_bits])) ctg_apply<NL, CMP>(t, p, b, last_sweep, cold, s_red);
@@ -2631,19 +2702,34 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
     }
     __syncthreads();
     const uint32_t n_list = s_fin[0];
-    uint32_t surv_mask = 0, spos[SPT];
-    uint16_t c16[SPT], fslot[SPT];
-    char L[SPT], R_[SPT];
+    // per listed slot of this thread: sp = slot | output position << 16 (both < 2^16), row = count | L << 16 | R << 24
+    uint32_t surv_mask = 0, sp[SPT], row[SPT];
+    // (uniform) the survivors' key words go to registers: the table may be cleared before the output is written
+    const bool kfast = KREG && n_list <= (uint32_t)(KJ * C_THREADS);
+    K kreg[KJ][NL];
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
       const uint32_t i = (uint32_t)tid + (uint32_t)j * C_THREADS;
-      spos[j] = 0;
-      fslot[j] = 0;
+      sp[j] = 0;
+      row[j] = 0;
       bool sv = false;
       if (i < n_list) {
         const int slot = flist[i];
-        fslot[j] = (uint16_t)slot;
-        sv = slot_survives(t, slot, p, slot_count(t, slot, cold), c16[j], L[j], R_[j]);
+        sp[j] = (uint32_t)slot;
+        uint16_t c16;
+        char L, R_;
+        const uint32_t cw = t.cnt[slot], e0 = t.ext[slot], e1 = t.ext[t.cap + slot], e2 = t.ext[2 * t.cap + slot],
+                       e3 = t.ext[3 * t.cap + slot];
+        if (KREG && j < KJ) {  // (with the counters: the same round trip)
+#pragma unroll
+          for (int w = 0; w < NL; w++) kreg[j < KJ ? j : 0][w] = t.keys[w * t.cap + slot];
+        }
+        // slot_count's cold encoding from the words already read
+        const uint32_t c32 = !cold ? cw
+                             : (cw >> 31) ? cw & 0x7fffffffu
+                                          : cw + (e0 & 0xffffu) + (e0 >> 16) + (e1 & 0xffffu) + (e1 >> 16);
+        sv = slot_survives(c32, e0, e1, e2, e3, p, c16, L, R_);
+        row[j] = (uint32_t)c16 | (uint32_t)(uint8_t)L << 16 | (uint32_t)(uint8_t)R_ << 24;
       }
       // one reservation per wave for its survivors (ballot + lane prefix)
       const uint64_t bal = __ballot(sv);
@@ -2653,15 +2739,27 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
         sb = __builtin_amdgcn_readfirstlane(sb);
         if (sv) {
           surv_mask |= 1u << j;
-          spos[j] = sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          sp[j] |= (sb + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))) << 16;
         }
       }
     }
     const uint32_t mine = __popc(surv_mask);
     __syncthreads();
+    // The survivors take one global reservation. With their key words in registers (kfast) the table is cleared for
+    // the next sweep while it is in flight, and the output rows are written after one barrier with the next sweep's
+    // rounds right behind them (two barriers fewer per bucket than clearing at the sweep's start).
+    unsigned long long gret = 0;
+    uint32_t acc = 0;
     if (tid == 0) {
-      const uint32_t acc = s_fin[1];
-      unsigned long long gb = acc ? atomicAdd(p.out_cursor, (unsigned long long)acc) : 0ull;
+      acc = s_fin[1];
+      if (acc) gret = atomicAdd(p.out_cursor, (unsigned long long)acc);
+    }
+    STAMP(t_c0);
+    if (kfast) clear_table();
+    STAMP(t_c1);
+    reset_sweep();  // (every thread read what it needs of the sweep's scalars above)
+    if (tid == 0) {
+      unsigned long long gb = gret;
       if (acc && gb + acc > p.out_cap) {  // the output is full: write nothing, flag the launch (the cursor still
         atomicOr(p.err, 16u);             // counts: the host grows the output to it and redoes the pass)
         gb = ~0ull;
@@ -2676,49 +2774,56 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #pragma unroll
     for (int j = 0; j < SPT; j++) {
       if ((surv_mask >> j) & 1u) {
-        const int slot = fslot[j];
-        const unsigned long long g = s_gbase + spos[j];
+        const int slot = (int)(sp[j] & 0xffffu);
+        // the key words: from registers (kfast: every listed slot is one of a thread's first KJ) or from the table
+        auto kw_of = [&](int w) -> K { return (KREG && j < KJ && kfast) ? kreg[j < KJ ? j : 0][w] : t.keys[w * t.cap + slot]; };
+        const unsigned long long g = s_gbase + (sp[j] >> 16);
         uint64_t *ok = p.out_keys + g * (uint64_t)p.nlo;
         if (RK::C32) {  // key = cunmix(global fine bucket digits | stored bits)
           const int B = 2 * p.k, rb = B - p.coarse_bits - p.fine_bits;
-          const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          const uint64_t y = ((uint64_t)(p.bucket0 + b) << rb) | (kw_of(0) >> EXT_BITS);
           ok[0] = cunmix(y, B) << (64 - B);
         } else if (RK::M2) {  // key = m2_unmix(global fine bucket digits | stored L' bits, R')
           const int rb = p.k - p.coarse_bits - p.fine_bits;
-          const uint64_t L = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          const uint64_t L = ((uint64_t)(p.bucket0 + b) << rb) | (kw_of(0) >> EXT_BITS);
           uint64_t kw[2];
-          m2_unmix(L, t.keys[t.cap + slot], p.k, kw);
+          m2_unmix(L, kw_of(1), p.k, kw);
           ok[0] = kw[0];
           ok[1] = kw[1];
         } else if (RK::MX) {  // key = mx_unmix(global fine bucket digits | stored w0' bits, r[1..])
           const int rb = 64 - p.coarse_bits - p.fine_bits;
           uint64_t r[NL], kw[NL];
-          r[0] = ((uint64_t)(p.bucket0 + b) << rb) | (t.keys[slot] >> EXT_BITS);
+          r[0] = ((uint64_t)(p.bucket0 + b) << rb) | (kw_of(0) >> EXT_BITS);
 #pragma unroll
-          for (int w = 1; w < NL; w++) r[w] = t.keys[w * t.cap + slot];
+          for (int w = 1; w < NL; w++) r[w] = kw_of(w);
           mx_unmix<NL>(r, kw);
 #pragma unroll
           for (int w = 0; w < NL; w++) ok[w] = kw[w];
         } else {
 #pragma unroll
-          for (int w = 0; w < NL; w++) ok[w] = t.keys[w * t.cap + slot];
+          for (int w = 0; w < NL; w++) ok[w] = kw_of(w);
         }
         for (int w = NL; w < p.nlo; w++) ok[w] = 0;
-        p.out_counts[g] = c16[j];
-        p.out_left[g] = L[j];
-        p.out_right[g] = R_[j];
+        p.out_counts[g] = (uint16_t)row[j];
+        p.out_left[g] = (char)(row[j] >> 16);
+        p.out_right[g] = (char)(row[j] >> 24);
       }
     }
     my_occ += occ;
     my_purged += occ;  // minus the survivors, in 64 bits: with two passes a lane's survivors are not its slots
     my_purged -= mine;
     my_sum += sum;
-    __syncthreads();
+    if (!kfast) {  // the output read the table: clear it after
+      __syncthreads();
+      clear_table();
+      __syncthreads();
+    }
     STAMP(t_f1);
-    STAMP_ADD(5, t_f1 - t_f0);
-    if (s_err && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
+    STAMP_ADD(0, t_c1 - t_c0);
+    STAMP_ADD(5, t_f1 - t_f0 - (t_c1 - t_c0));
+    if (err_sw && tid == 0) atomicAdd(&p.stats[STAT_N - 1], 1ull);
     if (last_sweep) break;
-    n = s_ovf;
+    n = n_def;
     lim = n;
     if (dyn_sweep) {  // the deferred records, dense in pd, are the next sweep's; the region it read takes its deferrals
       const Src t_ = ps;
@@ -2726,19 +2831,15 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
       pd = t_;
       nw = NONE;
     } else {  // each wave re-reads its own deferred records; the rounds cover the largest share
-      nw = s_wdef[wid];
-      uint32_t mx = 0;
-#pragma unroll
-      for (int w = 0; w < C_THREADS / 64; w++) mx = mx > s_wdef[w] ? mx : s_wdef[w];
-      lim = (mx + (uint32_t)(64 * R) - 1) / (uint32_t)(64 * R) * RND;
+      nw = nw_def;
+      lim = (mx_def + (uint32_t)(64 * R) - 1) / (uint32_t)(64 * R) * RND;
     }
     my_sweeps++;
-    // overflow records were written by this workgroup: make them visible to its own loads
+    // the deferred records of every wave (released before the finalize's barriers) are visible to this wave's loads
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    __syncthreads();
   }  // sweeps
   if (b_next >= p.n_buckets) break;
-  b = b_next;  // the finalize above ended with a barrier: the table may be cleared for the next bucket
+  b = b_next;  // (the finalize cleared the table for the next bucket)
   ps = ps_next;
   n = nb_next;
   pd = spill;
@@ -2748,6 +2849,11 @@ __global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
 #if MHMKC_STAMP
   if (lane == 0)
     for (int i = 0; i < 6; i++) atomicAdd(&p.stats[8 + i], (unsigned long long)st_acc[i]);
+  if (tid == 0) {  // the workgroup's cycles: sum and largest (the launch's tail)
+    const uint64_t el = __builtin_amdgcn_s_memtime() - st_wg0;
+    atomicAdd(&p.stats[14], (unsigned long long)el);
+    atomicMax(&p.stats[15], (unsigned long long)el);
+  }
 #endif
   // block reduction of the statistics
   my_occ = wave_sum_u64(my_occ);
@@ -2960,9 +3066,9 @@ hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hi
   MHM_DISPATCH(nl, packed, do_part_scatter, (p, s));
 }
 
-hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_run, int tile, hipStream_t s) {
+hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, SChunk *chunks, int tile, hipStream_t s) {
   if (!n_runs) return hipSuccess;
-  k_chunk_runs<<<dim3(n_runs), dim3(256), 0, s>>>(runs, chunk_run, tile);
+  k_chunk_runs<<<dim3(n_runs), dim3(256), 0, s>>>(runs, chunks, tile);
   return hipGetLastError();
 }
 

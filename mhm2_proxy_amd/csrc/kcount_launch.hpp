@@ -108,7 +108,7 @@ struct SRun {
 
 struct PartitionParams {
   const SRun *runs;                 // [n_runs]
-  const uint32_t *chunk_run;        // [n_chunks]: run of each chunk (launch_chunk_runs fills it)
+  const SChunk *chunks;             // [n_chunks]: each chunk's span (launch_chunk_runs expands the runs into them)
   uint32_t n_runs;
   uint32_t n_chunks;
   // XCD-aware launch: the chunks are ordered by XCD class (coarse bucket % 8); class x holds chunks
@@ -296,7 +296,7 @@ hipError_t launch_init_fine(const unsigned long long *coarse_base, const unsigne
 hipError_t launch_extract_hist(const ExtractParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_extract_scatter(const ExtractParams &p, int nl, bool packed, hipStream_t s);
 // chunk_run[c] for every chunk of the runs (one workgroup per run)
-hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, uint32_t *chunk_run, int tile, hipStream_t s);
+hipError_t launch_chunk_runs(const SRun *runs, uint32_t n_runs, SChunk *chunks, int tile, hipStream_t s);
 hipError_t launch_part_hist(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 hipError_t launch_part_scatter(const PartitionParams &p, int nl, bool packed, hipStream_t s);
 // HyperLogLog sketch of the distinct keys in chunks [0, n_chunks) of p's chunk table (one coarse bucket):

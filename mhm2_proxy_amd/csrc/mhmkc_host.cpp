@@ -1609,12 +1609,13 @@ int mhmkc::upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_
   hipError_t e;
   const size_t rb = align_up(std::max<size_t>(1, rt.runs.size()) * sizeof(mhm::SRun), 256);
   const bool main = s == stream;  // (main stream: earlier kernels may still read the buffers, grow waits for them)
-  if ((e = main ? grow(buf, rb + 4 * (rt.n_chunks + 1) + 256) : buf.ensure(rb + 4 * (rt.n_chunks + 1) + 256)) != hipSuccess)
+  const size_t cb_ = sizeof(mhm::SChunk) * (rt.n_chunks + 1) + 256;
+  if ((e = main ? grow(buf, rb + cb_) : buf.ensure(rb + cb_)) != hipSuccess)
     return hip_fail(e, "chunk table");
   const size_t sb = std::max<size_t>(1, rt.ps.size()) * sizeof(mhm::PlaneSet) + 64;
   if ((e = main ? grow(sbuf, sb) : sbuf.ensure(sb)) != hipSuccess) return hip_fail(e, "source table");
   mhm::SRun *d_runs = buf.as<mhm::SRun>();
-  uint32_t *d_chunk_run = (uint32_t *)(buf.as<char>() + rb);
+  mhm::SChunk *d_chunk_run = (mhm::SChunk *)(buf.as<char>() + rb);
   if (!rt.runs.empty()) {
     if ((e = hipMemcpyAsync(d_runs, rt.runs.data(), rt.runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, s)) !=
         hipSuccess)
@@ -1627,7 +1628,7 @@ int mhmkc::upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_
           hipSuccess)
     return hip_fail(e, "source H2D");
   pp.runs = d_runs;
-  pp.chunk_run = d_chunk_run;
+  pp.chunks = d_chunk_run;
   pp.n_runs = (uint32_t)rt.runs.size();
   pp.n_chunks = (uint32_t)rt.n_chunks;
   for (int x = 0; x < 9; x++) pp.xcd_start[x] = (uint32_t)rt.xcd_start[x];
@@ -2069,11 +2070,12 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     if (n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
     uint64_t xcd_max = 0;
     for (int x = 0; x < 8; x++) xcd_max = std::max(xcd_max, xcd_start[x + 1] - xcd_start[x]);
-    if ((e = grow(d_chunks, std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun) + 4 * (n_chunks + 1) + 256)) !=
+    if ((e = grow(d_chunks, align_up(std::max<size_t>(1, runs.size()) * sizeof(mhm::SRun), 256) +
+                                sizeof(mhm::SChunk) * (n_chunks + 1) + 256)) !=
         hipSuccess)
       return hip_fail(e, "chunk table");
     mhm::SRun *d_runs = d_chunks.as<mhm::SRun>();
-    uint32_t *d_chunk_run = (uint32_t *)(d_chunks.as<char>() + align_up(runs.size() * sizeof(mhm::SRun), 256));
+    mhm::SChunk *d_chunk_run = (mhm::SChunk *)(d_chunks.as<char>() + align_up(runs.size() * sizeof(mhm::SRun), 256));
     if ((e = grow(d_srcs, std::max<size_t>(1, ps.size()) * sizeof(mhm::PlaneSet) + 64)) != hipSuccess ||
         (e = grow(d_cfit, 16 * (size_t)np_ + 64)) != hipSuccess)
       return hip_fail(e, "source table");
@@ -2100,7 +2102,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
       if (n_c0) {
         mhm::PartitionParams sp{};
         sp.runs = d_runs;
-        sp.chunk_run = d_chunk_run;
+        sp.chunks = d_chunk_run;
         sp.n_runs = (uint32_t)runs.size();
         sp.n_chunks = (uint32_t)n_chunks;
         sp.srcs = d_srcs.as<mhm::PlaneSet>();
@@ -2163,7 +2165,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
 
     mhm::PartitionParams pp{};
     pp.runs = d_runs;
-    pp.chunk_run = d_chunk_run;
+    pp.chunks = d_chunk_run;
     pp.n_runs = (uint32_t)runs.size();
     pp.n_chunks = (uint32_t)n_chunks;
     for (int x = 0; x < 9; x++) pp.xcd_start[x] = (uint32_t)xcd_start[x];
@@ -2277,7 +2279,8 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     for (int i = 0; i < 6; i++) tot += (double)acc_stats[8 + i];
     fprintf(stderr, "k_count stamps:");
     for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.1f%%", names[i], tot > 0 ? 100.0 * acc_stats[8 + i] / tot : 0.0);
-    fprintf(stderr, " (total %.3g wave-cycles)\n", tot);
+    fprintf(stderr, " (total %.3g wave-cycles); workgroup cycles mean %.4g max %.4g\n", tot,
+            (double)acc_stats[14] / std::max(1, n_cu), (double)acc_stats[15]);
   }
 #endif
   st.distinct = acc_stats[mhm::STAT_DISTINCT];
