@@ -299,6 +299,13 @@ int mhmkc_fetch_ordered_range(mhmkc_t h, uint64_t row0, uint64_t n_rows, uint64_
 int mhmkc_fetch_map_range(mhmkc_t h, uint64_t capacity, uint64_t row0, uint64_t n_rows, uint64_t *keys,
                           uint16_t *counts, char *left, char *right, uint32_t *slots, uint8_t *tags);
 
+/* Pinned (page-locked) host memory for a caller's fetch buffers: a fetch into it is one DMA per array, with no copy
+ * through the library's staging buffers (mhmkc_fetch copies into pageable memory chunk by chunk). Freed blocks are
+ * kept by the library for the next mhmkc_host_alloc (up to 2 GiB), since pinning costs more than one copy. NULL when
+ * the allocation fails; mhmkc_host_free ignores pointers it did not hand out. */
+void *mhmkc_host_alloc(uint64_t bytes);
+void mhmkc_host_free(void *p);
+
 /* Device pointers of the finished table (valid until the next reset/destroy). */
 int mhmkc_device_output(mhmkc_t h, const uint64_t **d_keys, const uint16_t **d_counts, const char **d_left,
                         const char **d_right, uint64_t *n_out);

@@ -785,36 +785,54 @@ void load_ordered(mhmkc_t h, KmerMap<MAX_K> &map, uint64_t n, int threads = 0, u
   const auto tb = clk::now();
   const int nl = Kmer<MAX_K>::N_LONGS;
   const uint64_t m = std::min<uint64_t>(std::max<uint64_t>(chunk_rows, 1), std::max<uint64_t>(n, 1));
+  // a chunk's arrays in one block of pinned host memory from the library (one DMA per array straight into it, and the
+  // block reused by the next hand-off), else of the heap (then the fetch copies through the library's staging)
+  struct Block {
+    void *p = nullptr;
+    bool pinned = false;
+    ~Block() {
+      if (pinned)
+        mhmkc_host_free(p);
+      else
+        delete[] (char *)p;
+    }
+  };
   struct Chunk {  // (not zero-filled: the fetch writes every row it is read for)
-    std::unique_ptr<uint64_t[]> keys;
-    std::unique_ptr<uint16_t[]> counts;
-    std::unique_ptr<char[]> left, right;
-    std::unique_ptr<uint32_t[]> slots;
-    std::unique_ptr<uint8_t[]> tags;
+    Block blk;
+    uint64_t *keys = nullptr;
+    uint16_t *counts = nullptr;
+    char *left = nullptr, *right = nullptr;
+    uint32_t *slots = nullptr;
+    uint8_t *tags = nullptr;
   } buf[2];
   map.fill_begin(n, threads);
   // into an empty map (the usual case): each row's slot and tag come from the device (mhmkc_fetch_map_range, a prefix
   // maximum over the ordered rows' home slots), and the fill threads write the rows straight to their slots
   const bool by_slots = map.fill_by_slots();
   const uint64_t cap = map.bucket_count();
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t kb = al(m * 8 * nl), cb = al(m * 2), lb = al(m), sb = by_slots ? al(m * 4) : 0, gb = by_slots ? al(m) : 0;
   for (auto &b : buf) {
-    b.keys.reset(new uint64_t[m * nl]);
-    b.counts.reset(new uint16_t[m]);
-    b.left.reset(new char[m]);
-    b.right.reset(new char[m]);
+    const size_t tot = kb + cb + 2 * lb + sb + gb;
+    b.blk.p = mhmkc_host_alloc(tot);
+    b.blk.pinned = b.blk.p != nullptr;
+    if (!b.blk.p) b.blk.p = new char[tot];
+    char *q = (char *)b.blk.p;
+    b.keys = (uint64_t *)q;
+    b.counts = (uint16_t *)(q + kb);
+    b.left = q + kb + cb;
+    b.right = q + kb + cb + lb;
     if (by_slots) {
-      b.slots.reset(new uint32_t[m]);
-      b.tags.reset(new uint8_t[m]);
+      b.slots = (uint32_t *)(q + kb + cb + 2 * lb);
+      b.tags = (uint8_t *)(q + kb + cb + 2 * lb + sb);
     }
   }
   auto fetch = [&](uint64_t c) {
     Chunk &b = buf[c & 1];
     const uint64_t r0 = c * m;
     if (by_slots)
-      return mhmkc_fetch_map_range(h, cap, r0, std::min(m, n - r0), b.keys.get(), b.counts.get(), b.left.get(),
-                                   b.right.get(), b.slots.get(), b.tags.get());
-    return mhmkc_fetch_ordered_range(h, r0, std::min(m, n - r0), b.keys.get(), b.counts.get(), b.left.get(),
-                                     b.right.get());
+      return mhmkc_fetch_map_range(h, cap, r0, std::min(m, n - r0), b.keys, b.counts, b.left, b.right, b.slots, b.tags);
+    return mhmkc_fetch_ordered_range(h, r0, std::min(m, n - r0), b.keys, b.counts, b.left, b.right);
   };
   const uint64_t n_ch = (n + m - 1) / m;
   // (the map's fresh memory is faulted in by the fill threads as they write it: a separate parallel pass to fault it in
@@ -840,10 +858,9 @@ void load_ordered(mhmkc_t h, KmerMap<MAX_K> &map, uint64_t n, int threads = 0, u
     const Chunk &b = buf[c & 1];
     auto t1 = clk::now();
     if (by_slots)
-      map.fill_chunk_slots(b.keys.get(), b.counts.get(), b.left.get(), b.right.get(), b.slots.get(), b.tags.get(),
-                           std::min(m, n - c * m));
+      map.fill_chunk_slots(b.keys, b.counts, b.left, b.right, b.slots, b.tags, std::min(m, n - c * m));
     else
-      map.fill_chunk(b.keys.get(), b.counts.get(), b.left.get(), b.right.get(), std::min(m, n - c * m));
+      map.fill_chunk(b.keys, b.counts, b.left, b.right, std::min(m, n - c * m));
     lt.fill += ms_since(t1);
     t1 = clk::now();
     if (f.joinable()) f.join();

@@ -38,7 +38,8 @@ STAGES = ["tileidx", "extract_hist", "extract_scatter", "exchange", "part_hist",
 ABI_SYMBOLS = [
     "mhmkc_config_init", "mhmkc_create", "mhmkc_destroy", "mhmkc_comm_id", "mhmkc_add_reads",
     "mhmkc_add_reads_device", "mhmkc_add_seqs", "mhmkc_add_ctgs", "mhmkc_finish", "mhmkc_fetch", "mhmkc_fetch_ordered",
-    "mhmkc_fetch_ordered_range", "mhmkc_fetch_map_range", "mhmkc_device_output",
+    "mhmkc_fetch_ordered_range", "mhmkc_fetch_map_range", "mhmkc_host_alloc", "mhmkc_host_free",
+    "mhmkc_device_output",
     "mhmkc_get_stats", "mhmkc_reset", "mhmkc_set_profiling", "mhmkc_last_error", "mhmkc_abi_version",
     "mhmkc_build_id",
     "mhmkc_add_fastq", "mhmkc_add_fastq_device", "mhmkc_add_fastq_pairs", "mhmkc_add_fastq_pairs_device",
@@ -217,6 +218,10 @@ def lib() -> C.CDLL:
     L.mhmkc_fetch_ordered.argtypes = [VP, VP, VP, VP, VP]
     L.mhmkc_fetch_ordered_range.argtypes = [VP, U64, U64, VP, VP, VP, VP]
     L.mhmkc_fetch_map_range.argtypes = [VP, U64, U64, U64, VP, VP, VP, VP, VP, VP]
+    L.mhmkc_host_alloc.argtypes = [U64]
+    L.mhmkc_host_alloc.restype = VP
+    L.mhmkc_host_free.argtypes = [VP]
+    L.mhmkc_host_free.restype = None
     L.mhmkc_debug_set.argtypes = [C.c_char_p, C.c_int64]
     L.mhmkc_debug_reset.argtypes = []
     L.mhmkc_debug_reset.restype = None

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 #include <mutex>
@@ -3291,6 +3292,62 @@ int mhmkc_fetch_ordered_range(mhmkc_t h, uint64_t row0, uint64_t n_rows, uint64_
   if (e == hipSuccess && right) e = h->d2h(right, o.right + row0, n_rows);
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fetch_ordered");
+}
+
+// Pinned host blocks handed out by mhmkc_host_alloc, and the freed ones kept for the next caller (pinning a buffer of
+// a fetch chunk's size costs more than copying through the staging buffers once; a hand-off per k round reuses them).
+namespace {
+struct HostPool {
+  std::mutex mu;
+  std::map<void *, size_t> live;            // block -> bytes
+  std::multimap<size_t, void *> free_;      // bytes -> block
+  size_t free_bytes = 0;
+};
+HostPool &host_pool() {
+  static HostPool *p = new HostPool();  // (process lifetime)
+  return *p;
+}
+constexpr size_t HOST_POOL_KEEP = 2ull << 30;  // freed blocks kept for reuse, at most this many bytes
+}  // namespace
+
+void *mhmkc_host_alloc(uint64_t bytes) {
+  if (!bytes) bytes = 1;
+  HostPool &hp = host_pool();
+  {
+    std::lock_guard<std::mutex> l(hp.mu);
+    auto it = hp.free_.lower_bound(bytes);
+    if (it != hp.free_.end() && it->first <= 2 * bytes) {
+      void *p = it->second;
+      hp.live[p] = it->first;
+      hp.free_bytes -= it->first;
+      hp.free_.erase(it);
+      return p;
+    }
+  }
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> l(hp.mu);
+  hp.live[p] = bytes;
+  return p;
+}
+
+void mhmkc_host_free(void *p) {
+  if (!p) return;
+  HostPool &hp = host_pool();
+  std::lock_guard<std::mutex> l(hp.mu);
+  auto it = hp.live.find(p);
+  if (it == hp.live.end()) return;  // (not a block of mhmkc_host_alloc)
+  const size_t b = it->second;
+  hp.live.erase(it);
+  if (hp.free_bytes + b <= HOST_POOL_KEEP) {
+    hp.free_.emplace(b, p);
+    hp.free_bytes += b;
+  } else {
+    (void)hipHostFree(p);
+  }
 }
 
 int mhmkc_fetch_map_range(mhmkc_t h, uint64_t capacity, uint64_t row0, uint64_t n_rows, uint64_t *keys,
