@@ -16,6 +16,7 @@
 // gzip through zlib: link with -lz.
 #pragma once
 
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <zlib.h>
@@ -209,17 +210,20 @@ class FillPool {
   FillPool(const FillPool &) = delete;
   FillPool &operator=(const FillPool &) = delete;
   int size() const { return n_; }
-  // f(t) for every t in [0, size()), the caller as thread 0; returns when all are done
+  // f(t) for every t in [0, size()), the caller as thread 0; returns when all are done (the caller sleeps on a
+  // condition variable, not in a yield loop: with several ranks per node the fill threads of one rank would otherwise
+  // compete with a spinning caller for the rank's CPUs)
   void run(const std::function<void(int)> &f) {
     {
       std::lock_guard<std::mutex> l(mu_);
       job_ = &f;
-      left_.store(n_ - 1);
+      left_ = n_ - 1;
       gen_++;
     }
     cv_.notify_all();
     f(0);
-    while (left_.load(std::memory_order_acquire)) std::this_thread::yield();
+    std::unique_lock<std::mutex> l(mu_);
+    done_cv_.wait(l, [&] { return left_ == 0; });
   }
 
  private:
@@ -235,17 +239,18 @@ class FillPool {
         j = job_;
       }
       (*j)(t);
-      left_.fetch_sub(1, std::memory_order_release);
+      std::lock_guard<std::mutex> l(mu_);
+      if (--left_ == 0) done_cv_.notify_one();
     }
   }
   int n_;
   std::vector<std::thread> th_;
   std::mutex mu_;
-  std::condition_variable cv_;
+  std::condition_variable cv_, done_cv_;
   const std::function<void(int)> *job_ = nullptr;
   uint64_t gen_ = 0;
   bool stop_ = false;
-  std::atomic<int> left_{0};
+  int left_ = 0;  // (under mu_)
 };
 
 template <int MAX_K>
@@ -432,12 +437,16 @@ class KmerMap {
     fs_hash_.shrink_to_fit();
   }
 
-  // Threads of a bulk fill: OMP_NUM_THREADS when set (the rank's CPU share), else the hardware threads, at most 16.
+  // Threads of a bulk fill: OMP_NUM_THREADS when set (the rank's CPU share), else the CPUs this process may run on
+  // (its affinity mask: a rank pinned to its share of the node's cores fills with that many), at most 16.
   static int fill_threads() {
     if (const char *e = getenv("OMP_NUM_THREADS"))
       if (atoi(e) > 0) return std::min(64, atoi(e));
-    const unsigned hw = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(16u, hw));
+    cpu_set_t cs;
+    int cpus = 0;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) cpus = CPU_COUNT(&cs);
+    if (cpus <= 0) cpus = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(16, cpus));
   }
 
  private:
