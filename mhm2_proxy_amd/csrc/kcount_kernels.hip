@@ -2133,7 +2133,9 @@ __device__ __forceinline__ int count_tid() {
 }
 
 template <int NL, bool PACKED, bool CMP>
-__global__ __launch_bounds__(C_THREADS) void k_count(CountParams p) {
+// (C_SPLIT workgroups per CU must fit its registers together: 4 waves per SIMD, 128 VGPRs each, as one 1024-thread
+// workgroup has)
+__global__ __launch_bounds__(C_THREADS, 4) void k_count(CountParams p) {
   // A capped fine bucket overflowed in k_part_scatter (same stream, earlier launch): its cursor, which is
   // this kernel's bucket end, ran past the bucket, so reading up to it would leave the layout. The host
   // discards this launch and redoes the partition with exact bucket sizes. (Uniform: every lane reads the

@@ -225,9 +225,14 @@ constexpr int DYN_SWEEP_MAX_NL = 2;
 constexpr int E_THREADS = 256;  // default threads of the extract / partition workgroups
 constexpr int E_NSUB = 8;       // segments per coarse bucket: one per group of workgroups sharing an XCD
 // k_count: one persistent 1024-thread workgroup per CU with all 160 KB of LDS (two 512-thread workgroups with half
-// the LDS each measured slower once the fine partition's cost is counted, §4.2)
-constexpr int C_THREADS = 1024;
-constexpr size_t C_LDS = 163840;
+// the LDS each measured slower once the fine partition's cost is counted, §4.2). MHMKC_CSPLIT=2 builds (A/B variants
+// only) run that split: C_SPLIT workgroups per CU, each with 1/C_SPLIT of the threads, the LDS and the table.
+#ifndef MHMKC_CSPLIT
+#define MHMKC_CSPLIT 1
+#endif
+constexpr int C_SPLIT = MHMKC_CSPLIT;
+constexpr int C_THREADS = 1024 / C_SPLIT;
+constexpr size_t C_LDS = 163840 / C_SPLIT;
 
 // Hash bits stored in a packed record next to the ext code (bits [6, 6 + hbits) of the last word).
 inline int stored_hash_bits(int k, int nl, bool packed) {
@@ -259,7 +264,7 @@ inline int chunk_records(int nl) { return P_TILE[nl]; }
 constexpr int COUNT_CAP[5] = {0, 5120, 4000, 3264, 2752};
 __host__ __device__ constexpr int count_key_bytes(bool cmp) { return cmp ? 4 : 8; }
 __host__ __device__ constexpr int count_cap(int nl, bool cmp = false) {
-  return (cmp ? 6144 : COUNT_CAP[nl]) & ~3;
+  return ((cmp ? 6144 : COUNT_CAP[nl]) / C_SPLIT) & ~3;
 }
 __host__ __device__ constexpr size_t count_table_bytes(int nl, bool cmp = false) {
   return (size_t)count_cap(nl, cmp) * (count_key_bytes(cmp) * nl + 4 + 16) + 256;  // + k_count's scalars

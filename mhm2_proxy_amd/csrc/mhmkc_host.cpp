@@ -1549,7 +1549,9 @@ int mhmkc::finish_passes(uint64_t owned) const {
   // what every pass shares: k_count's spill area, the fine tables of the largest pass (at most 2^11 fine buckets per
   // coarse bucket, base + cursor + histogram), the output (sized later from the sketch; survivors are a fraction of
   // the records: 1/24 at C2, 1/16 at C4, budgeted at 1/8)
-  const double fixed = (nl <= mhm::DYN_SWEEP_MAX_NL ? (double)n_cu * mhm::SPILL_RECORDS * (compact ? 4 : rec_bytes()) : 0.0) +
+  const double fixed = (nl <= mhm::DYN_SWEEP_MAX_NL
+                            ? (double)n_cu * mhm::C_SPLIT * mhm::SPILL_RECORDS * (compact ? 4 : rec_bytes())
+                            : 0.0) +
                        (double)no * 2048.0 * 24.0 + (double)owned / 8.0 * (8.0 * nlo + 4.0);
   const double have = 0.8 * (double)fr + (double)d_r2.cap + (smer_slab ? (double)smer_slab->buf.cap : 0.0) +
                       (double)d_spill.cap + (double)d_out_keys.cap - fixed;
@@ -1904,7 +1906,7 @@ int mhmkc::finish(uint64_t *n_out_ret) {
     cp.fine_bits = fb;
     cp.bucket0 = (own_lo + c0) << fb;
     cp.n_buckets = n_fine;
-    cp.grid = (uint32_t)std::max(0, n_cu);  // persistent workgroups filling every CU's LDS
+    cp.grid = (uint32_t)std::max(0, n_cu * mhm::C_SPLIT);  // persistent workgroups filling every CU's LDS
     cp.k = k;
     cp.cap = mhm::count_cap(nl, compact);
     // (The fine bucket count is a power of two, so its distinct keys fill between FINE_LOAD / 2 and FINE_LOAD of the
@@ -2354,6 +2356,22 @@ hipError_t mhmkc::d2h(void *dst, const void *src, size_t bytes) {
   ev_pool.push_back(ev[1]);
   return e;
 }
+
+// Pinned host blocks handed out by mhmkc_host_alloc, and the freed ones kept for the next caller (pinning a buffer of
+// a fetch chunk's size costs more than copying through the staging buffers once; a hand-off per k round reuses them).
+namespace {
+struct HostPool {
+  std::mutex mu;
+  std::map<void *, size_t> live;            // block -> bytes
+  std::multimap<size_t, void *> free_;      // bytes -> block
+  size_t free_bytes = 0;
+};
+HostPool &host_pool() {
+  static HostPool *p = new HostPool();  // (process lifetime)
+  return *p;
+}
+constexpr size_t HOST_POOL_KEEP = 2ull << 30;  // freed blocks kept for reuse, at most this many bytes
+}  // namespace
 
 // ------------------------------------------------------------------------------------------------
 // C ABI
@@ -3293,22 +3311,6 @@ int mhmkc_fetch_ordered_range(mhmkc_t h, uint64_t row0, uint64_t n_rows, uint64_
   if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   return e == hipSuccess ? MHMKC_OK : h->hip_fail(e, "fetch_ordered");
 }
-
-// Pinned host blocks handed out by mhmkc_host_alloc, and the freed ones kept for the next caller (pinning a buffer of
-// a fetch chunk's size costs more than copying through the staging buffers once; a hand-off per k round reuses them).
-namespace {
-struct HostPool {
-  std::mutex mu;
-  std::map<void *, size_t> live;            // block -> bytes
-  std::multimap<size_t, void *> free_;      // bytes -> block
-  size_t free_bytes = 0;
-};
-HostPool &host_pool() {
-  static HostPool *p = new HostPool();  // (process lifetime)
-  return *p;
-}
-constexpr size_t HOST_POOL_KEEP = 2ull << 30;  // freed blocks kept for reuse, at most this many bytes
-}  // namespace
 
 void *mhmkc_host_alloc(uint64_t bytes) {
   if (!bytes) bytes = 1;
