@@ -547,6 +547,8 @@ def main():
                "h2d_GBps": round(hbytes / (sorted(h2d_ms)[len(h2d_ms) // 2] * 1e-3) / 1e9, 1) if h2d_ms[0] else None,
                "chunks": int(stt["h2d_chunks"]), "steps": len(ts), "warmup": 3, "statistic": "median",
                "input": "PackedRead bytes + offsets in pinned host memory (torch pin_memory)",
+               "wire": "bases as nibbles (code, q >= cutoff), packed by host threads" if hbytes < int(o[-1])
+               else "PackedRead bytes",
                "window": "BASELINE.md:74-75: from the first H2D of the reads to the finished device table"}
         del hb, ho
 

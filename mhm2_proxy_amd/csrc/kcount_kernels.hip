@@ -1632,6 +1632,36 @@ __global__ __launch_bounds__(256) void k_count_windows(ReadsView rv, int k, unsi
   }
 }
 
+// The bases of one H2D chunk of a host batch, sent as nibbles (mhmkc_host.cpp nib_pack: code | (q >= qcut) << 3, two
+// per byte, the first in the low half), written back into the arena as PackedRead bytes code | (q >= qcut ? 31 : 0) << 3:
+// load_tile's only use of the quality is q >= qcut, which these bytes answer as the originals do for every qcut.
+// Thread t writes the arena's 16-byte block t of [b0 & ~15, b0 + n) (bytes of that range outside [b0, b0 + n) belong to
+// the neighbouring chunks and are left alone).
+__global__ __launch_bounds__(256) void k_expand_nibbles(const uint8_t *nib, uint8_t *arena, uint64_t b0, uint64_t n) {
+  const uint64_t a0 = b0 & ~15ull, end = b0 + n;
+  const uint64_t p0 = a0 + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (p0 >= end) return;
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint64_t p = p0 + i;
+    if (p >= b0 && p < end) {
+      const uint64_t j = p - b0;
+      const uint32_t v = (nib[j >> 1] >> (4 * (uint32_t)(j & 1))) & 15u;
+      w[i >> 2] |= ((v & 7u) | ((v >> 3) * 0xf8u)) << (8 * (i & 3));
+    }
+  }
+  if (p0 >= b0 && p0 + 16 <= end) {
+    *(uint4 *)(arena + p0) = make_uint4(w[0], w[1], w[2], w[3]);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint64_t p = p0 + i;
+    if (p >= b0 && p < end) arena[p] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, unsigned long long *base,
                                                unsigned long long *cursor, uint32_t n) {
   __shared__ unsigned long long wsum[17];
@@ -3006,6 +3036,13 @@ hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *o
   if (!r.n_reads) return hipSuccess;
   const uint64_t blocks = std::min<uint64_t>(2048, (r.n_reads + 1023) / 1024);
   k_count_windows<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, k, out, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_expand_nibbles(const uint8_t *nib, uint8_t *arena, uint64_t b0, uint64_t n, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const uint64_t blocks16 = (b0 + n - (b0 & ~15ull) + 15) / 16;
+  k_expand_nibbles<<<dim3((unsigned)((blocks16 + 255) / 256)), dim3(256), 0, s>>>(nib, arena, b0, n);
   return hipGetLastError();
 }
 

@@ -287,6 +287,9 @@ size_t tile_starts_words(int nl);
 // total counted windows sum(max(0, L - k - 1)) of a batch, added to *out; err bit 2 (4) when the offsets are
 // not a valid PackedReads CSR (offs[0] != 0, decreasing, a read longer than 65535, offs[n] != n_bases)
 hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, unsigned int *err, hipStream_t s);
+// one H2D chunk of a host batch sent as nibbles (code | (q >= qcut) << 3, two per byte): arena[b0, b0 + n) as PackedRead
+// bytes again (code | (q >= qcut ? 31 : 0) << 3)
+hipError_t launch_expand_nibbles(const uint8_t *nib, uint8_t *arena, uint64_t b0, uint64_t n, hipStream_t s);
 // capped fine layout: base/cursor of bucket (c, d) = coarse_base[c] + d * coarse_fcap[c]
 // The incremental layout after its last round: a coarse bucket with a fine bucket past its capped
 // segment (k_part_scatter wrote none of that bucket's overflowing runs) gets skip[c] = 1 and all its fine buckets

@@ -18,7 +18,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -26,6 +28,8 @@
 #include <thread>
 
 #include <fcntl.h>
+#include <immintrin.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -53,6 +57,7 @@ struct DebugKnobs {
   int64_t smer = 1;           // 0: the minimizer owner at k >= 33 takes the record exchange + hand-off
   int64_t chunk_bytes = 0;    // H2D chunk of a host batch (0: CHUNK_BYTES)
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
+  int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles, 0 the PackedRead bytes, -1 nibbles with >= 4 host threads
   int64_t cb0[4] = {0, 0, 0, 0};  // coarse bits by key words (0: the default)
 };
 DebugKnobs g_dbg;
@@ -216,6 +221,137 @@ D2HStage &d2h_stage() {
 // Bytes of one H2D chunk of mhmkc_add_reads (MHMKC_CHUNK_BYTES overrides: tests force many chunks).
 constexpr uint64_t CHUNK_BYTES = 128ull << 20;
 
+// Host threads for the transcoding of host batches: the CPUs of the affinity mask, at most OMP_NUM_THREADS and 16.
+int host_threads() {
+  int n = 16;
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+  if (const char *e = getenv("OMP_NUM_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) n = std::min(n, v);
+  }
+  return std::max(1, std::min(16, n));
+}
+
+// The process's host worker threads (host_threads() of them, the caller being number 0), shared by its handles one job
+// at a time: run(fn) calls fn(t) for every t in [0, size()) and returns when all have returned.
+class Workers {
+ public:
+  static Workers &get() {
+    static std::mutex mu;
+    static Workers *w = nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    if (!w || w->pid_ != getpid()) w = new Workers(host_threads());  // (never freed; a forked child makes its own)
+    return *w;
+  }
+  int size() const { return n_; }
+  void run(const std::function<void(int)> &fn) {
+    std::lock_guard<std::mutex> job(job_mu_);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fn_ = &fn;
+      left_ = n_ - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  explicit Workers(int n) : n_(n), pid_(getpid()) {
+    for (int t = 1; t < n; t++) std::thread([this, t] { loop(t); }).detach();
+  }
+  void loop(int t) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)> *fn;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        fn = fn_;
+      }
+      (*fn)(t);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--left_ == 0) done_cv_.notify_one();
+    }
+  }
+  const int n_;
+  const pid_t pid_;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)> *fn_ = nullptr;
+  uint64_t gen_ = 0;
+  int left_ = 0;
+};
+
+// PackedRead bytes (code | min(q, 31) << 3, src/packed_reads.cpp:98-107) as the nibbles code | (q >= qcut) << 3 the
+// nibble H2D sends (k_expand_nibbles restores bytes that load_tile reads alike): n bytes of src into (n + 1) / 2 bytes
+// of dst, two per byte, the first in the low half. Eight bytes at a time in one u64: the per-byte sums q + 128 - qcut
+// stay below 256, so no carry crosses a byte, and bit 7 of each is q >= qcut.
+void nib_pack_swar(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut, uint64_t i = 0) {
+  const uint32_t qc = (uint32_t)std::min(std::max(qcut, 0), 32);
+  constexpr uint64_t L = 0x0101010101010101ull;
+  const uint64_t bias = (0x80ull - qc) * L;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t v;
+    memcpy(&v, src + i, 8);
+    const uint64_t c = v & (7 * L), q = (v >> 3) & (0x1f * L);
+    uint64_t x = c | (((q + bias) >> 4) & (8 * L));
+    x = (x | (x >> 4)) & 0x00ff00ff00ff00ffull;
+    x = (x | (x >> 8)) & 0x0000ffff0000ffffull;
+    const uint32_t y = (uint32_t)(x | (x >> 16));
+    memcpy(dst + i / 2, &y, 4);
+  }
+  for (; i < n; i++) {
+    const uint32_t b = src[i], v = (b & 7u) | ((b >> 3) >= qc ? 8u : 0u);
+    if (i & 1)
+      dst[i / 2] |= (uint8_t)(v << 4);
+    else
+      dst[i / 2] = (uint8_t)v;
+  }
+}
+
+// The same 64 bytes at a time (AVX2): nibble pairs summed as n0 + 16 n1 by maddubs, packed to bytes, lanes put in order.
+__attribute__((target("avx2"))) inline __m256i nib_pairs_avx2(__m256i v, __m256i qm1) {
+  const __m256i q = _mm256_and_si256(_mm256_srli_epi16(v, 3), _mm256_set1_epi8(0x1f));  // q <= 31, qm1 >= -1: signed
+  const __m256i ok = _mm256_and_si256(_mm256_cmpgt_epi8(q, qm1), _mm256_set1_epi8(8));
+  return _mm256_maddubs_epi16(_mm256_or_si256(_mm256_and_si256(v, _mm256_set1_epi8(7)), ok), _mm256_set1_epi16(0x1001));
+}
+
+__attribute__((target("avx2"))) void nib_pack_avx2(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut) {
+  const __m256i qm1 = _mm256_set1_epi8((char)(std::min(std::max(qcut, 0), 32) - 1));
+  uint64_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m256i a = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i)), qm1);
+    const __m256i b = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i + 32)), qm1);
+    _mm256_storeu_si256((__m256i *)(dst + i / 2), _mm256_permute4x64_epi64(_mm256_packus_epi16(a, b), 0xd8));
+  }
+  nib_pack_swar(src, n, dst, qcut, i);
+}
+
+void nib_pack(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2)
+    nib_pack_avx2(src, n, dst, qcut);
+  else
+    nib_pack_swar(src, n, dst, qcut);
+}
+
+// The pinned staging of the nibble H2D (two slots per add call), kept by the process for the next call (the reference
+// makes a new handle per k round): a handle takes two buffers for the length of one add call.
+struct H2DStage {
+  std::mutex mu;
+  std::vector<PinBuf *> free;
+};
+H2DStage &h2d_stage() {
+  static H2DStage *s = new H2DStage();  // (never freed: the process's pinned staging)
+  return *s;
+}
+
 }  // namespace
 
 struct mhmkc {
@@ -285,6 +421,13 @@ struct mhmkc {
   int pump();
   int resolve_one(Slab *sl, bool &redo);
   std::vector<hipEvent_t> chunk_ev;  // one per H2D chunk in flight (pool)
+  // the nibble H2D of host batches (add_host): device slots of a chunk's nibbles with the event after the expansion that
+  // last read each (the next copy into the slot waits for it), and the events after the copy out of each pinned slot
+  DevBuf d_nib[3];
+  hipEvent_t nib_ev[3] = {nullptr, nullptr, nullptr};
+  bool nib_used[3] = {false, false, false};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  int add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut, uint64_t chunk);
   DevBuf d_hist, d_tiles, d_tsb, d_err, d_stats, d_fine_hist, d_fine_base, d_fine_cursor, d_chunks, d_srcs;
   DevBuf d_r2, d_out_keys, d_out_counts, d_out_left, d_out_right, d_out_cursor, d_recv, d_xg;
   DevBuf d_hll, d_dest, d_ohist, d_out2_keys, d_out2_counts, d_out2_left, d_out2_right, d_mh;
@@ -722,6 +865,8 @@ int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads
     inc_expect += w;
     inc_announced += w;
   }
+  if (g_dbg.h2d_nib == 1 || (g_dbg.h2d_nib < 0 && host_threads() >= 4))
+    return add_host_nib(bytes, offs, n_reads, qcut, chunk);
   hipError_t e;
   Arena *ar = new_arena();
   if ((e = grow(ar->bytes, n_bases + 64)) != hipSuccess || (e = grow(ar->offs, (n_reads + 1) * 8)) != hipSuccess)
@@ -776,6 +921,166 @@ int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads
   }
   (void)hipEventRecord(ev_h2d1, copy_stream);
   // the caller's buffers are only borrowed for the call: wait for the copies (not for the extraction)
+  if ((e = hipStreamSynchronize(copy_stream)) != hipSuccess) return hip_fail(e, "input H2D");
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, ev_h2d0, ev_h2d1) == hipSuccess) st.ms_h2d = ms;
+  return MHMKC_OK;
+}
+
+// add_host with the bases sent as nibbles (half the PCIe bytes). Per chunk of whole reads the host
+// workers validate the offsets, count the windows and pack the bytes into a pinned slot (nib_pack) while the previous
+// chunk is on the wire; the copy lands in a device slot that k_expand_nibbles turns back into PackedRead bytes in the
+// arena, on the extraction's stream just before the chunk is extracted. The first chunk is a quarter of the others, so
+// that the wire starts early.
+int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut, uint64_t chunk) {
+  const uint64_t n_bases = offs[n_reads];
+  Workers &wk = Workers::get();
+  const int T = wk.size();
+  hipError_t e;
+  int rc;
+  Arena *ar = new_arena();
+  if ((e = grow(ar->bytes, n_bases + 64)) != hipSuccess || (e = grow(ar->offs, (n_reads + 1) * 8)) != hipSuccess)
+    return hip_fail(e, "input staging");
+  // a chunk holds at most `chunk` bytes plus one read (<= 65535 bytes)
+  const size_t slot = (size_t)(chunk / 2 + 65536 + 64);
+  for (int s = 0; s < 3; s++) {
+    if (slot > d_nib[s].cap) {
+      if (nib_used[s] && (e = hipEventSynchronize(nib_ev[s])) != hipSuccess) return hip_fail(e, "nibble slot");
+      if ((e = d_nib[s].ensure(slot)) != hipSuccess) return hip_fail(e, "nibble slot");
+    }
+    if (!nib_ev[s] && (e = hipEventCreateWithFlags(&nib_ev[s], hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "event");
+  }
+  for (int s = 0; s < 2; s++)
+    if (!stage_ev[s] && (e = hipEventCreateWithFlags(&stage_ev[s], hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "event");
+  // two pinned slots from the process's staging, given back (their copies done) however this call ends
+  struct Slots {
+    PinBuf *p[2] = {nullptr, nullptr};
+    hipStream_t cs;
+    ~Slots() {
+      (void)hipStreamSynchronize(cs);
+      H2DStage &g = h2d_stage();
+      std::lock_guard<std::mutex> lk(g.mu);
+      for (PinBuf *b : p)
+        if (b) g.free.push_back(b);
+    }
+  } sl;
+  sl.cs = copy_stream;
+  {
+    H2DStage &g = h2d_stage();
+    std::lock_guard<std::mutex> lk(g.mu);
+    for (PinBuf *&b : sl.p) {
+      if (!g.free.empty()) {
+        b = g.free.back();
+        g.free.pop_back();
+      } else {
+        b = new PinBuf();
+      }
+    }
+  }
+  for (PinBuf *b : sl.p)
+    if ((e = b->ensure(slot)) != hipSuccess) return hip_fail(e, "pinned staging");
+  bool stage_used[2] = {false, false};
+  qcut_pending = qcut;
+  // the copies must not overwrite an arena that earlier work on the stream still reads
+  (void)hipEventRecord(ev_h2d0, stream);
+  if ((e = hipStreamWaitEvent(copy_stream, ev_h2d0, 0)) != hipSuccess) return hip_fail(e, "copy stream");
+  (void)hipEventRecord(ev_h2d0, copy_stream);
+  uint8_t *db = ar->bytes.as<uint8_t>();
+  uint64_t *dofs = ar->offs.as<uint64_t>();
+  const uint64_t kk = (uint64_t)k;
+  size_t n_ev = 0;
+  for (uint64_t r0 = 0, ci = 0; r0 < n_reads; ci++) {
+    // the chunk [r0, r1): the first read r > r0 with offs[r] - b0 >= want ends it (a binary search; the offsets are
+    // validated below, and a chunk whose end lies before its start is only validated, for the error)
+    const uint64_t b0 = offs[r0], want = ci == 0 ? std::max<uint64_t>(64, chunk / 4) : chunk;
+    uint64_t lo = r0 + 1, hi = n_reads;
+    while (lo < hi) {
+      const uint64_t m = (lo + hi) / 2;
+      if (offs[m] >= b0 && offs[m] - b0 < want)
+        lo = m + 1;
+      else
+        hi = m;
+    }
+    const uint64_t r1 = lo, b1 = offs[r1];
+    const bool span_ok = b1 >= b0 && b1 - b0 <= chunk + 65535;
+    const int s = (int)(ci & 1), ds = (int)(ci % 3);
+    if (span_ok && stage_used[s] && (e = hipEventSynchronize(stage_ev[s])) != hipSuccess)
+      return hip_fail(e, "input H2D");
+    uint8_t *stage = sl.p[s]->as<uint8_t>();
+    const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
+    std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX);
+    std::vector<int> t_kind(T, 0);
+    wk.run([&](int t) {
+      // reads [r0 + t nr / T, r0 + (t + 1) nr / T): validated and their windows counted
+      const uint64_t ra = r0 + nr * t / T, rb = r0 + nr * (t + 1) / T;
+      uint64_t w = 0;
+      for (uint64_t r = ra; r < rb; r++) {
+        const uint64_t a = offs[r], b = offs[r + 1];
+        if (b < a || b - a > 65535) {
+          t_bad[t] = r;
+          t_kind[t] = b < a ? 1 : 2;
+          break;
+        }
+        if (b - a > kk + 1) w += b - a - kk - 1;
+      }
+      t_wins[t] = w;
+      // bases [b0 + x, b0 + y) of an even x: nibbles from byte x / 2 of the slot
+      const uint64_t per = ((nb + T - 1) / T + 1) & ~1ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
+      if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut);
+    });
+    uint64_t wins = 0;
+    for (int t = 0; t < T; t++) {
+      if (t_bad[t] != UINT64_MAX) {
+        if (t_kind[t] == 1)
+          return fail(MHMKC_EINVAL, "read_offsets must be non-decreasing (read %llu)", (unsigned long long)t_bad[t]);
+        return fail(MHMKC_EINVAL, "read %llu longer than 65535 (PackedRead read_len is uint16)",
+                    (unsigned long long)t_bad[t]);
+      }
+      wins += t_wins[t];
+    }
+    if (!span_ok) return fail(MHMKC_EHIP, "internal: H2D chunk of %llu bytes", (unsigned long long)(b1 - b0));
+    const uint64_t nbytes = (nb + 1) / 2;
+    if (nb) {
+      if (nib_used[ds] && (e = hipStreamWaitEvent(copy_stream, nib_ev[ds], 0)) != hipSuccess)
+        return hip_fail(e, "copy stream");
+      if ((e = hipMemcpyAsync(d_nib[ds].p, stage, nbytes, hipMemcpyHostToDevice, copy_stream)) != hipSuccess ||
+          (e = hipEventRecord(stage_ev[s], copy_stream)) != hipSuccess)
+        return hip_fail(e, "input H2D");
+      stage_used[s] = true;
+    }
+    if ((e = hipMemcpyAsync(dofs + r0, offs + r0, (nr + 1) * 8, hipMemcpyHostToDevice, copy_stream)) != hipSuccess)
+      return hip_fail(e, "input H2D");
+    if (n_ev == chunk_ev.size()) {
+      hipEvent_t ev = nullptr;
+      if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "event");
+      chunk_ev.push_back(ev);
+    }
+    hipEvent_t ev = chunk_ev[n_ev++];
+    if ((e = hipEventRecord(ev, copy_stream)) != hipSuccess || (e = hipStreamWaitEvent(stream, ev, 0)) != hipSuccess)
+      return hip_fail(e, "chunk event");
+    if (nb) {
+      if ((e = mhm::launch_expand_nibbles(d_nib[ds].as<uint8_t>(), db, b0, nb, stream)) != hipSuccess ||
+          (e = hipEventRecord(nib_ev[ds], stream)) != hipSuccess)
+        return hip_fail(e, "nibble expansion");
+      nib_used[ds] = true;
+    }
+    st.h2d_bytes += nbytes + (nr + 1) * 8;
+    st.h2d_chunks++;
+    // slice view, as add_host's (the bytes before b0 in its first 16 belong to the previous chunk, expanded earlier on
+    // the same stream)
+    mhm::ReadsView rv{};
+    rv.obase = b0 & ~15ull;
+    rv.head = (uint32_t)(b0 - rv.obase);
+    rv.bytes = db + rv.obase;
+    rv.offs = dofs + r0;
+    rv.n_reads = nr;
+    rv.n_bases = b1 - rv.obase;
+    if ((rc = add_view(rv, wins, true))) return rc;
+    r0 = r1;
+  }
+  (void)hipEventRecord(ev_h2d1, copy_stream);
   if ((e = hipStreamSynchronize(copy_stream)) != hipSuccess) return hip_fail(e, "input H2D");
   float ms = 0;
   if (hipEventElapsedTime(&ms, ev_h2d0, ev_h2d1) == hipSuccess) st.ms_h2d = ms;
@@ -2645,7 +2950,9 @@ void mhmkc_destroy(mhmkc_t h) {
   }
   for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : h->chunk_ev) (void)hipEventDestroy(ev);
-  hipEvent_t evs[] = {h->ev_begin, h->ev_end, h->ev_h2d0, h->ev_h2d1};
+  for (DevBuf &b : h->d_nib) b.release();
+  hipEvent_t evs[] = {h->ev_begin,  h->ev_end,    h->ev_h2d0,    h->ev_h2d1,       h->nib_ev[0],
+                      h->nib_ev[1], h->nib_ev[2], h->stage_ev[0], h->stage_ev[1]};
   for (hipEvent_t ev : evs)
     if (ev) (void)hipEventDestroy(ev);
   if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
@@ -3445,6 +3752,7 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
   else if (k == "smer") g_dbg.smer = value;
   else if (k == "chunk_bytes") g_dbg.chunk_bytes = value;
   else if (k == "d2h_chunk") g_dbg.d2h_chunk = value;
+  else if (k == "h2d_nib") g_dbg.h2d_nib = value;
   else if (k == "cb0") g_dbg.cb0[1] = value;
   else if (k == "cb0_2") g_dbg.cb0[2] = value;
   else if (k == "cb0_3") g_dbg.cb0[3] = value;

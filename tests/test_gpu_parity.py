@@ -349,21 +349,60 @@ def test_distinct_sketch_estimate(k):
 # ---- round 2: host chunks, stream ordering, dmin at finish, overflow guard ----------------------------
 
 
+@pytest.mark.parametrize("nib", [0, 1])
 @pytest.mark.parametrize("k,chunk", [(21, 700), (63, 1000), (33, 100000)])
-def test_host_chunks_equal_oracle(k, chunk, knob):
+def test_host_chunks_equal_oracle(k, chunk, nib, knob):
     """mhmkc_add_reads copies a host batch in chunks of whole reads, each extracted as a slice view (an aligned
     byte base plus a head offset) as soon as it lands: ragged reads (empty, shorter than k, N runs, poly-A)
-    over many chunk boundaries give the oracle's table."""
+    over many chunk boundaries give the oracle's table, with the bases sent as bytes (nib 0) or as nibbles that the
+    device expands back (nib 1: odd chunk starts and ends split nibble pairs)."""
     knob("chunk_bytes", chunk)
+    knob("h2d_nib", nib)
     b, o = edge_case_set(seed=17 + k)
     with m.KmerCounter(k) as c:
         c.add_packed_reads(b, o)
         c.finish()
         got, st = c.fetch(), c.stats()
     assert st["h2d_chunks"] >= (2 if chunk < 10000 else 1)
-    assert st["h2d_bytes"] == int(o[-1]) + 8 * (o.size - 1) + 8 * st["h2d_chunks"]
-    assert_tables_equal(got, oracle_table(b, o, k), f"host chunks k={k}")
+    offs_bytes = 8 * (o.size - 1) + 8 * st["h2d_chunks"]
+    if nib:
+        assert int(o[-1]) // 2 <= st["h2d_bytes"] - offs_bytes <= (int(o[-1]) + st["h2d_chunks"]) // 2
+    else:
+        assert st["h2d_bytes"] == int(o[-1]) + offs_bytes
+    assert_tables_equal(got, oracle_table(b, o, k), f"host chunks k={k} nib={nib}")
     check_stats(st)
+
+
+@pytest.mark.parametrize("qcut", [0, 1, 19, 20, 31, 32])
+def test_host_nibbles_quality_cutoffs(qcut, knob):
+    """The nibble H2D keeps one quality bit, q >= cutoff, per base: for cutoffs at both ends of the accepted [0, 32]
+    and around the default, the table equals the oracle's and the byte H2D's, with the codes A, C, G, T, N and every
+    quality 0-31 in the input (codes 5-7 are an input error: test_host_nibbles_bad_code_reported)."""
+    b, o = synth_set(600, 20000, 71)
+    rng = np.random.default_rng(qcut + 3)
+    b = ((b & 7) | (rng.integers(0, 32, b.size, dtype=np.uint8) << 3)).astype(np.uint8)
+    knob("chunk_bytes", 3001)
+    tabs = []
+    for nib in (1, 0):
+        knob("h2d_nib", nib)
+        got, st = hip_table(b, o, 21, qual_cutoff=qcut)
+        check_stats(st)
+        tabs.append(got)
+    assert_tables_equal(tabs[0], oracle_table(b, o, 21, qual_cutoff=qcut), f"nibbles qcut={qcut}")
+    assert_tables_equal(tabs[0], tabs[1], f"nibbles vs bytes qcut={qcut}")
+
+
+def test_host_nibbles_bad_code_reported(knob):
+    """A byte with code 5-7 sent as a nibble still reaches the device's input check (error, no table)."""
+    b, o = synth_set(200, 5000, 72)
+    b = b.copy()
+    b[int(o[100]) + 7] = (b[int(o[100]) + 7] & 0xF8) | 6
+    knob("h2d_nib", 1)
+    with m.KmerCounter(21) as c:
+        c.add_packed_reads(b, o)
+        with pytest.raises(m.MhmkcError) as e:
+            c.finish()
+        assert e.value.code == -6
 
 
 def test_device_input_ordered_after_torch_stream():
