@@ -1662,6 +1662,11 @@ __global__ __launch_bounds__(256) void k_expand_nibbles(const uint8_t *nib, uint
   }
 }
 
+// The chunk's offsets from the u32 distances to its first byte that the nibble H2D sends.
+__global__ __launch_bounds__(256) void k_offs_from_deltas(const uint32_t *d, uint64_t *offs, uint64_t n, uint64_t b0) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) offs[i] = b0 + d[i];
+}
+
 __global__ __launch_bounds__(1024) void k_scan(const unsigned long long *in, unsigned long long *base,
                                                unsigned long long *cursor, uint32_t n) {
   __shared__ unsigned long long wsum[17];
@@ -3036,6 +3041,12 @@ hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *o
   if (!r.n_reads) return hipSuccess;
   const uint64_t blocks = std::min<uint64_t>(2048, (r.n_reads + 1023) / 1024);
   k_count_windows<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, k, out, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_offs_from_deltas(const uint32_t *d, uint64_t *offs, uint64_t n, uint64_t b0, hipStream_t s) {
+  if (!n) return hipSuccess;
+  k_offs_from_deltas<<<dim3((unsigned)std::min<uint64_t>(4096, (n + 255) / 256)), dim3(256), 0, s>>>(d, offs, n, b0);
   return hipGetLastError();
 }
 

@@ -290,6 +290,8 @@ hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *o
 // one H2D chunk of a host batch sent as nibbles (code | (q >= qcut) << 3, two per byte): arena[b0, b0 + n) as PackedRead
 // bytes again (code | (q >= qcut ? 31 : 0) << 3)
 hipError_t launch_expand_nibbles(const uint8_t *nib, uint8_t *arena, uint64_t b0, uint64_t n, hipStream_t s);
+// offs[i] = b0 + d[i], i < n: a chunk's offsets from the u32 distances the nibble H2D sends
+hipError_t launch_offs_from_deltas(const uint32_t *d, uint64_t *offs, uint64_t n, uint64_t b0, hipStream_t s);
 // capped fine layout: base/cursor of bucket (c, d) = coarse_base[c] + d * coarse_fcap[c]
 // The incremental layout after its last round: a coarse bucket with a fine bucket past its capped
 // segment (k_part_scatter wrote none of that bucket's overflowing runs) gets skip[c] = 1 and all its fine buckets

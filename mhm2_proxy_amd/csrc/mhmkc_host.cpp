@@ -941,8 +941,10 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   Arena *ar = new_arena();
   if ((e = grow(ar->bytes, n_bases + 64)) != hipSuccess || (e = grow(ar->offs, (n_reads + 1) * 8)) != hipSuccess)
     return hip_fail(e, "input staging");
-  // a chunk holds at most `chunk` bytes plus one read (<= 65535 bytes)
-  const size_t slot = (size_t)(chunk / 2 + 65536 + 64);
+  // a chunk holds at most `chunk` bytes plus one read (<= 65535 bytes) and at most rmax reads; a slot holds its nibbles
+  // and then, from byte dof, its offsets as u32 distances from its first byte (half the offsets' bytes)
+  const uint64_t rmax = std::max<uint64_t>(64, chunk / 32);
+  const size_t dof = (size_t)align_up(chunk / 2 + 65536 + 64, 64), slot = dof + 4 * (size_t)(rmax + 1);
   for (int s = 0; s < 3; s++) {
     if (slot > d_nib[s].cap) {
       if (nib_used[s] && (e = hipEventSynchronize(nib_ev[s])) != hipSuccess) return hip_fail(e, "nibble slot");
@@ -995,7 +997,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     // the chunk [r0, r1): the first read r > r0 with offs[r] - b0 >= want ends it (a binary search; the offsets are
     // validated below, and a chunk whose end lies before its start is only validated, for the error)
     const uint64_t b0 = offs[r0], want = ci == 0 ? std::max<uint64_t>(64, chunk / 4) : chunk;
-    uint64_t lo = r0 + 1, hi = n_reads;
+    uint64_t lo = r0 + 1, hi = std::min(n_reads, r0 + rmax);
     while (lo < hi) {
       const uint64_t m = (lo + hi) / 2;
       if (offs[m] >= b0 && offs[m] - b0 < want)
@@ -1006,14 +1008,16 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     const uint64_t r1 = lo, b1 = offs[r1];
     const bool span_ok = b1 >= b0 && b1 - b0 <= chunk + 65535;
     const int s = (int)(ci & 1), ds = (int)(ci % 3);
-    if (span_ok && stage_used[s] && (e = hipEventSynchronize(stage_ev[s])) != hipSuccess)
+    if (stage_used[s] && (e = hipEventSynchronize(stage_ev[s])) != hipSuccess)
       return hip_fail(e, "input H2D");
     uint8_t *stage = sl.p[s]->as<uint8_t>();
+    uint32_t *sdelta = (uint32_t *)(stage + dof);
     const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
     std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX);
     std::vector<int> t_kind(T, 0);
     wk.run([&](int t) {
-      // reads [r0 + t nr / T, r0 + (t + 1) nr / T): validated and their windows counted
+      // reads [r0 + t nr / T, r0 + (t + 1) nr / T): validated, their windows counted, their offsets' distances from
+      // b0 staged (the last thread's also the chunk's end)
       const uint64_t ra = r0 + nr * t / T, rb = r0 + nr * (t + 1) / T;
       uint64_t w = 0;
       for (uint64_t r = ra; r < rb; r++) {
@@ -1024,7 +1028,9 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
           break;
         }
         if (b - a > kk + 1) w += b - a - kk - 1;
+        sdelta[r - r0] = (uint32_t)(a - b0);
       }
+      if (t == T - 1) sdelta[nr] = (uint32_t)(b1 - b0);
       t_wins[t] = w;
       // bases [b0 + x, b0 + y) of an even x: nibbles from byte x / 2 of the slot
       const uint64_t per = ((nb + T - 1) / T + 1) & ~1ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
@@ -1042,16 +1048,14 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     }
     if (!span_ok) return fail(MHMKC_EHIP, "internal: H2D chunk of %llu bytes", (unsigned long long)(b1 - b0));
     const uint64_t nbytes = (nb + 1) / 2;
-    if (nb) {
-      if (nib_used[ds] && (e = hipStreamWaitEvent(copy_stream, nib_ev[ds], 0)) != hipSuccess)
-        return hip_fail(e, "copy stream");
-      if ((e = hipMemcpyAsync(d_nib[ds].p, stage, nbytes, hipMemcpyHostToDevice, copy_stream)) != hipSuccess ||
-          (e = hipEventRecord(stage_ev[s], copy_stream)) != hipSuccess)
-        return hip_fail(e, "input H2D");
-      stage_used[s] = true;
-    }
-    if ((e = hipMemcpyAsync(dofs + r0, offs + r0, (nr + 1) * 8, hipMemcpyHostToDevice, copy_stream)) != hipSuccess)
+    uint8_t *dslot = d_nib[ds].as<uint8_t>();
+    if (nib_used[ds] && (e = hipStreamWaitEvent(copy_stream, nib_ev[ds], 0)) != hipSuccess)
+      return hip_fail(e, "copy stream");
+    if ((nb && (e = hipMemcpyAsync(dslot, stage, nbytes, hipMemcpyHostToDevice, copy_stream)) != hipSuccess) ||
+        (e = hipMemcpyAsync(dslot + dof, sdelta, 4 * (nr + 1), hipMemcpyHostToDevice, copy_stream)) != hipSuccess ||
+        (e = hipEventRecord(stage_ev[s], copy_stream)) != hipSuccess)
       return hip_fail(e, "input H2D");
+    stage_used[s] = true;
     if (n_ev == chunk_ev.size()) {
       hipEvent_t ev = nullptr;
       if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "event");
@@ -1060,13 +1064,12 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     hipEvent_t ev = chunk_ev[n_ev++];
     if ((e = hipEventRecord(ev, copy_stream)) != hipSuccess || (e = hipStreamWaitEvent(stream, ev, 0)) != hipSuccess)
       return hip_fail(e, "chunk event");
-    if (nb) {
-      if ((e = mhm::launch_expand_nibbles(d_nib[ds].as<uint8_t>(), db, b0, nb, stream)) != hipSuccess ||
-          (e = hipEventRecord(nib_ev[ds], stream)) != hipSuccess)
-        return hip_fail(e, "nibble expansion");
-      nib_used[ds] = true;
-    }
-    st.h2d_bytes += nbytes + (nr + 1) * 8;
+    if ((e = mhm::launch_expand_nibbles(dslot, db, b0, nb, stream)) != hipSuccess ||
+        (e = mhm::launch_offs_from_deltas((const uint32_t *)(dslot + dof), dofs + r0, nr + 1, b0, stream)) != hipSuccess ||
+        (e = hipEventRecord(nib_ev[ds], stream)) != hipSuccess)
+      return hip_fail(e, "nibble expansion");
+    nib_used[ds] = true;
+    st.h2d_bytes += nbytes + (nr + 1) * 4;
     st.h2d_chunks++;
     // slice view, as add_host's (the bytes before b0 in its first 16 belong to the previous chunk, expanded earlier on
     // the same stream)

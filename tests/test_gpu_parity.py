@@ -364,11 +364,11 @@ def test_host_chunks_equal_oracle(k, chunk, nib, knob):
         c.finish()
         got, st = c.fetch(), c.stats()
     assert st["h2d_chunks"] >= (2 if chunk < 10000 else 1)
-    offs_bytes = 8 * (o.size - 1) + 8 * st["h2d_chunks"]
-    if nib:
+    if nib:  # nibbles, and the offsets as u32 distances from each chunk's first byte
+        offs_bytes = 4 * (o.size - 1) + 4 * st["h2d_chunks"]
         assert int(o[-1]) // 2 <= st["h2d_bytes"] - offs_bytes <= (int(o[-1]) + st["h2d_chunks"]) // 2
     else:
-        assert st["h2d_bytes"] == int(o[-1]) + offs_bytes
+        assert st["h2d_bytes"] == int(o[-1]) + 8 * (o.size - 1) + 8 * st["h2d_chunks"]
     assert_tables_equal(got, oracle_table(b, o, k), f"host chunks k={k} nib={nib}")
     check_stats(st)
 
@@ -390,6 +390,20 @@ def test_host_nibbles_quality_cutoffs(qcut, knob):
         tabs.append(got)
     assert_tables_equal(tabs[0], oracle_table(b, o, 21, qual_cutoff=qcut), f"nibbles qcut={qcut}")
     assert_tables_equal(tabs[0], tabs[1], f"nibbles vs bytes qcut={qcut}")
+
+
+def test_host_nibbles_empty_read_runs(knob):
+    """Chunks are also cut at a read count (chunk_bytes / 32, at least 64): runs of hundreds of empty reads make chunks
+    with no bases at all between ordinary ones."""
+    b, o = synth_set(400, 20000, 73)
+    lens = np.diff(o.astype(np.int64))
+    lens = np.concatenate([lens[:150], np.zeros(700, np.int64), lens[150:300], np.zeros(130, np.int64), lens[300:]])
+    o2 = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    knob("chunk_bytes", 2048)
+    knob("h2d_nib", 1)
+    got, st = hip_table(b, o2, 21)
+    assert st["h2d_chunks"] >= 15
+    assert_tables_equal(got, oracle_table(b, o2, 21), "empty read runs")
 
 
 def test_host_nibbles_bad_code_reported(knob):
