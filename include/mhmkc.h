@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MHMKC_ABI_VERSION 13
+#define MHMKC_ABI_VERSION 14
 #define MHMKC_COMM_ID_BYTES 128
 
 enum {
@@ -134,6 +134,8 @@ typedef struct {
   double ms_finish_tail;   /* device time from the last transfer's end (or finish's start) to the finished table */
   uint64_t inc_redone_coarse; /* ... coarse buckets whose capped fine layout overflowed (skew), counted again exactly */
   double inc_slack;           /* ... the capped fine buckets' slack over their expected records (0.25 .. 2) */
+  double ms_h2d_pack;         /* last mhmkc_add_reads: host wall time packing its chunks for the wire (nibble H2D) */
+  double ms_h2d_wait;         /* ... host wall time waiting for a pinned staging slot's previous copy */
 } mhmkc_stats;
 
 enum {

@@ -25,8 +25,9 @@ extern "C" {
  *   smer          0: MHMKC_OWNER_MINIMIZER at k >= 33 takes the record exchange + hand-off, not supermers
  *   chunk_bytes   H2D chunk of a host batch (0: 128 MB)
  *   d2h_chunk     staging chunk of a fetch into pageable host memory (0: 8 MB)
- *   h2d_nib       H2D of a host batch (mhmkc_add_reads): 1 the bases as nibbles, 0 as PackedRead bytes, -1 (default)
- *                 nibbles when the process has at least 4 host threads
+ *   h2d_nib       H2D of a host batch (mhmkc_add_reads): 1 the bases as nibbles and the offsets as u32 distances, 2
+ *                 nibbles and u64 offsets, 0 PackedRead bytes and u64 offsets, -1 (default) 1 when the process has at
+ *                 least 4 host threads, else 0
  *   cb0, cb0_2, cb0_3  coarse bits for one-, two-, three/four-word keys (0: 8, 8, 7) */
 int mhmkc_debug_set(const char *knob, int64_t value);
 /* Every knob back to its default. */

@@ -122,6 +122,8 @@ class MhmkcStats(C.Structure):
         ("ms_finish_tail", C.c_double),
         ("inc_redone_coarse", C.c_uint64),
         ("inc_slack", C.c_double),
+        ("ms_h2d_pack", C.c_double),
+        ("ms_h2d_wait", C.c_double),
     ]
 
     def as_dict(self) -> dict:

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -57,7 +58,8 @@ struct DebugKnobs {
   int64_t smer = 1;           // 0: the minimizer owner at k >= 33 takes the record exchange + hand-off
   int64_t chunk_bytes = 0;    // H2D chunk of a host batch (0: CHUNK_BYTES)
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
-  int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles, 0 the PackedRead bytes, -1 nibbles with >= 4 host threads
+  int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
+                              // bytes, -1 1 with >= 4 host threads, else 0
   int64_t cb0[4] = {0, 0, 0, 0};  // coarse bits by key words (0: the default)
 };
 DebugKnobs g_dbg;
@@ -865,7 +867,7 @@ int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads
     inc_expect += w;
     inc_announced += w;
   }
-  if (g_dbg.h2d_nib == 1 || (g_dbg.h2d_nib < 0 && host_threads() >= 4))
+  if (g_dbg.h2d_nib > 0 || (g_dbg.h2d_nib < 0 && host_threads() >= 4))
     return add_host_nib(bytes, offs, n_reads, qcut, chunk);
   hipError_t e;
   Arena *ar = new_arena();
@@ -984,6 +986,12 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   for (PinBuf *b : sl.p)
     if ((e = b->ensure(slot)) != hipSuccess) return hip_fail(e, "pinned staging");
   bool stage_used[2] = {false, false};
+  double pack_ms = 0, wait_ms = 0;
+  const bool deltas = g_dbg.h2d_nib != 2;  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms_since = [](std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
   qcut_pending = qcut;
   // the copies must not overwrite an arena that earlier work on the stream still reads
   (void)hipEventRecord(ev_h2d0, stream);
@@ -1008,13 +1016,16 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     const uint64_t r1 = lo, b1 = offs[r1];
     const bool span_ok = b1 >= b0 && b1 - b0 <= chunk + 65535;
     const int s = (int)(ci & 1), ds = (int)(ci % 3);
+    auto tw = now();
     if (stage_used[s] && (e = hipEventSynchronize(stage_ev[s])) != hipSuccess)
       return hip_fail(e, "input H2D");
+    wait_ms += ms_since(tw);
     uint8_t *stage = sl.p[s]->as<uint8_t>();
     uint32_t *sdelta = (uint32_t *)(stage + dof);
     const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
     std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX);
     std::vector<int> t_kind(T, 0);
+    auto tp = now();
     wk.run([&](int t) {
       // reads [r0 + t nr / T, r0 + (t + 1) nr / T): validated, their windows counted, their offsets' distances from
       // b0 staged (the last thread's also the chunk's end)
@@ -1028,14 +1039,15 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
           break;
         }
         if (b - a > kk + 1) w += b - a - kk - 1;
-        sdelta[r - r0] = (uint32_t)(a - b0);
+        if (deltas) sdelta[r - r0] = (uint32_t)(a - b0);
       }
-      if (t == T - 1) sdelta[nr] = (uint32_t)(b1 - b0);
+      if (deltas && t == T - 1) sdelta[nr] = (uint32_t)(b1 - b0);
       t_wins[t] = w;
       // bases [b0 + x, b0 + y) of an even x: nibbles from byte x / 2 of the slot
       const uint64_t per = ((nb + T - 1) / T + 1) & ~1ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
       if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut);
     });
+    pack_ms += ms_since(tp);
     uint64_t wins = 0;
     for (int t = 0; t < T; t++) {
       if (t_bad[t] != UINT64_MAX) {
@@ -1052,8 +1064,9 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     if (nib_used[ds] && (e = hipStreamWaitEvent(copy_stream, nib_ev[ds], 0)) != hipSuccess)
       return hip_fail(e, "copy stream");
     if ((nb && (e = hipMemcpyAsync(dslot, stage, nbytes, hipMemcpyHostToDevice, copy_stream)) != hipSuccess) ||
-        (e = hipMemcpyAsync(dslot + dof, sdelta, 4 * (nr + 1), hipMemcpyHostToDevice, copy_stream)) != hipSuccess ||
-        (e = hipEventRecord(stage_ev[s], copy_stream)) != hipSuccess)
+        (deltas && (e = hipMemcpyAsync(dslot + dof, sdelta, 4 * (nr + 1), hipMemcpyHostToDevice, copy_stream)) != hipSuccess) ||
+        (e = hipEventRecord(stage_ev[s], copy_stream)) != hipSuccess ||
+        (!deltas && (e = hipMemcpyAsync(dofs + r0, offs + r0, (nr + 1) * 8, hipMemcpyHostToDevice, copy_stream)) != hipSuccess))
       return hip_fail(e, "input H2D");
     stage_used[s] = true;
     if (n_ev == chunk_ev.size()) {
@@ -1065,11 +1078,11 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     if ((e = hipEventRecord(ev, copy_stream)) != hipSuccess || (e = hipStreamWaitEvent(stream, ev, 0)) != hipSuccess)
       return hip_fail(e, "chunk event");
     if ((e = mhm::launch_expand_nibbles(dslot, db, b0, nb, stream)) != hipSuccess ||
-        (e = mhm::launch_offs_from_deltas((const uint32_t *)(dslot + dof), dofs + r0, nr + 1, b0, stream)) != hipSuccess ||
+        (deltas && (e = mhm::launch_offs_from_deltas((const uint32_t *)(dslot + dof), dofs + r0, nr + 1, b0, stream)) != hipSuccess) ||
         (e = hipEventRecord(nib_ev[ds], stream)) != hipSuccess)
       return hip_fail(e, "nibble expansion");
     nib_used[ds] = true;
-    st.h2d_bytes += nbytes + (nr + 1) * 4;
+    st.h2d_bytes += nbytes + (nr + 1) * (deltas ? 4 : 8);
     st.h2d_chunks++;
     // slice view, as add_host's (the bytes before b0 in its first 16 belong to the previous chunk, expanded earlier on
     // the same stream)
@@ -1087,6 +1100,8 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   if ((e = hipStreamSynchronize(copy_stream)) != hipSuccess) return hip_fail(e, "input H2D");
   float ms = 0;
   if (hipEventElapsedTime(&ms, ev_h2d0, ev_h2d1) == hipSuccess) st.ms_h2d = ms;
+  st.ms_h2d_pack = pack_ms;
+  st.ms_h2d_wait = wait_ms;
   return MHMKC_OK;
 }
 

@@ -32,7 +32,7 @@ def test_lib_exports_every_declared_symbol():
     lib = N.lib()
     for name in declared(ROOT / "include" / "mhmkc.h") + declared(ROOT / "include" / "mhmkc_debug.h"):
         assert hasattr(lib, name), name
-    assert lib.mhmkc_abi_version() == 13
+    assert lib.mhmkc_abi_version() == 14
     assert lib.mhmkc_debug_set(b"no_such_knob", 1) == -1
 
 

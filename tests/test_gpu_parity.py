@@ -349,13 +349,14 @@ def test_distinct_sketch_estimate(k):
 # ---- round 2: host chunks, stream ordering, dmin at finish, overflow guard ----------------------------
 
 
-@pytest.mark.parametrize("nib", [0, 1])
+@pytest.mark.parametrize("nib", [0, 1, 2])
 @pytest.mark.parametrize("k,chunk", [(21, 700), (63, 1000), (33, 100000)])
 def test_host_chunks_equal_oracle(k, chunk, nib, knob):
     """mhmkc_add_reads copies a host batch in chunks of whole reads, each extracted as a slice view (an aligned
     byte base plus a head offset) as soon as it lands: ragged reads (empty, shorter than k, N runs, poly-A)
     over many chunk boundaries give the oracle's table, with the bases sent as bytes (nib 0) or as nibbles that the
-    device expands back (nib 1: odd chunk starts and ends split nibble pairs)."""
+    device expands back (nib 1 with u32 offset distances, 2 with u64 offsets: odd chunk starts and ends split nibble
+    pairs)."""
     knob("chunk_bytes", chunk)
     knob("h2d_nib", nib)
     b, o = edge_case_set(seed=17 + k)
@@ -364,8 +365,8 @@ def test_host_chunks_equal_oracle(k, chunk, nib, knob):
         c.finish()
         got, st = c.fetch(), c.stats()
     assert st["h2d_chunks"] >= (2 if chunk < 10000 else 1)
-    if nib:  # nibbles, and the offsets as u32 distances from each chunk's first byte
-        offs_bytes = 4 * (o.size - 1) + 4 * st["h2d_chunks"]
+    if nib:  # nibbles, and the offsets as u32 distances from each chunk's first byte (2: as they are, u64)
+        offs_bytes = (4 if nib == 1 else 8) * (o.size - 1 + st["h2d_chunks"])
         assert int(o[-1]) // 2 <= st["h2d_bytes"] - offs_bytes <= (int(o[-1]) + st["h2d_chunks"]) // 2
     else:
         assert st["h2d_bytes"] == int(o[-1]) + 8 * (o.size - 1) + 8 * st["h2d_chunks"]

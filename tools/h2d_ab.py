@@ -1,5 +1,5 @@
 """Performance probe (not a test): the C2 reads counted from pinned host memory (mhmkc_add_reads, the bench's
-h2d_inclusive window) with the bases sent as bytes (h2d_nib 0) and as nibbles (h2d_nib 1), interleaved in one process:
+h2d_inclusive window) with the bases sent as bytes (h2d_nib 0) and as nibbles with u32 (1) or u64 (2) offsets, interleaved in one process:
 per mode the median window (reset + add + finish, synchronised), the copy stream's span and bytes, and the output rows
 and count sum (which must agree).
     python tools/h2d_ab.py [K] [steps]
@@ -23,11 +23,11 @@ def main():
     b, o = m.synth_reads(g, 10_000_000, 150, 2, threads=16)
     hb = torch.from_numpy(b).pin_memory().numpy()
     ho = torch.from_numpy(o.view(np.int64)).pin_memory().numpy().view(np.uint64)
-    res = {0: [], 1: []}
+    res = {0: [], 1: [], 2: []}
     ref = None
     with m.KmerCounter(k, device=0) as c:
         for rep in range(steps + 2):
-            for nib in (0, 1):
+            for nib in (0, 1, 2):
                 N.debug_set("h2d_nib", nib)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -42,13 +42,15 @@ def main():
                     ref = sig
                 assert sig == ref, (nib, sig, ref)
                 if rep >= 2:
-                    res[nib].append((dt, st["ms_h2d"], st["h2d_bytes"], st["h2d_chunks"]))
+                    res[nib].append((dt, st["ms_h2d"], st["h2d_bytes"], st["h2d_chunks"], st["ms_h2d_pack"],
+                                     st["ms_h2d_wait"]))
     N.debug_reset()
     for nib, rows in res.items():
         rows.sort()
-        dt, h2d, hb_, ch = rows[len(rows) // 2]
+        dt, h2d, hb_, ch, pk, wt = rows[len(rows) // 2]
         print(f"k={k} h2d_nib={nib}: window {dt:.2f} ms (min {rows[0][0]:.2f})  copy span {h2d:.2f} ms  "
-              f"{hb_ / 1e9:.3f} GB in {ch} chunks  ({hb_ / h2d / 1e6:.1f} GB/s)  n_out={ref[0]}", flush=True)
+              f"{hb_ / 1e9:.3f} GB in {ch} chunks  ({hb_ / h2d / 1e6:.1f} GB/s)  host packing {pk:.2f} ms, "
+              f"slot waits {wt:.2f} ms  n_out={ref[0]}", flush=True)
 
 
 if __name__ == "__main__":
