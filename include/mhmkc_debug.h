@@ -15,7 +15,7 @@ extern "C" {
 #endif
 
 /* Set one knob (returns MHMKC_OK, or MHMKC_EINVAL for an unknown name). Knobs read at mhmkc_create (wide_records,
- * smer, cb0, cb0_2, cb0_3) apply to handles created afterwards, the others to the next call that uses them:
+ * smer, local_rounds, cb0, cb0_2, cb0_3) apply to handles created afterwards, the others to the next call that uses them:
  *   exact         1: exact (histogram) layouts for every slab and finish pass
  *   cap           k_count's LDS table slots (>= 64; 0: the kernel's own)
  *   fine_bits     fine bits of the partition (-1: from the distinct-key sketch)
@@ -28,6 +28,8 @@ extern "C" {
  *   h2d_nib       H2D of a host batch (mhmkc_add_reads): 1 the bases as nibbles and the offsets as u32 distances, 2
  *                 nibbles and u64 offsets, 0 PackedRead bytes and u64 offsets, -1 (default) 1 when the process has at
  *                 least 4 host threads, else 0
+ *   local_rounds  0: one rank's host batches are fine-partitioned at finish, not chunk by chunk as they land (created
+ *                 handles)
  *   cb0, cb0_2, cb0_3  coarse bits for one-, two-, three/four-word keys (0: 8, 8, 7) */
 int mhmkc_debug_set(const char *knob, int64_t value);
 /* Every knob back to its default. */

@@ -58,6 +58,7 @@ struct DebugKnobs {
   int64_t smer = 1;           // 0: the minimizer owner at k >= 33 takes the record exchange + hand-off
   int64_t chunk_bytes = 0;    // H2D chunk of a host batch (0: CHUNK_BYTES)
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
+  int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
   int64_t cb0[4] = {0, 0, 0, 0};  // coarse bits by key words (0: the default)
@@ -414,6 +415,12 @@ struct mhmkc {
   uint64_t inc_out_est = 0;
   int inc_setup();
   int inc_round(size_t r);
+  // single rank, host batches: the slabs of the H2D chunks become the incremental partition's rounds
+  // as their extractions finish ("local rounds"); slabs [0, lq) are rounds
+  bool lrounds = false;
+  size_t lq = 0;
+  int local_rounds(bool all);
+  hipEvent_t round_event(size_t r) const { return lrounds ? slabs[(size_t)x_round_slab[r]]->ev : x_ev[2 * r + 1]; }
   void round_sources(size_t r, std::vector<Source> &srcs) const;
   int finish_inc(bool &done, uint64_t *n_out_ret);
   void make_runs(const std::vector<Source> &srcs, uint32_t c0, uint32_t c1, int T, RunTable &rt) const;
@@ -1023,7 +1030,9 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     uint8_t *stage = sl.p[s]->as<uint8_t>();
     uint32_t *sdelta = (uint32_t *)(stage + dof);
     const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
-    std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX);
+    std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX), t_rest(T, 0);
+    // (the second chunk's run also counts the windows of the reads after it: the local rounds' expected total)
+    const bool announce = lrounds && ci == 1;
     std::vector<int> t_kind(T, 0);
     auto tp = now();
     wk.run([&](int t) {
@@ -1046,6 +1055,15 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
       // bases [b0 + x, b0 + y) of an even x: nibbles from byte x / 2 of the slot
       const uint64_t per = ((nb + T - 1) / T + 1) & ~1ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
       if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut);
+      if (announce) {
+        const uint64_t rest = n_reads - r1, qa = r1 + rest * t / T, qb = r1 + rest * (t + 1) / T;
+        uint64_t wr = 0;
+        for (uint64_t r = qa; r < qb; r++) {
+          const uint64_t a = offs[r], b = offs[r + 1];
+          if (b > a + kk + 1) wr += b - a - kk - 1;
+        }
+        t_rest[t] = wr;
+      }
     });
     pack_ms += ms_since(tp);
     uint64_t wins = 0;
@@ -1059,6 +1077,12 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
       wins += t_wins[t];
     }
     if (!span_ok) return fail(MHMKC_EHIP, "internal: H2D chunk of %llu bytes", (unsigned long long)(b1 - b0));
+    if (announce) {
+      uint64_t rest = 0;
+      for (int t = 0; t < T; t++) rest += t_rest[t];
+      inc_expect += rest;
+      inc_announced += rest;
+    }
     const uint64_t nbytes = (nb + 1) / 2;
     uint8_t *dslot = d_nib[ds].as<uint8_t>();
     if (nib_used[ds] && (e = hipStreamWaitEvent(copy_stream, nib_ev[ds], 0)) != hipSuccess)
@@ -1094,6 +1118,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     rv.n_reads = nr;
     rv.n_bases = b1 - rv.obase;
     if ((rc = add_view(rv, wins, true))) return rc;
+    if (lrounds && (rc = local_rounds(false))) return rc;
     r0 = r1;
   }
   (void)hipEventRecord(ev_h2d1, copy_stream);
@@ -2007,6 +2032,39 @@ void mhmkc::round_sources(size_t r, std::vector<Source> &srcs) const {
     }
 }
 
+// Local rounds (one rank, host batches): every slab but the two newest (whose extractions may still
+// run; `all`: every slab) becomes a round of the incremental partition once its extraction is done, with the windows the
+// add calls announced as the expected total. The layout is set after two rounds, as the exchange's (§3.5f), and each
+// round is fine-partitioned on pstream while the later chunks are on the wire: finish is then k_count alone.
+int mhmkc::local_rounds(bool all) {
+  int rc;
+  while (lq < n_slabs && (all || n_slabs >= lq + 3)) {
+    Slab *sl = slabs[lq];
+    for (int pass = 0; sl->pending; pass++) {
+      bool redo = false;
+      if ((rc = resolve_one(sl, redo))) return rc;
+      if (redo && pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
+    }
+    if (x_rounds == 0) {  // round 0's shares of the coarse buckets (all owned: one rank)
+      x_r0_coarse.assign(n_owned(), 0);
+      x_r0_total = 0;
+      for (uint32_t i = 0; i < nb * NSUB; i++) {
+        x_r0_coarse[i / NSUB] += sl->counts[i];
+        x_r0_total += sl->counts[i];
+      }
+    }
+    x_expect_all = inc_expect;
+    x_round_slab.push_back((int)lq);
+    x_rounds++;
+    lq++;
+    if (!inc_tried && x_rounds >= 2 && (rc = inc_setup())) return rc;
+    if (inc)
+      for (; inc_parted < x_rounds; inc_parted++)
+        if ((rc = inc_round(inc_parted))) return rc;
+  }
+  return MHMKC_OK;
+}
+
 // The incremental partition's layout, after round 0 has landed. The fine bits need the distinct keys
 // per coarse bucket, which round 0 samples: a HyperLogLog sketch of its records of the first owned coarse bucket, and a
 // second one of about half of them (the even chunks), give the distinct keys D at two sample sizes n; with
@@ -2018,7 +2076,8 @@ void mhmkc::round_sources(size_t r, std::vector<Source> &srcs) const {
 int mhmkc::inc_setup() {
   inc_tried = true;
   const uint32_t no = n_owned();
-  if (!pstream || x_expect_all == 0 || x_r0_total == 0 || n_parts < 1 || g_dbg.exact || no == 0) return MHMKC_OK;
+  if (!pstream || x_expect_all == 0 || x_r0_total == 0 || (n_parts < 1 && !lrounds) || g_dbg.exact || no == 0)
+    return MHMKC_OK;
   hipError_t e;
   std::vector<Source> srcs;
   round_sources(0, srcs);
@@ -2027,7 +2086,7 @@ int mhmkc::inc_setup() {
   make_runs(srcs, 0, 1, T, sk.rt);  // the first owned coarse bucket of round 0
   if (!sk.rt.n_c0 || sk.rt.rec_c0 < 4096) return MHMKC_OK;
   mhm::PartitionParams sp{};
-  if ((e = hipStreamWaitEvent(pstream, x_ev[1], 0)) != hipSuccess) return hip_fail(e, "partition stream");
+  if ((e = hipStreamWaitEvent(pstream, round_event(0), 0)) != hipSuccess) return hip_fail(e, "partition stream");
   int rc = upload_runs(sk.rt, sk.chunks, sk.srcs, pstream, sp);
   if (rc) return rc;
   // (the records per fine digit too, at SKETCH_FB bits, when the stored key bits below the coarse digit have them)
@@ -2114,7 +2173,7 @@ int mhmkc::inc_round(size_t r) {
   make_runs(srcs, 0, no, mhm::chunk_records(nl), ir->rt);
   if (!ir->rt.n_chunks) return MHMKC_OK;
   hipError_t e;
-  if ((e = hipStreamWaitEvent(pstream, x_ev[2 * r + 1], 0)) != hipSuccess) return hip_fail(e, "partition stream");
+  if ((e = hipStreamWaitEvent(pstream, round_event(r), 0)) != hipSuccess) return hip_fail(e, "partition stream");
   mhm::PartitionParams pp{};
   int rc = upload_runs(ir->rt, ir->chunks, ir->srcs, pstream, pp);
   if (rc) return rc;
@@ -2191,6 +2250,11 @@ int mhmkc::finish(uint64_t *n_out_ret) {
   } else if (G() > 1) {
     if ((rc = exchange(srcs))) return rc;
   } else {
+    if (lrounds && lq > 0) {  // local rounds began in an add call: the remaining slabs are rounds too
+      if ((rc = local_rounds(true))) return rc;
+      if (inc && ((e = hipEventRecord(ev_pdone, pstream)) != hipSuccess || (e = hipStreamWaitEvent(stream, ev_pdone, 0)) != hipSuccess))
+        return hip_fail(e, "partition stream");
+    }
     for (size_t s = 0; s < n_slabs; s++) {
       Source src;
       src.planes = slabs[s]->planes;
@@ -2881,12 +2945,13 @@ int mhmkc_create(mhmkc_t *out, const mhmkc_config *cfg) {
   // other collective of the same ranks in between; without it the exchange runs once, in finish.
   const char *xp_env = getenv("MHMKC_XPIPE");
   h->xpipe = cfg->n_ranks > 1 && !h->smer && xp_env && atoi(xp_env);
+  h->lrounds = cfg->n_ranks == 1 && !h->smer && g_dbg.local_rounds != 0;
   if (const char *env = getenv("MHMKC_XPIECES")) h->xpieces = std::max(1, std::min(64, atoi(env)));
   if ((e = hipEventCreate(&h->ev_tail0)) != hipSuccess ||
       (h->xpipe && ((e = hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking)) != hipSuccess ||
-                    (e = hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking)) != hipSuccess ||
-                    (e = hipEventCreateWithFlags(&h->ev_pdone, hipEventDisableTiming)) != hipSuccess ||
-                    (e = hipEventCreate(&h->ev_xdone)) != hipSuccess || (e = hipEventCreate(&h->ev_xext)) != hipSuccess))) {
+                    (e = hipEventCreate(&h->ev_xdone)) != hipSuccess || (e = hipEventCreate(&h->ev_xext)) != hipSuccess)) ||
+      ((h->xpipe || h->lrounds) && ((e = hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking)) != hipSuccess ||
+                                    (e = hipEventCreateWithFlags(&h->ev_pdone, hipEventDisableTiming)) != hipSuccess))) {
     g_create_error = std::string("exchange stream: ") + hipGetErrorString(e);
     mhmkc_destroy(h);
     return MHMKC_EHIP;
@@ -3725,6 +3790,7 @@ int mhmkc_reset(mhmkc_t h) {
   h->inc_expect = h->inc_announced = h->x_expect_all = h->x_r0_total = 0;
   h->x_r0_coarse.clear();
   h->x_round_slab.clear();
+  h->lq = 0;
   h->inc_distinct = h->inc_ext_per_rec = 0;
   h->prof_collect();
   h->n_slabs = 0;
@@ -3771,6 +3837,7 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
   else if (k == "chunk_bytes") g_dbg.chunk_bytes = value;
   else if (k == "d2h_chunk") g_dbg.d2h_chunk = value;
   else if (k == "h2d_nib") g_dbg.h2d_nib = value;
+  else if (k == "local_rounds") g_dbg.local_rounds = value;
   else if (k == "cb0") g_dbg.cb0[1] = value;
   else if (k == "cb0_2") g_dbg.cb0[2] = value;
   else if (k == "cb0_3") g_dbg.cb0[3] = value;

@@ -407,6 +407,36 @@ def test_host_nibbles_empty_read_runs(knob):
     assert_tables_equal(got, oracle_table(b, o2, 21), "empty read runs")
 
 
+@pytest.mark.parametrize("k", [21, 63])
+def test_host_local_rounds_equal_oracle(k, knob):
+    """One rank, a host batch in many chunks: the chunks' slabs are fine-partitioned as they land (local rounds, the
+    incremental layout of DESIGN.md §3.5f set after two of them) and finish only counts; the table equals the CPU
+    restatement's and the one partitioned at finish (local_rounds 0)."""
+    b, o = synth_set(200000, 2_000_000, 74)
+    knob("chunk_bytes", 6 << 20)
+    knob("h2d_nib", 1)
+    got, st = hip_table(b, o, k)
+    assert st["inc_rounds"] >= 4 and st["inc_fallbacks"] == 0 and st["inc_redone_coarse"] == 0, st
+    check_stats(st)
+    exp = O.kcount_mt(b, o, k)
+    assert_tables_equal(got, m.KmerTable(k, *exp.fetch()), f"local rounds k={k}")
+    knob("local_rounds", 0)
+    ref, st0 = hip_table(b, o, k)
+    assert st0["inc_rounds"] == 0
+    assert_tables_equal(got, ref, f"local rounds vs at finish k={k}")
+
+
+def test_host_local_rounds_hot_kmer_redo(knob):
+    """Local rounds with a skewed batch: 800 poly-A reads at its end, after 120k random reads. The poly-A k-mer's fine
+    bucket overflows its capped segment; that coarse bucket alone is counted again with exact sizes at finish."""
+    b, o = hot_set(n_reads=120000, genome_len=400000, n_poly=800, seed=4)
+    knob("chunk_bytes", 5 << 20)
+    knob("h2d_nib", 1)
+    got, st = hip_table(b, o, 21)
+    assert st["inc_rounds"] >= 3 and st["inc_fallbacks"] == 0 and st["inc_redone_coarse"] == 1, st
+    assert_tables_equal(got, oracle_table(b, o, 21), "local rounds, hot k-mer")
+
+
 def test_host_nibbles_bad_code_reported(knob):
     """A byte with code 5-7 sent as a nibble still reaches the device's input check (error, no table)."""
     b, o = synth_set(200, 5000, 72)
