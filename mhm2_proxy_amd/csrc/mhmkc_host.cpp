@@ -58,6 +58,7 @@ struct DebugKnobs {
   int64_t smer = 1;           // 0: the minimizer owner at k >= 33 takes the record exchange + hand-off
   int64_t chunk_bytes = 0;    // H2D chunk of a host batch (0: CHUNK_BYTES)
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
+  int64_t h2d_threads = 0;   // nibble H2D: worker threads that pack (0: all)
   int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
@@ -325,9 +326,19 @@ __attribute__((target("avx2"))) inline __m256i nib_pairs_avx2(__m256i v, __m256i
   return _mm256_maddubs_epi16(_mm256_or_si256(_mm256_and_si256(v, _mm256_set1_epi8(7)), ok), _mm256_set1_epi16(0x1001));
 }
 
+// A 32-byte aligned dst is written with streaming stores (the staging is only read by the DMA engine: no read for
+// ownership, nothing evicted), fenced at the end.
 __attribute__((target("avx2"))) void nib_pack_avx2(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut) {
   const __m256i qm1 = _mm256_set1_epi8((char)(std::min(std::max(qcut, 0), 32) - 1));
   uint64_t i = 0;
+  if (((uintptr_t)dst & 31) == 0) {
+    for (; i + 64 <= n; i += 64) {
+      const __m256i a = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i)), qm1);
+      const __m256i b = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i + 32)), qm1);
+      _mm256_stream_si256((__m256i *)(dst + i / 2), _mm256_permute4x64_epi64(_mm256_packus_epi16(a, b), 0xd8));
+    }
+    _mm_sfence();
+  }
   for (; i + 64 <= n; i += 64) {
     const __m256i a = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i)), qm1);
     const __m256i b = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i + 32)), qm1);
@@ -994,7 +1005,8 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     if ((e = b->ensure(slot)) != hipSuccess) return hip_fail(e, "pinned staging");
   bool stage_used[2] = {false, false};
   double pack_ms = 0, wait_ms = 0;
-  const bool deltas = g_dbg.h2d_nib != 2;  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
+  const bool deltas = g_dbg.h2d_nib != 2;
+  const int TP = g_dbg.h2d_threads > 0 ? (int)std::min<int64_t>(T, g_dbg.h2d_threads) : T;  // threads that pack  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto ms_since = [](std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1052,8 +1064,8 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
       }
       if (deltas && t == T - 1) sdelta[nr] = (uint32_t)(b1 - b0);
       t_wins[t] = w;
-      // bases [b0 + x, b0 + y) of an even x: nibbles from byte x / 2 of the slot
-      const uint64_t per = ((nb + T - 1) / T + 1) & ~1ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
+      // bases [b0 + x, b0 + y) of an x that is a multiple of 64: nibbles from the 32-byte aligned byte x / 2 of the slot
+      const uint64_t per = ((nb + TP - 1) / TP + 63) & ~63ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
       if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut);
       if (announce) {
         const uint64_t rest = n_reads - r1, qa = r1 + rest * t / T, qb = r1 + rest * (t + 1) / T;
@@ -3838,6 +3850,7 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
   else if (k == "d2h_chunk") g_dbg.d2h_chunk = value;
   else if (k == "h2d_nib") g_dbg.h2d_nib = value;
   else if (k == "local_rounds") g_dbg.local_rounds = value;
+  else if (k == "h2d_threads") g_dbg.h2d_threads = value;
   else if (k == "cb0") g_dbg.cb0[1] = value;
   else if (k == "cb0_2") g_dbg.cb0[2] = value;
   else if (k == "cb0_3") g_dbg.cb0[3] = value;
