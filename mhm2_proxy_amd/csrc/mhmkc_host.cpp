@@ -59,6 +59,7 @@ struct DebugKnobs {
   int64_t chunk_bytes = 0;    // H2D chunk of a host batch (0: CHUNK_BYTES)
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
   int64_t h2d_threads = 0;   // nibble H2D: worker threads that pack (0: all)
+  int64_t h2d_nt = 1;        // nibble H2D: streaming stores into the staging (0: ordinary stores)
   int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
@@ -328,10 +329,10 @@ __attribute__((target("avx2"))) inline __m256i nib_pairs_avx2(__m256i v, __m256i
 
 // A 32-byte aligned dst is written with streaming stores (the staging is only read by the DMA engine: no read for
 // ownership, nothing evicted), fenced at the end.
-__attribute__((target("avx2"))) void nib_pack_avx2(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut) {
+__attribute__((target("avx2"))) void nib_pack_avx2(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut, bool nt) {
   const __m256i qm1 = _mm256_set1_epi8((char)(std::min(std::max(qcut, 0), 32) - 1));
   uint64_t i = 0;
-  if (((uintptr_t)dst & 31) == 0) {
+  if (nt && ((uintptr_t)dst & 31) == 0) {
     for (; i + 64 <= n; i += 64) {
       const __m256i a = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i)), qm1);
       const __m256i b = nib_pairs_avx2(_mm256_loadu_si256((const __m256i *)(src + i + 32)), qm1);
@@ -347,10 +348,10 @@ __attribute__((target("avx2"))) void nib_pack_avx2(const uint8_t *src, uint64_t 
   nib_pack_swar(src, n, dst, qcut, i);
 }
 
-void nib_pack(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut) {
+void nib_pack(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut, bool nt = true) {
   static const bool avx2 = __builtin_cpu_supports("avx2");
   if (avx2)
-    nib_pack_avx2(src, n, dst, qcut);
+    nib_pack_avx2(src, n, dst, qcut, nt);
   else
     nib_pack_swar(src, n, dst, qcut);
 }
@@ -1066,7 +1067,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
       t_wins[t] = w;
       // bases [b0 + x, b0 + y) of an x that is a multiple of 64: nibbles from the 32-byte aligned byte x / 2 of the slot
       const uint64_t per = ((nb + TP - 1) / TP + 63) & ~63ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
-      if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut);
+      if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut, g_dbg.h2d_nt != 0);
       if (announce) {
         const uint64_t rest = n_reads - r1, qa = r1 + rest * t / T, qb = r1 + rest * (t + 1) / T;
         uint64_t wr = 0;
@@ -3851,6 +3852,7 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
   else if (k == "h2d_nib") g_dbg.h2d_nib = value;
   else if (k == "local_rounds") g_dbg.local_rounds = value;
   else if (k == "h2d_threads") g_dbg.h2d_threads = value;
+  else if (k == "h2d_nt") g_dbg.h2d_nt = value;
   else if (k == "cb0") g_dbg.cb0[1] = value;
   else if (k == "cb0_2") g_dbg.cb0[2] = value;
   else if (k == "cb0_3") g_dbg.cb0[3] = value;
