@@ -409,10 +409,11 @@ def test_host_nibbles_empty_read_runs(knob):
 
 @pytest.mark.parametrize("k", [21, 63])
 def test_host_local_rounds_equal_oracle(k, knob):
-    """One rank, a host batch in many chunks: the chunks' slabs are fine-partitioned as they land (local rounds, the
-    incremental layout of DESIGN.md §3.5f set after two of them) and finish only counts; the table equals the CPU
-    restatement's and the one partitioned at finish (local_rounds 0)."""
+    """One rank, a host batch in many chunks, local rounds on (opt-in): the chunks' slabs are fine-partitioned as they
+    land (the incremental layout of DESIGN.md §3.5f, set after two of them) and finish only counts; the table equals
+    the CPU restatement's and the one partitioned at finish (local_rounds 0, the default)."""
     b, o = synth_set(200000, 2_000_000, 74)
+    knob("local_rounds", 1)
     knob("chunk_bytes", 8 << 20)  # (the first chunk, 2 MB, samples >= 4096 records of one coarse bucket also at k = 63)
     knob("h2d_nib", 1)
     got, st = hip_table(b, o, k)
@@ -431,6 +432,7 @@ def test_host_local_rounds_hot_kmer_redo(knob):
     """Local rounds with a skewed batch: 800 poly-A reads at its end, after 120k random reads. The poly-A k-mer's fine
     bucket overflows its capped segment; that coarse bucket alone is counted again with exact sizes at finish."""
     b, o = hot_set(n_reads=120000, genome_len=400000, n_poly=800, seed=4)
+    knob("local_rounds", 1)
     knob("chunk_bytes", 5 << 20)
     knob("h2d_nib", 1)
     got, st = hip_table(b, o, 21)
