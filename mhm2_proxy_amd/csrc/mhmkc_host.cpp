@@ -2048,8 +2048,9 @@ void mhmkc::round_sources(size_t r, std::vector<Source> &srcs) const {
 
 // Local rounds (one rank, host batches): every slab but the two newest (whose extractions may still
 // run; `all`: every slab) becomes a round of the incremental partition once its extraction is done, with the windows the
-// add calls announced as the expected total. The layout is set after two rounds, as the exchange's (§3.5f), and each
-// round is fine-partitioned on pstream while the later chunks are on the wire: finish is then k_count alone.
+// add calls announced as the expected total. The layout is set once the rounds hold 40 % of those windows (the
+// exchange's is set after two rounds, §3.5f), from a sketch of all of them, and then each round is fine-partitioned on
+// pstream while the later chunks are on the wire: finish is then k_count alone.
 int mhmkc::local_rounds(bool all) {
   int rc;
   while (lq < n_slabs && (all || n_slabs >= lq + 3)) {
@@ -2059,9 +2060,11 @@ int mhmkc::local_rounds(bool all) {
       if ((rc = resolve_one(sl, redo))) return rc;
       if (redo && pass) return fail(MHMKC_EHIP, "internal: exact extraction overflowed");
     }
-    if (x_rounds == 0) {  // round 0's shares of the coarse buckets (all owned: one rank)
-      x_r0_coarse.assign(n_owned(), 0);
-      x_r0_total = 0;
+    if (!inc_tried) {  // the sampled rounds' shares of the coarse buckets (all owned: one rank)
+      if (x_rounds == 0) {
+        x_r0_coarse.assign(n_owned(), 0);
+        x_r0_total = 0;
+      }
       for (uint32_t i = 0; i < nb * NSUB; i++) {
         x_r0_coarse[i / NSUB] += sl->counts[i];
         x_r0_total += sl->counts[i];
@@ -2071,7 +2074,17 @@ int mhmkc::local_rounds(bool all) {
     x_round_slab.push_back((int)lq);
     x_rounds++;
     lq++;
-    if (!inc_tried && x_rounds >= 2 && (rc = inc_setup())) return rc;
+    // the layout once the rounds hold 40 % of the announced windows: a genome k-mer has then been seen about 10 times
+    // at C2's coverage and the sketch's two-point extrapolation sees the errors' slope (at 1/48 of the reads, two
+    // rounds, it took the still rising genome part for errors, 3-5x too many distinct keys), or at finish
+    if (!inc_tried && x_rounds >= 2 && (double)x_r0_total >= 0.4 * (double)x_expect_all && (rc = inc_setup()))
+      return rc;
+    if (inc)
+      for (; inc_parted < x_rounds; inc_parted++)
+        if ((rc = inc_round(inc_parted))) return rc;
+  }
+  if (all && !inc_tried && x_rounds >= 2) {
+    if ((rc = inc_setup())) return rc;
     if (inc)
       for (; inc_parted < x_rounds; inc_parted++)
         if ((rc = inc_round(inc_parted))) return rc;
@@ -2095,6 +2108,12 @@ int mhmkc::inc_setup() {
   hipError_t e;
   std::vector<Source> srcs;
   round_sources(0, srcs);
+  if (lrounds)  // local rounds: the sample is every round so far (set up at 40 % of the windows, local_rounds())
+    for (size_t r = 1; r < x_rounds; r++) {
+      std::vector<Source> more;
+      round_sources(r, more);
+      for (auto &src : more) srcs.push_back(std::move(src));
+    }
   const int T = mhm::chunk_records(nl);
   IncRound sk;
   make_runs(srcs, 0, 1, T, sk.rt);  // the first owned coarse bucket of round 0
