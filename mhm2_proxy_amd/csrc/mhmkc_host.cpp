@@ -952,8 +952,8 @@ int mhmkc::add_host(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads
 // add_host with the bases sent as nibbles (half the PCIe bytes). Per chunk of whole reads the host
 // workers validate the offsets, count the windows and pack the bytes into a pinned slot (nib_pack) while the previous
 // chunk is on the wire; the copy lands in a device slot that k_expand_nibbles turns back into PackedRead bytes in the
-// arena, on the extraction's stream just before the chunk is extracted. The first chunk is a quarter of the others, so
-// that the wire starts early.
+// arena, on the extraction's stream just before the chunk is extracted. With one rank the first chunk is a quarter of
+// the others, so that the wire starts early.
 int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_reads, int qcut, uint64_t chunk) {
   const uint64_t n_bases = offs[n_reads];
   Workers &wk = Workers::get();
@@ -1025,7 +1025,9 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   for (uint64_t r0 = 0, ci = 0; r0 < n_reads; ci++) {
     // the chunk [r0, r1): the first read r > r0 with offs[r] - b0 >= want ends it (a binary search; the offsets are
     // validated below, and a chunk whose end lies before its start is only validated, for the error)
-    const uint64_t b0 = offs[r0], want = ci == 0 ? std::max<uint64_t>(64, chunk / 4) : chunk;
+    // (a quarter-size first chunk starts the wire early; not with the pipelined exchange, whose incremental layout
+    // extrapolates from round 0, this chunk's slab: a smaller sample overestimated its distinct keys and output)
+    const uint64_t b0 = offs[r0], want = ci == 0 && !xpipe ? std::max<uint64_t>(64, chunk / 4) : chunk;
     uint64_t lo = r0 + 1, hi = std::min(n_reads, r0 + rmax);
     while (lo < hi) {
       const uint64_t m = (lo + hi) / 2;
