@@ -136,6 +136,7 @@ typedef struct {
   double inc_slack;           /* ... the capped fine buckets' slack over their expected records (0.25 .. 2) */
   double ms_h2d_pack;         /* last mhmkc_add_reads: host wall time packing its chunks for the wire (nibble H2D) */
   double ms_h2d_wait;         /* ... host wall time waiting for a pinned staging slot's previous copy */
+  double ms_h2d_rounds;       /* ... host wall time enqueueing local rounds between its chunks (mhmkc_debug.h) */
 } mhmkc_stats;
 
 enum {

@@ -124,6 +124,7 @@ class MhmkcStats(C.Structure):
         ("inc_slack", C.c_double),
         ("ms_h2d_pack", C.c_double),
         ("ms_h2d_wait", C.c_double),
+        ("ms_h2d_rounds", C.c_double),
     ]
 
     def as_dict(self) -> dict:

@@ -199,6 +199,7 @@ struct RunTable {
 struct IncRound {
   RunTable rt;
   DevBuf chunks, srcs;
+  PinBuf pin;  // the tables' pinned copy (a pageable source made the host wait for the partition stream's earlier work)
 };
 
 // One device-to-device transfer of the exchange: `bytes` at `ptr` to (or from) rank `peer`.
@@ -437,7 +438,8 @@ struct mhmkc {
   void round_sources(size_t r, std::vector<Source> &srcs) const;
   int finish_inc(bool &done, uint64_t *n_out_ret);
   void make_runs(const std::vector<Source> &srcs, uint32_t c0, uint32_t c1, int T, RunTable &rt) const;
-  int upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_t s, mhm::PartitionParams &pp);
+  int upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_t s, mhm::PartitionParams &pp,
+                  PinBuf *pin = nullptr);
   int fine_layout(const std::vector<uint64_t> &per_coarse, double slack, std::vector<uint64_t> &cfit,
                   uint64_t &r2_size) const;
   int pump();
@@ -1006,7 +1008,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   for (PinBuf *b : sl.p)
     if ((e = b->ensure(slot)) != hipSuccess) return hip_fail(e, "pinned staging");
   bool stage_used[2] = {false, false};
-  double pack_ms = 0, wait_ms = 0;
+  double pack_ms = 0, wait_ms = 0, rounds_ms = 0;
   const bool deltas = g_dbg.h2d_nib != 2;
   const int TP = g_dbg.h2d_threads > 0 ? (int)std::min<int64_t>(T, g_dbg.h2d_threads) : T;  // threads that pack  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
   auto now = [] { return std::chrono::steady_clock::now(); };
@@ -1134,7 +1136,11 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     rv.n_reads = nr;
     rv.n_bases = b1 - rv.obase;
     if ((rc = add_view(rv, wins, true))) return rc;
-    if (lrounds && (rc = local_rounds(false))) return rc;
+    if (lrounds) {
+      auto tl = now();
+      if ((rc = local_rounds(false))) return rc;
+      rounds_ms += ms_since(tl);
+    }
     r0 = r1;
   }
   (void)hipEventRecord(ev_h2d1, copy_stream);
@@ -1143,6 +1149,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   if (hipEventElapsedTime(&ms, ev_h2d0, ev_h2d1) == hipSuccess) st.ms_h2d = ms;
   st.ms_h2d_pack = pack_ms;
   st.ms_h2d_wait = wait_ms;
+  st.ms_h2d_rounds = rounds_ms;
   return MHMKC_OK;
 }
 
@@ -1970,7 +1977,8 @@ void mhmkc::make_runs(const std::vector<Source> &srcs, uint32_t c0, uint32_t c1,
 
 // The run table on the device (buf: runs | chunk index, expanded on s; sbuf: the plane sets), and the partition
 // parameters that point at it. The host vectors of rt must live until the copies on s ran.
-int mhmkc::upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_t s, mhm::PartitionParams &pp) {
+int mhmkc::upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_t s, mhm::PartitionParams &pp,
+                       PinBuf *pin) {
   const int T = mhm::chunk_records(nl);
   if (rt.n_chunks >= 0x7fffffffull) return fail(MHMKC_EINVAL, "too many chunks");
   hipError_t e;
@@ -1983,16 +1991,24 @@ int mhmkc::upload_runs(const RunTable &rt, DevBuf &buf, DevBuf &sbuf, hipStream_
   if ((e = main ? grow(sbuf, sb) : sbuf.ensure(sb)) != hipSuccess) return hip_fail(e, "source table");
   mhm::SRun *d_runs = buf.as<mhm::SRun>();
   mhm::SChunk *d_chunk_run = (mhm::SChunk *)(buf.as<char>() + rb);
+  const void *h_runs = rt.runs.data(), *h_ps = rt.ps.data();
+  if (pin) {  // (the caller keeps *pin until the copies have run)
+    const size_t rbytes = rt.runs.size() * sizeof(mhm::SRun), pbytes = rt.ps.size() * sizeof(mhm::PlaneSet);
+    if ((e = pin->ensure(rb + pbytes + 64)) != hipSuccess) return hip_fail(e, "run table staging");
+    memcpy(pin->as<char>(), rt.runs.data(), rbytes);
+    memcpy(pin->as<char>() + rb, rt.ps.data(), pbytes);
+    h_runs = pin->as<char>();
+    h_ps = pin->as<char>() + rb;
+  }
   if (!rt.runs.empty()) {
-    if ((e = hipMemcpyAsync(d_runs, rt.runs.data(), rt.runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, s)) !=
+    if ((e = hipMemcpyAsync(d_runs, h_runs, rt.runs.size() * sizeof(mhm::SRun), hipMemcpyHostToDevice, s)) !=
         hipSuccess)
       return hip_fail(e, "run table H2D");
     if ((e = mhm::launch_chunk_runs(d_runs, (uint32_t)rt.runs.size(), d_chunk_run, T, s)) != hipSuccess)
       return hip_fail(e, "chunk index");
   }
   if (!rt.ps.empty() &&
-      (e = hipMemcpyAsync(sbuf.p, rt.ps.data(), rt.ps.size() * sizeof(mhm::PlaneSet), hipMemcpyHostToDevice, s)) !=
-          hipSuccess)
+      (e = hipMemcpyAsync(sbuf.p, h_ps, rt.ps.size() * sizeof(mhm::PlaneSet), hipMemcpyHostToDevice, s)) != hipSuccess)
     return hip_fail(e, "source H2D");
   pp.runs = d_runs;
   pp.chunks = d_chunk_run;
@@ -2210,7 +2226,7 @@ int mhmkc::inc_round(size_t r) {
   hipError_t e;
   if ((e = hipStreamWaitEvent(pstream, round_event(r), 0)) != hipSuccess) return hip_fail(e, "partition stream");
   mhm::PartitionParams pp{};
-  int rc = upload_runs(ir->rt, ir->chunks, ir->srcs, pstream, pp);
+  int rc = upload_runs(ir->rt, ir->chunks, ir->srcs, pstream, pp, &ir->pin);
   if (rc) return rc;
   unsigned long long *cf = d_cfit.as<unsigned long long>();
   pp.fine_hist = nullptr;
@@ -3017,6 +3033,7 @@ void mhmkc_destroy(mhmkc_t h) {
   for (IncRound *q : h->inc_pool) {
     q->chunks.release();
     q->srcs.release();
+    q->pin.release();
     delete q;
   }
   if (h->pstream) (void)hipStreamDestroy(h->pstream);
