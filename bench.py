@@ -138,6 +138,11 @@ def handoff_ms(counter, k: int, threads: int, runs: int = 3):
     if not lib_path.exists():
         return None
     lib = C.CDLL(str(lib_path))
+    from mhm2_proxy_amd import _native as N
+
+    abi = N.lib().mhmkc_abi_version()
+    if not hasattr(lib, "mhmkc_handoff_abi") or lib.mhmkc_handoff_abi() != abi:
+        return {"error": f"tools/bin/libmhmkc_handoff.so was built for another libmhmkc ABI than {abi}: run build()"}
     lib.mhmkc_handoff_ms.restype = C.c_double
     lib.mhmkc_handoff_ms.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_uint64),
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_double)]

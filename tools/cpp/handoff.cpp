@@ -59,6 +59,10 @@ static double run(mhmkc_t h, int k, int threads, uint64_t chunk_rows, uint64_t *
   return ms;
 }
 
+// The ABI this tool was compiled against (mhmkc_stats lives on its stack: a tool older than the library would overflow
+// it); bench.py compares it with mhmkc_abi_version() before the first call.
+extern "C" int mhmkc_handoff_abi(void) { return MHMKC_ABI_VERSION; }
+
 extern "C" double mhmkc_handoff_ms(mhmkc_t h, int k, int threads, uint64_t chunk_rows, uint64_t *size_out,
                                    uint64_t *bad_out, double *parts_out) {
   switch (k / 32 + 1) {
