@@ -1052,11 +1052,22 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     // (the second chunk's run also counts the windows of the reads after it: the local rounds' expected total)
     const bool announce = lrounds && ci == 1;
     std::vector<int> t_kind(T, 0);
+    // local rounds due (slabs two chunks old): the calling thread enqueues them while the others pack
+    const bool rounds_here = lrounds && n_slabs >= lq + 3 && T >= 2;
+    const int U = rounds_here ? T - 1 : T, packers = std::min(TP, U);  // threads on the chunk's data
+    int rounds_rc = MHMKC_OK;
     auto tp = now();
     wk.run([&](int t) {
-      // reads [r0 + t nr / T, r0 + (t + 1) nr / T): validated, their windows counted, their offsets' distances from
+      if (rounds_here && t == 0) {
+        auto tl = now();
+        rounds_rc = local_rounds(false);
+        rounds_ms += ms_since(tl);
+        return;
+      }
+      const int u = rounds_here ? t - 1 : t;
+      // reads [r0 + u nr / U, r0 + (u + 1) nr / U): validated, their windows counted, their offsets' distances from
       // b0 staged (the last thread's also the chunk's end)
-      const uint64_t ra = r0 + nr * t / T, rb = r0 + nr * (t + 1) / T;
+      const uint64_t ra = r0 + nr * u / U, rb = r0 + nr * (u + 1) / U;
       uint64_t w = 0;
       for (uint64_t r = ra; r < rb; r++) {
         const uint64_t a = offs[r], b = offs[r + 1];
@@ -1068,13 +1079,14 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
         if (b - a > kk + 1) w += b - a - kk - 1;
         if (deltas) sdelta[r - r0] = (uint32_t)(a - b0);
       }
-      if (deltas && t == T - 1) sdelta[nr] = (uint32_t)(b1 - b0);
+      if (deltas && u == U - 1) sdelta[nr] = (uint32_t)(b1 - b0);
       t_wins[t] = w;
       // bases [b0 + x, b0 + y) of an x that is a multiple of 64: nibbles from the 32-byte aligned byte x / 2 of the slot
-      const uint64_t per = ((nb + TP - 1) / TP + 63) & ~63ull, x = std::min(nb, per * t), y = std::min(nb, x + per);
+      const uint64_t per = ((nb + packers - 1) / packers + 63) & ~63ull, x = std::min(nb, per * u),
+                     y = std::min(nb, x + per);
       if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut, g_dbg.h2d_nt != 0);
       if (announce) {
-        const uint64_t rest = n_reads - r1, qa = r1 + rest * t / T, qb = r1 + rest * (t + 1) / T;
+        const uint64_t rest = n_reads - r1, qa = r1 + rest * u / U, qb = r1 + rest * (u + 1) / U;
         uint64_t wr = 0;
         for (uint64_t r = qa; r < qb; r++) {
           const uint64_t a = offs[r], b = offs[r + 1];
@@ -1084,6 +1096,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
       }
     });
     pack_ms += ms_since(tp);
+    if (rounds_rc) return rounds_rc;
     uint64_t wins = 0;
     for (int t = 0; t < T; t++) {
       if (t_bad[t] != UINT64_MAX) {
@@ -1136,12 +1149,12 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     rv.n_reads = nr;
     rv.n_bases = b1 - rv.obase;
     if ((rc = add_view(rv, wins, true))) return rc;
-    if (lrounds) {
-      auto tl = now();
-      if ((rc = local_rounds(false))) return rc;
-      rounds_ms += ms_since(tl);
-    }
     r0 = r1;
+  }
+  if (lrounds) {  // (the rounds that the last chunk made due)
+    auto tl = now();
+    if ((rc = local_rounds(false))) return rc;
+    rounds_ms += ms_since(tl);
   }
   (void)hipEventRecord(ev_h2d1, copy_stream);
   if ((e = hipStreamSynchronize(copy_stream)) != hipSuccess) return hip_fail(e, "input H2D");
