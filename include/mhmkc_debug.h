@@ -30,8 +30,8 @@ extern "C" {
  *                 least 4 host threads, else 0
  *   h2d_threads   nibble H2D: host worker threads that pack the bases (0: all of them)
  *   h2d_nt        nibble H2D: 0 ordinary stores into the pinned staging instead of streaming stores
- *   local_rounds  1: one rank's host batches are fine-partitioned chunk by chunk as they land, not at finish (created
- *                 handles; off by default)
+ *   local_rounds  0: one rank's host batches are fine-partitioned at finish, not chunk by chunk as they land (created
+ *                 handles)
  *   cb0, cb0_2, cb0_3  coarse bits for one-, two-, three/four-word keys (0: 8, 8, 7) */
 int mhmkc_debug_set(const char *knob, int64_t value);
 /* Every knob back to its default. */

@@ -60,8 +60,7 @@ struct DebugKnobs {
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
   int64_t h2d_threads = 0;   // nibble H2D: worker threads that pack (0: all)
   int64_t h2d_nt = 1;        // nibble H2D: streaming stores into the staging (0: ordinary stores)
-  int64_t local_rounds = 0;  // 1: one rank's host batches' chunks fine-partitioned as they land (created handles; opt-in:
-                             // the layout's extrapolated distinct keys overshoot at C2)
+  int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
   int64_t cb0[4] = {0, 0, 0, 0};  // coarse bits by key words (0: the default)

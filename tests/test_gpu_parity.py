@@ -409,9 +409,9 @@ def test_host_nibbles_empty_read_runs(knob):
 
 @pytest.mark.parametrize("k", [21, 63])
 def test_host_local_rounds_equal_oracle(k, knob):
-    """One rank, a host batch in many chunks, local rounds on (opt-in): the chunks' slabs are fine-partitioned as they
-    land (the incremental layout of DESIGN.md §3.5f, set after two of them) and finish only counts; the table equals
-    the CPU restatement's and the one partitioned at finish (local_rounds 0, the default)."""
+    """One rank, a host batch in many chunks (local rounds, the default): the chunks' slabs are fine-partitioned as
+    they land (the incremental layout of DESIGN.md §3.5f, set once they hold 40 % of the windows) and finish only
+    counts; the table equals the CPU restatement's and the one partitioned at finish (local_rounds 0)."""
     b, o = synth_set(200000, 2_000_000, 74)
     knob("local_rounds", 1)
     knob("chunk_bytes", 8 << 20)  # (the first chunk, 2 MB, samples >= 4096 records of one coarse bucket also at k = 63)
