@@ -581,7 +581,7 @@ def test_capped_overflow_in_last_bucket(k):
     "all key ranges) supersedes it inside the driver's test window (MHMKC_SCALE_TESTS=1 runs it)")), 99])
 def test_c2_full_table_vs_cpu_restatement(k):
     """config C2 at full size (10M x 150 bp, G = 50 Mbp, seed 2) through the host path
-    (chunked H2D), every row of the table compared with the multi-threaded CPU restatement (oracle/kcount_mt.c,
+    (chunked nibble H2D, local rounds), every row of the table compared with the multi-threaded CPU restatement (oracle/kcount_mt.c,
     itself pinned to the single-threaded oracle and the golden fixtures); k = 21, k = 63 (with MHMKC_SCALE_TESTS=1;
     the eight-rank C4 test covers k = 63 at 8.6e9 occurrences) and k = 99 (mixed four-word records, DESIGN.md
     §3.7c)."""
@@ -590,6 +590,8 @@ def test_c2_full_table_vs_cpu_restatement(k):
     del g
     got, st = hip_table(b, o, k)
     assert st["occurrences"] == 10_000_000 * (150 - k - 1)
+    # (one rank, twelve 128 MB chunks: fine-partitioned as they land)
+    assert st["inc_rounds"] >= 10 and st["inc_fallbacks"] == 0, (st["inc_rounds"], st["inc_fallbacks"])
     check_stats(st)
     t = O.kcount_mt(b, o, k, threads=16)
     keys, c, l, r = t.fetch()
