@@ -2083,6 +2083,9 @@ void mhmkc::round_sources(size_t r, std::vector<Source> &srcs) const {
 // pstream while the later chunks are on the wire: finish is then k_count alone.
 int mhmkc::local_rounds(bool all) {
   int rc;
+  // (between chunks at most two rounds are partitioned per call, so that the backlog of the round that sets the layout
+  // is spread over the next chunks instead of holding one chunk's packing back)
+  int budget = all ? 1 << 30 : 2;
   while (lq < n_slabs && (all || n_slabs >= lq + 3)) {
     Slab *sl = slabs[lq];
     for (int pass = 0; sl->pending; pass++) {
@@ -2110,9 +2113,12 @@ int mhmkc::local_rounds(bool all) {
     if (!inc_tried && x_rounds >= 2 && (double)x_r0_total >= 0.4 * (double)x_expect_all && (rc = inc_setup()))
       return rc;
     if (inc)
-      for (; inc_parted < x_rounds; inc_parted++)
+      for (; inc_parted < x_rounds && budget > 0; inc_parted++, budget--)
         if ((rc = inc_round(inc_parted))) return rc;
   }
+  if (inc)  // (what the budget left, and at finish all of it)
+    for (; inc_parted < x_rounds && budget > 0; inc_parted++, budget--)
+      if ((rc = inc_round(inc_parted))) return rc;
   if (all && !inc_tried && x_rounds >= 2) {
     if ((rc = inc_setup())) return rc;
     if (inc)
