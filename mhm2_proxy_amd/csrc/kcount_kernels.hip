@@ -143,7 +143,7 @@ __device__ void load_tile(const ReadsView &rv, uint32_t tile, uint32_t first_rea
     const int64_t gi = gA + g;
     // the group's read-start word first, so that its load is in flight with the bases' (issued after them it was
     // a second global round trip per tile: the bases' loads are waited for and decoded before it)
-    const uint32_t sw = tile_starts ? gload(tile_starts + (uint64_t)tile * NG + g) : 0u;
+    const uint32_t sw = tile_starts ? gload(tile_starts + (uint64_t)tile * (T / 32) + g) : 0u;
     uint64_t f = 0;
     uint32_t gd = 0;
     if (gi >= 0 && (uint64_t)gi * 32 < rv.n_bases) {
@@ -522,38 +522,18 @@ __global__ void k_tile_first_read(ReadsView rv, uint32_t *out, uint32_t n_tiles,
   out[t] = (uint32_t)a;
 }
 
-// Read-start bitmaps of the extraction tiles (what load_tile builds from the offsets: bit 31 - (d & 31) of word d >> 5
-// for a read start at tile-local position d of the kGroups<NL>() staged groups), one wave per tile. The extraction
-// then loads its tile's bitmap beside the bases instead of first loading the tile's first read and then the offsets
-// after it: two dependent global round trips per tile that four workgroups per CU did not hide. This kernel has the
-// same chain, but one wave per tile and little LDS, so many tiles are in flight.
-template <int NL>
-__global__ __launch_bounds__(256) void k_tile_starts(ReadsView rv, const uint32_t *tile_first, uint32_t *out,
-                                                     uint32_t n_tiles) {
-  constexpr int T = kTile<NL>(), NG = kGroups<NL>();
-  __shared__ uint32_t w[4][NG];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t tile = blockIdx.x * 4 + wv;
-  for (int g = lane; g < NG; g += 64) w[wv][g] = 0;
-  __syncthreads();
-  if (tile < n_tiles) {
-    const int64_t gA = (int64_t)tile * (T / 32) - 1;
-    const int64_t lo = gA * 32, hi = (gA + NG) * 32;
-    // (the tile's first read from k_tile_first_read: a 64-ary search across the wave here, four dependent loads per
-    // tile, made the tile-index stage 0.17 -> 0.23 ms)
-    const uint64_t first = tile_first[tile];
-    for (uint64_t r = first + lane; r <= rv.n_reads; r += 64) {
-      const int64_t s = (int64_t)(rv.offs[r] - rv.obase);
-      if (s >= hi) break;
-      if (s >= lo) {
-        const int64_t d = s - lo;
-        atomicOr(&w[wv][d >> 5], 1u << (31 - (d & 31)));
-      }
-    }
+// Read-start bits of a batch (or slice view), flat: bit 31 - (s & 31) of word (s >> 5) + 1 for every read start (and
+// the end) at position s from the view's base, on zeroed words; word 0 is the group left of position 0 (tile 0's
+// halo), so a tile's kGroups<NL>() staged groups are words [tile T / 32, tile T / 32 + kGroups) (load_tile). One atomic
+// per read: the extraction then loads its tile's start words beside the bases instead of first loading the tile's first
+// read and then the offsets after it, two dependent global round trips per tile. (The previous version, per-tile
+// bitmaps built by one wave per tile from a searched first read, took 37 + 87 us at C2.)
+__global__ __launch_bounds__(256) void k_read_start_bits(ReadsView rv, uint32_t *bits) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= rv.n_reads; r += stride) {
+    const uint64_t s = rv.offs[r] - rv.obase;
+    atomicOr(&bits[(s >> 5) + 1], 1u << (31 - (uint32_t)(s & 31)));
   }
-  __syncthreads();
-  if (tile < n_tiles)
-    for (int g = lane; g < NG; g += 64) out[(uint64_t)tile * NG + g] = w[wv][g];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3019,21 +2999,17 @@ hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_
   return hipGetLastError();
 }
 
-size_t tile_starts_words(int nl) {
-  return nl == 1 ? kGroups<1>() : nl == 2 ? kGroups<2>() : nl == 3 ? kGroups<3>() : kGroups<4>();
+uint64_t read_start_words(uint64_t n_tiles, int nl) {
+  const uint64_t T = nl == 1 ? kTile<1>() : nl == 2 ? kTile<2>() : nl == 3 ? kTile<3>() : kTile<4>();
+  const uint64_t NG = nl == 1 ? kGroups<1>() : nl == 2 ? kGroups<2>() : nl == 3 ? kGroups<3>() : kGroups<4>();
+  return n_tiles * (T / 32) + NG + 2;
 }
 
-hipError_t launch_tile_starts(const ReadsView &r, const uint32_t *tile_first, uint32_t *out, uint32_t n_tiles, int nl,
-                              hipStream_t s) {
-  if (!n_tiles) return hipSuccess;
-  const dim3 grid((n_tiles + 3) / 4), block(256);
-  switch (nl) {
-    case 1: k_tile_starts<1><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
-    case 2: k_tile_starts<2><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
-    case 3: k_tile_starts<3><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
-    case 4: k_tile_starts<4><<<grid, block, 0, s>>>(r, tile_first, out, n_tiles); break;
-    default: return hipErrorInvalidValue;
-  }
+hipError_t launch_read_start_bits(const ReadsView &r, uint32_t *bits, uint64_t n_words, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(bits, 0, n_words * 4, s);
+  if (e != hipSuccess) return e;
+  const uint64_t blocks = std::min<uint64_t>(4096, (r.n_reads + 1 + 255) / 256);
+  k_read_start_bits<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, bits);
   return hipGetLastError();
 }
 

@@ -44,7 +44,8 @@ struct ExtractParams {
   PlaneSet out;                     // (E-scatter)
   unsigned int *err;                // bit 0: input byte with code > 4
   unsigned int *ovf;                // bit 1: a capped bin of this slab overflowed (per slab)
-  const uint32_t *tile_starts;      // per tile: its read-start bitmap (k_tile_starts, kGroups words), or nullptr:
+  const uint32_t *tile_starts;      // the batch's flat read-start bits (k_read_start_bits; tile t's groups are words
+                                    // [t tile / 32, t tile / 32 + kGroups)), or nullptr:
                                     // load_tile builds it from the offsets
   uint32_t bin_lo, bin_hi;          // k_smer_extract: only records of coarse bins [bin_lo, bin_hi) are kept (a finish
                                     // pass over part of the hash range); 0, n_bins = all
@@ -280,10 +281,10 @@ static_assert(count_lds_bytes(1) <= C_LDS && count_lds_bytes(2) <= C_LDS && coun
               "k_count LDS budget");
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);
-// per extraction tile its read-start bitmap (tile_starts_words(nl) u32 per tile), from tile_first_read
-hipError_t launch_tile_starts(const ReadsView &r, const uint32_t *tile_first, uint32_t *out, uint32_t n_tiles, int nl,
-                              hipStream_t s);
-size_t tile_starts_words(int nl);
+// the batch's read-start bits for the extraction (read_start_words(n_tiles, nl) u32, zeroed here): ExtractParams
+// tile_starts
+hipError_t launch_read_start_bits(const ReadsView &r, uint32_t *bits, uint64_t n_words, hipStream_t s);
+uint64_t read_start_words(uint64_t n_tiles, int nl);
 // total counted windows sum(max(0, L - k - 1)) of a batch, added to *out; err bit 2 (4) when the offsets are
 // not a valid PackedReads CSR (offs[0] != 0, decreasing, a read longer than 65535, offs[n] != n_bases)
 hipError_t launch_count_windows(const ReadsView &r, int k, unsigned long long *out, unsigned int *err, hipStream_t s);

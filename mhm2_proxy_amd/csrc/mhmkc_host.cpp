@@ -716,15 +716,13 @@ int mhmkc::extract(Slab *sl, bool exact) {
   p.bin_hi = filt ? bhi : 0;
   uint64_t shift = 0;
   if (!sl->recv) {  // (the received supermers' tile index is made once by smer_exchange)
+    // the batch's read-start bits (k_read_start_bits: the extraction loads its tile's words beside the bases, no
+    // dependent round trip through the tile's first read)
     prof_begin(MHMKC_STAGE_TILEIDX);
-    e = mhm::launch_tile_first_read(sl->rv, d_tiles.as<uint32_t>(), sl->tiles, T, stream);
-    // the tiles' read-start bitmaps (k_tile_starts: one dependent global round trip fewer per extraction tile)
-    if (e == hipSuccess) {
-      const size_t words = (size_t)sl->tiles * mhm::tile_starts_words(nl);
-      if ((e = grow(d_tsb, words * 4 + 64)) == hipSuccess) {
-        e = mhm::launch_tile_starts(sl->rv, d_tiles.as<uint32_t>(), d_tsb.as<uint32_t>(), sl->tiles, nl, stream);
-        p.tile_starts = d_tsb.as<uint32_t>();
-      }
+    const uint64_t words = mhm::read_start_words(sl->tiles, nl);
+    if ((e = grow(d_tsb, words * 4 + 64)) == hipSuccess) {
+      e = mhm::launch_read_start_bits(sl->rv, d_tsb.as<uint32_t>(), words, stream);
+      p.tile_starts = d_tsb.as<uint32_t>();
     }
     prof_end();
     if (e != hipSuccess) return hip_fail(e, "tile index");
