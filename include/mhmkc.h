@@ -137,6 +137,7 @@ typedef struct {
   double ms_h2d_pack;         /* last mhmkc_add_reads: host wall time packing its chunks for the wire (nibble H2D) */
   double ms_h2d_wait;         /* ... host wall time waiting for a pinned staging slot's previous copy */
   double ms_h2d_rounds;       /* ... host wall time enqueueing local rounds between its chunks (mhmkc_debug.h) */
+  uint64_t h2d_raw_chunks;    /* ... its chunks sent as PackedRead bytes (the wire had drained while the host packed) */
 } mhmkc_stats;
 
 enum {

@@ -125,6 +125,7 @@ class MhmkcStats(C.Structure):
         ("ms_h2d_pack", C.c_double),
         ("ms_h2d_wait", C.c_double),
         ("ms_h2d_rounds", C.c_double),
+        ("h2d_raw_chunks", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -60,6 +60,7 @@ struct DebugKnobs {
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
   int64_t h2d_threads = 0;   // nibble H2D: worker threads that pack (0: all)
   int64_t h2d_nt = 1;        // nibble H2D: streaming stores into the staging (0: ordinary stores)
+  int64_t h2d_adapt = 1;     // nibble H2D: 1 a chunk goes raw when the wire drained, 0 never, 2 every other chunk
   int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
@@ -1006,8 +1007,17 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     if ((e = b->ensure(slot)) != hipSuccess) return hip_fail(e, "pinned staging");
   bool stage_used[2] = {false, false};
   double pack_ms = 0, wait_ms = 0, rounds_ms = 0;
-  const bool deltas = g_dbg.h2d_nib != 2;
-  const int TP = g_dbg.h2d_threads > 0 ? (int)std::min<int64_t>(T, g_dbg.h2d_threads) : T;  // threads that pack  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
+  const bool deltas = g_dbg.h2d_nib != 2;  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
+  const int TP = g_dbg.h2d_threads > 0 ? (int)std::min<int64_t>(T, g_dbg.h2d_threads) : T;  // threads that pack
+  // A chunk goes as it is (PackedRead bytes straight from the caller's buffer) when the wire has drained while the
+  // host was packing: on a host that packs slower than the copy runs, raw and packed chunks then share the work
+  // between the wire and the host. Only from pinned memory (a pageable copy would hold the host).
+  hipPointerAttribute_t pa{};
+  const bool user_pinned = hipPointerGetAttributes(&pa, bytes) == hipSuccess && pa.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  const int adapt = user_pinned ? (int)g_dbg.h2d_adapt : 0;  // 1: when drained, 2: every other chunk (tests)
+  hipEvent_t last_copy = nullptr;  // the event after the newest chunk's copies
+  uint64_t raw_chunks = 0;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto ms_since = [](std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1045,6 +1055,8 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     uint8_t *stage = sl.p[s]->as<uint8_t>();
     uint32_t *sdelta = (uint32_t *)(stage + dof);
     const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
+    // (the first chunk too: nothing is on the wire yet, and the next chunk is packed while it is)
+    const bool raw = adapt == 2 ? (ci & 1) != 0 : adapt == 1 && (!last_copy || hipEventQuery(last_copy) == hipSuccess);
     std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX), t_rest(T, 0);
     // (the second chunk's run also counts the windows of the reads after it: the local rounds' expected total)
     const bool announce = lrounds && ci == 1;
@@ -1081,7 +1093,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
       // bases [b0 + x, b0 + y) of an x that is a multiple of 64: nibbles from the 32-byte aligned byte x / 2 of the slot
       const uint64_t per = ((nb + packers - 1) / packers + 63) & ~63ull, x = std::min(nb, per * u),
                      y = std::min(nb, x + per);
-      if (y > x) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut, g_dbg.h2d_nt != 0);
+      if (y > x && !raw) nib_pack(bytes + b0 + x, y - x, stage + x / 2, qcut, g_dbg.h2d_nt != 0);
       if (announce) {
         const uint64_t rest = n_reads - r1, qa = r1 + rest * u / U, qb = r1 + rest * (u + 1) / U;
         uint64_t wr = 0;
@@ -1111,16 +1123,19 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
       inc_expect += rest;
       inc_announced += rest;
     }
-    const uint64_t nbytes = (nb + 1) / 2;
+    const uint64_t nbytes = raw ? nb : (nb + 1) / 2;
     uint8_t *dslot = d_nib[ds].as<uint8_t>();
     if (nib_used[ds] && (e = hipStreamWaitEvent(copy_stream, nib_ev[ds], 0)) != hipSuccess)
       return hip_fail(e, "copy stream");
-    if ((nb && (e = hipMemcpyAsync(dslot, stage, nbytes, hipMemcpyHostToDevice, copy_stream)) != hipSuccess) ||
+    if ((nb && !raw && (e = hipMemcpyAsync(dslot, stage, nbytes, hipMemcpyHostToDevice, copy_stream)) != hipSuccess) ||
+        (nb && raw && (e = hipMemcpyAsync(db + b0, bytes + b0, nb, hipMemcpyHostToDevice, copy_stream)) != hipSuccess) ||
         (deltas && (e = hipMemcpyAsync(dslot + dof, sdelta, 4 * (nr + 1), hipMemcpyHostToDevice, copy_stream)) != hipSuccess) ||
         (e = hipEventRecord(stage_ev[s], copy_stream)) != hipSuccess ||
         (!deltas && (e = hipMemcpyAsync(dofs + r0, offs + r0, (nr + 1) * 8, hipMemcpyHostToDevice, copy_stream)) != hipSuccess))
       return hip_fail(e, "input H2D");
     stage_used[s] = true;
+    last_copy = stage_ev[s];
+    raw_chunks += raw;
     if (n_ev == chunk_ev.size()) {
       hipEvent_t ev = nullptr;
       if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "event");
@@ -1129,7 +1144,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     hipEvent_t ev = chunk_ev[n_ev++];
     if ((e = hipEventRecord(ev, copy_stream)) != hipSuccess || (e = hipStreamWaitEvent(stream, ev, 0)) != hipSuccess)
       return hip_fail(e, "chunk event");
-    if ((e = mhm::launch_expand_nibbles(dslot, db, b0, nb, stream)) != hipSuccess ||
+    if ((!raw && (e = mhm::launch_expand_nibbles(dslot, db, b0, nb, stream)) != hipSuccess) ||
         (deltas && (e = mhm::launch_offs_from_deltas((const uint32_t *)(dslot + dof), dofs + r0, nr + 1, b0, stream)) != hipSuccess) ||
         (e = hipEventRecord(nib_ev[ds], stream)) != hipSuccess)
       return hip_fail(e, "nibble expansion");
@@ -1160,6 +1175,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   st.ms_h2d_pack = pack_ms;
   st.ms_h2d_wait = wait_ms;
   st.ms_h2d_rounds = rounds_ms;
+  st.h2d_raw_chunks = raw_chunks;
   return MHMKC_OK;
 }
 
@@ -3908,6 +3924,7 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
   else if (k == "local_rounds") g_dbg.local_rounds = value;
   else if (k == "h2d_threads") g_dbg.h2d_threads = value;
   else if (k == "h2d_nt") g_dbg.h2d_nt = value;
+  else if (k == "h2d_adapt") g_dbg.h2d_adapt = value;
   else if (k == "cb0") g_dbg.cb0[1] = value;
   else if (k == "cb0_2") g_dbg.cb0[2] = value;
   else if (k == "cb0_3") g_dbg.cb0[3] = value;

@@ -441,6 +441,29 @@ def test_host_local_rounds_hot_kmer_redo(knob):
     assert_tables_equal(got, oracle_table(b, o, 21), "local rounds, hot k-mer")
 
 
+@pytest.mark.parametrize("adapt", [1, 2])
+def test_host_nibbles_mixed_raw_chunks(adapt, knob):
+    """From pinned host memory a chunk goes as PackedRead bytes when the wire has drained while the host packed
+    (h2d_adapt 1; 2 forces every other chunk): raw and nibble chunks in one batch, odd chunk boundaries, every quality,
+    give the oracle's table."""
+    torch = pytest.importorskip("torch")
+    b, o = synth_set(3000, 20000, 75)
+    rng = np.random.default_rng(76)
+    b = ((b & 7) | (rng.integers(0, 32, b.size, dtype=np.uint8) << 3)).astype(np.uint8)
+    hb = torch.from_numpy(b).pin_memory().numpy()
+    knob("chunk_bytes", 7001)
+    knob("h2d_nib", 1)
+    knob("h2d_adapt", adapt)
+    with m.KmerCounter(21) as c:
+        c.add_packed_reads(hb, o)
+        c.finish()
+        got, st = c.fetch(), c.stats()
+    assert st["h2d_raw_chunks"] >= (st["h2d_chunks"] // 2 if adapt == 2 else 1), (st["h2d_raw_chunks"], st["h2d_chunks"])
+    if adapt == 2:
+        assert st["h2d_raw_chunks"] < st["h2d_chunks"]
+    assert_tables_equal(got, oracle_table(b, o, 21), f"raw and nibble chunks, adapt={adapt}")
+
+
 def test_host_nibbles_bad_code_reported(knob):
     """A byte with code 5-7 sent as a nibble still reaches the device's input check (error, no table)."""
     b, o = synth_set(200, 5000, 72)
