@@ -523,16 +523,33 @@ __global__ void k_tile_first_read(ReadsView rv, uint32_t *out, uint32_t n_tiles,
 }
 
 // Read-start bits of a batch (or slice view), flat: bit 31 - (s & 31) of word (s >> 5) + 1 for every read start (and
-// the end) at position s from the view's base, on zeroed words; word 0 is the group left of position 0 (tile 0's
-// halo), so a tile's kGroups<NL>() staged groups are words [tile T / 32, tile T / 32 + kGroups) (load_tile). One atomic
-// per read: the extraction then loads its tile's start words beside the bases instead of first loading the tile's first
-// read and then the offsets after it, two dependent global round trips per tile. (The previous version, per-tile
-// bitmaps built by one wave per tile from a searched first read, took 37 + 87 us at C2.)
-__global__ __launch_bounds__(256) void k_read_start_bits(ReadsView rv, uint32_t *bits) {
+// the end) at position s from the view's base; word 0 is the group left of position 0 (tile 0's halo), so a tile's
+// kGroups<NL>() staged groups are words [tile T / 32, tile T / 32 + kGroups) (load_tile). The extraction then loads its
+// tile's start words beside the bases instead of first loading the tile's first read and then the offsets after it,
+// two dependent global round trips per tile. Every word is written once, by the read that starts first in it or whose
+// start precedes it: thread r writes its start's word (with the bits of the later reads starting in it) and zeros up
+// to the next start's word; the first read also the words before its own, the end the words after. (Per-tile bitmaps
+// by one wave per tile from a searched first read took 37 + 87 us at C2; a zeroed array and one atomicOr per read
+// 26 + 118 us.)
+__global__ __launch_bounds__(256) void k_read_start_bits(ReadsView rv, uint32_t *bits, uint64_t n_words) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= rv.n_reads; r += stride) {
-    const uint64_t s = rv.offs[r] - rv.obase;
-    atomicOr(&bits[(s >> 5) + 1], 1u << (31 - (uint32_t)(s & 31)));
+    const uint64_t s = rv.offs[r] - rv.obase, w = (s >> 5) + 1;
+    if (r > 0 && ((rv.offs[r - 1] - rv.obase) >> 5) + 1 == w) continue;  // an earlier read starts in this word
+    uint32_t v = 1u << (31 - (uint32_t)(s & 31));
+    uint64_t wn = n_words;  // the next word holding a start
+    for (uint64_t q = r + 1; q <= rv.n_reads; q++) {
+      const uint64_t sq = rv.offs[q] - rv.obase, wq = (sq >> 5) + 1;
+      if (wq != w) {
+        wn = wq;
+        break;
+      }
+      v |= 1u << (31 - (uint32_t)(sq & 31));
+    }
+    bits[w] = v;
+    for (uint64_t x = w + 1; x < wn; x++) bits[x] = 0;
+    if (r == 0)
+      for (uint64_t x = 0; x < w; x++) bits[x] = 0;
   }
 }
 
@@ -3006,10 +3023,8 @@ uint64_t read_start_words(uint64_t n_tiles, int nl) {
 }
 
 hipError_t launch_read_start_bits(const ReadsView &r, uint32_t *bits, uint64_t n_words, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(bits, 0, n_words * 4, s);
-  if (e != hipSuccess) return e;
-  const uint64_t blocks = std::min<uint64_t>(4096, (r.n_reads + 1 + 255) / 256);
-  k_read_start_bits<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, bits);
+  const uint64_t blocks = std::min<uint64_t>(8192, (r.n_reads + 1 + 255) / 256);
+  k_read_start_bits<<<dim3((unsigned)blocks), dim3(256), 0, s>>>(r, bits, n_words);
   return hipGetLastError();
 }
 

@@ -281,8 +281,8 @@ static_assert(count_lds_bytes(1) <= C_LDS && count_lds_bytes(2) <= C_LDS && coun
               "k_count LDS budget");
 
 hipError_t launch_tile_first_read(const ReadsView &r, uint32_t *out, uint32_t n_tiles, int tile, hipStream_t s);
-// the batch's read-start bits for the extraction (read_start_words(n_tiles, nl) u32, zeroed here): ExtractParams
-// tile_starts
+// the batch's read-start bits for the extraction (read_start_words(n_tiles, nl) u32, every word written):
+// ExtractParams tile_starts
 hipError_t launch_read_start_bits(const ReadsView &r, uint32_t *bits, uint64_t n_words, hipStream_t s);
 uint64_t read_start_words(uint64_t n_tiles, int nl);
 // total counted windows sum(max(0, L - k - 1)) of a batch, added to *out; err bit 2 (4) when the offsets are
