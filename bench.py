@@ -526,7 +526,7 @@ def main():
         hb = torch.from_numpy(b).pin_memory().numpy()
         ho = torch.from_numpy(o.view(np.int64)).pin_memory().numpy().view(np.uint64)
         counter.set_profiling(False)
-        ts, h2d_ms, pack_ms = [], [], []
+        ts, h2d_ms, pack_ms, raw_chunks = [], [], [], []
         for i in range(args.h2d_steps + 3):
             if dist:
                 dist.barrier()
@@ -545,12 +545,13 @@ def main():
                 ts.append(dt)
                 h2d_ms.append(counter.stats()["ms_h2d"])
                 pack_ms.append(counter.stats()["ms_h2d_pack"])
+                raw_chunks.append(counter.stats()["h2d_raw_chunks"])
         tmed = sorted(ts)[len(ts) // 2]
         stt = counter.stats()
         hbytes = stt["h2d_bytes"]
         h2d = {"value": round(occ_total / steps * 1.0 / tmed, 1), "unit": "k-mers/s", "ms_per_step": round(tmed * 1e3, 3),
                "h2d_ms": round(sorted(h2d_ms)[len(h2d_ms) // 2], 3), "h2d_bytes_per_gpu": int(hbytes),
-               "host_pack_ms": round(sorted(pack_ms)[len(pack_ms) // 2], 3),
+               "host_pack_ms": round(sorted(pack_ms)[len(pack_ms) // 2], 3), "raw_chunks_per_step": raw_chunks,
                "h2d_GBps": round(hbytes / (sorted(h2d_ms)[len(h2d_ms) // 2] * 1e-3) / 1e9, 1) if h2d_ms[0] else None,
                "chunks": int(stt["h2d_chunks"]), "steps": len(ts), "warmup": 3, "statistic": "median",
                "input": "PackedRead bytes + offsets in pinned host memory (torch pin_memory)",

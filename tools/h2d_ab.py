@@ -56,13 +56,13 @@ def main():
             assert sig == ref, (cfg, sig, ref)
             if rep >= 2:
                 res[cfg].append((dt, st["ms_h2d"], st["h2d_bytes"], st["h2d_chunks"], st["ms_h2d_pack"],
-                                 st["ms_h2d_wait"], st["inc_rounds"], st["ms_finish_tail"], st["ms_h2d_rounds"]))
+                                 st["ms_h2d_wait"], st["inc_rounds"], st["ms_finish_tail"], st["ms_h2d_rounds"], st["h2d_raw_chunks"]))
     N.debug_reset()
     for cfg, rows in res.items():
         rows.sort()
-        dt, h2d, hb_, ch, pk, wt, ir, tail, rms = rows[len(rows) // 2]
+        dt, h2d, hb_, ch, pk, wt, ir, tail, rms, raw = rows[len(rows) // 2]
         print(f"k={k} [{cfg}]: window {dt:.2f} ms (min {rows[0][0]:.2f})  copy span {h2d:.2f} ms  "
-              f"{hb_ / 1e9:.3f} GB in {ch} chunks ({hb_ / h2d / 1e6:.1f} GB/s)  host packing {pk:.2f} ms  "
+              f"{hb_ / 1e9:.3f} GB in {ch} chunks, {raw} raw ({hb_ / h2d / 1e6:.1f} GB/s)  host packing {pk:.2f} ms  "
               f"slot waits {wt:.2f} ms  rounds partitioned as they landed {ir} (host {rms:.2f} ms)  "
               f"finish tail {tail:.2f} ms  "
               f"n_out={ref[0]}", flush=True)
