@@ -1009,15 +1009,17 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   double pack_ms = 0, wait_ms = 0, rounds_ms = 0;
   const bool deltas = g_dbg.h2d_nib != 2;  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
   const int TP = g_dbg.h2d_threads > 0 ? (int)std::min<int64_t>(T, g_dbg.h2d_threads) : T;  // threads that pack
-  // A chunk goes as it is (PackedRead bytes straight from the caller's buffer) when the wire has drained while the
-  // host was packing: on a host that packs slower than the copy runs, raw and packed chunks then share the work
-  // between the wire and the host. Only from pinned memory (a pageable copy would hold the host).
+  // A chunk goes as it is (PackedRead bytes straight from the caller's buffer) when the wire drained while the host
+  // packed the chunk before: on a host that packs slower than the copy runs, raw and packed chunks then alternate and
+  // share the work between the wire and the host. The first chunk goes raw (nothing is on the wire yet; the next one
+  // is packed meanwhile). Only from pinned memory (a pageable copy would hold the host).
   hipPointerAttribute_t pa{};
   const bool user_pinned = hipPointerGetAttributes(&pa, bytes) == hipSuccess && pa.type == hipMemoryTypeHost;
   (void)hipGetLastError();
   const int adapt = user_pinned ? (int)g_dbg.h2d_adapt : 0;  // 1: when drained, 2: every other chunk (tests)
   hipEvent_t last_copy = nullptr;  // the event after the newest chunk's copies
   uint64_t raw_chunks = 0;
+  bool raw_next = adapt == 1;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto ms_since = [](std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1055,8 +1057,7 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     uint8_t *stage = sl.p[s]->as<uint8_t>();
     uint32_t *sdelta = (uint32_t *)(stage + dof);
     const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
-    // (the first chunk too: nothing is on the wire yet, and the next chunk is packed while it is)
-    const bool raw = adapt == 2 ? (ci & 1) != 0 : adapt == 1 && (!last_copy || hipEventQuery(last_copy) == hipSuccess);
+    const bool raw = adapt == 2 ? (ci & 1) != 0 : raw_next;
     std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX), t_rest(T, 0);
     // (the second chunk's run also counts the windows of the reads after it: the local rounds' expected total)
     const bool announce = lrounds && ci == 1;
@@ -1106,6 +1107,8 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     });
     pack_ms += ms_since(tp);
     if (rounds_rc) return rounds_rc;
+    // (packed, and the previous chunk's copies ended meanwhile: the wire waits for the host, the next chunk goes raw)
+    raw_next = adapt == 1 && !raw && last_copy && hipEventQuery(last_copy) == hipSuccess;
     uint64_t wins = 0;
     for (int t = 0; t < T; t++) {
       if (t_bad[t] != UINT64_MAX) {
