@@ -1009,17 +1009,18 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   double pack_ms = 0, wait_ms = 0, rounds_ms = 0;
   const bool deltas = g_dbg.h2d_nib != 2;  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
   const int TP = g_dbg.h2d_threads > 0 ? (int)std::min<int64_t>(T, g_dbg.h2d_threads) : T;  // threads that pack
-  // A chunk goes as it is (PackedRead bytes straight from the caller's buffer) when the wire drained while the host
-  // packed the chunk before: on a host that packs slower than the copy runs, raw and packed chunks then alternate and
-  // share the work between the wire and the host. The first chunk goes raw (nothing is on the wire yet; the next one
-  // is packed meanwhile). Only from pinned memory (a pageable copy would hold the host).
+  // A chunk goes as it is (PackedRead bytes straight from the caller's buffer, twice the wire time, no host time) when
+  // that ends the call sooner: per chunk the choice that keeps max(host time, wire time) so far smaller, with the
+  // host's packing rate measured on the chunks it packed and the wire at WIRE_BPMS. A host that packs faster than the
+  // wire runs never sends one raw; a host at half that rate about one chunk in three. Only from pinned memory (a
+  // pageable copy would hold the host).
   hipPointerAttribute_t pa{};
   const bool user_pinned = hipPointerGetAttributes(&pa, bytes) == hipSuccess && pa.type == hipMemoryTypeHost;
   (void)hipGetLastError();
   const int adapt = user_pinned ? (int)g_dbg.h2d_adapt : 0;  // 1: when drained, 2: every other chunk (tests)
-  hipEvent_t last_copy = nullptr;  // the event after the newest chunk's copies
+  constexpr double WIRE_BPMS = 54e6;  // PCIe bytes per ms (the byte wire's measured 54-55 GB/s)
+  double host_t = 0, wire_t = 0, packed_b = 0;  // the call's packing and (modelled) wire time so far, bytes packed
   uint64_t raw_chunks = 0;
-  bool raw_next = adapt == 1;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto ms_since = [](std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1057,7 +1058,11 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     uint8_t *stage = sl.p[s]->as<uint8_t>();
     uint32_t *sdelta = (uint32_t *)(stage + dof);
     const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
-    const bool raw = adapt == 2 ? (ci & 1) != 0 : raw_next;
+    bool raw = adapt == 2 && (ci & 1) != 0;
+    if (adapt == 1 && packed_b > 0) {
+      const double p_est = host_t / packed_b * (double)nb, c_nib = (double)nb / 2 / WIRE_BPMS;
+      raw = std::max(host_t, wire_t + 2 * c_nib) < std::max(host_t + p_est, wire_t + c_nib);
+    }
     std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX), t_rest(T, 0);
     // (the second chunk's run also counts the windows of the reads after it: the local rounds' expected total)
     const bool announce = lrounds && ci == 1;
@@ -1105,10 +1110,14 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
         t_rest[t] = wr;
       }
     });
-    pack_ms += ms_since(tp);
+    const double run_ms = ms_since(tp);
+    pack_ms += run_ms;
     if (rounds_rc) return rounds_rc;
-    // (packed, and the previous chunk's copies ended meanwhile: the wire waits for the host, the next chunk goes raw)
-    raw_next = adapt == 1 && !raw && last_copy && hipEventQuery(last_copy) == hipSuccess;
+    wire_t += (double)nb / (raw ? 1 : 2) / WIRE_BPMS;
+    if (!raw) {
+      host_t += run_ms;
+      packed_b += (double)nb;
+    }
     uint64_t wins = 0;
     for (int t = 0; t < T; t++) {
       if (t_bad[t] != UINT64_MAX) {
@@ -1137,7 +1146,6 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
         (!deltas && (e = hipMemcpyAsync(dofs + r0, offs + r0, (nr + 1) * 8, hipMemcpyHostToDevice, copy_stream)) != hipSuccess))
       return hip_fail(e, "input H2D");
     stage_used[s] = true;
-    last_copy = stage_ev[s];
     raw_chunks += raw;
     if (n_ev == chunk_ev.size()) {
       hipEvent_t ev = nullptr;
