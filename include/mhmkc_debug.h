@@ -38,6 +38,11 @@ extern "C" {
 int mhmkc_debug_set(const char *knob, int64_t value);
 /* Every knob back to its default. */
 void mhmkc_debug_reset(void);
+/* The nibble H2D's host packing (no GPU): n PackedRead bytes of src as (n + 1) / 2 bytes of nibbles
+ * code | (q >= qcut) << 3 into dst, the first in the low half; mode 0 as mhmkc_add_reads packs (AVX2 when the CPU has
+ * it, streaming stores into a 32-byte aligned dst), 1 the portable 8-bytes-at-a-time path, 2 AVX2 with ordinary stores
+ * (MHMKC_EUNSUPPORTED without AVX2). */
+int mhmkc_debug_nib_pack(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut, int mode);
 
 #ifdef __cplusplus
 }

@@ -49,7 +49,7 @@ ABI_SYMBOLS = [
 ]
 SYNTH_SYMBOLS = ["mhmkc_synth_config_init", "mhmkc_synth_genome", "mhmkc_synth_reads"]
 # the test-only entry point (include/mhmkc_debug.h)
-DEBUG_SYMBOLS = ["mhmkc_debug_reset", "mhmkc_debug_set"]
+DEBUG_SYMBOLS = ["mhmkc_debug_nib_pack", "mhmkc_debug_reset", "mhmkc_debug_set"]
 
 
 class MhmkcConfig(C.Structure):
@@ -229,6 +229,7 @@ def lib() -> C.CDLL:
     L.mhmkc_debug_set.argtypes = [C.c_char_p, C.c_int64]
     L.mhmkc_debug_reset.argtypes = []
     L.mhmkc_debug_reset.restype = None
+    L.mhmkc_debug_nib_pack.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.c_int]
     L.mhmkc_device_output.argtypes = [VP, P(VP), P(VP), P(VP), P(VP), P(U64)]
     L.mhmkc_get_stats.argtypes = [VP, P(MhmkcStats)]
     L.mhmkc_reset.argtypes = [VP]

@@ -3945,4 +3945,19 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
 
 void mhmkc_debug_reset(void) { g_dbg = DebugKnobs(); }
 
+int mhmkc_debug_nib_pack(const uint8_t *src, uint64_t n, uint8_t *dst, int qcut, int mode) {
+  if ((!src || !dst) && n) return MHMKC_EINVAL;
+  if (mode == 0) {
+    nib_pack(src, n, dst, qcut);
+  } else if (mode == 1) {
+    nib_pack_swar(src, n, dst, qcut);
+  } else if (mode == 2) {
+    if (!__builtin_cpu_supports("avx2")) return MHMKC_EUNSUPPORTED;
+    nib_pack_avx2(src, n, dst, qcut, false);
+  } else {
+    return MHMKC_EINVAL;
+  }
+  return MHMKC_OK;
+}
+
 }  // extern "C"

@@ -102,3 +102,32 @@ def test_mixed_record_bijection_and_flatness(tmp_path):
         coarse, fine, group = float(r[3]), float(r[5]), float(r[7])
         # 256 coarse bins of ~7800 windows, up to 2^17 fine bins of ~15 (Poisson max), 1000 groups of 2000
         assert coarse < 1.08 and group < 1.12 and fine < 3.0, r
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_nibble_packing(mode):
+    """The nibble H2D's host packing (mhmkc_host.cpp nib_pack) against a numpy restatement: every
+    byte value, odd lengths and unaligned starts, cutoffs across [0, 32]; two nibbles per byte, the first low."""
+    import ctypes as C
+
+    from mhm2_proxy_amd import _native as N
+
+    rng = np.random.default_rng(mode + 11)
+    for n, off, qcut in [(0, 0, 20), (1, 0, 20), (7, 3, 0), (63, 0, 1), (64, 0, 31), (65, 5, 32), (1000, 32, 20),
+                         (4099, 1, 19), (100_000, 0, 20), (100_001, 17, 7)]:
+        buf = np.zeros(n + 64, np.uint8)
+        src = buf[off:off + n]
+        src[:] = rng.integers(0, 256, n, dtype=np.uint8)
+        if n >= 256:
+            src[:256] = np.arange(256, dtype=np.uint8)
+        out = np.full((n + 1) // 2 + 64, 0xAB, np.uint8)
+        rc = N.lib().mhmkc_debug_nib_pack(src.ctypes.data, n, out.ctypes.data, qcut, mode)
+        if rc == -7 and mode == 2:  # MHMKC_EUNSUPPORTED: no AVX2 on this CPU
+            pytest.skip("no AVX2")
+        assert rc == 0
+        nib = (src & 7) | np.where((src >> 3) >= min(max(qcut, 0), 32), 8, 0).astype(np.uint8)
+        if n & 1:
+            nib = np.concatenate([nib, np.zeros(1, np.uint8)])
+        exp = (nib[0::2] | (nib[1::2] << 4)).astype(np.uint8)
+        assert np.array_equal(out[:(n + 1) // 2], exp), (n, off, qcut)
+        assert (out[(n + 1) // 2:] == 0xAB).all()  # nothing written past the packed bytes
