@@ -28,8 +28,6 @@ extern "C" {
  *   h2d_nib       H2D of a host batch (mhmkc_add_reads): 1 the bases as nibbles and the offsets as u32 distances, 2
  *                 nibbles and u64 offsets, 0 PackedRead bytes and u64 offsets, -1 (default) 1 when the process has at
  *                 least 4 host threads, else 0
- *   local_pieces  one rank with local rounds: a device batch is cut into this many slabs, each fine-partitioned while
- *                 the later ones are extracted (0: one slab)
  *   h2d_threads   nibble H2D: host worker threads that pack the bases (0: all of them)
  *   h2d_nt        nibble H2D: 0 ordinary stores into the pinned staging instead of streaming stores
  *   h2d_adapt     nibble H2D from pinned memory: 1 (default) a chunk goes as PackedRead bytes when the copies have

@@ -61,7 +61,6 @@ struct DebugKnobs {
   int64_t h2d_threads = 0;   // nibble H2D: worker threads that pack (0: all)
   int64_t h2d_nt = 1;        // nibble H2D: streaming stores into the staging (0: ordinary stores)
   int64_t h2d_adapt = 1;     // nibble H2D: 1 a chunk goes raw when the wire drained, 0 never, 2 every other chunk
-  int64_t local_pieces = 0;  // one rank, local rounds: a device batch cut into this many slabs (0, 1: one slab)
   int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
@@ -3150,11 +3149,8 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_
   if (n_reads == 0) return MHMKC_OK;
   if (n_reads >= 0xffffffffull) return h->fail(MHMKC_EINVAL, "at most 2^32-2 reads per batch");
   h->qcut_pending = h->cfg.qual_cutoff;
-  // (one rank with local rounds: g_dbg.local_pieces slabs, each fine-partitioned on pstream while the later ones are
-  // extracted)
-  const bool lpieces = !h->xpipe && h->lrounds && g_dbg.local_pieces > 1;
-  const uint64_t P = lpieces ? (uint64_t)g_dbg.local_pieces : (uint64_t)h->xpieces;
-  if ((h->xpipe || lpieces) && P > 1 && n_reads >= 64 * P) {
+  const uint64_t P = (uint64_t)h->xpieces;
+  if (h->xpipe && P > 1 && n_reads >= 64 * P) {
     // pipelined exchange: the batch as xpieces slabs of whole reads, so that each one's round overlaps the next
     // one's extraction (the cut points' offsets come from the device)
     std::vector<uint64_t> cut(P + 1);
@@ -3204,10 +3200,8 @@ int mhmkc_add_reads_device(mhmkc_t h, const uint8_t *d_bytes, const uint64_t *d_
     for (uint64_t w : wins) tot += w;
     h->inc_expect += tot;
     h->inc_announced += tot;
-    for (uint64_t i = 0; i < P; i++) {
+    for (uint64_t i = 0; i < P; i++)
       if ((rc = h->add_view(rvs[i], wins[i], true))) return rc;
-      if (lpieces && (rc = h->local_rounds(false))) return rc;
-    }
     return MHMKC_OK;
   }
   mhm::ReadsView rv{d_bytes, d_offs, n_reads, n_bases, 0, 0, 0};
@@ -3939,7 +3933,6 @@ int mhmkc_debug_set(const char *knob, int64_t value) {
   else if (k == "d2h_chunk") g_dbg.d2h_chunk = value;
   else if (k == "h2d_nib") g_dbg.h2d_nib = value;
   else if (k == "local_rounds") g_dbg.local_rounds = value;
-  else if (k == "local_pieces") g_dbg.local_pieces = value;
   else if (k == "h2d_threads") g_dbg.h2d_threads = value;
   else if (k == "h2d_nt") g_dbg.h2d_nt = value;
   else if (k == "h2d_adapt") g_dbg.h2d_adapt = value;
