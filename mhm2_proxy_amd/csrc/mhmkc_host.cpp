@@ -60,7 +60,7 @@ struct DebugKnobs {
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
   int64_t h2d_threads = 0;   // nibble H2D: worker threads that pack (0: all)
   int64_t h2d_nt = 1;        // nibble H2D: streaming stores into the staging (0: ordinary stores)
-  int64_t h2d_adapt = 1;     // nibble H2D: 1 a chunk goes raw when the wire drained, 0 never, 2 every other chunk
+  int64_t h2d_adapt = 0;     // nibble H2D from pinned memory: 1 raw chunks by the host/wire model, 0 never, 2 every other
   int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
