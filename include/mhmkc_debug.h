@@ -30,8 +30,8 @@ extern "C" {
  *                 least 4 host threads, else 0
  *   h2d_threads   nibble H2D: host worker threads that pack the bases (0: all of them)
  *   h2d_nt        nibble H2D: 0 ordinary stores into the pinned staging instead of streaming stores
- *   h2d_adapt     nibble H2D from pinned memory: 1 a chunk goes as PackedRead bytes when a host/wire time model says
- *                 that ends the call sooner, 0 (default) never, 2 every other chunk
+ *   h2d_adapt     nibble H2D from pinned memory: 1 (default) some chunks go as PackedRead bytes when the host packs
+ *                 much slower than the wire runs, 0 never, 2 every other chunk
  *   local_rounds  0: one rank's host batches are fine-partitioned at finish, not chunk by chunk as they land (created
  *                 handles)
  *   cb0, cb0_2, cb0_3  coarse bits for one-, two-, three/four-word keys (0: 8, 8, 7) */

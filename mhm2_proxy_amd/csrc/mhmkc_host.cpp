@@ -60,7 +60,8 @@ struct DebugKnobs {
   int64_t d2h_chunk = 0;      // staging chunk of a D2H into pageable memory (0: 8 MB)
   int64_t h2d_threads = 0;   // nibble H2D: worker threads that pack (0: all)
   int64_t h2d_nt = 1;        // nibble H2D: streaming stores into the staging (0: ordinary stores)
-  int64_t h2d_adapt = 0;     // nibble H2D from pinned memory: 1 raw chunks by the host/wire model, 0 never, 2 every other
+  int64_t h2d_adapt = 1;     // nibble H2D from pinned memory: 1 raw chunks on a slow host (the model in add_host_nib), 0
+                             // never, 2 every other chunk
   int64_t local_rounds = 1;  // one rank: host batches' chunks fine-partitioned as they land (created handles; 0: at finish)
   int64_t h2d_nib = -1;       // H2D of a host batch: 1 nibbles + u32 offsets, 2 nibbles + u64 offsets, 0 the PackedRead
                               // bytes, -1 1 with >= 4 host threads, else 0
@@ -1009,17 +1010,16 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
   double pack_ms = 0, wait_ms = 0, rounds_ms = 0;
   const bool deltas = g_dbg.h2d_nib != 2;  // (2: the offsets as they are, u64, from the caller's buffer; A/B runs)
   const int TP = g_dbg.h2d_threads > 0 ? (int)std::min<int64_t>(T, g_dbg.h2d_threads) : T;  // threads that pack
-  // A chunk goes as it is (PackedRead bytes straight from the caller's buffer, twice the wire time, no host time) when
-  // that ends the call sooner: per chunk the choice that keeps max(host time, wire time) so far smaller, with the
-  // host's packing rate measured on the chunks it packed and the wire at WIRE_BPMS. A host that packs faster than the
-  // wire runs never sends one raw; a host at half that rate about one chunk in three. Only from pinned memory (a
+  // A chunk can go as it is (PackedRead bytes straight from the caller's buffer: twice the wire time, no host time) on
+  // a host that packs much slower than the wire runs (see below; the wire at WIRE_BPMS). Only from pinned memory (a
   // pageable copy would hold the host).
   hipPointerAttribute_t pa{};
   const bool user_pinned = hipPointerGetAttributes(&pa, bytes) == hipSuccess && pa.type == hipMemoryTypeHost;
   (void)hipGetLastError();
   const int adapt = user_pinned ? (int)g_dbg.h2d_adapt : 0;  // 1: when drained, 2: every other chunk (tests)
   constexpr double WIRE_BPMS = 54e6;  // PCIe bytes per ms (the byte wire's measured 54-55 GB/s)
-  double host_t = 0, wire_t = 0, packed_b = 0;  // the call's packing and (modelled) wire time so far, bytes packed
+  double host_t = 0, packed_b = 0;  // the call's packing time and bytes packed so far
+  double raw_acc = 0;                // the raw chunks owed so far (fraction)
   uint64_t raw_chunks = 0;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto ms_since = [](std::chrono::steady_clock::time_point t0) {
@@ -1059,9 +1059,19 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     uint32_t *sdelta = (uint32_t *)(stage + dof);
     const uint64_t nr = r1 - r0, nb = span_ok ? b1 - b0 : 0;
     bool raw = adapt == 2 && (ci & 1) != 0;
-    if (adapt == 1 && packed_b > 0) {
-      const double p_est = host_t / packed_b * (double)nb, c_nib = (double)nb / 2 / WIRE_BPMS;
-      raw = std::max(host_t, wire_t + 2 * c_nib) < std::max(host_t + p_est, wire_t + c_nib);
+    if (adapt == 1 && ci >= 2 && packed_b > 0) {
+      // from the third chunk on, with the packing rate of the first two: packing the whole batch P vs its nibbles on
+      // the wire C. Below 1.6 C everything is packed (near P = C a raw chunk only lengthens the wire); above, a
+      // fraction 2C / (P + C) of the chunks is packed and the rest sent raw, spread evenly, which balances the host's
+      // f P against the wire's (2 - f) C
+      const double P = host_t / packed_b * (double)n_bases, C = (double)n_bases / 2 / WIRE_BPMS;
+      if (P > 1.6 * C) {
+        raw_acc += 1.0 - 2 * C / (P + C);
+        if (raw_acc >= 1.0) {
+          raw = true;
+          raw_acc -= 1.0;
+        }
+      }
     }
     std::vector<uint64_t> t_wins(T, 0), t_bad(T, UINT64_MAX), t_rest(T, 0);
     // (the second chunk's run also counts the windows of the reads after it: the local rounds' expected total)
@@ -1113,7 +1123,6 @@ int mhmkc::add_host_nib(const uint8_t *bytes, const uint64_t *offs, uint64_t n_r
     const double run_ms = ms_since(tp);
     pack_ms += run_ms;
     if (rounds_rc) return rounds_rc;
-    wire_t += (double)nb / (raw ? 1 : 2) / WIRE_BPMS;
     if (!raw) {
       host_t += run_ms;
       packed_b += (double)nb;
